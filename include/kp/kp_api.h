@@ -1,0 +1,371 @@
+/*
+ * kp_api.h — C-ABI of the MI355X batched placement engine ("kp") for Karmada's
+ * scheduling hot path (genericScheduler.Schedule).
+ *
+ * Two layers live in this header:
+ *
+ *   1. The OBJECT MODEL: plain C structs that mirror the subset of the Karmada
+ *      API types the placement path reads. A cgo shim fills them from the Go
+ *      objects; the Python test harness fills them through
+ *      ctypes. Field names follow the Go/JSON names of the reference types:
+ *        kp_cluster          <- clusterv1alpha1.Cluster
+ *                               (pkg/apis/cluster/v1alpha1/types.go:43-377)
+ *        kp_binding          <- workv1alpha2.ResourceBindingSpec + Status subset
+ *                               (pkg/apis/work/v1alpha2/binding_types.go:71-300,443-467)
+ *        kp_cluster_affinity <- policyv1alpha1.ClusterAffinity
+ *                               (pkg/apis/policy/v1alpha1/propagation_types.go:445-772)
+ *      Strings are (ptr,len) views; slices are (ptr,count). Nothing is retained
+ *      after a call returns (cgo pointer rules): the engine copies/packs inputs.
+ *
+ *   2. The ENTRY POINTS (kp_*), each replacing a reference interface:
+ *        kp_schedule_batch          <- core.ScheduleAlgorithm.Schedule
+ *                                      (pkg/scheduler/core/generic_scheduler.go:37-49,71-116)
+ *        kp_filter_batch            <- framework.FilterPlugin.Filter for the in-tree filter set
+ *                                      (pkg/scheduler/framework/interface.go:85-98,
+ *                                       pkg/scheduler/framework/runtime/framework.go:93-122)
+ *        kp_score_batch             <- framework.ScorePlugin.Score summed by RunScorePlugins
+ *                                      (pkg/scheduler/framework/interface.go:215-232,
+ *                                       pkg/scheduler/framework/runtime/framework.go:126-170)
+ *        kp_max_available_replicas  <- estimatorclient.ReplicaEstimator.MaxAvailableReplicas
+ *                                      for the GeneralEstimator
+ *                                      (pkg/estimator/client/interface.go:39-71,
+ *                                       pkg/estimator/client/general.go:57-108)
+ *        kp_snapshot_create         <- cache.Cache.Snapshot (pkg/scheduler/cache/cache.go:124-139)
+ *
+ * Return convention: 0 = OK, <0 = KP_E* ; kp_last_error() gives the text.
+ * No exceptions cross the ABI. An engine handle is not re-entrant.
+ */
+#ifndef KP_API_H
+#define KP_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KP_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------- */
+/* Object model                                                              */
+/* ------------------------------------------------------------------------- */
+
+typedef struct kp_str {
+  const char* ptr;
+  uint32_t len;
+} kp_str;
+
+/* map[string]string entry (labels, matchLabels). */
+typedef struct kp_label {
+  kp_str key;
+  kp_str value;
+} kp_label;
+
+/* metav1.LabelSelectorRequirement / corev1.NodeSelectorRequirement. `op` is the
+ * operator string exactly as in the API ("In", "NotIn", "Exists", ...). */
+typedef struct kp_requirement {
+  kp_str key;
+  kp_str op;
+  const kp_str* values;
+  uint32_t n_values;
+} kp_requirement;
+
+/* policyv1alpha1.ClusterAffinity (propagation_types.go). */
+typedef struct kp_cluster_affinity {
+  uint8_t has_label_selector; /* LabelSelector != nil */
+  const kp_label* match_labels;
+  uint32_t n_match_labels;
+  const kp_requirement* match_expressions;
+  uint32_t n_match_expressions;
+  uint8_t has_field_selector; /* FieldSelector != nil */
+  const kp_requirement* field_expressions;
+  uint32_t n_field_expressions;
+  const kp_str* cluster_names;
+  uint32_t n_cluster_names;
+  const kp_str* exclude_clusters;
+  uint32_t n_exclude_clusters;
+} kp_cluster_affinity;
+
+/* policyv1alpha1.ClusterAffinityTerm: {AffinityName, ClusterAffinity, OverflowAffinities}. */
+typedef struct kp_affinity_term {
+  kp_str affinity_name;
+  kp_cluster_affinity affinity;
+  const kp_cluster_affinity* overflow; /* OverflowAffinities[i].ClusterAffinity */
+  uint32_t n_overflow;
+} kp_affinity_term;
+
+/* corev1.Toleration (TolerationSeconds is irrelevant for placement). */
+typedef struct kp_toleration {
+  kp_str key;
+  kp_str op; /* "", "Equal", "Exists", "Lt", "Gt", ... */
+  kp_str value;
+  kp_str effect;
+} kp_toleration;
+
+/* corev1.Taint. */
+typedef struct kp_taint {
+  kp_str key;
+  kp_str value;
+  kp_str effect;
+} kp_taint;
+
+/* policyv1alpha1.SpreadConstraint (MaxGroups/MinGroups are Go `int`). */
+typedef struct kp_spread_constraint {
+  kp_str spread_by_field; /* "cluster" | "region" | "zone" | "provider" | "" */
+  kp_str spread_by_label;
+  int64_t max_groups;
+  int64_t min_groups;
+} kp_spread_constraint;
+
+/* policyv1alpha1.StaticClusterWeight. */
+typedef struct kp_static_weight {
+  kp_cluster_affinity target;
+  int64_t weight;
+} kp_static_weight;
+
+/* corev1.ResourceList entry: name + resource.Quantity string ("100m", "2Gi", ...). */
+typedef struct kp_resource {
+  kp_str name;
+  kp_str quantity;
+} kp_resource;
+
+/* workv1alpha2.TargetCluster (Components omitted: multi-template gate is off). */
+typedef struct kp_target_cluster {
+  kp_str name;
+  int32_t replicas;
+} kp_target_cluster;
+
+/* ResourceBindingSpec + the status fields Schedule reads. */
+typedef struct kp_binding {
+  kp_str uid; /* spec.Resource.UID: FNV tie-break (pkg/util/helper/binding.go:117-144) */
+  kp_str api_version;
+  kp_str kind;
+  kp_str namespace_;
+  kp_str name;
+  int32_t replicas;
+  uint8_t has_replica_requirements; /* spec.ReplicaRequirements != nil */
+  uint8_t has_node_claim;           /* ReplicaRequirements.NodeClaim != nil */
+  const kp_resource* resource_request;
+  uint32_t n_resource_request;
+  uint32_t n_components; /* len(spec.Components) */
+  const kp_target_cluster* clusters; /* spec.Clusters (previous result) */
+  uint32_t n_clusters;
+  const kp_str* eviction_from; /* spec.GracefulEvictionTasks[].FromCluster */
+  uint32_t n_eviction_from;
+  uint8_t has_reschedule_triggered_at;
+  uint8_t has_last_scheduled_time;
+  int64_t reschedule_triggered_at_ns; /* unix nanoseconds */
+  int64_t last_scheduled_time_ns;
+  kp_str observed_affinity_name; /* status.SchedulerObservedAffinityName */
+  /* spec.Placement */
+  uint8_t has_cluster_affinity;
+  kp_cluster_affinity cluster_affinity;
+  const kp_affinity_term* cluster_affinities;
+  uint32_t n_cluster_affinities;
+  const kp_toleration* tolerations; /* ClusterTolerations */
+  uint32_t n_tolerations;
+  const kp_spread_constraint* spread_constraints;
+  uint32_t n_spread_constraints;
+  uint8_t has_replica_scheduling;
+  kp_str replica_scheduling_type;     /* "Duplicated" | "Divided" */
+  kp_str replica_division_preference; /* "Aggregated" | "Weighted" */
+  uint8_t has_weight_preference;
+  const kp_static_weight* static_weights;
+  uint32_t n_static_weights;
+  kp_str dynamic_weight; /* "AvailableReplicas" | "" */
+} kp_binding;
+
+/* Cluster.Status.APIEnablements flattened to (GroupVersion, Resources[].Kind) pairs. */
+typedef struct kp_api_enablement {
+  kp_str group_version;
+  kp_str kind;
+} kp_api_enablement;
+
+/* clusterv1alpha1.ResourceModelRange / ResourceModel / AllocatableModeling. */
+typedef struct kp_model_range {
+  kp_str name;
+  kp_str min;
+  kp_str max;
+} kp_model_range;
+
+typedef struct kp_resource_model {
+  uint32_t grade;
+  const kp_model_range* ranges;
+  uint32_t n_ranges;
+} kp_resource_model;
+
+typedef struct kp_allocatable_modeling {
+  uint32_t grade;
+  int64_t count;
+} kp_allocatable_modeling;
+
+/* clusterv1alpha1.Cluster subset. */
+typedef struct kp_cluster {
+  kp_str name;
+  uint8_t deleting; /* !DeletionTimestamp.IsZero() */
+  const kp_label* labels;
+  uint32_t n_labels;
+  kp_str provider;
+  kp_str region;
+  kp_str zone;
+  const kp_str* zones;
+  uint32_t n_zones;
+  const kp_taint* taints;
+  uint32_t n_taints;
+  const kp_api_enablement* api_enablements;
+  uint32_t n_api_enablements;
+  const kp_resource_model* resource_models; /* Spec.ResourceModels */
+  uint32_t n_resource_models;
+  uint8_t has_resource_summary; /* Status.ResourceSummary != nil */
+  const kp_resource* allocatable;
+  uint32_t n_allocatable;
+  const kp_resource* allocated;
+  uint32_t n_allocated;
+  const kp_resource* allocating;
+  uint32_t n_allocating;
+  const kp_allocatable_modeling* allocatable_modelings;
+  uint32_t n_allocatable_modelings;
+} kp_cluster;
+
+/* In-tree plugin names (pkg/scheduler/framework/plugins/registry.go:33-50). */
+enum {
+  KP_PLUGIN_API_ENABLEMENT = 1u << 0,
+  KP_PLUGIN_TAINT_TOLERATION = 1u << 1,
+  KP_PLUGIN_CLUSTER_AFFINITY = 1u << 2,
+  KP_PLUGIN_SPREAD_CONSTRAINT = 1u << 3,
+  KP_PLUGIN_CLUSTER_LOCALITY = 1u << 4,
+  KP_PLUGIN_CLUSTER_EVICTION = 1u << 5,
+  KP_PLUGIN_ALL = 0x3fu
+};
+
+/* Flags and gates that change results (cmd/scheduler/app/options/options.go:130-165,
+ * pkg/features/features.go:162-189). */
+typedef struct kp_options {
+  uint8_t enable_empty_workload_propagation;   /* --enable-empty-workload-propagation */
+  uint8_t customized_cluster_resource_modeling; /* feature gate, default on */
+  uint32_t enabled_plugins;                     /* KP_PLUGIN_* bitmask (--plugins) */
+} kp_options;
+
+/* ------------------------------------------------------------------------- */
+/* Results                                                                   */
+/* ------------------------------------------------------------------------- */
+
+/* Error class of one Schedule call (framework/types.go:61-99). */
+enum {
+  KP_STATUS_OK = 0,
+  KP_STATUS_FIT_ERROR = 1,     /* *framework.FitError */
+  KP_STATUS_UNSCHEDULABLE = 2, /* *framework.UnschedulableError (possibly wrapped) */
+  KP_STATUS_ERROR = 3          /* any other error */
+};
+
+/* The reference error site that produced a non-OK status. */
+enum {
+  KP_ERR_NONE = 0,
+  KP_ERR_FIT = 1,                    /* generic_scheduler.go:84-89; arg = NumAllClusters */
+  KP_ERR_REGION_MIN_GROUPS = 2,      /* select_clusters_by_region.go:30-32 */
+  KP_ERR_REGION_CLUSTER_MIN = 3,     /* select_clusters_by_region.go:37-39 */
+  KP_ERR_CLUSTER_MIN_GROUPS = 4,     /* select_clusters_by_cluster.go:28-30 */
+  KP_ERR_CLUSTER_RESOURCE = 5,       /* select_clusters_by_cluster.go:39-41; arg = needCnt */
+  KP_ERR_SPREAD_UNSUPPORTED = 6,     /* select_clusters.go:54 */
+  KP_ERR_NO_CLUSTERS = 7,            /* common.go:55-57 */
+  KP_ERR_UNSUPPORTED_STRATEGY = 8,   /* common.go:143-148 */
+  KP_ERR_OVERFLOW_NOT_ENOUGH = 9,    /* common.go:132-134 */
+  KP_ERR_FRESH_NOT_ENOUGH = 10,      /* assignment.go:218-221 wrapping division_algorithm.go:76-78; arg = available */
+  KP_ERR_SCALE_DOWN_NOT_ENOUGH = 11, /* assignment.go:228-231; arg = available */
+  KP_ERR_SCALE_UP_NOT_ENOUGH = 12,   /* assignment.go:236-239; arg = available */
+  KP_ERR_UNDEFINED_STRATEGY = 13     /* division_algorithm.go:97-99 */
+};
+
+/* Per-batch results, engine-owned, valid until the next call on the engine.
+ * Targets of binding b are entries [offsets[b], offsets[b+1]) of cluster_idx /
+ * replicas; cluster_idx indexes the caller's cluster array given to
+ * kp_snapshot_create. Order inside one binding follows the reference where it
+ * is deterministic; compare as a multiset (test/helper/scheduler.go:26-40). */
+typedef struct kp_results {
+  uint64_t n_bindings;
+  const int32_t* status;   /* KP_STATUS_* */
+  const int32_t* err_code; /* KP_ERR_* */
+  const int64_t* err_arg;
+  const uint64_t* offsets; /* n_bindings + 1 */
+  const uint32_t* cluster_idx;
+  const int32_t* replicas;
+  uint64_t n_targets;
+} kp_results;
+
+/* Per-stage timing of the last kp_schedule_batch call (milliseconds, host clock
+ * around device work; kernel-only numbers come from rocprof). */
+typedef struct kp_stage_times {
+  double pair_ms;      /* filter + score + estimate kernel */
+  double select_ms;    /* candidate/group/select/divide kernels */
+  double host_ms;      /* host group-combination (region DFS) */
+  double copy_ms;      /* device -> host result copies */
+  double total_ms;
+  float pair_kernel_ms; /* HIP event time of the pair kernel */
+  float select_kernel_ms;
+} kp_stage_times;
+
+/* ------------------------------------------------------------------------- */
+/* Entry points                                                              */
+/* ------------------------------------------------------------------------- */
+
+typedef struct kp_engine kp_engine;
+typedef struct kp_snapshot kp_snapshot;
+typedef struct kp_batch kp_batch;
+
+enum {
+  KP_OK = 0,
+  KP_EINVAL = -1,
+  KP_ENOMEM = -2,
+  KP_EDEVICE = -3,
+  KP_ENOTSUP = -4,
+  KP_ESTATE = -5
+};
+
+int kp_abi_version(void);
+
+/* Creates an engine bound to HIP device `device` (one HIP stream). */
+int kp_engine_create(int device, kp_engine** out);
+void kp_engine_destroy(kp_engine* e);
+const char* kp_last_error(const kp_engine* e);
+
+/* Packs a cluster list (cache.Snapshot) into the device SoA layout and uploads it.
+ * Replaces the per-Schedule List+DeepCopy (cache.go:124-139) by one upload. */
+int kp_snapshot_create(kp_engine* e, const kp_cluster* clusters, uint64_t n_clusters,
+                       const kp_options* opts, kp_snapshot** out);
+void kp_snapshot_destroy(kp_snapshot* s);
+/* Packed snapshot as one relocatable byte image (for RCCL broadcast) and back. */
+int kp_snapshot_export(const kp_snapshot* s, const void** bytes, uint64_t* n_bytes);
+int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_snapshot** out);
+
+/* Packs a batch of bindings against a snapshot and uploads them to HBM. */
+int kp_batch_create(kp_engine* e, const kp_snapshot* s, const kp_binding* bindings,
+                    uint64_t n_bindings, kp_batch** out);
+void kp_batch_destroy(kp_batch* b);
+
+/* genericScheduler.Schedule for every binding of the batch. */
+int kp_schedule_batch(kp_engine* e, kp_batch* b, kp_results* out);
+
+/* FilterPlugin boundary: feasibility of every (binding, cluster) pair after
+ * RunFilterPlugins (+ the skip-deleting rule of findClustersThatFit).
+ * out_mask: n_bindings * ceil(n_clusters/64) words, bit c%64 of word c/64 set
+ * when cluster c (caller order) fits. */
+int kp_filter_batch(kp_engine* e, kp_batch* b, uint64_t* out_mask);
+
+/* ScorePlugin boundary: summed score (RunScorePlugins) per pair; n_bindings*n_clusters. */
+int kp_score_batch(kp_engine* e, kp_batch* b, int64_t* out_scores);
+
+/* ReplicaEstimator boundary (GeneralEstimator.MaxAvailableReplicas): for binding
+ * `binding` of the batch and the given caller cluster indices, writes the
+ * estimator answer per cluster in input order (general.go:57-64). */
+int kp_max_available_replicas(kp_engine* e, kp_batch* b, uint64_t binding,
+                              const uint32_t* cluster_idx, uint64_t n, int32_t* out);
+
+/* Last schedule call's stage timings. */
+int kp_last_stage_times(const kp_engine* e, kp_stage_times* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KP_API_H */

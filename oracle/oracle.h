@@ -1,0 +1,115 @@
+/*
+ * oracle.h — CPU restatement of Karmada's genericScheduler.Schedule path.
+ *
+ * TEST INFRASTRUCTURE ONLY. This library is the checker for the HIP engine and
+ * the CPU baseline of bench.py. Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it. The product (karmada_amd/, libkp.so)
+ * never links or calls it.
+ *
+ * The restatement follows the Go sources of /root/reference (cited file:line in
+ * oracle.cpp) over the object model of include/kp/kp_api.h. Parity pinning:
+ * the reference is Go and no Go toolchain exists here, so the
+ * oracle is pinned by the reference's own table-driven tests, transcribed into
+ * tests/golden/ JSON files (see tests/test_oracle_golden.py).
+ *
+ * Modes:
+ *   KPO_FAITHFUL — the reference's algorithmic shape: per-call snapshot deep
+ *                  copy (cache.go:124-139), per-pair selector compile
+ *                  (selector.go:116), first-fit simulator loop
+ *                  (scheduling_simulator_components.go:51-130), heap Webster
+ *                  (webstermethod.go:112-161), Go pdqsort emulation.
+ *   KPO_FAST     — same results; no per-call deep copy and the closed-form grade
+ *                  walk instead of the FF loop.
+ */
+#ifndef KPO_ORACLE_H
+#define KPO_ORACLE_H
+
+#include <stdint.h>
+
+#include "../include/kp/kp_api.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { KPO_FAITHFUL = 0, KPO_FAST = 1 };
+
+typedef struct kpo_world kpo_world;
+
+typedef struct kpo_results {
+  uint64_t n;
+  int32_t* status;
+  int32_t* err_code;
+  int64_t* err_arg;
+  uint64_t* offsets; /* n+1 */
+  uint32_t* cluster_idx;
+  int32_t* replicas;
+  uint64_t n_targets;
+} kpo_results;
+
+/* A ClusterDetailInfo (spreadconstraint/group_clusters.go:78-93) for unit hooks. */
+typedef struct kpo_candidate {
+  kp_str name;
+  int64_t score;
+  int32_t overflow_order;
+  int64_t available_replicas;
+  int32_t allocatable_replicas;
+  int32_t cluster; /* index into the hook's cluster array, or -1 */
+} kpo_candidate;
+
+kpo_world* kpo_world_create(const kp_cluster* clusters, uint64_t n, const kp_options* opts);
+void kpo_world_destroy(kpo_world* w);
+
+/* Schedule bindings with `n_threads` host threads (<=0: 1). */
+int kpo_schedule(kpo_world* w, const kp_binding* b, uint64_t n, int mode, int n_threads,
+                 kpo_results** out);
+void kpo_results_free(kpo_results* r);
+
+/* ---- unit hooks used by the golden-vector tests ---- */
+int kpo_quantity(const char* s, uint32_t len, int milli, int64_t* out); /* 0 ok, -1 parse error */
+int kpo_cluster_matches(const kp_cluster* c, const kp_cluster_affinity* a);
+/* Filter plugins in canonical order; returns 0 when the cluster fits, else the
+ * KP_PLUGIN_* bit of the first failing plugin. */
+uint32_t kpo_filter(const kp_cluster* c, const kp_binding* b, const kp_options* opts);
+int64_t kpo_score(const kp_cluster* c, const kp_binding* b, const kp_options* opts);
+int32_t kpo_max_available_replicas(const kp_cluster* c, const kp_binding* b,
+                                   const kp_options* opts, int mode);
+/* helper.AllocateWebsterSeats; parties = union of names in votes/init, output is in
+ * ascending name order: out_seats[k] for the k-th distinct name. Returns #parties. */
+int kpo_allocate_webster(int32_t new_seats, const kp_str* vote_names, const int64_t* votes,
+                         uint32_t n_votes, const kp_str* init_names, const int32_t* init_seats,
+                         uint32_t n_init, int tie_mode, kp_str uid, int32_t* out_seats,
+                         uint32_t out_cap);
+/* helper.SpreadReplicasByTargetClusters / Dispenser.AllocateByWeight;
+ * returns #targets written (name order), names as indices into `tcs`. */
+int kpo_spread_replicas(int32_t num, const kp_target_cluster* tcs, uint32_t n,
+                        const kp_target_cluster* init, uint32_t n_init, kp_str uid,
+                        kp_target_cluster* out, uint32_t out_cap);
+/* core.AssignReplicas (level 0), the strategy function alone (level 1) or
+ * buildScheduledClusters+dynamicScaleUp (level 2) over explicit candidates;
+ * `clusters` backs StaticWeight ClusterMatches (candidate.cluster indexes it).
+ * Returns #targets, or -status on error. */
+int kpo_assign_replicas(const kpo_candidate* cands, uint32_t n, const kp_cluster* clusters,
+                        uint32_t n_clusters, const kp_binding* b, int level, int32_t* err_code,
+                        int64_t* err_arg, kp_target_cluster* out, uint32_t out_cap);
+/* spreadconstraint.selectGroups: returns #selected; out = indices into input. */
+int kpo_select_groups(const kp_str* names, const int64_t* values, const int64_t* weights,
+                      uint32_t n, int64_t min_c, int64_t max_c, int64_t target, uint32_t* out);
+/* spreadconstraint.(GroupClustersInfo).calcGroupScore. */
+int64_t kpo_calc_group_score(const kpo_candidate* cands, uint32_t n, const kp_binding* b,
+                             int64_t min_groups);
+/* GroupClustersWithScore + SelectBestClusters from a scored cluster list with
+ * precomputed estimator answers; returns #selected (candidate indices) or <0 =
+ * -KP_ERR_*. */
+int kpo_select_clusters(const kp_cluster* clusters, const int64_t* scores, const int32_t* avail,
+                        uint32_t n, const kp_binding* b, int32_t need_replicas, uint32_t* out,
+                        uint32_t out_cap);
+/* Go 1.26 sort.Sort emulation on TargetClustersList (Less = Replicas desc). */
+void kpo_sort_target_clusters(int32_t* replicas, uint32_t* ids, uint32_t n);
+uint32_t kpo_fnv32a(const char* s, uint32_t len);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif
