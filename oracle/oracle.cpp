@@ -2141,6 +2141,33 @@ int32_t kpo_max_available_replicas(const kp_cluster* c, const kp_binding* b, con
   return maxAvailableReplicas(cl, convBinding(*b), convOptions(opts), mode);
 }
 
+
+int kpo_estimator_part(const kp_cluster* c, const kp_binding* b, const kp_options* opts, int part, int mode,
+                       int64_t* out) {
+  bool ok = true;
+  Cluster cl = convCluster(*c, 0, &ok);
+  Binding bb = convBinding(*b);
+  Options o = convOptions(opts);
+  switch (part) {
+    case 0:
+      *out = maxAvailableReplicas(cl, bb, o, mode);
+      return 0;
+    case 1: {
+      i64 v = -1;
+      bool r = getMaximumReplicasBasedOnResourceModels(cl, bb, mode, &v);
+      *out = r ? v : -1;
+      return r ? 0 : -1;
+    }
+    case 2:
+      *out = getMaximumReplicasBasedOnClusterSummary(cl, bb.request);
+      return 0;
+    case 3:
+      *out = getAllowedPodNumber(cl);
+      return 0;
+  }
+  return -1;
+}
+
 int kpo_allocate_webster(int32_t new_seats, const kp_str* vote_names, const int64_t* votes, uint32_t n_votes,
                          const kp_str* init_names, const int32_t* init_seats, uint32_t n_init, int tie_mode,
                          kp_str uid, int32_t* out_seats, uint32_t out_cap) {

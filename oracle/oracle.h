@@ -74,6 +74,10 @@ uint32_t kpo_filter(const kp_cluster* c, const kp_binding* b, const kp_options* 
 int64_t kpo_score(const kp_cluster* c, const kp_binding* b, const kp_options* opts);
 int32_t kpo_max_available_replicas(const kp_cluster* c, const kp_binding* b,
                                    const kp_options* opts, int mode);
+/* GeneralEstimator pieces: part 0 maxAvailableReplicas, 1 getMaximumReplicasBased-
+ * OnResourceModels (returns -1 on error), 2 ...OnClusterSummary, 3 getAllowedPodNumber. */
+int kpo_estimator_part(const kp_cluster* c, const kp_binding* b, const kp_options* opts, int part,
+                       int mode, int64_t* out);
 /* helper.AllocateWebsterSeats; parties = union of names in votes/init, output is in
  * ascending name order: out_seats[k] for the k-th distinct name. Returns #parties. */
 int kpo_allocate_webster(int32_t new_seats, const kp_str* vote_names, const int64_t* votes,

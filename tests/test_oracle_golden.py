@@ -126,3 +126,60 @@ def test_assign(case):
     assert got is not None, (status, err)
     wants = case.get("wants") or [case["want"]]
     assert any(multiset_eq(got, [tuple(x) for x in want]) for want in wants), got
+
+
+# --------------------------------------------------------------------------- selectors
+SEL = load("selector.json")
+
+
+@pytest.mark.parametrize("case", SEL["cases"], ids=ids(SEL["cases"]))
+def test_cluster_matches(case):
+    L = O.lib()
+    w = api.World()
+    c = w.cluster(SEL["cluster"])
+    a = w.affinity(case["affinity"])
+    assert L.kpo_cluster_matches(C.byref(c), C.byref(a)) == int(case["want"])
+
+
+@pytest.mark.parametrize("case", SEL["zoneCases"], ids=ids(SEL["zoneCases"]))
+def test_match_zones(case):
+    L = O.lib()
+    w = api.World()
+    c = w.cluster({"name": "c", "zones": case["zones"]})
+    a = w.affinity({"fieldSelector": {"matchExpressions": [case["expr"]]}})
+    assert L.kpo_cluster_matches(C.byref(c), C.byref(a)) == int(case["want"])
+
+
+# --------------------------------------------------------------------------- estimator
+EST = load("estimator.json")
+O.lib().kpo_estimator_part.argtypes = [C.POINTER(api.kp_cluster), C.POINTER(api.kp_binding),
+                                       C.POINTER(api.kp_options), C.c_int, C.c_int, C.POINTER(C.c_int64)]
+
+
+def _expand(v):
+    if isinstance(v, str) and v.startswith("$"):
+        return EST[v[1:]]
+    if isinstance(v, dict):
+        return {k: _expand(x) for k, x in v.items()}
+    return v
+
+
+@pytest.mark.parametrize("mode", [O.FAITHFUL, O.FAST])
+@pytest.mark.parametrize("case", EST["cases"], ids=ids(EST["cases"]))
+def test_estimator(case, mode):
+    L = O.lib()
+    w = api.World()
+    c = w.cluster(_expand(case["cluster"]))
+    spec = {"replicas": 1}
+    if case.get("request") is not None:
+        spec["replicaRequirements"] = {"resourceRequest": case["request"]}
+    b = w.binding(spec)
+    part = {"max": 0, "models": 1, "summary": 2, "allowed": 3}[case["fn"]]
+    out = C.c_int64()
+    opts = api.options(models_gate=case.get("modelsGate", True))
+    rc = L.kpo_estimator_part(C.byref(c), C.byref(b), C.byref(opts), part, mode, C.byref(out))
+    if case.get("expectError"):
+        assert rc != 0
+    else:
+        assert rc == 0
+    assert out.value == case["expected"]
