@@ -1,0 +1,1372 @@
+// engine.cpp — host side of the kp placement engine: the C-ABI of
+// include/kp/kp_api.h, the snapshot/binding packer, kernel orchestration on one
+// HIP stream, and the host-kept selectGroups step of region spreading.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/kp/kp_api.h"
+#include "k8s.h"
+#include "kp_layout.h"
+#include "kp_launch.h"
+#include "kp_paths.h"
+
+using namespace kp;
+
+namespace {
+
+std::string S(const kp_str& s) { return (s.ptr && s.len) ? std::string(s.ptr, s.len) : std::string(); }
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct Dict {
+  std::unordered_map<std::string, int32_t> m;
+  std::vector<std::string> names;
+  int32_t add(const std::string& s) {
+    auto it = m.find(s);
+    if (it != m.end()) return it->second;
+    int32_t id = (int32_t)names.size();
+    m.emplace(s, id);
+    names.push_back(s);
+    return id;
+  }
+  int32_t get(const std::string& s) const {
+    auto it = m.find(s);
+    return it == m.end() ? -1 : it->second;
+  }
+};
+
+// One device allocation carved into aligned sub-buffers.
+struct Arena {
+  std::vector<std::pair<void**, size_t>> req;
+  void* base = nullptr;
+  size_t total = 0;
+  template <class T>
+  void add(T** p, size_t count) {
+    req.push_back({(void**)p, count * sizeof(T)});
+  }
+  hipError_t alloc() {
+    total = 0;
+    for (auto& r : req) total += (r.second + 255) & ~(size_t)255;
+    if (total == 0) total = 256;
+    hipError_t e = hipMalloc(&base, total);
+    if (e != hipSuccess) return e;
+    char* p = (char*)base;
+    for (auto& r : req) {
+      *r.first = p;
+      p += (r.second + 255) & ~(size_t)255;
+    }
+    return hipSuccess;
+  }
+  ~Arena() {
+    if (base) (void)hipFree(base);
+  }
+};
+
+#define HIPCHK(x)                                                            \
+  do {                                                                       \
+    hipError_t _e = (x);                                                     \
+    if (_e != hipSuccess) {                                                  \
+      e->err = std::string(#x) + ": " + hipGetErrorString(_e);               \
+      return KP_EDEVICE;                                                     \
+    }                                                                        \
+  } while (0)
+
+}  // namespace
+
+// ============================================================================
+// Engine / snapshot / batch objects
+// ============================================================================
+struct kp_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[6];
+  std::string err;
+  kp_stage_times times{};
+  int n_threads = 8;
+  size_t max_lds = 65536;
+};
+
+struct kp_snapshot {
+  kp_engine* e = nullptr;
+  kp_options opts{};
+  int C = 0, Cp = 0, W = 0;
+  Dict str, keys, gvk, res, regions;
+  std::unordered_map<std::string, int32_t> rank_of;  // cluster name -> rank
+  std::vector<uint32_t> perm;                        // rank -> caller index
+  std::vector<int32_t> inv;                          // caller index -> rank
+  int32_t rid_cpu = -1, rid_mem = -1, rid_eph = -1;
+  int n_tmpl = 0;
+  // host copies
+  std::vector<uint32_t> flags;
+  std::vector<int32_t> provider, region, region_idx, zone_off, zone_ids, label_val, taint_off, taint_key, taint_val,
+      taint_eff, mgrp_off, mgrp_tid;
+  std::vector<int64_t> provider_int, region_int, allowed, avail, mgrp_cnt, tmpl;
+  std::vector<uint64_t> api_bits;
+  Arena dev;
+  SnapView view{};
+};
+
+struct kp_batch {
+  kp_snapshot* snap = nullptr;
+  int B = 0;
+  std::vector<BindHdr> hdr;
+  std::vector<int32_t> ipool;
+  std::vector<int64_t> lpool;
+  std::vector<Tol> tols;
+  std::vector<Prog> progs;
+  std::vector<Instr> instrs;
+  std::vector<int32_t> l_all, l_cluster, l_region, l_slow;
+  uint64_t out_cap = 0;
+  Arena dev;
+  BatchView view{};
+  // device work buffers
+  uint64_t* fmask = nullptr;
+  int32_t* est = nullptr;
+  int32_t *d_all = nullptr, *d_cluster = nullptr, *d_region = nullptr, *d_slowlist = nullptr;
+  int32_t *status = nullptr, *errc = nullptr, *slow = nullptr;
+  int64_t* arg = nullptr;
+  uint64_t* start = nullptr;
+  uint32_t* count = nullptr;
+  unsigned long long* counter = nullptr;
+  uint32_t* out_idx = nullptr;
+  int32_t* out_rep = nullptr;
+  uint64_t* offsets_d = nullptr;
+  uint32_t* cidx_d = nullptr;
+  int32_t* crep_d = nullptr;
+  RegionOut* rout = nullptr;
+  int32_t *rstat = nullptr, *rsel = nullptr, *rnsel = nullptr;
+  unsigned char* slow_scratch = nullptr;
+  size_t slow_slot = 0;
+  int slow_grid = 0, slow_cap = 0;
+  // host results
+  std::vector<int32_t> h_status, h_err, h_rstat, h_rsel, h_rnsel;
+  std::vector<int64_t> h_arg;
+  std::vector<uint64_t> h_start, h_offsets;
+  std::vector<uint32_t> h_count, h_cidx;
+  std::vector<int32_t> h_crep;
+  std::vector<RegionOut> h_rout;
+};
+
+// ============================================================================
+// Snapshot packing (cache.Snapshot, cache.go:124-139, packed once)
+// ============================================================================
+namespace {
+
+typedef std::map<std::string, k8s::Qty> QtyMap;
+bool qmap(const kp_resource* r, uint32_t n, QtyMap* m) {
+  bool ok = true;
+  for (uint32_t i = 0; i < n; i++) {
+    k8s::Qty q;
+    if (!k8s::parse_quantity(S(r[i].quantity), &q)) ok = false;
+    (*m)[S(r[i].name)] = q;
+  }
+  return ok;
+}
+
+int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_options* o, kp_snapshot* s) {
+  s->opts = o ? *o : kp_options{0, 1, KP_PLUGIN_ALL};
+  if (n > (uint64_t)kMaxClusters) {
+    e->err = "too many clusters";
+    return KP_ENOTSUP;
+  }
+  const int C = (int)n;
+  s->C = C;
+  s->Cp = ((C + 63) / 64) * 64;
+  if (s->Cp == 0) s->Cp = 64;
+  s->W = s->Cp / 64;
+  const int Cp = s->Cp;
+  std::vector<uint32_t> order(C);
+  std::vector<std::string> names(C);
+  for (int i = 0; i < C; i++) {
+    order[i] = i;
+    names[i] = S(cl[i].name);
+  }
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return names[a] < names[b]; });
+  s->perm = order;
+  s->inv.assign(C, -1);
+  for (int r = 0; r < C; r++) {
+    s->inv[order[r]] = r;
+    if (!s->rank_of.emplace(names[order[r]], r).second) {
+      e->err = "duplicate cluster name " + names[order[r]];
+      return KP_EINVAL;
+    }
+  }
+  // pass 1: dictionaries
+  std::vector<std::string> regs;
+  for (int r = 0; r < C; r++) {
+    const kp_cluster& c = cl[order[r]];
+    for (uint32_t i = 0; i < c.n_labels; i++) {
+      s->keys.add(S(c.labels[i].key));
+      s->str.add(S(c.labels[i].value));
+    }
+    s->str.add(S(c.provider));
+    s->str.add(S(c.region));
+    for (uint32_t i = 0; i < c.n_zones; i++) s->str.add(S(c.zones[i]));
+    for (uint32_t i = 0; i < c.n_taints; i++) {
+      s->str.add(S(c.taints[i].key));
+      s->str.add(S(c.taints[i].value));
+    }
+    for (uint32_t i = 0; i < c.n_api_enablements; i++)
+      s->gvk.add(S(c.api_enablements[i].group_version) + '\0' + S(c.api_enablements[i].kind));
+    for (uint32_t i = 0; i < c.n_allocatable; i++) s->res.add(S(c.allocatable[i].name));
+    for (uint32_t m = 0; m < c.n_resource_models; m++)
+      for (uint32_t j = 0; j < c.resource_models[m].n_ranges; j++) s->res.add(S(c.resource_models[m].ranges[j].name));
+    if (c.region.len) regs.push_back(S(c.region));
+  }
+  s->rid_cpu = s->res.add("cpu");
+  s->rid_mem = s->res.add("memory");
+  s->rid_eph = s->res.add("ephemeral-storage");
+  std::sort(regs.begin(), regs.end());
+  regs.erase(std::unique(regs.begin(), regs.end()), regs.end());
+  for (auto& r : regs) s->regions.add(r);
+  const int K = (int)s->keys.names.size(), AW = ((int)s->gvk.names.size() + 63) / 64, R = (int)s->res.names.size();
+  s->flags.assign(Cp, 0);
+  s->provider.assign(Cp, -1);
+  s->region.assign(Cp, -1);
+  s->region_idx.assign(Cp, -1);
+  s->provider_int.assign(Cp, 0);
+  s->region_int.assign(Cp, 0);
+  s->label_val.assign((size_t)std::max(K, 1) * Cp, -1);
+  s->api_bits.assign((size_t)std::max(AW, 1) * Cp, 0);
+  s->allowed.assign(Cp, 0);
+  s->avail.assign((size_t)std::max(R, 1) * Cp, 0);
+  s->zone_off.assign(C + 1, 0);
+  s->taint_off.assign(C + 1, 0);
+  s->mgrp_off.assign(C + 1, 0);
+  std::map<std::vector<int64_t>, int32_t> tmpl_ids;
+  for (int r = 0; r < C; r++) {
+    const kp_cluster& c = cl[order[r]];
+    uint32_t f = 0;
+    if (c.deleting) f |= CF_DELETING;
+    std::string prov = S(c.provider), reg = S(c.region);
+    if (!prov.empty()) {
+      f |= CF_HAS_PROVIDER;
+      s->provider[r] = s->str.get(prov);
+      int64_t v;
+      if (k8s::parse_int64(prov, &v)) {
+        f |= CF_PROVIDER_INT;
+        s->provider_int[r] = v;
+      }
+    }
+    if (!reg.empty()) {
+      f |= CF_HAS_REGION;
+      s->region[r] = s->str.get(reg);
+      s->region_idx[r] = s->regions.get(reg);
+      int64_t v;
+      if (k8s::parse_int64(reg, &v)) {
+        f |= CF_REGION_INT;
+        s->region_int[r] = v;
+      }
+    }
+    if (c.n_zones) f |= CF_HAS_ZONES;
+    for (uint32_t i = 0; i < c.n_zones; i++) s->zone_ids.push_back(s->str.get(S(c.zones[i])));
+    s->zone_off[r + 1] = (int32_t)s->zone_ids.size();
+    for (uint32_t i = 0; i < c.n_labels; i++)  // map semantics: later entries win
+      s->label_val[(size_t)s->keys.get(S(c.labels[i].key)) * Cp + r] = s->str.get(S(c.labels[i].value));
+    for (uint32_t i = 0; i < c.n_taints; i++) {
+      std::string eff = S(c.taints[i].effect);
+      int32_t ef = eff == "NoSchedule" ? EFF_NOSCHEDULE : (eff == "NoExecute" ? EFF_NOEXECUTE : 0);
+      if (!ef) continue;  // only NoSchedule/NoExecute are filtered (taint_toleration.go:65-67)
+      s->taint_key.push_back(s->str.get(S(c.taints[i].key)));
+      s->taint_val.push_back(s->str.get(S(c.taints[i].value)));
+      s->taint_eff.push_back(ef);
+    }
+    s->taint_off[r + 1] = (int32_t)s->taint_key.size();
+    for (uint32_t i = 0; i < c.n_api_enablements; i++) {
+      int32_t g = s->gvk.get(S(c.api_enablements[i].group_version) + '\0' + S(c.api_enablements[i].kind));
+      s->api_bits[(size_t)(g >> 6) * Cp + r] |= 1ull << (g & 63);
+    }
+    if (c.has_resource_summary) {
+      f |= CF_HAS_SUMMARY;
+      QtyMap al, ad, ag;
+      bool ok = qmap(c.allocatable, c.n_allocatable, &al) & qmap(c.allocated, c.n_allocated, &ad) &
+                qmap(c.allocating, c.n_allocating, &ag);
+      if (!ok) {
+        e->err = "unparsable quantity in cluster " + names[order[r]];
+        return KP_EINVAL;
+      }
+      auto pods = [](const QtyMap& m) {
+        auto it = m.find("pods");
+        return it == m.end() ? 0 : k8s::value(it->second);
+      };
+      int64_t allowed = pods(al) - pods(ad) - pods(ag);  // getAllowedPodNumber (general.go:445-463)
+      s->allowed[r] = allowed > 0 ? allowed : 0;
+      for (auto& kv : al) {  // getMaximumReplicasBasedOnClusterSummary operands (general.go:465-505)
+        k8s::Qty q = kv.second;
+        auto x = ad.find(kv.first);
+        if (x != ad.end()) q.nano -= x->second.nano;
+        x = ag.find(kv.first);
+        if (x != ag.end()) q.nano -= x->second.nano;
+        int64_t v = k8s::value(q);
+        int64_t d = v <= 0 ? 0 : (kv.first == "cpu" ? k8s::milli(q) : v);
+        s->avail[(size_t)s->res.get(kv.first) * Cp + r] = d;
+      }
+      // buildModelNodes (general.go:296-361)
+      if (s->opts.customized_cluster_resource_modeling && c.n_allocatable_modelings > 0 && c.n_resource_models > 0) {
+        bool neg = false;
+        std::map<uint32_t, int64_t> cnt;
+        for (uint32_t i = 0; i < c.n_allocatable_modelings; i++) {
+          if (c.allocatable_modelings[i].count < 0) neg = true;
+          cnt[c.allocatable_modelings[i].grade] += c.allocatable_modelings[i].count;
+        }
+        if (!neg) {
+          std::map<uint32_t, std::vector<int64_t>> caps;
+          for (uint32_t m = 0; m < c.n_resource_models; m++) {
+            std::vector<int64_t> t(R, 0);
+            QtyMap rl;
+            for (uint32_t j = 0; j < c.resource_models[m].n_ranges; j++) {
+              k8s::Qty q;
+              if (!k8s::parse_quantity(S(c.resource_models[m].ranges[j].min), &q)) {
+                e->err = "unparsable resource model quantity";
+                return KP_EINVAL;
+              }
+              rl[S(c.resource_models[m].ranges[j].name)] = q;
+            }
+            for (auto& kv : rl) {  // util.NewResource (resource.go:46-75); pods forced to 110
+              const std::string& nm = kv.first;
+              int32_t rid = s->res.get(nm);
+              if (nm == "cpu") t[rid] += k8s::milli(kv.second);
+              else if (nm == "memory" || nm == "ephemeral-storage") t[rid] += k8s::value(kv.second);
+              else if (nm == "pods") continue;
+              else if (k8s::scalar_resource(nm)) t[rid] += k8s::value(kv.second);
+            }
+            caps[c.resource_models[m].grade] = t;
+          }
+          for (auto& kv : caps) {  // grades ascending
+            auto it = cnt.find(kv.first);
+            int64_t k = it == cnt.end() ? 0 : it->second;
+            if (k == 0) continue;
+            auto ti = tmpl_ids.find(kv.second);
+            int32_t tid;
+            if (ti == tmpl_ids.end()) {
+              tid = (int32_t)tmpl_ids.size();
+              tmpl_ids.emplace(kv.second, tid);
+            } else {
+              tid = ti->second;
+            }
+            s->mgrp_tid.push_back(tid);
+            s->mgrp_cnt.push_back(k);
+          }
+          f |= CF_MODEL_OK;
+        }
+      }
+    }
+    s->mgrp_off[r + 1] = (int32_t)s->mgrp_tid.size();
+    s->flags[r] = f;
+  }
+  s->n_tmpl = (int)tmpl_ids.size();
+  s->tmpl.assign((size_t)std::max(s->n_tmpl, 1) * std::max(R, 1), 0);
+  for (auto& kv : tmpl_ids)
+    for (int j = 0; j < R; j++) s->tmpl[(size_t)kv.second * R + j] = kv.first[j];
+  auto pad1 = [](auto& v) {
+    if (v.empty()) v.resize(1);
+  };
+  pad1(s->zone_ids);
+  pad1(s->taint_key);
+  pad1(s->taint_val);
+  pad1(s->taint_eff);
+  pad1(s->mgrp_tid);
+  pad1(s->mgrp_cnt);
+  // upload
+  SnapView& v = s->view;
+  v.C = C;
+  v.Cp = Cp;
+  v.W = s->W;
+  v.n_label_keys = K;
+  v.api_words = AW;
+  v.n_res = R;
+  v.n_tmpl = s->n_tmpl;
+  v.n_regions = (int)s->regions.names.size();
+  Arena& a = s->dev;
+  uint32_t *d_flags, *d_perm;
+  int32_t *d_prov, *d_reg, *d_regidx, *d_zoff, *d_zid, *d_lbl, *d_toff, *d_tk, *d_tv, *d_te, *d_moff, *d_mtid;
+  int64_t *d_pint, *d_rint, *d_allowed, *d_avail, *d_mcnt, *d_tmpl;
+  uint64_t* d_api;
+  a.add(&d_flags, Cp);
+  a.add(&d_perm, Cp);
+  a.add(&d_prov, Cp);
+  a.add(&d_reg, Cp);
+  a.add(&d_regidx, Cp);
+  a.add(&d_zoff, C + 1);
+  a.add(&d_zid, s->zone_ids.size());
+  a.add(&d_lbl, s->label_val.size());
+  a.add(&d_toff, C + 1);
+  a.add(&d_tk, s->taint_key.size());
+  a.add(&d_tv, s->taint_val.size());
+  a.add(&d_te, s->taint_eff.size());
+  a.add(&d_moff, C + 1);
+  a.add(&d_mtid, s->mgrp_tid.size());
+  a.add(&d_pint, Cp);
+  a.add(&d_rint, Cp);
+  a.add(&d_allowed, Cp);
+  a.add(&d_avail, s->avail.size());
+  a.add(&d_mcnt, s->mgrp_cnt.size());
+  a.add(&d_tmpl, s->tmpl.size());
+  a.add(&d_api, s->api_bits.size());
+  HIPCHK(a.alloc());
+  std::vector<uint32_t> permp(Cp, 0);
+  for (int r = 0; r < C; r++) permp[r] = s->perm[r];
+  auto up = [&](void* d, const void* h, size_t bytes) { return hipMemcpy(d, h, bytes, hipMemcpyHostToDevice); };
+  HIPCHK(up(d_flags, s->flags.data(), 4 * Cp));
+  HIPCHK(up(d_perm, permp.data(), 4 * Cp));
+  HIPCHK(up(d_prov, s->provider.data(), 4 * Cp));
+  HIPCHK(up(d_reg, s->region.data(), 4 * Cp));
+  HIPCHK(up(d_regidx, s->region_idx.data(), 4 * Cp));
+  HIPCHK(up(d_zoff, s->zone_off.data(), 4 * (C + 1)));
+  HIPCHK(up(d_zid, s->zone_ids.data(), 4 * s->zone_ids.size()));
+  HIPCHK(up(d_lbl, s->label_val.data(), 4 * s->label_val.size()));
+  HIPCHK(up(d_toff, s->taint_off.data(), 4 * (C + 1)));
+  HIPCHK(up(d_tk, s->taint_key.data(), 4 * s->taint_key.size()));
+  HIPCHK(up(d_tv, s->taint_val.data(), 4 * s->taint_val.size()));
+  HIPCHK(up(d_te, s->taint_eff.data(), 4 * s->taint_eff.size()));
+  HIPCHK(up(d_moff, s->mgrp_off.data(), 4 * (C + 1)));
+  HIPCHK(up(d_mtid, s->mgrp_tid.data(), 4 * s->mgrp_tid.size()));
+  HIPCHK(up(d_pint, s->provider_int.data(), 8 * Cp));
+  HIPCHK(up(d_rint, s->region_int.data(), 8 * Cp));
+  HIPCHK(up(d_allowed, s->allowed.data(), 8 * Cp));
+  HIPCHK(up(d_avail, s->avail.data(), 8 * s->avail.size()));
+  HIPCHK(up(d_mcnt, s->mgrp_cnt.data(), 8 * s->mgrp_cnt.size()));
+  HIPCHK(up(d_tmpl, s->tmpl.data(), 8 * s->tmpl.size()));
+  HIPCHK(up(d_api, s->api_bits.data(), 8 * s->api_bits.size()));
+  v.flags = d_flags;
+  v.perm = d_perm;
+  v.provider = d_prov;
+  v.region = d_reg;
+  v.region_idx = d_regidx;
+  v.provider_int = d_pint;
+  v.region_int = d_rint;
+  v.zone_off = d_zoff;
+  v.zone_ids = d_zid;
+  v.label_val = d_lbl;
+  v.taint_off = d_toff;
+  v.taint_key = d_tk;
+  v.taint_val = d_tv;
+  v.taint_eff = d_te;
+  v.api_bits = d_api;
+  v.allowed = d_allowed;
+  v.avail = d_avail;
+  v.mgrp_off = d_moff;
+  v.mgrp_tid = d_mtid;
+  v.mgrp_cnt = d_mcnt;
+  v.tmpl = d_tmpl;
+  return KP_OK;
+}
+
+// ============================================================================
+// Binding packing
+// ============================================================================
+struct Packer {
+  kp_snapshot* s;
+  kp_batch* bt;
+
+  int32_t list(const std::vector<int32_t>& v) {
+    int32_t off = (int32_t)bt->ipool.size();
+    bt->ipool.insert(bt->ipool.end(), v.begin(), v.end());
+    return off;
+  }
+  std::vector<int32_t> ranks(const kp_str* names, uint32_t n) {
+    std::vector<int32_t> r;
+    for (uint32_t i = 0; i < n; i++) {
+      auto it = s->rank_of.find(S(names[i]));
+      if (it != s->rank_of.end()) r.push_back(it->second);
+    }
+    return r;
+  }
+  std::vector<int32_t> vals(const kp_str* v, uint32_t n) {
+    std::vector<int32_t> r;
+    for (uint32_t i = 0; i < n; i++) {
+      int32_t id = s->str.get(S(v[i]));
+      if (id >= 0) r.push_back(id);
+    }
+    return r;
+  }
+  void ins(std::vector<Instr>& out, int32_t op, int32_t a = 0, int32_t b = 0, int32_t c = 0, int64_t v = 0) {
+    Instr i;
+    i.op = op;
+    i.a = a;
+    i.b = b;
+    i.c = c;
+    i.v = v;
+    out.push_back(i);
+  }
+  // labels.NewRequirement validation (labels/selector.go:150-230)
+  static bool valid_req(const std::string& key, const std::string& op, const kp_str* v, uint32_t n) {
+    bool ok = k8s::label_key(key);
+    if (op == "In" || op == "NotIn") ok = ok && n > 0;
+    else if (op == "=") ok = ok && n == 1;
+    else if (op == "Exists" || op == "DoesNotExist") ok = ok && n == 0;
+    else if (op == "Gt" || op == "Lt") {
+      ok = ok && n == 1;
+      for (uint32_t i = 0; i < n; i++) {
+        int64_t x;
+        if (!k8s::parse_int64(S(v[i]), &x)) ok = false;
+      }
+    } else {
+      ok = false;
+    }
+    for (uint32_t i = 0; i < n; i++)
+      if (!k8s::label_value(S(v[i]))) ok = false;
+    return ok;
+  }
+  // util.ClusterMatches compiled to a conjunction program (selector.go:97-155)
+  int32_t compile(const kp_cluster_affinity& a) {
+    std::vector<Instr> out;
+    bool never = false;
+    if (a.n_exclude_clusters) {
+      auto r = ranks(a.exclude_clusters, a.n_exclude_clusters);
+      if (!r.empty()) ins(out, OP_EXCLUDE, list(r), (int32_t)r.size());
+    }
+    if (a.has_label_selector) {  // metav1.LabelSelectorAsSelector (helpers.go:36-74)
+      std::map<std::string, std::string> ml;
+      for (uint32_t i = 0; i < a.n_match_labels; i++) ml[S(a.match_labels[i].key)] = S(a.match_labels[i].value);
+      for (auto& kv : ml) {
+        kp_str v{kv.second.c_str(), (uint32_t)kv.second.size()};
+        if (!valid_req(kv.first, "=", &v, 1)) never = true;
+        int32_t slot = s->keys.get(kv.first);
+        int32_t id = s->str.get(kv.second);
+        if (slot < 0 || id < 0) never = never || true;
+        else {
+          std::vector<int32_t> one{id};
+          ins(out, OP_LBL_IN, slot, list(one), 1);
+        }
+      }
+      for (uint32_t i = 0; i < a.n_match_expressions; i++) {
+        const kp_requirement& r = a.match_expressions[i];
+        std::string key = S(r.key), op = S(r.op);
+        if (!(op == "In" || op == "NotIn" || op == "Exists" || op == "DoesNotExist") ||
+            !valid_req(key, op, r.values, r.n_values)) {
+          never = true;
+          continue;
+        }
+        int32_t slot = s->keys.get(key);
+        if (op == "In") {
+          auto v = vals(r.values, r.n_values);
+          if (slot < 0 || v.empty()) never = true;
+          else ins(out, OP_LBL_IN, slot, list(v), (int32_t)v.size());
+        } else if (op == "NotIn") {
+          auto v = vals(r.values, r.n_values);
+          if (slot >= 0) ins(out, OP_LBL_NOTIN, slot, list(v), (int32_t)v.size());
+        } else if (op == "Exists") {
+          if (slot < 0) never = true;
+          else ins(out, OP_LBL_EXISTS, slot);
+        } else if (slot >= 0) {
+          ins(out, OP_LBL_DNE, slot);
+        }
+      }
+    }
+    if (a.has_field_selector) {
+      bool any_other = false;
+      bool others_ok = true;
+      for (uint32_t i = 0; i < a.n_field_expressions; i++) {
+        const kp_requirement& r = a.field_expressions[i];
+        std::string key = S(r.key), op = S(r.op);
+        if (key == "zone") {  // matchZones (selector.go:208-235)
+          auto v = vals(r.values, r.n_values);
+          if (op == "In") ins(out, OP_ZONE_IN, 0, list(v), (int32_t)v.size());
+          else if (op == "NotIn") ins(out, OP_ZONE_NOTIN, 0, list(v), (int32_t)v.size());
+          else if (op == "Exists") ins(out, OP_ZONE_EXISTS);
+          else if (op == "DoesNotExist") ins(out, OP_ZONE_DNE);
+          else never = true;
+          continue;
+        }
+        any_other = true;
+        // lifted.NodeSelectorRequirementsAsSelector (nodeaffinity.go:36-71)
+        if (!(op == "In" || op == "NotIn" || op == "Exists" || op == "DoesNotExist" || op == "Gt" || op == "Lt") ||
+            !valid_req(key, op, r.values, r.n_values)) {
+          others_ok = false;
+          continue;
+        }
+        int field = key == "provider" ? 0 : (key == "region" ? 1 : 2);  // extractClusterFields
+        if (op == "In") {
+          auto v = vals(r.values, r.n_values);
+          if (field == 2 || v.empty()) never = true;
+          else ins(out, OP_FLD_IN, field, list(v), (int32_t)v.size());
+        } else if (op == "NotIn") {
+          auto v = vals(r.values, r.n_values);
+          if (field != 2) ins(out, OP_FLD_NOTIN, field, list(v), (int32_t)v.size());
+        } else if (op == "Exists") {
+          if (field == 2) never = true;
+          else ins(out, OP_FLD_EXISTS, field);
+        } else if (op == "DoesNotExist") {
+          if (field != 2) ins(out, OP_FLD_DNE, field);
+        } else {
+          int64_t x = 0;
+          k8s::parse_int64(S(r.values[0]), &x);
+          if (field == 2) never = true;
+          else ins(out, op == "Gt" ? OP_FLD_GT : OP_FLD_LT, field, 0, 0, x);
+        }
+      }
+      if (any_other && !others_ok) never = true;
+    }
+    if (a.n_cluster_names) {
+      auto r = ranks(a.cluster_names, a.n_cluster_names);
+      if (r.empty()) never = true;
+      else ins(out, OP_NAMES, list(r), (int32_t)r.size());
+    }
+    if (never) {
+      out.clear();
+      ins(out, OP_FALSE);
+    }
+    Prog p;
+    p.ins_off = (int32_t)bt->instrs.size();
+    p.ins_cnt = (int32_t)out.size();
+    bt->instrs.insert(bt->instrs.end(), out.begin(), out.end());
+    bt->progs.push_back(p);
+    return (int32_t)bt->progs.size() - 1;
+  }
+
+  void pack(const kp_binding& b, BindHdr& h) {
+    memset(&h, 0, sizeof(h));
+    const kp_options& o = s->opts;
+    h.replicas = b.replicas;
+    h.enabled = (int32_t)o.enabled_plugins;
+    uint32_t f = 0;
+    if (b.has_replica_requirements) f |= BF_HAS_RR;
+    if (b.replicas == 0 && b.n_components == 0) f |= BF_NONWORKLOAD_EST;
+    if ((b.replicas > 0 || b.has_replica_requirements) && b.n_components <= 1) f |= BF_WORKLOAD_ASSIGN;
+    if (b.has_reschedule_triggered_at && b.has_last_scheduled_time &&
+        b.reschedule_triggered_at_ns > b.last_scheduled_time_ns)
+      f |= BF_FRESH;
+    if (b.uid.len && (k8s::fnv32a(b.uid.ptr, b.uid.len) & 1)) f |= BF_UID_DESC;
+    if (o.enable_empty_workload_propagation) f |= BF_EMPTY_PROP;
+    if (b.has_weight_preference) f |= BF_HAS_WP;
+    // APIEnablement GVK (group_version.go:211-226,300-305)
+    {
+      std::string av = S(b.api_version), g, ver;
+      size_t slashes = std::count(av.begin(), av.end(), '/');
+      if (!(av.empty() || av == "/")) {
+        if (slashes == 0) ver = av;
+        else if (slashes == 1) {
+          g = av.substr(0, av.find('/'));
+          ver = av.substr(av.find('/') + 1);
+        }
+      }
+      std::string gv = g.empty() ? ver : g + "/" + ver;
+      h.gvk = s->gvk.get(gv + '\0' + S(b.kind));
+    }
+    // spec.Clusters
+    h.n_targets_all = (int32_t)b.n_clusters;
+    {
+      std::vector<int32_t> t;
+      std::vector<char> seen(s->C, 0);
+      for (uint32_t i = 0; i < b.n_clusters; i++) {
+        auto it = s->rank_of.find(S(b.clusters[i].name));
+        if (it == s->rank_of.end()) continue;
+        if (seen[it->second]) f |= BF_DUP_TARGETS;
+        seen[it->second] = 1;
+        t.push_back(it->second);
+        t.push_back(b.clusters[i].replicas);
+      }
+      h.tgt_off = list(t);
+      h.tgt_cnt = (int32_t)t.size() / 2;
+      if (b.n_clusters > 0 && (o.enabled_plugins & KP_PLUGIN_CLUSTER_LOCALITY)) f |= BF_SCORE_LOCALITY;
+    }
+    {
+      auto r = ranks(b.eviction_from, b.n_eviction_from);
+      h.evict_off = list(r);
+      h.evict_cnt = (int32_t)r.size();
+    }
+    // tolerations
+    h.tol_off = (int32_t)bt->tols.size();
+    for (uint32_t i = 0; i < b.n_tolerations; i++) {
+      const kp_toleration& t = b.tolerations[i];
+      std::string eff = S(t.effect), key = S(t.key), op = S(t.op);
+      Tol x;
+      if (eff.empty()) x.eff = EFF_ANY;
+      else if (eff == "NoSchedule") x.eff = EFF_NOSCHEDULE;
+      else if (eff == "NoExecute") x.eff = EFF_NOEXECUTE;
+      else continue;
+      if (key.empty()) x.key = -1;
+      else if ((x.key = s->str.get(key)) < 0) continue;
+      if (op.empty() || op == "Equal") {
+        x.op = TOL_EQUAL;
+        if ((x.val = s->str.get(S(t.value))) < 0) continue;
+      } else if (op == "Exists") {
+        x.op = TOL_EXISTS;
+        x.val = -1;
+      } else {
+        continue;  // Lt/Gt disabled, unknown operators never tolerate
+      }
+      bt->tols.push_back(x);
+    }
+    h.tol_cnt = (int32_t)bt->tols.size() - h.tol_off;
+    // ClusterAffinity filter list + overflow order programs
+    {
+      std::vector<int32_t> filt, ovf;
+      bool have = false;
+      const kp_affinity_term* term = nullptr;
+      if (b.has_cluster_affinity) {
+        filt.push_back(compile(b.cluster_affinity));
+        have = true;
+      } else {
+        std::string obs = S(b.observed_affinity_name);
+        for (uint32_t i = 0; i < b.n_cluster_affinities; i++)
+          if (S(b.cluster_affinities[i].affinity_name) == obs) {
+            term = &b.cluster_affinities[i];
+            break;
+          }
+        if (term) {
+          have = true;
+          ovf.push_back(compile(term->affinity));
+          filt.push_back(ovf[0]);
+          std::vector<int32_t> ov;
+          for (uint32_t j = 0; j < term->n_overflow; j++) ov.push_back(compile(term->overflow[j]));
+          ovf.insert(ovf.end(), ov.begin(), ov.end());
+          bool workload = b.replicas > 0 || b.has_replica_requirements || b.n_components >= 1;
+          if (workload) filt.insert(filt.end(), ov.begin(), ov.end());
+        }
+      }
+      if (!have) f |= BF_AFF_ALL;
+      h.filt_off = list(filt);
+      h.filt_cnt = (int32_t)filt.size();
+      if (b.has_cluster_affinity || b.n_cluster_affinities == 0) h.ovf_mode = OVF_ZERO;
+      else if (!term) h.ovf_mode = OVF_1000;
+      else h.ovf_mode = OVF_PROGS;
+      h.ovf_off = list(ovf);
+      h.ovf_cnt = (int32_t)ovf.size();
+      // enableOverflow (common.go:156-170)
+      if (!b.has_cluster_affinity && b.n_cluster_affinities > 0 && b.observed_affinity_name.len > 0 && term &&
+          term->n_overflow > 0)
+        f |= BF_OVERFLOW;
+    }
+    // static weights
+    {
+      std::vector<int32_t> ids;
+      std::vector<int64_t> ws;
+      for (uint32_t i = 0; i < b.n_static_weights; i++) {
+        ids.push_back(compile(b.static_weights[i].target));
+        ws.push_back(b.static_weights[i].weight);
+      }
+      h.sw_off = list(ids);
+      h.sw_cnt = (int32_t)ids.size();
+      h.sw_w_off = (int32_t)bt->lpool.size();
+      bt->lpool.insert(bt->lpool.end(), ws.begin(), ws.end());
+    }
+    // requests
+    {
+      QtyMap rq;
+      if (!qmap(b.resource_request, b.n_resource_request, &rq)) f |= BF_BAD;
+      std::vector<int32_t> sr, mr;
+      std::vector<int64_t> sq, mq;
+      for (auto& kv : rq) {
+        const std::string& nm = kv.first;
+        int64_t v = k8s::value(kv.second);
+        if (v > 0) {  // summary path: every resource name (general.go:467-471)
+          sr.push_back(s->res.get(nm));
+          sq.push_back(nm == "cpu" ? k8s::milli(kv.second) : v);
+        }
+        // model path: util.NewResource classes (resource.go:46-75)
+        if (nm == "cpu") {
+          int64_t m = k8s::milli(kv.second);
+          if (m > 0) {
+            mr.push_back(s->res.get(nm));
+            mq.push_back(m);
+          }
+        } else if (nm == "memory" || nm == "ephemeral-storage" || (nm != "pods" && k8s::scalar_resource(nm))) {
+          if (v > 0) {
+            mr.push_back(s->res.get(nm));
+            mq.push_back(v);
+          }
+        }
+      }
+      h.sreq_off = list(sr);
+      h.sreq_cnt = (int32_t)sr.size();
+      h.sreq_q_off = (int32_t)bt->lpool.size();
+      bt->lpool.insert(bt->lpool.end(), sq.begin(), sq.end());
+      h.mreq_off = list(mr);
+      h.mreq_cnt = (int32_t)mr.size();
+      h.mreq_q_off = (int32_t)bt->lpool.size();
+      bt->lpool.insert(bt->lpool.end(), mq.begin(), mq.end());
+    }
+    // spread constraints: filter presence + selection kind (select_clusters.go:28-80)
+    std::string rst = b.has_replica_scheduling ? S(b.replica_scheduling_type) : std::string("Duplicated");
+    std::string div = S(b.replica_division_preference);
+    bool hasRegion = false, hasCluster = false;
+    for (uint32_t i = 0; i < b.n_spread_constraints; i++) {
+      const kp_spread_constraint& sc = b.spread_constraints[i];
+      std::string fld = S(sc.spread_by_field);
+      if (fld == "provider") f |= BF_NEED_PROVIDER;
+      if (fld == "region") {
+        f |= BF_NEED_REGION;
+        hasRegion = true;
+        h.region_min = sc.min_groups;
+        h.region_max = sc.max_groups;
+      }
+      if (fld == "zone") f |= BF_NEED_ZONES;
+      if (fld == "cluster") {
+        hasCluster = true;
+        h.cluster_min = sc.min_groups;
+        h.cluster_max = sc.max_groups;
+      }
+    }
+    bool ignoreSpread = b.has_replica_scheduling && S(b.replica_scheduling_type) == "Divided" && div == "Weighted" &&
+                        (!b.has_weight_preference || (b.n_static_weights != 0 && b.dynamic_weight.len == 0));
+    if (b.n_spread_constraints == 0 || ignoreSpread) h.sel = SEL_ALL;
+    else if (hasRegion) h.sel = SEL_REGION;
+    else if (hasCluster) h.sel = SEL_CLUSTER;
+    else h.sel = SEL_ERR_UNSUPPORTED;
+    h.need_replicas = (!b.has_replica_scheduling || S(b.replica_scheduling_type) == "Duplicated") ? -1 : b.replicas;
+    if (rst == "Duplicated") f |= BF_GROUP_DUP;
+    // strategy (assignment.go:95-123)
+    if (rst == "Duplicated") h.strategy = ST_DUPLICATED;
+    else if (rst == "Divided") {
+      if (div == "Aggregated") h.strategy = ST_AGGREGATED;
+      else if (div == "Weighted")
+        h.strategy = (b.has_weight_preference && b.dynamic_weight.len) ? ST_DYNAMIC : ST_STATIC;
+      else h.strategy = ST_NONE;
+    } else {
+      h.strategy = ST_NONE;
+    }
+    h.flags = f;
+    uint64_t C = (uint64_t)s->C;
+    bool big = !(f & BF_WORKLOAD_ASSIGN) || h.strategy == ST_DUPLICATED || (f & BF_EMPTY_PROP);
+    uint64_t rep = b.replicas > 0 ? (uint64_t)b.replicas : 0;
+    h.out_cap = (big ? C : std::min<uint64_t>(C, rep)) + (uint64_t)h.tgt_cnt;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// selectGroups (select_groups.go:102-224): the host-kept group combination.
+// groups: (region id == name order, value = #clusters, weight = group score).
+// ---------------------------------------------------------------------------
+struct G {
+  int id;
+  int64_t value, weight;
+};
+std::vector<int> select_groups(std::vector<G> groups, int64_t minC, int64_t maxC, int64_t target) {
+  if (groups.empty()) return {};
+  if (groups.size() > 1)
+    std::sort(groups.begin(), groups.end(), [](const G& a, const G& b) {
+      if (a.value != b.value) return a.value < b.value;
+      if (a.weight != b.weight) return a.weight > b.weight;
+      return a.id < b.id;
+    });
+  struct Path {
+    int id;
+    int64_t weight, value;
+    std::vector<int> g;  // indices into groups, sorted by (weight desc, id asc)
+  };
+  std::vector<Path> paths;
+  std::vector<int> root;
+  int pid = 0;
+  const int n = (int)groups.size();
+  std::function<void(int64_t, int)> dfs = [&](int64_t sum, int begin) {
+    int64_t len = (int64_t)root.size();
+    if (sum >= target && len >= minC && len <= maxC) {
+      Path p;
+      p.id = ++pid;
+      p.weight = 0;
+      p.value = 0;
+      p.g = root;
+      for (int i : p.g) {
+        p.weight += groups[i].weight;
+        p.value += groups[i].value;
+      }
+      std::sort(p.g.begin(), p.g.end(), [&](int a, int b) {
+        if (groups[a].weight != groups[b].weight) return groups[a].weight > groups[b].weight;
+        return groups[a].id < groups[b].id;
+      });
+      paths.push_back(std::move(p));
+      return;
+    }
+    if (len >= maxC) return;
+    for (int i = begin; i < n; i++) {
+      sum += groups[i].value;
+      root.push_back(i);
+      dfs(sum, i + 1);
+      if ((int64_t)n == minC) break;  // select_groups.go:179-182 (no backtracking)
+      sum -= groups[i].value;
+      root.pop_back();
+    }
+  };
+  dfs(0, 0);
+  if (paths.empty()) return {};
+  const Path* fin = &paths[0];
+  if (paths.size() > 1) {
+    std::sort(paths.begin(), paths.end(), [](const Path& a, const Path& b) {
+      if (a.weight != b.weight) return a.weight > b.weight;
+      if (a.value != b.value) return a.value > b.value;
+      return a.id < b.id;
+    });
+    fin = &paths[0];
+    for (size_t i = 1; i < paths.size(); i++) {
+      const Path& sp = paths[i];
+      bool m = sp.g.size() < fin->g.size();
+      for (size_t k = 0; m && k < sp.g.size(); k++) m = groups[fin->g[k]].id == groups[sp.g[k]].id;
+      if (m) fin = &paths[i];
+    }
+  }
+  std::vector<int> out;
+  for (int i : fin->g) out.push_back(groups[i].id);
+  return out;
+}
+
+template <class F>
+void parallel_for(int n, int threads, F fn) {
+  if (n <= 0) return;
+  if (threads <= 1 || n < 64) {
+    for (int i = 0; i < n; i++) fn(i);
+    return;
+  }
+  std::atomic<int> next(0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; t++)
+    th.emplace_back([&]() {
+      for (;;) {
+        int i = next.fetch_add(16);
+        if (i >= n) break;
+        for (int k = i; k < std::min(n, i + 16); k++) fn(k);
+      }
+    });
+  for (auto& t : th) t.join();
+}
+
+size_t smem_pair(const kp_snapshot* s, int md_cap) {
+  int words = (s->Cp + 31) >> 5;
+  return 512 + 8 * (size_t)words + 4 * (size_t)md_cap + 64;
+}
+size_t smem_all(const kp_snapshot* s) {
+  int words = (s->Cp + 31) >> 5;
+  return 512 + 4 * (size_t)words + 8 * (size_t)s->Cp + 64;
+}
+size_t smem_cluster(const kp_snapshot* s, int cap) {
+  int words = (s->Cp + 31) >> 5;
+  size_t area = std::max(8 * (size_t)s->Cp, serial_scratch_bytes(cap));
+  return 512 + 1024 + sizeof(Item) * 2 * kSmallMax + 16 * kSmallMax + 4 * (size_t)((words + 3) & ~3) + area + 64;
+}
+size_t smem_region_a(const kp_snapshot* s) {
+  int words = (s->Cp + 31) >> 5;
+  size_t R = s->view.n_regions;
+  return 512 + 80 * R + 4 * (size_t)((words + 3) & ~3) + 8 * (size_t)s->Cp + 64;
+}
+size_t smem_region_b(const kp_snapshot* s, int cap) {
+  int words = (s->Cp + 31) >> 5;
+  size_t R = s->view.n_regions;
+  size_t area = std::max(8 * (size_t)s->Cp, serial_scratch_bytes(cap));
+  return 512 + 1024 + sizeof(Item) * 2 * kSmallMax + 16 * kSmallMax + 8 * R + 4 * ((R + 3) & ~3) +
+         4 * (size_t)((words + 3) & ~3) + area + 64;
+}
+const int kMdCap = 4096;
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int kp_abi_version(void) { return KP_ABI_VERSION; }
+
+int kp_engine_create(int device, kp_engine** out) {
+  if (!out) return KP_EINVAL;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device) return KP_EDEVICE;
+  auto* e = new kp_engine();
+  e->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete e;
+    return KP_EDEVICE;
+  }
+  for (auto& ev : e->ev) (void)hipEventCreate(&ev);
+  int lds = 0;
+  if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && lds > 0)
+    e->max_lds = (size_t)lds;
+  unsigned hc = std::thread::hardware_concurrency();
+  e->n_threads = (int)std::max(1u, std::min(16u, hc));
+  *out = e;
+  return KP_OK;
+}
+
+void kp_engine_destroy(kp_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  for (auto& ev : e->ev) (void)hipEventDestroy(ev);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+const char* kp_last_error(const kp_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+int kp_snapshot_create(kp_engine* e, const kp_cluster* clusters, uint64_t n, const kp_options* opts,
+                       kp_snapshot** out) {
+  if (!e || !out || (n && !clusters)) return KP_EINVAL;
+  (void)hipSetDevice(e->device);
+  auto* s = new kp_snapshot();
+  s->e = e;
+  int rc = build_snapshot(e, clusters, n, opts, s);
+  if (rc != KP_OK) {
+    delete s;
+    return rc;
+  }
+  *out = s;
+  return KP_OK;
+}
+
+void kp_snapshot_destroy(kp_snapshot* s) { delete s; }
+
+int kp_snapshot_export(const kp_snapshot*, const void**, uint64_t*) { return KP_ENOTSUP; }
+int kp_snapshot_import(kp_engine*, const void*, uint64_t, kp_snapshot**) { return KP_ENOTSUP; }
+
+int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindings, uint64_t n, kp_batch** out) {
+  if (!e || !sc || !out || (n && !bindings)) return KP_EINVAL;
+  if (n > (uint64_t)INT32_MAX) return KP_ENOTSUP;
+  (void)hipSetDevice(e->device);
+  kp_snapshot* s = const_cast<kp_snapshot*>(sc);
+  auto* bt = new kp_batch();
+  std::unique_ptr<kp_batch> guard(bt);
+  bt->snap = s;
+  bt->B = (int)n;
+  bt->hdr.resize(n);
+  Packer pk{s, bt};
+  for (uint64_t i = 0; i < n; i++) {
+    pk.pack(bindings[i], bt->hdr[i]);
+    bt->out_cap += bt->hdr[i].out_cap;
+    const BindHdr& h = bt->hdr[i];
+    if (h.sel == SEL_CLUSTER) bt->l_cluster.push_back((int32_t)i);
+    else if (h.sel == SEL_REGION) bt->l_region.push_back((int32_t)i);
+    else bt->l_all.push_back((int32_t)i);
+  }
+  bt->l_slow = bt->l_all;
+  bt->l_slow.insert(bt->l_slow.end(), bt->l_cluster.begin(), bt->l_cluster.end());
+  if (s->view.n_regions > kRegionMax && !bt->l_region.empty()) {
+    e->err = "region spread over more than 256 regions is not supported";
+    return KP_ENOTSUP;
+  }
+  {
+    const int cap = kSmallMax + kTgtSmallMax + 16;
+    size_t need = smem_pair(s, kMdCap);
+    if (!bt->l_all.empty()) need = std::max(need, smem_all(s));
+    if (!bt->l_cluster.empty()) need = std::max(need, smem_cluster(s, cap));
+    if (!bt->l_region.empty()) need = std::max({need, smem_region_a(s), smem_region_b(s, cap)});
+    if (need > e->max_lds) {
+      e->err = "snapshot too large for one workgroup's LDS (" + std::to_string(need) + " > " +
+               std::to_string(e->max_lds) + " bytes)";
+      return KP_ENOTSUP;
+    }
+  }
+  auto pad1 = [](auto& v) {
+    if (v.empty()) v.resize(1);
+  };
+  pad1(bt->ipool);
+  pad1(bt->lpool);
+  pad1(bt->tols);
+  pad1(bt->progs);
+  pad1(bt->instrs);
+  const int B = bt->B ? bt->B : 1;
+  const int nr = (int)bt->l_region.size(), R = std::max(1, s->view.n_regions);
+  int max_tgt = 0;
+  for (auto& h : bt->hdr) max_tgt = std::max(max_tgt, (int)h.tgt_cnt);
+  bt->slow_cap = s->Cp + max_tgt + 64;
+  int P = 1;
+  while (P < s->Cp) P <<= 1;
+  bt->slow_slot = (size_t)s->Cp * 8 + (size_t)P * 8 + sizeof(Item) * s->Cp + 4 * (size_t)s->Cp +
+                  serial_scratch_bytes(bt->slow_cap) + 1024;
+  bt->slow_slot = (bt->slow_slot + 255) & ~(size_t)255;
+  bt->slow_grid = 256;
+  Arena& a = bt->dev;
+  BindHdr* d_hdr;
+  int32_t* d_ipool;
+  int64_t* d_lpool;
+  Tol* d_tols;
+  Prog* d_progs;
+  Instr* d_instrs;
+  a.add(&d_hdr, B);
+  a.add(&d_ipool, bt->ipool.size());
+  a.add(&d_lpool, bt->lpool.size());
+  a.add(&d_tols, bt->tols.size());
+  a.add(&d_progs, bt->progs.size());
+  a.add(&d_instrs, bt->instrs.size());
+  a.add(&bt->fmask, (size_t)B * s->W);
+  a.add(&bt->est, (size_t)B * s->Cp);
+  a.add(&bt->d_all, std::max<size_t>(1, bt->l_all.size()));
+  a.add(&bt->d_cluster, std::max<size_t>(1, bt->l_cluster.size()));
+  a.add(&bt->d_region, std::max<size_t>(1, bt->l_region.size()));
+  a.add(&bt->d_slowlist, std::max<size_t>(1, bt->l_slow.size()));
+  a.add(&bt->status, B);
+  a.add(&bt->errc, B);
+  a.add(&bt->slow, B);
+  a.add(&bt->arg, B);
+  a.add(&bt->start, B);
+  a.add(&bt->count, B);
+  a.add(&bt->counter, 1);
+  a.add(&bt->out_idx, std::max<uint64_t>(1, bt->out_cap));
+  a.add(&bt->out_rep, std::max<uint64_t>(1, bt->out_cap));
+  a.add(&bt->offsets_d, B + 1);
+  a.add(&bt->cidx_d, std::max<uint64_t>(1, bt->out_cap));
+  a.add(&bt->crep_d, std::max<uint64_t>(1, bt->out_cap));
+  a.add(&bt->rout, (size_t)std::max(1, nr) * R);
+  a.add(&bt->rstat, std::max(1, nr));
+  a.add(&bt->rsel, (size_t)std::max(1, nr) * R);
+  a.add(&bt->rnsel, std::max(1, nr));
+  a.add(&bt->slow_scratch, bt->slow_slot * bt->slow_grid);
+  HIPCHK(a.alloc());
+  auto up = [&](void* d, const void* h, size_t bytes) {
+    return bytes ? hipMemcpy(d, h, bytes, hipMemcpyHostToDevice) : hipSuccess;
+  };
+  HIPCHK(up(d_hdr, bt->hdr.data(), sizeof(BindHdr) * bt->hdr.size()));
+  HIPCHK(up(d_ipool, bt->ipool.data(), 4 * bt->ipool.size()));
+  HIPCHK(up(d_lpool, bt->lpool.data(), 8 * bt->lpool.size()));
+  HIPCHK(up(d_tols, bt->tols.data(), sizeof(Tol) * bt->tols.size()));
+  HIPCHK(up(d_progs, bt->progs.data(), sizeof(Prog) * bt->progs.size()));
+  HIPCHK(up(d_instrs, bt->instrs.data(), sizeof(Instr) * bt->instrs.size()));
+  HIPCHK(up(bt->d_all, bt->l_all.data(), 4 * bt->l_all.size()));
+  HIPCHK(up(bt->d_cluster, bt->l_cluster.data(), 4 * bt->l_cluster.size()));
+  HIPCHK(up(bt->d_region, bt->l_region.data(), 4 * bt->l_region.size()));
+  HIPCHK(up(bt->d_slowlist, bt->l_slow.data(), 4 * bt->l_slow.size()));
+  HIPCHK(hipMemset(bt->slow, 0, 4 * (size_t)B));
+  BatchView& v = bt->view;
+  v.B = bt->B;
+  v.hdr = d_hdr;
+  v.ipool = d_ipool;
+  v.lpool = d_lpool;
+  v.tols = d_tols;
+  v.progs = d_progs;
+  v.instrs = d_instrs;
+  *out = guard.release();
+  return KP_OK;
+}
+
+void kp_batch_destroy(kp_batch* b) { delete b; }
+
+int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
+  if (!e || !bt || !out) return KP_EINVAL;
+  (void)hipSetDevice(e->device);
+  kp_snapshot* s = bt->snap;
+  const int B = bt->B;
+  double t0 = now_ms();
+  kp_stage_times tm{};
+  hipStream_t st = e->stream;
+  if (B == 0) {
+    memset(out, 0, sizeof(*out));
+    bt->h_offsets.assign(1, 0);
+    out->offsets = bt->h_offsets.data();
+    return KP_OK;
+  }
+  HIPCHK(hipMemsetAsync(bt->counter, 0, sizeof(unsigned long long), st));
+  KArgs ka;
+  ka.s = s->view;
+  ka.bv = bt->view;
+  ka.fmask = bt->fmask;
+  ka.est = bt->est;
+  ka.sink.out_idx = bt->out_idx;
+  ka.sink.out_rep = bt->out_rep;
+  ka.sink.counter = bt->counter;
+  ka.sink.status = bt->status;
+  ka.sink.err = bt->errc;
+  ka.sink.arg = bt->arg;
+  ka.sink.start = bt->start;
+  ka.sink.count = bt->count;
+  ka.slow = bt->slow;
+  HIPCHK(hipEventRecord(e->ev[0], st));
+  HIPCHK(launch_pair(st, s->view, bt->view, 0, B, bt->fmask, bt->est, nullptr, 0, kMdCap, smem_pair(s, kMdCap)));
+  HIPCHK(hipEventRecord(e->ev[1], st));
+  SelectExtra sx;
+  sx.rout = bt->rout;
+  sx.rstat = bt->rstat;
+  sx.rsel = bt->rsel;
+  sx.rnsel = bt->rnsel;
+  sx.scratch = bt->slow_scratch;
+  sx.slot_bytes = bt->slow_slot;
+  sx.grid = bt->slow_grid;
+  const int cap = kSmallMax + kTgtSmallMax + 16;
+  if (!bt->l_all.empty()) {
+    KArgs k = ka;
+    k.list = bt->d_all;
+    k.n = (int)bt->l_all.size();
+    HIPCHK(launch_select(st, SEL_LAUNCH_ALL, k, smem_all(s), cap, sx));
+  }
+  if (!bt->l_cluster.empty()) {
+    KArgs k = ka;
+    k.list = bt->d_cluster;
+    k.n = (int)bt->l_cluster.size();
+    HIPCHK(launch_select(st, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sx));
+  }
+  double th0 = 0, th1 = 0;
+  if (!bt->l_region.empty()) {
+    const int nr = (int)bt->l_region.size(), R = s->view.n_regions;
+    KArgs k = ka;
+    k.list = bt->d_region;
+    k.n = nr;
+    HIPCHK(launch_select(st, SEL_LAUNCH_REGION_A, k, smem_region_a(s), cap, sx));
+    bt->h_rout.resize((size_t)nr * std::max(R, 1));
+    bt->h_rstat.resize(nr);
+    HIPCHK(hipMemcpyAsync(bt->h_rout.data(), bt->rout, sizeof(RegionOut) * bt->h_rout.size(), hipMemcpyDeviceToHost,
+                          st));
+    HIPCHK(hipMemcpyAsync(bt->h_rstat.data(), bt->rstat, 4 * nr, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    th0 = now_ms();
+    bt->h_rsel.assign((size_t)nr * std::max(R, 1), -1);
+    bt->h_rnsel.assign(nr, 0);
+    parallel_for(nr, e->n_threads, [&](int j) {
+      if (bt->h_rstat[j] != 0) {
+        bt->h_rnsel[j] = -1000;
+        return;
+      }
+      const BindHdr& h = bt->hdr[bt->l_region[j]];
+      std::vector<G> groups;
+      for (int r = 0; r < R; r++) {
+        const RegionOut& ro = bt->h_rout[(size_t)j * R + r];
+        if (ro.count > 0) groups.push_back({r, ro.count, ro.score});
+      }
+      // selectBestClustersByRegion (select_clusters_by_region.go:25-40)
+      if ((int64_t)groups.size() < h.region_min) {
+        bt->h_rnsel[j] = -KP_ERR_REGION_MIN_GROUPS;
+        return;
+      }
+      auto sel = select_groups(groups, h.region_min, h.region_max, h.cluster_min);
+      if (sel.empty()) {
+        bt->h_rnsel[j] = -KP_ERR_REGION_CLUSTER_MIN;
+        return;
+      }
+      for (size_t q = 0; q < sel.size(); q++) bt->h_rsel[(size_t)j * R + q] = sel[q];
+      bt->h_rnsel[j] = (int32_t)sel.size();
+    });
+    th1 = now_ms();
+    HIPCHK(hipMemcpyAsync(bt->rsel, bt->h_rsel.data(), 4 * bt->h_rsel.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(bt->rnsel, bt->h_rnsel.data(), 4 * nr, hipMemcpyHostToDevice, st));
+    HIPCHK(launch_select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sx));
+  }
+  if (!bt->l_slow.empty()) {
+    KArgs k = ka;
+    k.list = bt->d_slowlist;
+    k.n = (int)bt->l_slow.size();
+    HIPCHK(launch_select(st, SEL_LAUNCH_SLOW, k, 1024 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4), bt->slow_cap, sx));
+  }
+  HIPCHK(hipEventRecord(e->ev[2], st));
+  // results -> host, compacted to CSR
+  bt->h_status.resize(B);
+  bt->h_err.resize(B);
+  bt->h_arg.resize(B);
+  bt->h_start.resize(B);
+  bt->h_count.resize(B);
+  HIPCHK(hipMemcpyAsync(bt->h_status.data(), bt->status, 4 * (size_t)B, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(bt->h_err.data(), bt->errc, 4 * (size_t)B, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(bt->h_arg.data(), bt->arg, 8 * (size_t)B, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(bt->h_count.data(), bt->count, 4 * (size_t)B, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  double tc0 = now_ms();
+  bt->h_offsets.resize(B + 1);
+  uint64_t tot = 0;
+  for (int i = 0; i < B; i++) {
+    bt->h_offsets[i] = tot;
+    tot += bt->h_status[i] == KP_STATUS_OK ? bt->h_count[i] : 0;
+    if (bt->h_status[i] != KP_STATUS_OK) bt->h_count[i] = 0;
+  }
+  bt->h_offsets[B] = tot;
+  HIPCHK(hipMemcpyAsync(bt->offsets_d, bt->h_offsets.data(), 8 * (size_t)(B + 1), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(bt->count, bt->h_count.data(), 4 * (size_t)B, hipMemcpyHostToDevice, st));
+  HIPCHK(launch_compact(st, bt->start, bt->count, bt->offsets_d, bt->out_idx, bt->out_rep, bt->cidx_d, bt->crep_d, B));
+  bt->h_cidx.resize(std::max<uint64_t>(1, tot));
+  bt->h_crep.resize(std::max<uint64_t>(1, tot));
+  if (tot) {
+    HIPCHK(hipMemcpyAsync(bt->h_cidx.data(), bt->cidx_d, 4 * tot, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(bt->h_crep.data(), bt->crep_d, 4 * tot, hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(hipGetLastError());
+  double t1 = now_ms();
+  float ms_pair = 0, ms_sel = 0;
+  (void)hipEventElapsedTime(&ms_pair, e->ev[0], e->ev[1]);
+  (void)hipEventElapsedTime(&ms_sel, e->ev[1], e->ev[2]);
+  tm.pair_kernel_ms = ms_pair;
+  tm.select_kernel_ms = ms_sel;
+  tm.pair_ms = ms_pair;
+  tm.select_ms = ms_sel;
+  tm.host_ms = th1 - th0;
+  tm.copy_ms = t1 - tc0;
+  tm.total_ms = t1 - t0;
+  e->times = tm;
+  out->n_bindings = (uint64_t)B;
+  out->status = bt->h_status.data();
+  out->err_code = bt->h_err.data();
+  out->err_arg = bt->h_arg.data();
+  out->offsets = bt->h_offsets.data();
+  out->cluster_idx = bt->h_cidx.data();
+  out->replicas = bt->h_crep.data();
+  out->n_targets = tot;
+  return KP_OK;
+}
+
+// Runs the pair kernel and returns the rank-ordered device row pointers.
+static int run_pair(kp_engine* e, kp_batch* bt, int64_t* score, int est_mode, int b0, int nb) {
+  kp_snapshot* s = bt->snap;
+  HIPCHK(launch_pair(e->stream, s->view, bt->view, b0, nb, bt->fmask, bt->est, score, est_mode, kMdCap,
+                     smem_pair(s, kMdCap)));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return KP_OK;
+}
+
+int kp_filter_batch(kp_engine* e, kp_batch* bt, uint64_t* out_mask) {
+  if (!e || !bt || !out_mask) return KP_EINVAL;
+  (void)hipSetDevice(e->device);
+  kp_snapshot* s = bt->snap;
+  if (bt->B == 0) return KP_OK;
+  int rc = run_pair(e, bt, nullptr, 0, 0, bt->B);
+  if (rc) return rc;
+  std::vector<uint64_t> m((size_t)bt->B * s->W);
+  HIPCHK(hipMemcpy(m.data(), bt->fmask, 8 * m.size(), hipMemcpyDeviceToHost));
+  const int Wc = (s->C + 63) / 64;
+  memset(out_mask, 0, 8 * (size_t)bt->B * Wc);
+  for (int b = 0; b < bt->B; b++)
+    for (int r = 0; r < s->C; r++)
+      if ((m[(size_t)b * s->W + (r >> 6)] >> (r & 63)) & 1) {
+        uint32_t c = s->perm[r];
+        out_mask[(size_t)b * Wc + (c >> 6)] |= 1ull << (c & 63);
+      }
+  return KP_OK;
+}
+
+int kp_score_batch(kp_engine* e, kp_batch* bt, int64_t* out_scores) {
+  if (!e || !bt || !out_scores) return KP_EINVAL;
+  (void)hipSetDevice(e->device);
+  kp_snapshot* s = bt->snap;
+  if (bt->B == 0) return KP_OK;
+  int64_t* d = nullptr;
+  size_t n = (size_t)bt->B * std::max(1, s->C);
+  HIPCHK(hipMalloc(&d, 8 * n));
+  int rc = run_pair(e, bt, d, 0, 0, bt->B);
+  std::vector<int64_t> h(n);
+  if (rc == KP_OK) rc = hipMemcpy(h.data(), d, 8 * n, hipMemcpyDeviceToHost) == hipSuccess ? KP_OK : KP_EDEVICE;
+  (void)hipFree(d);
+  if (rc) return rc;
+  for (int b = 0; b < bt->B; b++)
+    for (int r = 0; r < s->C; r++) out_scores[(size_t)b * s->C + s->perm[r]] = h[(size_t)b * s->C + r];
+  return KP_OK;
+}
+
+int kp_max_available_replicas(kp_engine* e, kp_batch* bt, uint64_t binding, const uint32_t* cluster_idx, uint64_t n,
+                              int32_t* out) {
+  if (!e || !bt || (n && (!cluster_idx || !out)) || binding >= (uint64_t)bt->B) return KP_EINVAL;
+  (void)hipSetDevice(e->device);
+  kp_snapshot* s = bt->snap;
+  int rc = run_pair(e, bt, nullptr, 1, (int)binding, 1);
+  if (rc) return rc;
+  std::vector<int32_t> row(s->Cp);
+  HIPCHK(hipMemcpy(row.data(), bt->est + (size_t)binding * s->Cp, 4 * (size_t)s->Cp, hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < n; i++) {
+    if (cluster_idx[i] >= (uint32_t)s->C) return KP_EINVAL;
+    out[i] = row[s->inv[cluster_idx[i]]];
+  }
+  return KP_OK;
+}
+
+int kp_last_stage_times(const kp_engine* e, kp_stage_times* out) {
+  if (!e || !out) return KP_EINVAL;
+  *out = e->times;
+  return KP_OK;
+}
+
+}  // extern "C"

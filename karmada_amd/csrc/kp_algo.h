@@ -1,0 +1,646 @@
+// kp_algo.h — kernel bodies of the placement engine, written once as
+// __host__ __device__ templates over a block policy (kp_blk.h).
+//
+// Stage map (reference functions, /root/reference):
+//   pair stage   findClustersThatFit + RunFilterPlugins  core/generic_scheduler.go:119-163
+//                GeneralEstimator.maxAvailableReplicas   estimator/client/general.go:66-108
+//                calAvailableReplicas                    core/util.go:57-110
+//   select stage GroupClustersWithScore / sortClusters   spreadconstraint/group_clusters.go:103-378, util.go:43-61
+//                SelectBestClusters                      spreadconstraint/select_clusters*.go
+//                AssignReplicas + strategies             core/common.go:51-170, assignment.go, division_algorithm.go
+//                Dispenser / AllocateWebsterSeats        util/helper/binding.go:51-183, webstermethod.go:112-161
+#pragma once
+#include <stdint.h>
+
+#include "kp_blk.h"
+#include "kp_layout.h"
+
+namespace kp {
+
+// ============================================================================
+// small helpers
+// ============================================================================
+KP_HD inline bool list_has(const int32_t* p, int n, int32_t x) {
+  for (int i = 0; i < n; i++)
+    if (p[i] == x) return true;
+  return false;
+}
+KP_HD inline bool bit_test(const uint32_t* bits, int c) { return (bits[c >> 5] >> (c & 31)) & 1u; }
+KP_HD inline bool mask_test(const uint64_t* row, int c) { return (row[c >> 6] >> (c & 63)) & 1ull; }
+KP_HD inline int32_t wrap32(int64_t x) { return (int32_t)(uint32_t)(uint64_t)x; }
+KP_HD inline int32_t add32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+KP_HD inline int32_t sub32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
+KP_HD inline int64_t add64(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+KP_HD inline int64_t mul64(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+KP_HD inline int popc64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __popcll(x);
+#else
+  return __builtin_popcountll(x);
+#endif
+}
+KP_HD inline int ctz64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ffsll((unsigned long long)x) - 1;
+#else
+  return __builtin_ctzll(x);
+#endif
+}
+KP_HD inline uint64_t dbits(double d) {
+  union {
+    double d;
+    uint64_t u;
+  } x;
+  x.d = d;
+  return x.u;
+}
+KP_HD inline double bitsd(uint64_t u) {
+  union {
+    double d;
+    uint64_t u;
+  } x;
+  x.u = u;
+  return x.d;
+}
+KP_HD inline double kp_floor(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return floor(x);
+#else
+  return __builtin_floor(x);
+#endif
+}
+KP_HD inline double kp_ceil(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return ceil(x);
+#else
+  return __builtin_ceil(x);
+#endif
+}
+
+// ============================================================================
+// Sort key of sortClusters (spreadconstraint/util.go:43-61): ascending u64 order ==
+// (OverflowOrder asc, Score desc, AvailableReplicas desc, Name asc).
+// [63:54] overflow (10b) | [53] score==0 | [52:18] ~(avail + 2^33) (35b) | [17:0] rank
+// Scores are the in-tree plugin sums {0, 100}.
+// ============================================================================
+KP_HD inline uint64_t sort_key(int32_t ovf, int64_t score, int64_t avail, uint32_t rank) {
+  uint64_t o = (uint64_t)(ovf > 1023 ? 1023 : ovf) << 54;
+  uint64_t sc = (score > 0 ? 0ull : 1ull) << 53;
+  uint64_t a = ((1ull << 35) - 1) - (uint64_t)(avail + (1ll << 33));
+  return o | sc | ((a & ((1ull << 35) - 1)) << 18) | (uint64_t)(rank & 0x3ffff);
+}
+KP_HD inline uint32_t key_rank(uint64_t k) { return (uint32_t)(k & 0x3ffff); }
+KP_HD inline int64_t key_avail(uint64_t k) {
+  uint64_t a = (k >> 18) & ((1ull << 35) - 1);
+  return (int64_t)(((1ull << 35) - 1) - a) - (1ll << 33);
+}
+KP_HD inline int64_t key_score(uint64_t k) { return ((k >> 53) & 1) ? 0 : 100; }
+KP_HD inline int32_t key_ovf(uint64_t k) { return (int32_t)(k >> 54); }
+// (AvailableReplicas desc, then sortClusters position) for the swap step of
+// selectClustersByAvailableResource (select_clusters_by_cluster.go:55-78).
+KP_HD inline uint64_t avail_key(uint64_t k) {
+  uint64_t a = (k >> 18) & ((1ull << 35) - 1);
+  return (a << 29) | ((uint64_t)(k >> 54) << 19) | (((k >> 53) & 1) << 18) | (k & 0x3ffff);
+}
+
+// ============================================================================
+// Selector programs: util.ClusterMatches compiled (pkg/util/selector.go:97-155)
+// ============================================================================
+KP_HD inline bool prog_match(const SnapView& s, const BatchView& bv, int32_t prog_id, int c) {
+  const Prog p = bv.progs[prog_id];
+  for (int i = 0; i < p.ins_cnt; i++) {
+    const Instr in = bv.instrs[p.ins_off + i];
+    bool ok = true;
+    switch (in.op) {
+      case OP_FALSE:
+        return false;
+      case OP_TRUE:
+        break;
+      case OP_EXCLUDE:
+        ok = !list_has(bv.ipool + in.a, in.b, c);
+        break;
+      case OP_NAMES:
+        ok = list_has(bv.ipool + in.a, in.b, c);
+        break;
+      case OP_LBL_IN:
+      case OP_LBL_NOTIN:
+      case OP_LBL_EXISTS:
+      case OP_LBL_DNE: {
+        int32_t v = s.label_val[(size_t)in.a * s.Cp + c];
+        if (in.op == OP_LBL_IN) ok = v >= 0 && list_has(bv.ipool + in.b, in.c, v);
+        else if (in.op == OP_LBL_NOTIN) ok = v < 0 || !list_has(bv.ipool + in.b, in.c, v);
+        else if (in.op == OP_LBL_EXISTS) ok = v >= 0;
+        else ok = v < 0;
+        break;
+      }
+      case OP_FLD_IN:
+      case OP_FLD_NOTIN:
+      case OP_FLD_EXISTS:
+      case OP_FLD_DNE: {
+        int32_t v = in.a == 0 ? s.provider[c] : s.region[c];
+        if (in.op == OP_FLD_IN) ok = v >= 0 && list_has(bv.ipool + in.b, in.c, v);
+        else if (in.op == OP_FLD_NOTIN) ok = v < 0 || !list_has(bv.ipool + in.b, in.c, v);
+        else if (in.op == OP_FLD_EXISTS) ok = v >= 0;
+        else ok = v < 0;
+        break;
+      }
+      case OP_FLD_GT:
+      case OP_FLD_LT: {
+        uint32_t f = s.flags[c];
+        bool has = in.a == 0 ? (f & CF_PROVIDER_INT) : (f & CF_REGION_INT);
+        int64_t x = in.a == 0 ? s.provider_int[c] : s.region_int[c];
+        ok = has && (in.op == OP_FLD_GT ? x > in.v : x < in.v);
+        break;
+      }
+      case OP_ZONE_IN:
+      case OP_ZONE_NOTIN: {
+        int z0 = s.zone_off[c], z1 = s.zone_off[c + 1];
+        bool hit = false;
+        for (int z = z0; z < z1 && !hit; z++) hit = list_has(bv.ipool + in.b, in.c, s.zone_ids[z]);
+        ok = in.op == OP_ZONE_IN ? (z1 > z0 && hit) : !hit;
+        break;
+      }
+      case OP_ZONE_EXISTS:
+        ok = s.zone_off[c + 1] > s.zone_off[c];
+        break;
+      case OP_ZONE_DNE:
+        ok = s.zone_off[c + 1] == s.zone_off[c];
+        break;
+      default:
+        return false;
+    }
+    if (!ok) return false;
+  }
+  return true;
+}
+
+// ============================================================================
+// Pair stage
+// ============================================================================
+// TaintToleration.Filter (taint_toleration.go:53-84), FindMatchingUntoleratedTaint
+// (component-helpers/scheduling/corev1/helpers.go:79-102), ToleratesTaint with
+// comparison operators disabled (core/v1/toleration.go:52-77). Only
+// NoSchedule/NoExecute taints are packed.
+KP_HD inline bool taints_tolerated(const SnapView& s, const BatchView& bv, const BindHdr& h, int c) {
+  int t0 = s.taint_off[c], t1 = s.taint_off[c + 1];
+  for (int t = t0; t < t1; t++) {
+    int32_t k = s.taint_key[t], v = s.taint_val[t], e = s.taint_eff[t];
+    bool tol = false;
+    for (int j = 0; j < h.tol_cnt && !tol; j++) {
+      const Tol tl = bv.tols[h.tol_off + j];
+      tol = (tl.eff == EFF_ANY || tl.eff == e) && (tl.key < 0 || tl.key == k) && (tl.op == TOL_EXISTS || tl.val == v);
+    }
+    if (!tol) return false;
+  }
+  return true;
+}
+
+// findClustersThatFit skip-deleting + RunFilterPlugins over the enabled plugins.
+KP_HD inline bool pair_feasible(const SnapView& s, const BatchView& bv, const BindHdr& h, int c,
+                                const uint32_t* tgt_bits, const uint32_t* evict_bits) {
+  if (c >= s.C) return false;
+  uint32_t f = s.flags[c];
+  if (f & CF_DELETING) return false;
+  int en = h.enabled;
+  bool in_t = h.tgt_cnt > 0 && bit_test(tgt_bits, c);
+  if ((en & 1) && !in_t) {  // APIEnablement (api_enablement.go:51-78)
+    if (h.gvk < 0) return false;
+    uint64_t w = s.api_bits[(size_t)(h.gvk >> 6) * s.Cp + c];
+    if (!((w >> (h.gvk & 63)) & 1ull)) return false;
+  }
+  if ((en & 2) && !in_t && !taints_tolerated(s, bv, h, c)) return false;
+  if ((en & 4) && !(h.flags & BF_AFF_ALL)) {  // ClusterAffinity (cluster_affinity.go:51-94)
+    bool m = false;
+    for (int j = 0; j < h.filt_cnt && !m; j++) m = prog_match(s, bv, bv.ipool[h.filt_off + j], c);
+    if (!m) return false;
+  }
+  if (en & 8) {  // SpreadConstraint (spread_constraint.go:49-66)
+    if ((h.flags & BF_NEED_PROVIDER) && !(f & CF_HAS_PROVIDER)) return false;
+    if ((h.flags & BF_NEED_REGION) && !(f & CF_HAS_REGION)) return false;
+    if ((h.flags & BF_NEED_ZONES) && !(f & CF_HAS_ZONES)) return false;
+  }
+  if ((en & 32) && h.evict_cnt > 0 && bit_test(evict_bits, c)) return false;  // ClusterEviction
+  return true;
+}
+
+// MaxDivided of one model template for this binding's request (resource.go:191-220),
+// pods capped at 110 (general.go:318-330).
+KP_HD inline int32_t template_md(const SnapView& s, const BatchView& bv, const BindHdr& h, int tid) {
+  int64_t res = kMaxPodsPerNode;
+  for (int j = 0; j < h.mreq_cnt; j++) {
+    int32_t rid = bv.ipool[h.mreq_off + j];
+    int64_t q = bv.lpool[h.mreq_q_off + j];
+    int64_t have = rid < 0 ? 0 : s.tmpl[(size_t)tid * s.n_res + rid];
+    int64_t d = have / q;
+    if (d < res) res = d;
+  }
+  return (int32_t)res;
+}
+
+// GeneralEstimator.maxAvailableReplicas (general.go:66-108), assumed workloads empty.
+// md: per-template MaxDivided table (LDS) or nullptr to compute per pair.
+KP_HD inline int32_t general_estimate(const SnapView& s, const BatchView& bv, const BindHdr& h, int c,
+                                      const int32_t* md) {
+  uint32_t f = s.flags[c];
+  if (!(f & CF_HAS_SUMMARY)) return 0;
+  int64_t m = s.allowed[c];
+  if (m <= 0) return 0;
+  if (!(h.flags & BF_HAS_RR)) return (int32_t)m;
+  if ((f & CF_MODEL_OK) && !(h.flags & BF_MODEL_ERR)) {
+    // getMaximumReplicasBasedOnResourceModels: each identical model node absorbs
+    // exactly its initial MaxDivided, capped at MaxInt32.
+    int64_t total = 0;
+    for (int g = s.mgrp_off[c]; g < s.mgrp_off[c + 1]; g++) {
+      int64_t d = md ? md[s.mgrp_tid[g]] : template_md(s, bv, h, s.mgrp_tid[g]);
+      int64_t cnt = s.mgrp_cnt[g];
+      if (d > 0 && cnt > (int64_t)kInt32Max / d) {
+        total = kInt32Max;
+        break;
+      }
+      total += d * cnt;
+      if (total >= kInt32Max) {
+        total = kInt32Max;
+        break;
+      }
+    }
+    if (total < m) m = total;
+    return (int32_t)m;
+  }
+  // getMaximumReplicasBasedOnClusterSummary (general.go:465-505)
+  int64_t num = INT64_MAX;
+  for (int j = 0; j < h.sreq_cnt; j++) {
+    int32_t rid = bv.ipool[h.sreq_off + j];
+    if (rid < 0) return 0;
+    int64_t a = s.avail[(size_t)rid * s.Cp + c];
+    if (a <= 0) return 0;
+    int64_t d = a / bv.lpool[h.sreq_q_off + j];
+    if (d < num) num = d;
+  }
+  if (num < m) m = num;
+  return (int32_t)m;
+}
+
+// calAvailableReplicas (core/util.go:57-110) with the GeneralEstimator only.
+KP_HD inline int32_t cal_available(const SnapView& s, const BatchView& bv, const BindHdr& h, int c,
+                                   const int32_t* md) {
+  if (h.flags & BF_NONWORKLOAD_EST) return kInt32Max;
+  int32_t r = general_estimate(s, bv, h, c, md);
+  int32_t v = kInt32Max;
+  if (r != -1 && v > r) v = r;  // mergeReplicaResults skips UnauthenticReplica (-1)
+  if (v == kInt32Max) v = h.replicas;
+  return v;
+}
+
+// getClusterOverflowOrder (group_clusters.go:517-543)
+KP_HD inline int32_t overflow_order(const SnapView& s, const BatchView& bv, const BindHdr& h, int c) {
+  if (h.ovf_mode == OVF_ZERO) return 0;
+  if (h.ovf_mode == OVF_1000) return 1000;
+  for (int j = 0; j < h.ovf_cnt; j++)
+    if (prog_match(s, bv, bv.ipool[h.ovf_off + j], c)) return j;
+  return 1000;
+}
+
+// ============================================================================
+// Per-binding candidate view
+// ============================================================================
+struct Cands {
+  uint32_t* r;  // rank | overflow << kRankBits
+  int32_t* v;   // AllocatableReplicas (or static weight for SEL_ALL StaticWeight)
+  int32_t F;
+};
+KP_HD inline uint32_t c_rank(const Cands& cd, int i) { return cd.r[i] & kRankMask; }
+KP_HD inline int32_t c_ovf(const Cands& cd, int i) { return (int32_t)(cd.r[i] >> kRankBits); }
+
+// AssignedReplicasForCluster (binding_types_helper.go:124-132): first spec.Clusters entry.
+KP_HD inline int32_t assigned_of(const BatchView& bv, const BindHdr& h, const uint32_t* tgt_bits, uint32_t rank) {
+  if (h.tgt_cnt == 0 || !bit_test(tgt_bits, (int)rank)) return 0;
+  for (int j = 0; j < h.tgt_cnt; j++)
+    if ((uint32_t)bv.ipool[h.tgt_off + 2 * j] == rank) return bv.ipool[h.tgt_off + 2 * j + 1];
+  return 0;
+}
+KP_HD inline int64_t locality_score(const BindHdr& h, const uint32_t* tgt_bits, uint32_t rank) {
+  return ((h.flags & BF_SCORE_LOCALITY) && bit_test(tgt_bits, (int)rank)) ? 100 : 0;
+}
+
+// ============================================================================
+// Result sink
+// ============================================================================
+struct Sink {
+  uint32_t* out_idx;   // caller cluster index
+  int32_t* out_rep;
+  unsigned long long* counter;
+  int32_t* status;
+  int32_t* err;
+  int64_t* arg;
+  uint64_t* start;
+  uint32_t* count;
+};
+
+// ============================================================================
+// Go sort.Sort (pdqsort) on TargetClustersList (division_algorithm.go:31-36),
+// restated from the structure of sort/zsortinterface.go (go1.26). Parity for
+// n > 12 is unpinned by reference tests (SURVEY hazard H2).
+// ============================================================================
+struct TCL {
+  uint32_t* name;
+  int32_t* rep;
+  KP_HD bool Less(int i, int j) const { return rep[i] > rep[j]; }
+  KP_HD void Swap(int i, int j) const {
+    uint32_t a = name[i];
+    name[i] = name[j];
+    name[j] = a;
+    int32_t b = rep[i];
+    rep[i] = rep[j];
+    rep[j] = b;
+  }
+};
+KP_HD inline int bits_len(uint64_t x) {
+  int n = 0;
+  while (x) {
+    n++;
+    x >>= 1;
+  }
+  return n;
+}
+template <class D>
+KP_HD void pdq_insertion(const D& d, int a, int b) {
+  for (int i = a + 1; i < b; i++)
+    for (int j = i; j > a && d.Less(j, j - 1); j--) d.Swap(j, j - 1);
+}
+template <class D>
+KP_HD void pdq_sift(const D& d, int lo, int hi, int first) {
+  int root = lo;
+  for (;;) {
+    int child = 2 * root + 1;
+    if (child >= hi) return;
+    if (child + 1 < hi && d.Less(first + child, first + child + 1)) child++;
+    if (!d.Less(first + root, first + child)) return;
+    d.Swap(first + root, first + child);
+    root = child;
+  }
+}
+template <class D>
+KP_HD void pdq_heapsort(const D& d, int a, int b) {
+  int first = a, hi = b - a;
+  for (int i = (hi - 1) / 2; i >= 0; i--) pdq_sift(d, i, hi, first);
+  for (int i = hi - 1; i >= 0; i--) {
+    d.Swap(first, first + i);
+    pdq_sift(d, 0, i, first);
+  }
+}
+template <class D>
+KP_HD int pdq_median(const D& d, int a, int b, int c, int& swaps) {
+  if (d.Less(b, a)) {
+    swaps++;
+    int t = a;
+    a = b;
+    b = t;
+  }
+  if (d.Less(c, b)) {
+    swaps++;
+    int t = b;
+    b = c;
+    c = t;
+  }
+  if (d.Less(b, a)) {
+    swaps++;
+    int t = a;
+    a = b;
+    b = t;
+  }
+  return b;
+}
+template <class D>
+KP_HD void pdqsort_go(const D& d, int a, int b, int limit) {
+  bool wasBalanced = true, wasPartitioned = true;
+  for (;;) {
+    int length = b - a;
+    if (length <= 12) {
+      pdq_insertion(d, a, b);
+      return;
+    }
+    if (limit == 0) {
+      pdq_heapsort(d, a, b);
+      return;
+    }
+    if (!wasBalanced) {  // breakPatterns
+      if (length >= 8) {
+        uint64_t r = (uint64_t)length;
+        uint64_t modulus = 1ull << bits_len((uint64_t)length);
+        int idx = a + (length / 4) * 2 - 1;
+        for (int i = 0; i < 3; i++) {
+          r ^= r << 13;
+          r ^= r >> 7;
+          r ^= r << 17;
+          int other = (int)((unsigned)r & (modulus - 1));
+          if (other >= length) other -= length;
+          d.Swap(idx - 1 + i, a + other);
+        }
+      }
+      limit--;
+    }
+    // choosePivot
+    int swaps = 0;
+    int pi = a + length / 4 * 1, pj = a + length / 4 * 2, pk = a + length / 4 * 3;
+    if (length >= 8) {
+      if (length >= 50) {
+        pi = pdq_median(d, pi - 1, pi, pi + 1, swaps);
+        pj = pdq_median(d, pj - 1, pj, pj + 1, swaps);
+        pk = pdq_median(d, pk - 1, pk, pk + 1, swaps);
+      }
+      pj = pdq_median(d, pi, pj, pk, swaps);
+    }
+    int hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
+    int pivot = pj;
+    if (hint == 2) {
+      int i = a, j = b - 1;
+      while (i < j) {
+        d.Swap(i, j);
+        i++;
+        j--;
+      }
+      pivot = (b - 1) - (pivot - a);
+      hint = 1;
+    }
+    if (wasBalanced && wasPartitioned && hint == 1) {  // partialInsertionSort
+      int i = a + 1;
+      bool sorted = false;
+      for (int step = 0; step < 5; step++) {
+        while (i < b && !d.Less(i, i - 1)) i++;
+        if (i == b) {
+          sorted = true;
+          break;
+        }
+        if (b - a < 50) break;
+        d.Swap(i, i - 1);
+        if (i - a >= 2) {
+          for (int j = i - 1; j >= 1; j--) {
+            if (!d.Less(j, j - 1)) break;
+            d.Swap(j, j - 1);
+          }
+        }
+        if (b - i >= 2) {
+          for (int j = i + 1; j < b; j++) {
+            if (!d.Less(j, j - 1)) break;
+            d.Swap(j, j - 1);
+          }
+        }
+      }
+      if (sorted) return;
+    }
+    if (a > 0 && !d.Less(a - 1, pivot)) {  // partitionEqual
+      d.Swap(a, pivot);
+      int i = a + 1, j = b - 1;
+      for (;;) {
+        while (i <= j && !d.Less(a, i)) i++;
+        while (i <= j && d.Less(a, j)) j--;
+        if (i > j) break;
+        d.Swap(i, j);
+        i++;
+        j--;
+      }
+      a = i;
+      continue;
+    }
+    // partition
+    d.Swap(a, pivot);
+    int i = a + 1, j = b - 1;
+    bool already = false;
+    while (i <= j && d.Less(i, a)) i++;
+    while (i <= j && !d.Less(j, a)) j--;
+    int mid;
+    if (i > j) {
+      d.Swap(j, a);
+      mid = j;
+      already = true;
+    } else {
+      d.Swap(i, j);
+      i++;
+      j--;
+      for (;;) {
+        while (i <= j && d.Less(i, a)) i++;
+        while (i <= j && !d.Less(j, a)) j--;
+        if (i > j) break;
+        d.Swap(i, j);
+        i++;
+        j--;
+      }
+      d.Swap(j, a);
+      mid = j;
+    }
+    wasPartitioned = already;
+    int leftLen = mid - a, rightLen = b - mid;
+    int balanceThreshold = length / 8;
+    if (leftLen < rightLen) {
+      wasBalanced = leftLen >= balanceThreshold;
+      pdqsort_go(d, a, mid, limit);
+      a = mid + 1;
+    } else {
+      wasBalanced = rightLen >= balanceThreshold;
+      pdqsort_go(d, mid + 1, b, limit);
+      b = mid;
+    }
+  }
+}
+KP_HD inline void sort_tcl(uint32_t* name, int32_t* rep, int n) {
+  if (n <= 1) return;
+  TCL d{name, rep};
+  pdqsort_go(d, 0, n, bits_len((uint64_t)n));
+}
+
+// ============================================================================
+// Webster / Sainte-Lague priorities (webstermethod.go:57-85)
+// ============================================================================
+// float64(Votes) / float64(2*Seats+1) with Seats < 2^30 (no int32 wrap).
+KP_HD inline double w_prio(int64_t v, int64_t k) { return (double)v / (double)(2 * k + 1); }
+
+// #{k >= 0 : prio(v,k) >= t} (ge) or > t, for v >= 0, t > 0, saturating at cap.
+KP_HD inline int64_t w_count(int64_t v, double t, int64_t cap, bool ge) {
+  if (v <= 0) return 0;
+  double r = (double)v / t;
+  double kf = r < 1.0 ? 0.0 : kp_floor((r - 1.0) * 0.5) + 1.0;
+  int64_t k = kf > (double)cap ? cap : (int64_t)kf;
+  while (k > 0) {
+    double p = w_prio(v, k - 1);
+    if (ge ? p >= t : p > t) break;
+    k--;
+  }
+  while (k < cap) {
+    double p = w_prio(v, k);
+    if (!(ge ? p >= t : p > t)) break;
+    k++;
+  }
+  return k;
+}
+
+// Serial exact AllocateWebsterSeats for parties with unique names and votes >= 0
+// (dispenser with nil init): result seats[] per party. Names order: rank asc,
+// `desc` flips the name tie-break (tieBreakerByUID, binding.go:117-144).
+// Works from a count threshold t0 with cnt_gt(t0) <= N (every element above t0
+// is in the top-N), then continues with Go's heap order for the rest.
+struct WHeap {
+  const uint32_t* name;
+  const int64_t* votes;
+  int32_t* seats;
+  int32_t* h;  // heap of party indices
+  bool desc;
+  KP_HD double pr(int i) const { return (double)votes[i] / (double)add32((int32_t)(2u * (uint32_t)seats[i]), 1); }
+  KP_HD bool less(int a, int b) const {  // a before b
+    double pa = pr(a), pb = pr(b);
+    if (pa == pb) {
+      if (seats[a] != seats[b]) return seats[a] < seats[b];
+      return desc ? name[a] > name[b] : name[a] < name[b];
+    }
+    return pa > pb;
+  }
+  KP_HD void down(int i0, int n) {
+    int i = i0;
+    for (;;) {
+      int j1 = 2 * i + 1;
+      if (j1 >= n || j1 < 0) break;
+      int j = j1;
+      if (j1 + 1 < n && less(h[j1 + 1], h[j1])) j = j1 + 1;
+      if (!less(h[j], h[i])) break;
+      int t = h[i];
+      h[i] = h[j];
+      h[j] = t;
+      i = j;
+    }
+  }
+};
+KP_HD inline void webster_serial(const uint32_t* name, const int64_t* votes, int32_t* seats, int32_t* heap, int n,
+                                 int32_t N, bool desc) {
+  for (int i = 0; i < n; i++) seats[i] = 0;
+  if (n == 0 || N <= 0) return;
+  bool neg = false;
+  int64_t V = 0;
+  for (int i = 0; i < n; i++) {
+    if (votes[i] < 0) neg = true;
+    V += votes[i];
+  }
+  int32_t done = 0;
+  if (!neg && V > 0) {
+    double t0 = N > n ? (double)V / (2.0 * (double)(N - n)) : (double)V;
+    for (int iter = 0; iter < 80; iter++) {
+      int64_t S = 0;
+      for (int i = 0; i < n; i++) S += w_count(votes[i], t0, (int64_t)N + 1, false);
+      if (S <= N) break;
+      t0 *= 2.0;
+    }
+    for (int i = 0; i < n; i++) {
+      seats[i] = (int32_t)w_count(votes[i], t0, (int64_t)N + 1, false);
+      done += seats[i];
+    }
+  }
+  WHeap w{name, votes, seats, heap, desc};
+  for (int i = 0; i < n; i++) heap[i] = i;
+  for (int i = n / 2 - 1; i >= 0; i--) w.down(i, n);
+  for (int32_t rem = N - done; rem > 0; rem--) {
+    // heap.Pop + Seats++ + heap.Push == increase the top's key and sift down
+    int top = heap[0];
+    seats[top] = add32(seats[top], 1);
+    w.down(0, n);
+  }
+}
+
+}  // namespace kp

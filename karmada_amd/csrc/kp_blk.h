@@ -1,0 +1,136 @@
+// kp_blk.h — block-execution policies for the kernel bodies in kp_algo.h.
+//
+// GpuBlk: one HIP workgroup (wave64 x N waves) with wave-shuffle reductions and
+// a small LDS scratch for cross-wave combination.
+// CpuBlk: a 1-thread "workgroup" used only by the CPU unit-test build of the
+// kernel bodies (tests/, libkp_cpusim.so); it is never linked into libkp.so.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define KP_HD __host__ __device__
+#define KP_DEV __device__
+#define KP_INLINE __device__ __forceinline__
+#else
+#define KP_HD
+#define KP_DEV
+#define KP_INLINE inline
+#endif
+
+namespace kp {
+
+#if defined(__HIPCC__) || defined(__HIP__)
+struct GpuBlk {
+  int64_t* red;  // >= 32 int64 of LDS
+
+  KP_INLINE int tid() const { return (int)threadIdx.x; }
+  KP_INLINE int nth() const { return (int)blockDim.x; }
+  KP_INLINE int lane() const { return (int)(threadIdx.x & 63); }
+  KP_INLINE int wid() const { return (int)(threadIdx.x >> 6); }
+  KP_INLINE int nwaves() const { return (int)(blockDim.x >> 6); }
+  KP_INLINE void sync() const { __syncthreads(); }
+
+  template <class T, class Op>
+  KP_INLINE T wave_reduce(T v, Op op) const {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = op(v, (T)__shfl_xor(v, o, 64));
+    return v;
+  }
+  template <class T, class Op>
+  KP_INLINE T reduce(T v, Op op) const {
+    v = wave_reduce(v, op);
+    sync();
+    if (lane() == 0) red[wid()] = (int64_t)v;
+    sync();
+    T r = (T)red[0];
+    for (int w = 1; w < nwaves(); w++) r = op(r, (T)red[w]);
+    sync();
+    return r;
+  }
+  KP_INLINE int64_t sum64(int64_t v) const { return reduce(v, [](int64_t a, int64_t b) { return a + b; }); }
+  KP_INLINE uint64_t minu64(uint64_t v) const {
+    return reduce(v, [](uint64_t a, uint64_t b) { return a < b ? a : b; });
+  }
+  KP_INLINE int64_t max64(int64_t v) const { return reduce(v, [](int64_t a, int64_t b) { return a > b ? a : b; }); }
+  KP_INLINE int64_t min64(int64_t v) const { return reduce(v, [](int64_t a, int64_t b) { return a < b ? a : b; }); }
+  KP_INLINE bool any(bool p) const { return sum64(p ? 1 : 0) != 0; }
+  // Exclusive prefix sum of per-thread counts in thread order; *total = sum.
+  KP_INLINE int32_t excl_scan(int32_t v, int32_t* total) const {
+    int32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      int32_t y = __shfl_up(x, o, 64);
+      if (lane() >= o) x += y;
+    }
+    sync();
+    if (lane() == 63) red[wid()] = x;
+    sync();
+    int32_t base = 0, tot = 0;
+    for (int w = 0; w < nwaves(); w++) {
+      int32_t s = (int32_t)red[w];
+      if (w < wid()) base += s;
+      tot += s;
+    }
+    sync();
+    *total = tot;
+    return base + x - v;
+  }
+  // Value of thread 0 to every thread.
+  template <class T>
+  KP_INLINE T bcast(T v) const {
+    sync();
+    if (tid() == 0) red[0] = (int64_t)v;
+    sync();
+    T r = (T)red[0];
+    sync();
+    return r;
+  }
+};
+#endif
+
+struct CpuBlk {
+  int64_t* red;
+  int tid() const { return 0; }
+  int nth() const { return 1; }
+  int lane() const { return 0; }
+  int wid() const { return 0; }
+  int nwaves() const { return 1; }
+  void sync() const {}
+  int64_t sum64(int64_t v) const { return v; }
+  uint64_t minu64(uint64_t v) const { return v; }
+  int64_t max64(int64_t v) const { return v; }
+  int64_t min64(int64_t v) const { return v; }
+  bool any(bool p) const { return p; }
+  int32_t excl_scan(int32_t v, int32_t* total) const {
+    *total = v;
+    return 0;
+  }
+  template <class T>
+  T bcast(T v) const {
+    return v;
+  }
+};
+
+// Atomics on LDS/global memory, usable from both builds.
+template <class T>
+KP_HD inline T kp_atomic_add(T* p, T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return atomicAdd(p, v);
+#else
+  T o = *p;
+  *p = o + v;
+  return o;
+#endif
+}
+KP_HD inline unsigned long long kp_atomic_min_u64(unsigned long long* p, unsigned long long v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return atomicMin(p, v);
+#else
+  unsigned long long o = *p;
+  if (v < o) *p = v;
+  return o;
+#endif
+}
+
+}  // namespace kp

@@ -1,0 +1,630 @@
+// kp_paths.h — per-binding select/assign paths (one workgroup per binding).
+//
+//   sel_all_fast      SelectBestClusters "select all" + AssignReplicas, block-parallel
+//                     (Duplicated, StaticWeight, DynamicWeight, Aggregated).
+//   sel_cluster_fast  selectBestClustersByCluster: top-MaxGroups + swap step, then
+//                     the serial AssignReplicas on the selected list.
+//   region_a/_b       generateRegionInfo/calcGroupScore on device; selectGroups DFS
+//                     on the host; region heads + top-up + AssignReplicas on device.
+//   slow_path         exact serial emulation over the fully sorted candidate list
+//                     for the rare hazards the fast paths refuse (Aggregated ties
+//                     at the prefix cut, int32 wrap risk, overflow tiers, ...).
+#pragma once
+#include "kp_select.h"
+
+namespace kp {
+
+constexpr int kRegionMax = 256;
+
+KP_HD inline uint64_t cand_key(const SelCtx& x, const Cands& cd, int i, int32_t est) {
+  uint32_t rank = c_rank(cd, i);
+  int64_t avail = (int64_t)est + (int64_t)assigned_of(*x.bv, *x.h, x.tgt_bits, rank);
+  return sort_key(c_ovf(cd, i), locality_score(*x.h, x.tgt_bits, rank), avail, rank);
+}
+KP_HD inline Item item_from_key(const SelCtx& x, uint64_t k) {
+  Item it;
+  it.rank = key_rank(k);
+  it.alloc = x.erow[it.rank];
+  it.avail = key_avail(k);
+  it.ovf = key_ovf(k);
+  it.pad = 0;
+  return it;
+}
+
+// scheduledClusters helpers: spec.Clusters entries whose cluster is a candidate
+// (assignment.go:125-142). Targets are unique here (BF_DUP_TARGETS goes slow).
+KP_HD inline int32_t sched_rep_of(const SelCtx& x, uint32_t rank) {
+  return assigned_of(*x.bv, *x.h, x.tgt_bits, rank);
+}
+KP_HD inline bool in_sched(const SelCtx& x, uint32_t rank) {
+  return x.h->tgt_cnt > 0 && bit_test(x.tgt_bits, (int)rank) && mask_test(x.frow, (int)rank);
+}
+
+// Block-parallel emission of per-candidate results. rep(i) returns the replicas
+// of candidate i in the result; `keep_all` emits every candidate (non-workload /
+// EnableEmptyWorkloadPropagation), otherwise only rep > 0 (removeZeroReplicasCluster).
+template <class BLK, class RepFn>
+KP_HD void emit_par(const BLK& B, const SelCtx& x, const Cands& cd, RepFn rep, bool keep_all) {
+  int64_t cnt = 0;
+  for (int i = B.tid(); i < cd.F; i += B.nth())
+    if (keep_all || rep(i) > 0) cnt++;
+  cnt = B.sum64(cnt);
+  unsigned long long base = 0;
+  if (B.tid() == 0) {
+    base = cnt > 0 ? kp_atomic_add(x.sink.counter, (unsigned long long)cnt) : 0ull;
+    x.sink.status[x.b] = KP_STATUS_OK;
+    x.sink.err[x.b] = KP_ERR_NONE;
+    x.sink.arg[x.b] = 0;
+    x.sink.start[x.b] = base;
+    x.sink.count[x.b] = (uint32_t)cnt;
+  }
+  base = B.bcast(base);
+  int64_t run = 0;
+  for (int t0 = 0; t0 < cd.F; t0 += B.nth()) {
+    int i = t0 + B.tid();
+    int32_t r = 0;
+    bool e = false;
+    if (i < cd.F) {
+      r = rep(i);
+      e = keep_all || r > 0;
+      if (keep_all && r < 0) r = 0;
+    }
+    int32_t tot;
+    int32_t off = B.excl_scan(e ? 1 : 0, &tot);
+    if (e) {
+      uint64_t o = base + (uint64_t)run + (uint64_t)off;
+      x.sink.out_idx[o] = x.s->perm[c_rank(cd, i)];
+      x.sink.out_rep[o] = r;
+    }
+    run += tot;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// SEL_ALL: every feasible cluster is selected (select_clusters.go:29-32).
+// Returns false when the binding needs the exact serial path (nothing written).
+// ----------------------------------------------------------------------------
+template <class BLK>
+KP_HD bool sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
+  const BindHdr& h = *x.h;
+  const bool desc = (h.flags & BF_UID_DESC) != 0;
+  const bool prop = (h.flags & BF_EMPTY_PROP) != 0;
+  if (!(h.flags & BF_WORKLOAD_ASSIGN)) {  // non-workload: all candidates, 0 replicas (common.go:72-82)
+    emit_par(B, x, cd, [&](int) { return (int32_t)0; }, true);
+    return true;
+  }
+  if (h.flags & (BF_OVERFLOW | BF_DUP_TARGETS)) return false;
+  const int st = h.strategy;
+  if (st == ST_NONE) {
+    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_UNSUPPORTED_STRATEGY, 0);
+    return true;
+  }
+  if (st == ST_DUPLICATED) {
+    int32_t rep = h.replicas;
+    emit_par(B, x, cd, [&](int) { return rep > 0 ? rep : (int32_t)0; }, prop);
+    return true;
+  }
+  if (st == ST_STATIC) {
+    int64_t wmax = 0, wsum = 0;
+    for (int i = B.tid(); i < cd.F; i += B.nth()) {
+      int64_t w = cd.v[i];
+      if (w > wmax) wmax = w;
+      wsum += w > 0 ? w : 0;
+    }
+    wmax = B.max64(wmax);
+    wsum = B.sum64(wsum);
+    if (wmax >= kInt32Max) return false;
+    bool all1 = wsum == 0;  // getStaticWeightInfoList: every candidate weight 1
+    auto party = [&](int i) { return all1 || cd.v[i] > 0; };
+    auto vote = [&](int i) { return all1 ? (int64_t)1 : (int64_t)cd.v[i]; };
+    WebRes w = webster_par(B, cd, party, vote, h.replicas, desc);
+    emit_par(B, x, cd, [&](int i) { return party(i) ? web_seats(w, vote(i), c_rank(cd, i)) : (int32_t)0; }, prop);
+    return true;
+  }
+  // Dynamic / Aggregated (assignment.go:213-244)
+  int32_t assigned = 0, ns = 0;
+  bool anyPriorPos = false;
+  if (B.tid() == 0) {
+    for (int j = 0; j < h.tgt_cnt; j++) {
+      uint32_t r = (uint32_t)x.bv->ipool[h.tgt_off + 2 * j];
+      if (mask_test(x.frow, (int)r)) {
+        int32_t v = x.bv->ipool[h.tgt_off + 2 * j + 1];
+        assigned = add32(assigned, v);
+        ns++;
+        if (v > 0) anyPriorPos = true;
+      }
+    }
+  }
+  assigned = B.bcast(assigned);
+  ns = B.bcast(ns);
+  anyPriorPos = B.bcast(anyPriorPos ? 1 : 0) != 0;
+  const bool fresh = (h.flags & BF_FRESH) != 0;
+  int mode;  // 0 fresh, 1 scale up, 2 unchanged, 3 scale down
+  if (fresh) mode = 0;
+  else if (assigned > h.replicas) mode = 3;
+  else if (assigned < h.replicas) mode = 1;
+  else mode = 2;
+  if (mode == 3) return false;  // parties = scheduledClusters: exact serial path
+  if (mode == 2) {              // unchanged: scheduledClusters, removeZero
+    emit_par(B, x, cd, [&](int i) { return in_sched(x, c_rank(cd, i)) ? sched_rep_of(x, c_rank(cd, i)) : (int32_t)0; },
+             prop);
+    return true;
+  }
+  auto vote32 = [&](int i) -> int32_t {
+    int32_t v = cd.v[i];
+    if (mode == 0 && in_sched(x, c_rank(cd, i))) v = add32(v, sched_rep_of(x, c_rank(cd, i)));
+    return v;
+  };
+  int64_t sabs = 0, vmin = 0, vtot = 0;
+  for (int i = B.tid(); i < cd.F; i += B.nth()) {
+    int64_t v = vote32(i);
+    sabs += v < 0 ? -v : v;
+    if (v < vmin) vmin = v;
+    vtot += v;
+  }
+  sabs = B.sum64(sabs);
+  vmin = B.min64(vmin);
+  vtot = B.sum64(vtot);
+  if (vmin < 0 || sabs >= (int64_t)kInt32Max) return false;  // int32 wrap hazard
+  int32_t target = mode == 0 ? h.replicas : sub32(h.replicas, assigned);
+  if ((int32_t)vtot < target) {
+    if (B.tid() == 0)
+      sink_error(x, KP_STATUS_UNSCHEDULABLE, mode == 0 ? KP_ERR_FRESH_NOT_ENOUGH : KP_ERR_SCALE_UP_NOT_ENOUGH, vtot);
+    return true;
+  }
+  const bool merge = mode == 1;
+  auto prior = [&](int i) { return merge && anyPriorPos && in_sched(x, c_rank(cd, i)) && sched_rep_of(x, c_rank(cd, i)) > 0; };
+  // Aggregated prefix cut (division_algorithm.go:81-89) over sort.Sort order
+  // (Replicas desc) with prior clusters first: membership is exact unless a
+  // tie group straddles the cut (then the pdqsort permutation matters).
+  int64_t vstar = -1;   // members: X elements with v > vstar, plus the whole tie group when tie_all
+  bool xIsPrior = false, tie_all = true, noCut = false;
+  if (st == ST_AGGREGATED) {
+    int64_t SP = 0, nP = 0;
+    for (int i = B.tid(); i < cd.F; i += B.nth())
+      if (prior(i)) {
+        SP += vote32(i);
+        nP++;
+      }
+    SP = B.sum64(SP);
+    nP = B.sum64(nP);
+    xIsPrior = nP > 0 && SP >= target;
+    int64_t tX = xIsPrior ? (int64_t)target : (int64_t)target - SP;
+    auto inX = [&](int i) { return prior(i) == xIsPrior; };
+    int64_t xmax = -1, xsum = 0;
+    for (int i = B.tid(); i < cd.F; i += B.nth())
+      if (inX(i)) {
+        int64_t v = vote32(i);
+        if (v > xmax) xmax = v;
+        xsum += v;
+      }
+    xmax = B.max64(xmax);
+    xsum = B.sum64(xsum);
+    if (xmax < 0 || xsum < tX) {
+      noCut = true;  // every element of X is taken
+    } else {
+      auto sge = [&](int64_t v0) {
+        int64_t s = 0;
+        for (int i = B.tid(); i < cd.F; i += B.nth())
+          if (inX(i)) {
+            int64_t v = vote32(i);
+            if (v >= v0) s += v;
+          }
+        return B.sum64(s);
+      };
+      if (tX <= 0) {
+        vstar = xmax;  // the first element alone reaches the target
+      } else {
+        int64_t lo = 0, hi = xmax;  // largest v with sge(v) >= tX
+        while (lo < hi) {
+          int64_t mid = lo + (hi - lo + 1) / 2;
+          if (sge(mid) >= tX) lo = mid;
+          else hi = mid - 1;
+        }
+        vstar = lo;
+      }
+      int64_t sgt = 0, ceq = 0;
+      for (int i = B.tid(); i < cd.F; i += B.nth())
+        if (inX(i)) {
+          int64_t v = vote32(i);
+          if (v > vstar) sgt += v;
+          if (v == vstar) ceq++;
+        }
+      sgt = B.sum64(sgt);
+      ceq = B.sum64(ceq);
+      int64_t need = tX - sgt;
+      int64_t j = need <= 0 ? 1 : (vstar > 0 ? (need + vstar - 1) / vstar : ceq);
+      if (j < ceq) return false;  // tie group straddles the cut
+      tie_all = true;
+    }
+  }
+  auto member = [&](int i) {
+    if (st != ST_AGGREGATED) return true;
+    bool p = prior(i);
+    if (!xIsPrior && p) return true;  // X = non-prior: every prior cluster precedes the cut
+    if (p != xIsPrior) return false;
+    if (noCut) return true;
+    int64_t v = vote32(i);
+    return v > vstar || (v == vstar && tie_all);
+  };
+  auto vote = [&](int i) { return (int64_t)vote32(i); };
+  WebRes w = webster_par(B, cd, member, vote, target, desc);
+  emit_par(
+      B, x, cd,
+      [&](int i) {
+        uint32_t rk = c_rank(cd, i);
+        int32_t r = member(i) ? web_seats(w, vote32(i), rk) : 0;
+        if (merge && in_sched(x, rk)) r = add32(r, sched_rep_of(x, rk));
+        return r;
+      },
+      prop);
+  return true;
+}
+
+// ----------------------------------------------------------------------------
+// Small selected list -> serial AssignReplicas (thread 0) -> sink.
+// ----------------------------------------------------------------------------
+template <class BLK>
+KP_HD void assign_small(const BLK& B, const SelCtx& x, const Item* items, int n, void* scratch, int cap) {
+  if (B.tid() == 0) {
+    SerialScratch sc = serial_scratch_carve(scratch, cap);
+    SerialAssign sa{x, sc, (x.h->flags & BF_UID_DESC) != 0};
+    SerialOut o = sa.run(items, n);
+    sink_serial(x, sc, o);
+  }
+  B.sync();
+}
+
+// ----------------------------------------------------------------------------
+// SEL_CLUSTER: selectBestClustersByCluster (select_clusters_by_cluster.go:25-102)
+// items: LDS buffer of kSmallMax*2 Items. Returns false -> slow path.
+// ----------------------------------------------------------------------------
+template <class BLK>
+KP_HD bool sel_cluster_fast(const BLK& B, const SelCtx& x, const Cands& cd, uint32_t* hist, Item* items,
+                            uint64_t* keys, void* scratch, int cap) {
+  const BindHdr& h = *x.h;
+  const int F = cd.F;
+  if ((int64_t)F < h.cluster_min) {
+    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_CLUSTER_MIN_GROUPS, 0);
+    return true;
+  }
+  int64_t needCnt = (int64_t)F < h.cluster_max ? (int64_t)F : h.cluster_max;
+  if (needCnt < 0) needCnt = 0;
+  if (needCnt > kSmallMax || h.tgt_cnt > kTgtSmallMax) return false;
+  const int32_t need = h.need_replicas;
+  if (needCnt == 0) {
+    if (B.tid() == 0) {
+      if (need == -1) sink_error(x, KP_STATUS_ERROR, KP_ERR_NO_CLUSTERS, 0);
+      else sink_error(x, KP_STATUS_ERROR, KP_ERR_CLUSTER_RESOURCE, 0);
+    }
+    return true;
+  }
+  auto key = [&](int i) { return cand_key(x, cd, i, cd.v[i]); };
+  auto all = [&](int) { return true; };
+  uint64_t kth = radix_select(B, hist, F, all, key, needCnt);
+  // compact the selected keys
+  int n = 0;
+  for (int t0 = 0; t0 < F; t0 += B.nth()) {
+    int i = t0 + B.tid();
+    uint64_t k = 0;
+    bool e = false;
+    if (i < F) {
+      k = key(i);
+      e = k <= kth;
+    }
+    int32_t tot;
+    int32_t off = B.excl_scan(e ? 1 : 0, &tot);
+    if (e) keys[n + off] = k;
+    n += tot;
+  }
+  B.sync();
+  if (B.tid() == 0) {  // sorted order (sortClusters)
+    for (int i = 1; i < n; i++) {
+      uint64_t k0 = keys[i];
+      int j = i - 1;
+      while (j >= 0 && keys[j] > k0) {
+        keys[j + 1] = keys[j];
+        j--;
+      }
+      keys[j + 1] = k0;
+    }
+    for (int i = 0; i < n; i++) items[i] = item_from_key(x, keys[i]);
+  }
+  B.sync();
+  if (need != -1) {
+    int64_t tot = 0;
+    for (int i = 0; i < n; i++) tot += items[i].avail;
+    if (tot < (int64_t)need) {
+      // candidates for the swap step: the best rest clusters by (avail desc, position)
+      int64_t m2 = (int64_t)F - needCnt;
+      if (m2 > needCnt) m2 = needCnt;
+      int nr = 0;
+      Item* rest = items + kSmallMax;
+      uint64_t* rkeys = keys + kSmallMax;
+      if (m2 > 0) {
+        auto isrest = [&](int i) { return key(i) > kth; };
+        auto akey = [&](int i) { return avail_key(key(i)); };
+        uint64_t kth2 = radix_select(B, hist, F, isrest, akey, m2);
+        for (int t0 = 0; t0 < F; t0 += B.nth()) {
+          int i = t0 + B.tid();
+          uint64_t k = 0;
+          bool e = false;
+          if (i < F) {
+            k = key(i);
+            e = k > kth && avail_key(k) <= kth2;
+          }
+          int32_t tt;
+          int32_t off = B.excl_scan(e ? 1 : 0, &tt);
+          if (e) rkeys[nr + off] = k;
+          nr += tt;
+        }
+        B.sync();
+        // position in the rest slice = #{candidates with smaller key} - needCnt
+        for (int z = 0; z < nr; z++) {
+          uint64_t kz = rkeys[z];
+          int64_t c = 0;
+          for (int i = B.tid(); i < F; i += B.nth())
+            if (key(i) < kz) c++;
+          c = B.sum64(c);
+          if (B.tid() == 0) {
+            rest[z] = item_from_key(x, kz);
+            rest[z].pad = (int32_t)(c - needCnt);  // position
+          }
+        }
+        B.sync();
+      }
+      int ok = 1;
+      if (B.tid() == 0) {
+        // selectClustersByAvailableResource swap loop with explicit positions
+        for (int i = 0; i < n; i++) items[i].pad = -1;
+        int64_t upd = needCnt - 1;
+        auto check = [&]() {
+          int64_t s = 0;
+          for (int i = 0; i < n; i++) s += items[i].avail;
+          return s >= (int64_t)need;
+        };
+        while (!check() && upd >= 0) {
+          // GetClusterWithMaxAvailableResource: first (by position) maximum above the
+          // slot's AvailableReplicas
+          int64_t bv = items[upd].avail;
+          int best = -1;
+          for (int z = 0; z < nr; z++) {
+            if (rest[z].avail > bv) {
+              best = z;
+              bv = rest[z].avail;
+            } else if (best >= 0 && rest[z].avail == bv && rest[z].pad < rest[best].pad) {
+              best = z;
+            }
+          }
+          if (best < 0) {
+            upd--;
+            continue;
+          }
+          Item out = items[upd];
+          out.pad = rest[best].pad;  // the swapped-out cluster takes the taken slot's position
+          items[upd] = rest[best];
+          items[upd].pad = -1;
+          rest[best] = out;
+          upd--;
+        }
+        ok = check() ? 1 : 0;
+        if (!ok) sink_error(x, KP_STATUS_ERROR, KP_ERR_CLUSTER_RESOURCE, needCnt);
+      }
+      ok = B.bcast(ok);
+      if (!ok) return true;
+    }
+  }
+  assign_small(B, x, items, n, scratch, cap);
+  return true;
+}
+
+// ----------------------------------------------------------------------------
+// Region stage A: generateRegionInfo + calcGroupScore (group_clusters.go:156-351,
+// 418-457) for every region; out[r] = {count, score}.
+// ----------------------------------------------------------------------------
+struct RegionOut {
+  int32_t count;
+  int32_t pad;
+  int64_t score;
+};
+struct RegionLds {
+  int32_t* cnt;
+  int32_t* dvalid;
+  int32_t* wcnt;
+  int32_t* done;
+  int64_t* sumAvail;
+  int64_t* sumScore;
+  int64_t* dscore;
+  int64_t* wsum;
+  int64_t* wscore;
+  int64_t* amin;
+  unsigned long long* minkey;
+  unsigned long long* last;
+};
+KP_HD inline int64_t go_ceil_div_i64(int32_t a, int64_t b) {
+  double q = kp_ceil((double)a / (double)b);
+  if (q != q || q >= 9223372036854775808.0 || q < -9223372036854775808.0) return INT64_MIN;  // amd64 CVTTSD2SQ
+  return (int64_t)q;
+}
+template <class BLK>
+KP_HD void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L, RegionOut* out) {
+  const BindHdr& h = *x.h;
+  const int R = x.s->n_regions;
+  for (int r = B.tid(); r < R; r += B.nth()) {
+    L.cnt[r] = 0;
+    L.dvalid[r] = 0;
+    L.wcnt[r] = 0;
+    L.done[r] = 0;
+    L.sumAvail[r] = 0;
+    L.sumScore[r] = 0;
+    L.dscore[r] = 0;
+    L.wsum[r] = 0;
+    L.wscore[r] = 0;
+    L.amin[r] = 0;
+    L.last[r] = 0;
+  }
+  B.sync();
+  const bool dup = (h.flags & BF_GROUP_DUP) != 0;
+  for (int i = B.tid(); i < cd.F; i += B.nth()) {
+    uint32_t rk = c_rank(cd, i);
+    int r = x.s->region_idx[rk];
+    if (r < 0) continue;
+    uint64_t k = cand_key(x, cd, i, cd.v[i]);
+    int64_t av = key_avail(k), sc = key_score(k);
+    kp_atomic_add(&L.cnt[r], 1);
+    kp_atomic_add((unsigned long long*)&L.sumAvail[r], (unsigned long long)av);
+    kp_atomic_add((unsigned long long*)&L.sumScore[r], (unsigned long long)sc);
+    if (av < 0) kp_atomic_add((unsigned long long*)&L.amin[r], 1ull);  // negative count
+    if (dup && av >= (int64_t)h.replicas) {
+      kp_atomic_add(&L.dvalid[r], 1);
+      kp_atomic_add((unsigned long long*)&L.dscore[r], (unsigned long long)sc);
+    }
+  }
+  B.sync();
+  if (dup) {  // calcGroupScoreForDuplicate
+    for (int r = B.tid(); r < R; r += B.nth()) {
+      int64_t v = L.dvalid[r];
+      out[r].count = L.cnt[r];
+      out[r].score = v == 0 ? 0 : add64(mul64(v, 1000), L.dscore[r] / v);
+    }
+    B.sync();
+    return;
+  }
+  // calcGroupScore (divided): walk each region's clusters in sortClusters order
+  const int64_t target = go_ceil_div_i64(h.replicas, h.region_min);
+  int64_t m = h.cluster_min;  // clusterMinGroups (last cluster constraint)
+  if (m < h.region_min) m = h.region_min;
+  for (int r = B.tid(); r < R; r += B.nth()) {
+    bool monotone = L.amin[r] == 0;
+    if (L.cnt[r] == 0 || (monotone && L.sumAvail[r] < target)) L.done[r] = 1;  // never breaks: totals
+  }
+  B.sync();
+  for (;;) {
+    bool any = false;
+    for (int r = B.tid(); r < R; r += B.nth()) {
+      if (!L.done[r]) any = true;
+      L.minkey[r] = ~0ull;
+    }
+    if (!B.any(any)) break;
+    for (int i = B.tid(); i < cd.F; i += B.nth()) {
+      uint32_t rk = c_rank(cd, i);
+      int r = x.s->region_idx[rk];
+      if (r < 0 || L.done[r]) continue;
+      uint64_t k = cand_key(x, cd, i, cd.v[i]);
+      if (L.wcnt[r] > 0 && k <= L.last[r]) continue;
+      kp_atomic_min_u64(&L.minkey[r], k);
+    }
+    B.sync();
+    for (int r = B.tid(); r < R; r += B.nth()) {
+      if (L.done[r]) continue;
+      uint64_t k = L.minkey[r];
+      if (k == ~0ull) {
+        L.done[r] = 1;
+        continue;
+      }
+      L.last[r] = k;
+      L.wcnt[r]++;
+      L.wsum[r] = add64(L.wsum[r], key_avail(k));
+      L.wscore[r] = add64(L.wscore[r], key_score(k));
+      if ((int64_t)L.wcnt[r] >= m && L.wsum[r] >= target) L.done[r] = 2;
+    }
+    B.sync();
+  }
+  for (int r = B.tid(); r < R; r += B.nth()) {
+    out[r].count = L.cnt[r];
+    if (L.cnt[r] == 0) {
+      out[r].score = 0;
+      continue;
+    }
+    int64_t sa, ss, valid;
+    if (L.done[r] == 2) {
+      sa = L.wsum[r];
+      ss = L.wscore[r];
+      valid = L.wcnt[r];
+    } else {  // walked (or skipped) the whole region
+      sa = L.sumAvail[r];
+      ss = L.sumScore[r];
+      valid = L.cnt[r];
+    }
+    if (sa < target) out[r].score = add64(mul64(sa, 1000), ss / (int64_t)L.cnt[r]);
+    else out[r].score = add64(mul64(target, 1000), ss / valid);
+  }
+  B.sync();
+}
+
+// ----------------------------------------------------------------------------
+// Region stage B: selectBestClustersByRegion after the host group selection
+// (select_clusters_by_region.go:41-63). sel: selected region ids in path order.
+// ----------------------------------------------------------------------------
+template <class BLK>
+KP_HD void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_t* sel, int nsel, uint32_t* hist,
+                    unsigned long long* heads, int32_t* rsel, Item* items, uint64_t* keys, void* scratch, int cap) {
+  const BindHdr& h = *x.h;
+  const int R = x.s->n_regions;
+  for (int r = B.tid(); r < R; r += B.nth()) {
+    heads[r] = ~0ull;
+    rsel[r] = -1;
+  }
+  B.sync();
+  for (int j = B.tid(); j < nsel; j += B.nth()) rsel[sel[j]] = j;
+  B.sync();
+  int64_t total = 0;
+  for (int i = B.tid(); i < cd.F; i += B.nth()) {
+    int r = x.s->region_idx[c_rank(cd, i)];
+    if (r < 0 || rsel[r] < 0) continue;
+    total++;
+    kp_atomic_min_u64(&heads[r], cand_key(x, cd, i, cd.v[i]));
+  }
+  total = B.sum64(total);
+  int64_t needCnt = total < h.cluster_max ? total : h.cluster_max;
+  int64_t restCnt = needCnt - nsel;
+  if (restCnt > kSmallMax - nsel) {  // engine limit: selected list capacity
+    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, -1);
+    return;
+  }
+  int n = 0;
+  if (B.tid() == 0)
+    for (int j = 0; j < nsel; j++) items[n++] = item_from_key(x, heads[sel[j]]);
+  n = nsel;
+  B.sync();
+  if (restCnt > 0) {
+    auto incand = [&](int i) {
+      int r = x.s->region_idx[c_rank(cd, i)];
+      return r >= 0 && rsel[r] >= 0 && cand_key(x, cd, i, cd.v[i]) != heads[r];
+    };
+    auto key = [&](int i) { return cand_key(x, cd, i, cd.v[i]); };
+    uint64_t kth = radix_select(B, hist, cd.F, incand, key, restCnt);
+    int m = 0;
+    for (int t0 = 0; t0 < cd.F; t0 += B.nth()) {
+      int i = t0 + B.tid();
+      uint64_t k = 0;
+      bool e = false;
+      if (i < cd.F && incand(i)) {
+        k = key(i);
+        e = k <= kth;
+      }
+      int32_t tt;
+      int32_t off = B.excl_scan(e ? 1 : 0, &tt);
+      if (e) keys[m + off] = k;
+      m += tt;
+    }
+    B.sync();
+    if (B.tid() == 0) {
+      for (int i = 1; i < m; i++) {
+        uint64_t k0 = keys[i];
+        int j = i - 1;
+        while (j >= 0 && keys[j] > k0) {
+          keys[j + 1] = keys[j];
+          j--;
+        }
+        keys[j + 1] = k0;
+      }
+      for (int i = 0; i < m; i++) items[nsel + i] = item_from_key(x, keys[i]);
+    }
+    n = nsel + m;
+    B.sync();
+  }
+  assign_small(B, x, items, n, scratch, cap);
+}
+
+}  // namespace kp

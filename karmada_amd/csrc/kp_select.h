@@ -1,0 +1,663 @@
+// kp_select.h — per-binding select/assign bodies (one workgroup per binding).
+#pragma once
+#include "kp_algo.h"
+
+namespace kp {
+
+constexpr int kSmallMax = 256;   // selected-list capacity of the small (serial) path
+constexpr int kTgtSmallMax = 256;
+
+struct Item {
+  uint32_t rank;
+  int32_t alloc;   // AllocatableReplicas
+  int64_t avail;   // AvailableReplicas
+  int32_t ovf;
+  int32_t pad;
+};
+
+struct SerialScratch {
+  int cap;
+  Item* tier;                    // overflow tier list
+  uint32_t* en;  int64_t* ew;    // dispense input entries (name, weight)
+  uint32_t* pn;  int64_t* pv;    // parties (name, votes)
+  int32_t* ps;   int32_t* ph;    // seats, heap
+  uint32_t* an;  int32_t* ar;    // available list (TargetClustersList)
+  uint32_t* xn;  int32_t* xr;    // temp (resort, merge map names/values)
+  int32_t* xf;                   // merge map presence
+  uint32_t* tn;  int32_t* tr;    // one strategy call's result
+  uint32_t* sn;  int32_t* sr;    // scheduledClusters
+  uint32_t* rn;  int32_t* rr;    // final result
+  int32_t* pos;                  // optional rank-indexed scratch (all -1 between uses)
+};
+KP_HD inline size_t serial_scratch_bytes(int cap) {
+  return (size_t)cap * (sizeof(Item) + 2 * sizeof(int64_t) + 14 * sizeof(uint32_t)) + 256;
+}
+KP_HD inline SerialScratch serial_scratch_carve(void* mem, int cap) {
+  SerialScratch s;
+  s.cap = cap;
+  char* p = (char*)mem;
+  auto take = [&](size_t bytes) {
+    char* q = p;
+    p += (bytes + 15) & ~(size_t)15;
+    return q;
+  };
+  s.ew = (int64_t*)take((size_t)cap * 8);
+  s.pv = (int64_t*)take((size_t)cap * 8);
+  s.tier = (Item*)take((size_t)cap * sizeof(Item));
+  s.en = (uint32_t*)take((size_t)cap * 4);
+  s.pn = (uint32_t*)take((size_t)cap * 4);
+  s.ps = (int32_t*)take((size_t)cap * 4);
+  s.ph = (int32_t*)take((size_t)cap * 4);
+  s.an = (uint32_t*)take((size_t)cap * 4);
+  s.ar = (int32_t*)take((size_t)cap * 4);
+  s.xn = (uint32_t*)take((size_t)cap * 4);
+  s.xr = (int32_t*)take((size_t)cap * 4);
+  s.xf = (int32_t*)take((size_t)cap * 4);
+  s.tn = (uint32_t*)take((size_t)cap * 4);
+  s.tr = (int32_t*)take((size_t)cap * 4);
+  s.sn = (uint32_t*)take((size_t)cap * 4);
+  s.sr = (int32_t*)take((size_t)cap * 4);
+  s.rn = (uint32_t*)take((size_t)cap * 4);
+  s.rr = (int32_t*)take((size_t)cap * 4);
+  s.pos = nullptr;
+  return s;
+}
+
+struct SelCtx {
+  const SnapView* s;
+  const BatchView* bv;
+  const BindHdr* h;
+  int b;
+  const uint64_t* frow;
+  const int32_t* erow;
+  const uint32_t* tgt_bits;
+  Sink sink;
+};
+
+struct SerialOut {
+  int status = 0;
+  int err = 0;
+  int64_t arg = 0;
+  int n = 0;
+};
+
+// ----------------------------------------------------------------------------
+// Serial exact emulation (thread 0) of AssignReplicas over an explicit list.
+// ----------------------------------------------------------------------------
+struct SerialAssign {
+  const SelCtx& x;
+  SerialScratch& sc;
+  bool desc;
+
+  KP_HD int tgt_cnt() const { return x.h->tgt_cnt; }
+  KP_HD uint32_t tgt_rank(int j) const { return (uint32_t)x.bv->ipool[x.h->tgt_off + 2 * j]; }
+  KP_HD int32_t tgt_rep(int j) const { return x.bv->ipool[x.h->tgt_off + 2 * j + 1]; }
+
+  // Dispenser(num, nil, uid).AllocateByWeight over entries en/ew[0..ne)
+  // (binding.go:94-115, webstermethod.go:112-161); all parties with their seats
+  // (name order) into tn/tr; returns the count.
+  KP_HD int dispense(int32_t num, int ne) {
+    int64_t sum = 0;
+    for (int i = 0; i < ne; i++) sum = add64(sum, sc.ew[i]);
+    if (sum == 0) return 0;
+    int np = 0;
+    for (int i = 0; i < ne; i++) {  // partyVotes map: later entries overwrite
+      int k = -1;
+      if (sc.pos) {
+        k = sc.pos[sc.en[i]];
+      } else {
+        for (int j = 0; j < np; j++)
+          if (sc.pn[j] == sc.en[i]) {
+            k = j;
+            break;
+          }
+      }
+      if (k < 0) {
+        k = np++;
+        sc.pn[k] = sc.en[i];
+        if (sc.pos) sc.pos[sc.en[i]] = k;
+      }
+      sc.pv[k] = sc.ew[i];
+    }
+    if (sc.pos)
+      for (int k = 0; k < np; k++) sc.pos[sc.pn[k]] = -1;
+    // Parties keep list order: the heap compares names itself and the result is
+    // compared as a multiset, so the final sort by name is not materialised.
+    webster_serial(sc.pn, sc.pv, sc.ps, sc.ph, np, num, desc);
+    for (int i = 0; i < np; i++) {
+      sc.tn[i] = sc.pn[i];
+      sc.tr[i] = sc.ps[i];
+    }
+    return np;
+  }
+
+  // util.MergeTargetClusters (pkg/util/binding.go:91-115) of old=(sn,sr,ns)
+  // with new=(tn,tr,nt) into (tn,tr); returns the count.
+  KP_HD int merge(int ns, int nt) {
+    if (ns == 0) return nt;
+    if (nt == 0) {
+      for (int i = 0; i < ns; i++) {
+        sc.tn[i] = sc.sn[i];
+        sc.tr[i] = sc.sr[i];
+      }
+      return ns;
+    }
+    int nu = 0;  // oldMap, last value wins
+    for (int i = 0; i < ns; i++) {
+      int k = -1;
+      if (sc.pos) {
+        k = sc.pos[sc.sn[i]];
+      } else {
+        for (int j = 0; j < nu; j++)
+          if (sc.xn[j] == sc.sn[i]) k = j;
+      }
+      if (k < 0) {
+        k = nu++;
+        sc.xn[k] = sc.sn[i];
+        if (sc.pos) sc.pos[sc.sn[i]] = k;
+      }
+      sc.xr[k] = sc.sr[i];
+      sc.xf[k] = 1;
+    }
+    for (int i = 0; i < nt; i++) {
+      int k = -1;
+      if (sc.pos) {
+        k = sc.pos[sc.tn[i]];
+      } else {
+        for (int j = 0; j < nu; j++)
+          if (sc.xn[j] == sc.tn[i]) {
+            k = j;
+            break;
+          }
+      }
+      if (k >= 0 && sc.xf[k]) {
+        sc.tr[i] = add32(sc.tr[i], sc.xr[k]);
+        sc.xf[k] = 0;
+      }
+    }
+    for (int j = 0; j < nu; j++) {
+      if (sc.pos) sc.pos[sc.xn[j]] = -1;
+      if (sc.xf[j]) {
+        sc.tn[nt] = sc.xn[j];
+        sc.tr[nt] = sc.xr[j];
+        nt++;
+      }
+    }
+    return nt;
+  }
+
+  // dynamicDivideReplicas (division_algorithm.go:75-101); available list in
+  // an/ar[0..na); scheduled (for merge) in sn/sr[0..ns).
+  KP_HD bool divide(int na, int32_t target, int ns, int code, SerialOut& o, int* nt_out) {
+    int32_t availableReplicas = 0;
+    for (int i = 0; i < na; i++) availableReplicas = add32(availableReplicas, sc.ar[i]);
+    if (availableReplicas < target) {
+      o.status = KP_STATUS_UNSCHEDULABLE;
+      o.err = code;
+      o.arg = availableReplicas;
+      return false;
+    }
+    int st = x.h->strategy;
+    if (st == ST_AGGREGATED) {
+      // resortAvailableClusters (assignment.go:151-178): prior = scheduled with replicas > 0
+      bool anyPrior = false;
+      for (int j = 0; j < ns; j++)
+        if (sc.sr[j] > 0) anyPrior = true;
+      if (anyPrior) {
+        int k = 0;
+        if (sc.pos)
+          for (int j = 0; j < ns; j++)
+            if (sc.sr[j] > 0) sc.pos[sc.sn[j]] = 1;
+        for (int pass = 0; pass < 2; pass++)
+          for (int i = 0; i < na; i++) {
+            bool pr = false;
+            if (sc.pos) pr = sc.pos[sc.an[i]] == 1;
+            else
+              for (int j = 0; j < ns && !pr; j++) pr = sc.sr[j] > 0 && sc.sn[j] == sc.an[i];
+            if (pr == (pass == 0)) {
+              sc.xn[k] = sc.an[i];
+              sc.xr[k] = sc.ar[i];
+              k++;
+            }
+          }
+        for (int i = 0; i < na; i++) {
+          sc.an[i] = sc.xn[i];
+          sc.ar[i] = sc.xr[i];
+        }
+        if (sc.pos)
+          for (int j = 0; j < ns; j++) sc.pos[sc.sn[j]] = -1;
+      }
+      int32_t sum = 0;
+      for (int i = 0; i < na; i++) {
+        sum = add32(sum, sc.ar[i]);
+        if (sum >= target) {
+          na = i + 1;
+          break;
+        }
+      }
+    } else if (st != ST_DYNAMIC) {
+      o.status = KP_STATUS_ERROR;
+      o.err = KP_ERR_UNDEFINED_STRATEGY;
+      return false;
+    }
+    // SpreadReplicasByTargetClusters: weights = int64(Replicas) (binding.go:157-183)
+    for (int i = 0; i < na; i++) {
+      sc.en[i] = sc.an[i];
+      sc.ew[i] = (int64_t)sc.ar[i];
+    }
+    int nt = dispense(target, na);
+    *nt_out = merge(ns, nt);
+    return true;
+  }
+
+  // assignFuncMap strategies (assignment.go:181-244) over list[0..m) with `rep`
+  // replicas; result in tn/tr, count in *nt. Returns false on error.
+  KP_HD bool strategy(const Item* list, int m, int32_t rep, SerialOut& o, int* nt) {
+    const BindHdr& h = *x.h;
+    int st = h.strategy;
+    if (st == ST_NONE) {
+      o.status = KP_STATUS_ERROR;
+      o.err = KP_ERR_UNSUPPORTED_STRATEGY;
+      return false;
+    }
+    if (st == ST_DUPLICATED) {
+      for (int i = 0; i < m; i++) {
+        sc.tn[i] = list[i].rank;
+        sc.tr[i] = rep;
+      }
+      *nt = m;
+      return true;
+    }
+    if (st == ST_STATIC) {
+      // getStaticWeightInfoList (division_algorithm.go:38-72)
+      int ne = 0;
+      for (int i = 0; i < m; i++) {
+        int64_t w = 0;
+        if (!(h.flags & BF_HAS_WP)) {
+          w = 1;  // getDefaultWeightPreference: {ClusterNames:[name]} weight 1
+        } else {
+          for (int j = 0; j < h.sw_cnt; j++)
+            if (prog_match(*x.s, *x.bv, x.bv->ipool[h.sw_off + j], (int)list[i].rank)) {
+              int64_t rw = x.bv->lpool[h.sw_w_off + j];
+              if (rw > w) w = rw;
+            }
+        }
+        if (w > 0) {
+          sc.en[ne] = list[i].rank;
+          sc.ew[ne] = w;
+          ne++;
+        }
+      }
+      int64_t sum = 0;
+      for (int i = 0; i < ne; i++) sum = add64(sum, sc.ew[i]);
+      if (sum == 0)
+        for (int i = 0; i < m; i++) {
+          sc.en[ne] = list[i].rank;
+          sc.ew[ne] = 1;
+          ne++;
+        }
+      *nt = dispense(rep, ne);
+      return true;
+    }
+    // assignByDynamicStrategy
+    int ns = 0;
+    if (sc.pos)
+      for (int i = 0; i < m; i++) sc.pos[list[i].rank] = 1;
+    for (int j = 0; j < tgt_cnt(); j++) {  // buildScheduledClusters (assignment.go:125-142)
+      uint32_t r = tgt_rank(j);
+      bool cand = false;
+      if (sc.pos) cand = sc.pos[r] == 1;
+      else
+        for (int i = 0; i < m && !cand; i++) cand = list[i].rank == r;
+      if (cand) {
+        sc.sn[ns] = r;
+        sc.sr[ns] = tgt_rep(j);
+        ns++;
+      }
+    }
+    if (sc.pos)
+      for (int i = 0; i < m; i++) sc.pos[list[i].rank] = -1;
+    int32_t assigned = 0;
+    for (int j = 0; j < ns; j++) assigned = add32(assigned, sc.sr[j]);
+    if (h.flags & BF_FRESH) {  // dynamicFreshScale (division_algorithm.go:139-166)
+      for (int i = 0; i < m; i++) {
+        sc.an[i] = list[i].rank;
+        sc.ar[i] = list[i].alloc;
+      }
+      if (sc.pos) {
+        for (int i = m - 1; i >= 0; i--) sc.pos[sc.an[i]] = i;  // first occurrence
+        for (int j = 0; j < ns; j++) {
+          int i = sc.pos[sc.sn[j]];
+          if (i >= 0) sc.ar[i] = add32(sc.ar[i], sc.sr[j]);
+        }
+        for (int i = 0; i < m; i++) sc.pos[sc.an[i]] = -1;
+      } else {
+        for (int j = 0; j < ns; j++)
+          for (int i = 0; i < m; i++)
+            if (sc.an[i] == sc.sn[j]) {
+              sc.ar[i] = add32(sc.ar[i], sc.sr[j]);
+              break;
+            }
+      }
+      sort_tcl(sc.an, sc.ar, m);
+      return divide(m, rep, 0, KP_ERR_FRESH_NOT_ENOUGH, o, nt);
+    }
+    if (assigned > rep) {  // dynamicScaleDown (:103-119)
+      for (int j = 0; j < ns; j++) {
+        sc.an[j] = sc.sn[j];
+        sc.ar[j] = sc.sr[j];
+      }
+      sort_tcl(sc.an, sc.ar, ns);
+      return divide(ns, rep, 0, KP_ERR_SCALE_DOWN_NOT_ENOUGH, o, nt);
+    }
+    if (assigned < rep) {  // dynamicScaleUp (:121-136)
+      for (int i = 0; i < m; i++) {
+        sc.an[i] = list[i].rank;
+        sc.ar[i] = list[i].alloc;
+      }
+      sort_tcl(sc.an, sc.ar, m);
+      return divide(m, sub32(rep, assigned), ns, KP_ERR_SCALE_UP_NOT_ENOUGH, o, nt);
+    }
+    for (int j = 0; j < ns; j++) {
+      sc.tn[j] = sc.sn[j];
+      sc.tr[j] = sc.sr[j];
+    }
+    *nt = ns;
+    return true;
+  }
+
+  // assignReplicasToClusters (common.go:141-154): strategy + removeZeroReplicasCluster,
+  // appended to rn/rr at o.n.
+  KP_HD bool to_clusters(const Item* list, int m, int32_t rep, SerialOut& o) {
+    int nt = 0;
+    if (!strategy(list, m, rep, o, &nt)) return false;
+    for (int i = 0; i < nt; i++)
+      if (sc.tr[i] > 0) {
+        sc.rn[o.n] = sc.tn[i];
+        sc.rr[o.n] = sc.tr[i];
+        o.n++;
+      }
+    return true;
+  }
+
+  // AssignReplicas (common.go:51-83) + assignWorkloadReplicas (:97-139) +
+  // attachZeroReplicasCluster (util.go:174-186).
+  KP_HD SerialOut run(const Item* items, int n) {
+    SerialOut o;
+    const BindHdr& h = *x.h;
+    if (n == 0) {
+      o.status = KP_STATUS_ERROR;
+      o.err = KP_ERR_NO_CLUSTERS;
+      return o;
+    }
+    if (!(h.flags & BF_WORKLOAD_ASSIGN)) {
+      for (int i = 0; i < n; i++) {
+        sc.rn[i] = items[i].rank;
+        sc.rr[i] = 0;
+      }
+      o.n = n;
+    } else if (h.flags & BF_OVERFLOW) {
+      int maxOrder = 0;
+      for (int i = 0; i < n; i++)
+        if (items[i].ovf > maxOrder) maxOrder = items[i].ovf;
+      int32_t remaining = h.replicas;
+      for (int t = 0; t <= maxOrder; t++) {
+        int m = 0;
+        int64_t tierAvail = 0;
+        for (int i = 0; i < n; i++)
+          if (items[i].ovf == t) {
+            sc.tier[m++] = items[i];
+            tierAvail += items[i].avail;
+          }
+        if (m == 0) continue;
+        int32_t rep_t = (int32_t)((int64_t)remaining < tierAvail ? (int64_t)remaining : tierAvail);
+        if (!to_clusters(sc.tier, m, rep_t, o)) {
+          o.n = 0;
+          return o;
+        }
+        remaining = sub32(remaining, rep_t);
+        if (remaining <= 0) break;
+      }
+      if (remaining > 0) {
+        o.status = KP_STATUS_UNSCHEDULABLE;
+        o.err = KP_ERR_OVERFLOW_NOT_ENOUGH;
+        o.n = 0;
+        return o;
+      }
+    } else {
+      if (!to_clusters(items, n, h.replicas, o)) {
+        o.n = 0;
+        return o;
+      }
+    }
+    if (h.flags & BF_EMPTY_PROP) {
+      int base = o.n;
+      if (sc.pos)
+        for (int j = 0; j < base; j++) sc.pos[sc.rn[j]] = 1;
+      for (int i = 0; i < n; i++) {
+        bool have = false;
+        if (sc.pos) have = sc.pos[items[i].rank] == 1;
+        else
+          for (int j = 0; j < base && !have; j++) have = sc.rn[j] == items[i].rank;
+        if (!have) {
+          sc.rn[o.n] = items[i].rank;
+          sc.rr[o.n] = 0;
+          o.n++;
+        }
+      }
+      if (sc.pos)
+        for (int j = 0; j < base; j++) sc.pos[sc.rn[j]] = -1;
+    }
+    return o;
+  }
+};
+
+// Writes a serial result (thread 0 only).
+KP_HD inline void sink_serial(const SelCtx& x, const SerialScratch& sc, const SerialOut& o) {
+  const Sink& k = x.sink;
+  int b = x.b;
+  k.status[b] = o.status;
+  k.err[b] = o.err;
+  k.arg[b] = o.arg;
+  if (o.status != KP_STATUS_OK || o.n == 0) {
+    k.start[b] = 0;
+    k.count[b] = 0;
+    return;
+  }
+  unsigned long long base = kp_atomic_add(k.counter, (unsigned long long)o.n);
+  k.start[b] = base;
+  k.count[b] = (uint32_t)o.n;
+  for (int i = 0; i < o.n; i++) {
+    k.out_idx[base + i] = x.s->perm[sc.rn[i]];
+    k.out_rep[base + i] = sc.rr[i];
+  }
+}
+KP_HD inline void sink_error(const SelCtx& x, int status, int err, int64_t arg) {
+  const Sink& k = x.sink;
+  k.status[x.b] = status;
+  k.err[x.b] = err;
+  k.arg[x.b] = arg;
+  k.start[x.b] = 0;
+  k.count[x.b] = 0;
+}
+
+// ----------------------------------------------------------------------------
+// Candidate gather: feasible clusters of the binding in rank order.
+// ----------------------------------------------------------------------------
+template <class BLK>
+KP_HD int gather(const BLK& B, const SelCtx& x, Cands cd, bool weights) {
+  const SnapView& s = *x.s;
+  const BindHdr& h = *x.h;
+  int F = 0;
+  for (int w0 = 0; w0 < s.W; w0 += B.nth()) {
+    int w = w0 + B.tid();
+    uint64_t m = w < s.W ? x.frow[w] : 0ull;
+    int32_t tot;
+    int32_t off = B.excl_scan(popc64(m), &tot);
+    int pos = F + off;
+    while (m) {
+      int bit = ctz64(m);
+      m &= m - 1;
+      int c = w * 64 + bit;
+      uint32_t ovf = (uint32_t)overflow_order(s, *x.bv, h, c);
+      cd.r[pos] = (uint32_t)c | (ovf << kRankBits);
+      int32_t v = x.erow[c];
+      if (weights) {  // StaticWeight votes: max matching rule weight (division_algorithm.go:41-48)
+        int64_t wt = 0;
+        if (!(h.flags & BF_HAS_WP)) {
+          wt = 1;
+        } else {
+          for (int j = 0; j < h.sw_cnt; j++)
+            if (prog_match(s, *x.bv, x.bv->ipool[h.sw_off + j], c)) {
+              int64_t rw = x.bv->lpool[h.sw_w_off + j];
+              if (rw > wt) wt = rw;
+            }
+        }
+        v = (int32_t)(wt > kInt32Max ? kInt32Max : wt);
+      }
+      cd.v[pos] = v;
+      pos++;
+    }
+    F += tot;
+  }
+  B.sync();
+  return F;
+}
+
+// ----------------------------------------------------------------------------
+// Block-parallel exact Webster over a candidate subset with int32 votes >= 0.
+// ----------------------------------------------------------------------------
+struct WebRes {
+  int mode;       // 0 no parties, 1 all zero seats, 2 normal
+  double t;       // t*
+  uint64_t tie;   // tie-key threshold (inclusive)
+  int32_t N;
+  bool desc;
+};
+KP_HD inline uint64_t tie_key(int64_t base, uint32_t rank, bool desc) {
+  return ((uint64_t)base << kRankBits) | (desc ? (uint64_t)(kRankMask - rank) : (uint64_t)rank);
+}
+KP_HD inline int32_t web_seats(const WebRes& w, int64_t v, uint32_t rank) {
+  if (w.mode != 2) return 0;
+  int64_t base = w_count(v, w.t, (int64_t)w.N + 1, false);
+  if (base < w.N && w_prio(v, base) == w.t && tie_key(base, rank, w.desc) <= w.tie) base++;
+  return (int32_t)base;
+}
+
+template <class BLK, class Pred, class Vote>
+KP_HD WebRes webster_par(const BLK& B, const Cands& cd, Pred party, Vote vote, int32_t N, bool desc) {
+  WebRes r;
+  r.N = N;
+  r.desc = desc;
+  r.t = 0;
+  r.tie = 0;
+  int64_t V = 0, vmax = 0;
+  for (int i = B.tid(); i < cd.F; i += B.nth())
+    if (party(i)) {
+      int64_t v = vote(i);
+      V += v;
+      if (v > vmax) vmax = v;
+    }
+  V = B.sum64(V);
+  vmax = B.max64(vmax);
+  if (V == 0) {
+    r.mode = 0;
+    return r;
+  }
+  if (N <= 0) {
+    r.mode = 1;
+    return r;
+  }
+  r.mode = 2;
+  auto cnt_ge = [&](double t) {
+    int64_t c = 0;
+    for (int i = B.tid(); i < cd.F; i += B.nth())
+      if (party(i)) c += w_count(vote(i), t, (int64_t)N, true);
+    return B.sum64(c);
+  };
+  double tmax = (double)vmax;
+  double tstar;
+  if (cnt_ge(tmax) >= N) {
+    tstar = tmax;
+  } else {
+    uint64_t lo = 1, hi = dbits(tmax);  // cnt_ge(lo) >= N, cnt_ge(hi) < N
+    while (hi - lo > 1) {
+      uint64_t mid = lo + (hi - lo) / 2;
+      if (cnt_ge(bitsd(mid)) >= N) lo = mid;
+      else hi = mid;
+    }
+    tstar = bitsd(lo);
+  }
+  r.t = tstar;
+  // seats strictly above t*, then the tie group at t* ordered by (k asc, name)
+  int64_t S = 0, T = 0;
+  for (int i = B.tid(); i < cd.F; i += B.nth())
+    if (party(i)) {
+      int64_t v = vote(i);
+      int64_t base = w_count(v, tstar, (int64_t)N + 1, false);
+      S += base;
+      if (w_prio(v, base) == tstar) T++;
+    }
+  S = B.sum64(S);
+  T = B.sum64(T);
+  int64_t M = (int64_t)N - S;
+  if (M >= T) {
+    r.tie = ~0ull;
+  } else {
+    uint64_t lo = 0, hi = (uint64_t)1 << 62;  // smallest x with count(tk <= x) >= M
+    while (lo < hi) {
+      uint64_t mid = lo + (hi - lo) / 2;
+      int64_t c = 0;
+      for (int i = B.tid(); i < cd.F; i += B.nth())
+        if (party(i)) {
+          int64_t v = vote(i);
+          int64_t base = w_count(v, tstar, (int64_t)N + 1, false);
+          if (w_prio(v, base) == tstar && tie_key(base, c_rank(cd, i), desc) <= mid) c++;
+        }
+      c = B.sum64(c);
+      if (c >= M) hi = mid;
+      else lo = mid + 1;
+    }
+    r.tie = lo;
+  }
+  return r;
+}
+
+// ----------------------------------------------------------------------------
+// k-th smallest (1-based) 64-bit key over a predicate set: 8-bit radix select.
+// ----------------------------------------------------------------------------
+template <class BLK, class Pred, class Key>
+KP_HD uint64_t radix_select(const BLK& B, uint32_t* hist, int F, Pred pred, Key key, int64_t k) {
+  uint64_t prefix = 0;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int i = B.tid(); i < 256; i += B.nth()) hist[i] = 0;
+    B.sync();
+    uint64_t hm = shift == 56 ? 0ull : (~0ull << (shift + 8));
+    for (int i = B.tid(); i < F; i += B.nth())
+      if (pred(i)) {
+        uint64_t kk = key(i);
+        if ((kk & hm) == (prefix & hm)) kp_atomic_add(&hist[(kk >> shift) & 255], 1u);
+      }
+    B.sync();
+    int64_t sel = 0, kk2 = k;
+    if (B.tid() == 0) {
+      int64_t cum = 0;
+      int bin = 255;
+      for (int i = 0; i < 256; i++) {
+        if (cum + hist[i] >= k) {
+          bin = i;
+          break;
+        }
+        cum += hist[i];
+      }
+      sel = bin;
+      kk2 = k - cum;
+    }
+    sel = B.bcast(sel);
+    k = B.bcast(kk2);
+    prefix |= (uint64_t)sel << shift;
+  }
+  return prefix;
+}
+
+}  // namespace kp
