@@ -1,0 +1,192 @@
+"""Benchmark: ResourceBindings scheduled/sec through the HIP placement engine.
+
+Workload (BASELINE.json metric config, configs[2]): 100k bindings x 5k clusters,
+GeneralEstimator with 8 resource-model grades, 50% DynamicWeight / 50%
+Aggregated (synthetic universe of SURVEY.md §8(d), seed 3). A step = one
+kp_schedule_batch over the whole batch: filter -> score -> estimate -> select ->
+divide, results copied back to the host as CSR. Packed inputs are resident in
+HBM before the timed region (snapshot and binding packing are reported
+separately). Multi-GPU: one process per GPU, each schedules its own contiguous
+binding range of the universe against its own snapshot replica (weak scaling,
+no data-path collective).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+# SURVEY.md §8(d) streamed-row model, config 3: B_row = 140 filter + 52 summary + 192 grades
+B_ROW = {2: 184, 3: 384, 4: 192, 5: 384, 6: 384, 1: 184}
+B_BIND = 256
+
+
+def pair_bytes_per_binding(config, n_clusters):
+    """Algorithmic bytes of the pair kernel per binding: B_bind + C*B_row + C/8 + 4*C."""
+    C = n_clusters
+    return B_BIND + C * B_ROW[config] + C / 8.0 + 4.0 * C
+
+
+def cpu_baseline(u, opts, budget_s):
+    """Oracle (faithful C++ restatement, REFSHAPE mode) on a bounded sample, rank 0 only."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    threads = int(os.environ.get("KP_CPU_THREADS", "16"))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    out = {}
+    for th, share in ((1, 0.35), (threads, 0.65)):
+        n, done, t_used = 16, 0, 0.0
+        while True:
+            n = min(n, u.n_bindings)
+            ba, _ = u.binding_slice(0, n)
+            t0 = time.perf_counter()
+            O.schedule_c(u.clusters, u.n_clusters, ba, n, opts, O.REFSHAPE, th)
+            dt = time.perf_counter() - t0
+            done, t_used = n, dt
+            if dt >= budget_s * share / 3 or n >= u.n_bindings:
+                break
+            n *= 2
+        out[th] = (done / t_used, done, t_used)
+    rate, n, dt = out[threads]
+    r1, n1, dt1 = out[1]
+    return {
+        "value": round(rate, 2), "unit": "ResourceBindings/s", "cores": threads, "kind": "port",
+        "sample": (f"{n} bindings of the same workload in {dt:.1f}s on {threads} threads "
+                   f"(1 thread: {r1:.2f}/s over {n1} bindings in {dt1:.1f}s); oracle REFSHAPE mode = "
+                   "faithful restatement with per-binding snapshot deep copy, FF loop replaced by its "
+                   "closed form (the literal FF loop is intractable here), so a lower bound on the "
+                   "reference's cost"),
+        "single_thread_value": round(r1, 3),
+    }
+
+
+def load_traffic(config):
+    """Per-launch HBM bytes of the pair kernel from the committed PMC profile, if any."""
+    p = os.path.join(ROOT, "profiles", f"traffic_config{config}.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("k_pair_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--clusters", type=int, default=None)
+    ap.add_argument("--bindings", type=int, default=None, help="bindings per GPU")
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    from karmada_amd import api, synth
+    from karmada_amd.engine import Batch, Engine, Snapshot
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+
+    cfg = args.config
+    C_def, B_def = synth.CONFIGS[cfg]
+    C_ = args.clusters or C_def
+    B = args.bindings or B_def
+    seed = args.seed if args.seed is not None else cfg
+    lo, hi = rank * B, (rank + 1) * B
+
+    t0 = time.perf_counter()
+    u = synth.Universe(cfg, seed, C_, lo, hi)
+    gen_s = time.perf_counter() - t0
+    opts = api.options()
+    eng = Engine(local)
+    t0 = time.perf_counter()
+    snap = Snapshot.from_structs(eng, u.clusters, u.n_clusters, u.names, opts)
+    snap_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    batch = Batch(snap, structs=u.binding_slice(0, u.n_bindings))
+    pack_s = time.perf_counter() - t0
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        batch.schedule_raw()
+    barrier_sync()
+    pair_ms, sel_ms, host_ms = [], [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = batch.schedule_raw()
+        st = eng.stage_times()
+        pair_ms.append(st["pair_kernel_ms"])
+        sel_ms.append(st["select_kernel_ms"])
+        host_ms.append(st["host_ms"])
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    n_ok = sum(1 for i in range(r.n_bindings) if r.status[i] == 0)
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = (B * world) / (elapsed / args.steps)
+    avg_pair_ms = sum(pair_ms) / len(pair_ms)
+    achieved = pair_bytes_per_binding(cfg, C_) * B / (avg_pair_ms * 1e-3) / 1e9
+    traffic = load_traffic(cfg)
+    line = {
+        "metric": "ResourceBindings scheduled/sec at 100k bindings x 5k clusters",
+        "value": round(value, 1),
+        "unit": "ResourceBindings/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic",
+        "config": {"workload": f"config{cfg}: {B} bindings/GPU x {C_} clusters, seed {seed}, "
+                               "resource-model grades, DynamicWeight/Aggregated" if cfg == 3 else
+                   f"config{cfg}: {B} bindings/GPU x {C_} clusters, seed {seed}",
+                   "bindings_per_gpu": B, "clusters": C_, "parallelism": f"binding-shard x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "k_pair", "kernel_ms": round(avg_pair_ms, 4)},
+        "stages_ms": {"pair_kernel": round(avg_pair_ms, 3), "select_kernels": round(sum(sel_ms) / len(sel_ms), 3),
+                      "host_region": round(sum(host_ms) / len(host_ms), 3)},
+        "setup_s": {"generate": round(gen_s, 2), "snapshot_pack_upload": round(snap_s, 3),
+                    "binding_pack_upload": round(pack_s, 3)},
+        "scheduled_ok": n_ok,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(u, opts, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    batch.close()
+    snap.close()
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,260 @@
+"""Host-side mirror of the reference scheduling interface over libkp.so.
+
+The product path: Python objects -> kp_api.h structs (api.World) -> libkp.so
+(C-ABI, HIP kernels on gfx950). There is no CPU fallback: if libkp.so is
+missing or no GPU is visible, construction raises.
+
+Mirrors (reference file:line):
+  GenericScheduler.schedule  <- genericScheduler.Schedule
+                                 (pkg/scheduler/core/generic_scheduler.go:70-121)
+  GenericScheduler.filter    <- findClustersThatFit (generic_scheduler.go:123-150)
+  GenericScheduler.score     <- prioritizeClusters (generic_scheduler.go:152-181)
+  GenericScheduler.max_available_replicas
+                             <- estimator.ReplicaEstimator.MaxAvailableReplicas
+                                 (pkg/estimator/client/interface.go:34-37) via
+                                 calAvailableReplicas (core/util.go:56-118)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+from karmada_amd import api
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libkp.so")
+KP_ABI_VERSION = 1
+
+_LIB = None
+
+# C-ABI entry points declared in include/kp/kp_api.h
+EXPORTS = (
+    "kp_abi_version", "kp_engine_create", "kp_engine_destroy", "kp_last_error", "kp_snapshot_create",
+    "kp_snapshot_destroy", "kp_snapshot_export", "kp_snapshot_import", "kp_batch_create", "kp_batch_destroy",
+    "kp_schedule_batch", "kp_filter_batch", "kp_score_batch", "kp_max_available_replicas", "kp_last_stage_times",
+)
+
+KP_OK, KP_EINVAL, KP_ENOMEM, KP_EDEVICE, KP_ENOTSUP, KP_ESTATE = 0, -1, -2, -3, -4, -5
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH):
+    """Loads libkp.so and declares the C-ABI signatures. Raises if it is absent."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise EngineError(f"{path} is missing: build it with `make -C karmada_amd/csrc` "
+                          "(there is no CPU fallback)")
+    L = C.CDLL(path)
+    vp = C.c_void_p
+    L.kp_abi_version.restype = C.c_int
+    L.kp_engine_create.argtypes = [C.c_int, C.POINTER(vp)]
+    L.kp_engine_destroy.argtypes = [vp]
+    L.kp_last_error.restype = C.c_char_p
+    L.kp_last_error.argtypes = [vp]
+    L.kp_snapshot_create.argtypes = [vp, C.POINTER(api.kp_cluster), C.c_uint64, C.POINTER(api.kp_options),
+                                     C.POINTER(vp)]
+    L.kp_snapshot_destroy.argtypes = [vp]
+    L.kp_batch_create.argtypes = [vp, vp, C.POINTER(api.kp_binding), C.c_uint64, C.POINTER(vp)]
+    L.kp_batch_destroy.argtypes = [vp]
+    L.kp_schedule_batch.argtypes = [vp, vp, C.POINTER(api.kp_results)]
+    L.kp_filter_batch.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
+    L.kp_score_batch.argtypes = [vp, vp, C.POINTER(C.c_int64)]
+    L.kp_max_available_replicas.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint32), C.c_uint64,
+                                            C.POINTER(C.c_int32)]
+    L.kp_last_stage_times.argtypes = [vp, C.POINTER(api.kp_stage_times)]
+    if L.kp_abi_version() != KP_ABI_VERSION:
+        raise EngineError("libkp.so ABI version mismatch")
+    _LIB = L
+    return L
+
+
+@dataclass
+class TargetCluster:
+    """workv1alpha2.TargetCluster (pkg/apis/work/v1alpha2/binding_types.go)."""
+    name: str
+    replicas: int
+
+
+@dataclass
+class ScheduleResult:
+    """core.ScheduleResult (generic_scheduler.go:54-56) plus the error the reference returns."""
+    suggested_clusters: List[TargetCluster] = field(default_factory=list)
+    status: int = api.STATUS_OK
+    err: int = 0
+    arg: int = 0
+
+    @property
+    def error(self) -> Optional[str]:
+        if self.status == api.STATUS_OK:
+            return None
+        return f"{api.ERR_NAMES.get(self.err, self.err)} ({self.arg})"
+
+
+class Engine:
+    """One HIP device + stream (kp_engine)."""
+
+    def __init__(self, device: int = 0):
+        self.L = load_library()
+        h = C.c_void_p()
+        rc = self.L.kp_engine_create(device, C.byref(h))
+        if rc != KP_OK:
+            raise EngineError(f"kp_engine_create(device={device}) failed: rc={rc}")
+        self.h = h
+
+    def _check(self, rc: int, what: str):
+        if rc != KP_OK:
+            raise EngineError(f"{what}: rc={rc}: {self.L.kp_last_error(self.h).decode(errors='replace')}")
+
+    def close(self):
+        if self.h:
+            self.L.kp_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stage_times(self) -> Dict[str, float]:
+        t = api.kp_stage_times()
+        self._check(self.L.kp_last_stage_times(self.h, C.byref(t)), "kp_last_stage_times")
+        return {k: getattr(t, k) for k, _ in api.kp_stage_times._fields_}
+
+
+class Snapshot:
+    """cache.Snapshot (pkg/scheduler/cache/snapshot.go) packed into HBM."""
+
+    def __init__(self, engine: Engine, clusters: Sequence[dict], opts: Optional[api.kp_options] = None):
+        self.engine = engine
+        self.names = [c["name"] for c in clusters]
+        w = api.World()
+        ca, n = w.clusters(clusters)
+        self.opts = opts or api.options()
+        h = C.c_void_p()
+        engine._check(engine.L.kp_snapshot_create(engine.h, ca, n, C.byref(self.opts), C.byref(h)),
+                      "kp_snapshot_create")
+        self.h = h
+
+    @classmethod
+    def from_structs(cls, engine: Engine, ca, n: int, names: List[str], opts: api.kp_options):
+        self = cls.__new__(cls)
+        self.engine, self.names, self.opts = engine, names, opts
+        h = C.c_void_p()
+        engine._check(engine.L.kp_snapshot_create(engine.h, ca, n, C.byref(opts), C.byref(h)), "kp_snapshot_create")
+        self.h = h
+        return self
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.engine.L.kp_snapshot_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Batch:
+    """A batch of ResourceBindings packed against one snapshot (kp_batch)."""
+
+    def __init__(self, snap: Snapshot, bindings: Sequence[dict] = (), structs=None):
+        self.snap = snap
+        eng = snap.engine
+        if structs is None:
+            w = api.World()
+            ba, n = w.bindings(bindings)
+            self._w = w
+        else:
+            ba, n = structs
+        self.n = n
+        h = C.c_void_p()
+        eng._check(eng.L.kp_batch_create(eng.h, snap.h, ba, n, C.byref(h)), "kp_batch_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.snap.engine.L.kp_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def schedule_raw(self) -> api.kp_results:
+        r = api.kp_results()
+        eng = self.snap.engine
+        eng._check(eng.L.kp_schedule_batch(eng.h, self.h, C.byref(r)), "kp_schedule_batch")
+        return r
+
+    def schedule(self) -> List[dict]:
+        """Results as api.results_to_python dicts (cluster indices in snapshot input order)."""
+        r = self.schedule_raw()
+        return api.results_to_python(r.status, r.err_code, r.err_arg, r.offsets, r.cluster_idx, r.replicas,
+                                     r.n_bindings)
+
+
+class GenericScheduler:
+    """genericScheduler (generic_scheduler.go:38-121) over a snapshot, batched."""
+
+    def __init__(self, engine: Engine, clusters: Sequence[dict], opts: Optional[api.kp_options] = None):
+        self.snapshot = Snapshot(engine, clusters, opts)
+
+    def schedule(self, bindings: Sequence[dict]) -> List[ScheduleResult]:
+        b = Batch(self.snapshot, bindings)
+        out = []
+        names = self.snapshot.names
+        for r in b.schedule():
+            sr = ScheduleResult(status=r["status"], err=r["err"], arg=r["arg"])
+            sr.suggested_clusters = [TargetCluster(names[i], rep) for i, rep in r["targets"]]
+            out.append(sr)
+        b.close()
+        return out
+
+    def filter(self, bindings: Sequence[dict]) -> List[List[str]]:
+        """Feasible cluster names per binding (findClustersThatFit)."""
+        b = Batch(self.snapshot, bindings)
+        eng = self.snapshot.engine
+        C_ = len(self.snapshot.names)
+        W = (C_ + 63) // 64
+        m = (C.c_uint64 * max(1, b.n * W))()
+        eng._check(eng.L.kp_filter_batch(eng.h, b.h, m), "kp_filter_batch")
+        out = []
+        for i in range(b.n):
+            out.append([self.snapshot.names[c] for c in range(C_) if (m[i * W + (c >> 6)] >> (c & 63)) & 1])
+        b.close()
+        return out
+
+    def score(self, bindings: Sequence[dict]) -> List[List[int]]:
+        """Summed plugin scores per (binding, cluster) (prioritizeClusters)."""
+        b = Batch(self.snapshot, bindings)
+        eng = self.snapshot.engine
+        C_ = len(self.snapshot.names)
+        s = (C.c_int64 * max(1, b.n * C_))()
+        eng._check(eng.L.kp_score_batch(eng.h, b.h, s), "kp_score_batch")
+        out = [[int(s[i * C_ + c]) for c in range(C_)] for i in range(b.n)]
+        b.close()
+        return out
+
+    def max_available_replicas(self, binding: dict, clusters: Sequence[str]) -> List[int]:
+        """GeneralEstimator.MaxAvailableReplicas for one binding's request."""
+        b = Batch(self.snapshot, [binding])
+        eng = self.snapshot.engine
+        idx = {n: i for i, n in enumerate(self.snapshot.names)}
+        ci = (C.c_uint32 * max(1, len(clusters)))(*[idx[n] for n in clusters])
+        out = (C.c_int32 * max(1, len(clusters)))()
+        eng._check(eng.L.kp_max_available_replicas(eng.h, b.h, 0, ci, len(clusters), out),
+                   "kp_max_available_replicas")
+        b.close()
+        return [int(out[i]) for i in range(len(clusters))]

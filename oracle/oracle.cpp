@@ -1979,7 +1979,7 @@ ScheduleOut Schedule(const World& w, const Binding& b, int mode) {
   // g.schedulerCache.Snapshot(): List + DeepCopy of every cluster (cache.go:124-139)
   vector<Cluster> deep;
   const vector<Cluster>* snap = &w.clusters;
-  if (mode == KPO_FAITHFUL) {
+  if (mode != KPO_FAST) {
     deep = w.clusters;
     snap = &deep;
   }

@@ -20,6 +20,9 @@
  *                  (webstermethod.go:112-161), Go pdqsort emulation.
  *   KPO_FAST     — same results; no per-call deep copy and the closed-form grade
  *                  walk instead of the FF loop.
+ *   KPO_REFSHAPE — KPO_FAITHFUL except the FF loop, which is replaced by its
+ *                  closed form: the CPU baseline where the FF loop is
+ *                  intractable (config 3), a lower bound on the reference's cost.
  */
 #ifndef KPO_ORACLE_H
 #define KPO_ORACLE_H
@@ -32,7 +35,7 @@
 extern "C" {
 #endif
 
-enum { KPO_FAITHFUL = 0, KPO_FAST = 1 };
+enum { KPO_FAITHFUL = 0, KPO_FAST = 1, KPO_REFSHAPE = 2 };
 
 typedef struct kpo_world kpo_world;
 

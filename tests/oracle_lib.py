@@ -69,7 +69,7 @@ def lib():
     return L
 
 
-FAITHFUL, FAST = 0, 1
+FAITHFUL, FAST, REFSHAPE = 0, 1, 2
 
 
 def schedule(clusters, bindings, opts=None, mode=FAITHFUL, threads=1):

@@ -1,0 +1,153 @@
+"""GPU parity: libkp.so (HIP, gfx950) against the CPU oracle on seeded universes.
+
+Bit-exact bar: status, error code and argument, and the multiset of
+(cluster, replicas) targets per binding (IsScheduleResultEqual semantics:
+reference pkg/scheduler/core/generic_scheduler_test.go compares sorted
+TargetClusters). The oracle's fast mode is itself pinned to its faithful mode
+in tests/test_oracle_synth.py and to the reference golden vectors in
+tests/test_oracle_golden.py.
+"""
+import ctypes as C
+
+import pytest
+
+from karmada_amd import api, synth
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from karmada_amd.engine import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def gpu_schedule(engine, u, opts, lo=0, hi=None):
+    from karmada_amd.engine import Batch, Snapshot
+    hi = u.n_bindings if hi is None else hi
+    snap = Snapshot.from_structs(engine, u.clusters, u.n_clusters, u.names, opts)
+    b = Batch(snap, structs=u.binding_slice(lo, hi))
+    out = b.schedule()
+    b.close()
+    snap.close()
+    return out
+
+
+def oracle_schedule(u, opts, lo=0, hi=None):
+    hi = u.n_bindings if hi is None else hi
+    ba, n = u.binding_slice(lo, hi)
+    return O.schedule_c(u.clusters, u.n_clusters, ba, n, opts, O.FAST, 8)
+
+
+def compare(got, want, label):
+    assert len(got) == len(want)
+    bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    if bad:
+        lines = [f"{label}: {len(bad)}/{len(want)} bindings differ"]
+        for i in bad[:5]:
+            lines.append(f"  binding {i}: gpu={got[i]}")
+            lines.append(f"  binding {i}: ref={want[i]}")
+        pytest.fail("\n".join(lines))
+
+
+CASES = [
+    # (config, seed, clusters, bindings)
+    (1, 1, 10, 1000),
+    (2, 2, 1000, 2000),
+    (3, 3, 500, 1000),
+    (4, 4, 1000, 2000),
+    (6, 6, 300, 3000),
+    (6, 7, 64, 3000),
+    (6, 8, 1, 500),
+    (6, 9, 700, 2000),
+]
+
+
+@pytest.mark.parametrize("config,seed,n_clusters,n_bindings", CASES)
+def test_schedule_parity(engine, config, seed, n_clusters, n_bindings):
+    u = synth.Universe(config, seed, n_clusters, 0, n_bindings)
+    opts = api.options()
+    compare(gpu_schedule(engine, u, opts), oracle_schedule(u, opts), f"config {config} seed {seed}")
+
+
+@pytest.mark.parametrize("prop,plugins,gate", [
+    (True, api.PLUGIN_ALL, True),
+    (False, api.PLUGIN_ALL & ~api.PLUGIN_TAINT_TOLERATION, True),
+    (False, api.PLUGIN_ALL & ~api.PLUGIN_CLUSTER_LOCALITY, False),
+    (False, 0, True),
+])
+def test_schedule_parity_options(engine, prop, plugins, gate):
+    u = synth.Universe(6, 11, 200, 0, 1500)
+    opts = api.options(empty_workload_propagation=prop, models_gate=gate, plugins=plugins)
+    compare(gpu_schedule(engine, u, opts), oracle_schedule(u, opts), f"options {prop} {plugins} {gate}")
+
+
+def test_filter_score_estimate_parity(engine):
+    from karmada_amd.engine import Batch, Snapshot
+    u = synth.Universe(6, 12, 130, 0, 300)
+    opts = api.options()
+    snap = Snapshot.from_structs(engine, u.clusters, u.n_clusters, u.names, opts)
+    b = Batch(snap, structs=u.binding_slice(0, u.n_bindings))
+    L = engine.L
+    nC, nB = u.n_clusters, u.n_bindings
+    W = (nC + 63) // 64
+    mask = (C.c_uint64 * (nB * W))()
+    engine._check(L.kp_filter_batch(engine.h, b.h, mask), "filter")
+    score = (C.c_int64 * (nB * nC))()
+    engine._check(L.kp_score_batch(engine.h, b.h, score), "score")
+    OL = O.lib()
+    idx = (C.c_uint32 * nC)(*range(nC))
+    est = (C.c_int32 * nC)()
+    bad = []
+    for i in range(nB):
+        bp = C.pointer(u.bindings[i])
+        engine._check(L.kp_max_available_replicas(engine.h, b.h, i, idx, nC, est), "estimate")
+        for c in range(nC):
+            cp = C.pointer(u.clusters[c])
+            fit = OL.kpo_filter(cp, bp, C.byref(opts)) == 0 and not u.clusters[c].deleting
+            got = bool((mask[i * W + (c >> 6)] >> (c & 63)) & 1)
+            if got != fit:
+                bad.append(("filter", i, c, got, fit))
+            s = OL.kpo_score(cp, bp, C.byref(opts))
+            if score[i * nC + c] != s:
+                bad.append(("score", i, c, score[i * nC + c], s))
+            e = OL.kpo_max_available_replicas(cp, bp, C.byref(opts), O.FAST)
+            if est[c] != e:
+                bad.append(("estimate", i, c, est[c], e))
+    b.close()
+    snap.close()
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:8]}"
+
+
+def test_shard_ranges_match_whole(engine):
+    """Scheduling binding ranges separately equals scheduling the whole batch (sharding invariant)."""
+    u = synth.Universe(6, 13, 150, 0, 1200)
+    opts = api.options()
+    whole = gpu_schedule(engine, u, opts)
+    parts = []
+    for lo, hi in [(0, 1), (1, 500), (500, 1200)]:
+        parts += gpu_schedule(engine, u, opts, lo, hi)
+    assert whole == parts
+
+
+def test_repeat_is_deterministic(engine):
+    from karmada_amd.engine import Batch, Snapshot
+    u = synth.Universe(3, 14, 400, 0, 800)
+    snap = Snapshot.from_structs(engine, u.clusters, u.n_clusters, u.names, api.options())
+    b = Batch(snap, structs=u.binding_slice(0, u.n_bindings))
+    r1 = b.schedule()
+    r2 = b.schedule()
+    assert r1 == r2
+    b.close()
+    snap.close()
+
+
+def test_empty_batch(engine):
+    from karmada_amd.engine import Batch, Snapshot
+    u = synth.Universe(2, 15, 50, 0, 0)
+    snap = Snapshot.from_structs(engine, u.clusters, u.n_clusters, u.names, api.options())
+    b = Batch(snap, structs=(u.bindings, 0))
+    assert b.schedule() == []
