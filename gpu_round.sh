@@ -1,0 +1,20 @@
+#!/bin/bash
+# GPU-box driver for one gpurun call: smoke, GPU parity tests, short bench.
+# Stops at the first step that ends in a fault/abort/timeout (exit code >1).
+mkdir -p gpurun_out
+step() {
+  local name=$1 limit=$2; shift 2
+  timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -gt 1 ]; then exit $rc; fi
+}
+for s in "$@"; do
+  case $s in
+    smoke) step smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
+    tests) step gpu_tests 900 python -m pytest tests -m gpu -q -rf ;;
+    bench_small) step bench_small 300 python bench.py --steps 3 --warmup 1 --bindings 5000 --no-cpu ;;
+    bench) step bench 600 python bench.py --steps 5 --warmup 1 ;;
+  esac
+done

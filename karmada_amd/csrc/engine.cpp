@@ -1,7 +1,7 @@
 // engine.cpp — host side of the kp placement engine: the C-ABI of
 // include/kp/kp_api.h, the snapshot/binding packer, kernel orchestration on one
 // HIP stream, and the host-kept selectGroups step of region spreading.
-#include <hip/hip_runtime.h>
+#include "kp_dev.h"
 
 #include <algorithm>
 #include <atomic>
@@ -57,29 +57,27 @@ struct Arena {
   void add(T** p, size_t count) {
     req.push_back({(void**)p, count * sizeof(T)});
   }
-  hipError_t alloc() {
+  int alloc() {
     total = 0;
     for (auto& r : req) total += (r.second + 255) & ~(size_t)255;
     if (total == 0) total = 256;
-    hipError_t e = hipMalloc(&base, total);
-    if (e != hipSuccess) return e;
+    if (dev::alloc(&base, total)) return -1;
     char* p = (char*)base;
     for (auto& r : req) {
       *r.first = p;
       p += (r.second + 255) & ~(size_t)255;
     }
-    return hipSuccess;
+    return 0;
   }
   ~Arena() {
-    if (base) (void)hipFree(base);
+    if (base) dev::release(base);
   }
 };
 
 #define HIPCHK(x)                                                            \
   do {                                                                       \
-    hipError_t _e = (x);                                                     \
-    if (_e != hipSuccess) {                                                  \
-      e->err = std::string(#x) + ": " + hipGetErrorString(_e);               \
+    if ((x) != 0) {                                                          \
+      e->err = std::string(#x) + ": " + dev::last_error();                   \
       return KP_EDEVICE;                                                     \
     }                                                                        \
   } while (0)
@@ -91,8 +89,8 @@ struct Arena {
 // ============================================================================
 struct kp_engine {
   int device = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev[6];
+  dev::stream_t stream = nullptr;
+  dev::event_t ev[6] = {};
   std::string err;
   kp_stage_times times{};
   int n_threads = 8;
@@ -419,7 +417,7 @@ int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_opti
   HIPCHK(a.alloc());
   std::vector<uint32_t> permp(Cp, 0);
   for (int r = 0; r < C; r++) permp[r] = s->perm[r];
-  auto up = [&](void* d, const void* h, size_t bytes) { return hipMemcpy(d, h, bytes, hipMemcpyHostToDevice); };
+  auto up = [&](void* d, const void* h, size_t bytes) { return dev::h2d(d, h, bytes, e->stream); };
   HIPCHK(up(d_flags, s->flags.data(), 4 * Cp));
   HIPCHK(up(d_perm, permp.data(), 4 * Cp));
   HIPCHK(up(d_prov, s->provider.data(), 4 * Cp));
@@ -441,6 +439,7 @@ int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_opti
   HIPCHK(up(d_mcnt, s->mgrp_cnt.data(), 8 * s->mgrp_cnt.size()));
   HIPCHK(up(d_tmpl, s->tmpl.data(), 8 * s->tmpl.size()));
   HIPCHK(up(d_api, s->api_bits.data(), 8 * s->api_bits.size()));
+  HIPCHK(dev::sync(e->stream));
   v.flags = d_flags;
   v.perm = d_perm;
   v.provider = d_prov;
@@ -972,18 +971,15 @@ int kp_abi_version(void) { return KP_ABI_VERSION; }
 
 int kp_engine_create(int device, kp_engine** out) {
   if (!out) return KP_EINVAL;
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n <= device) return KP_EDEVICE;
+  if (device < 0 || dev::device_count() <= device) return KP_EDEVICE;
   auto* e = new kp_engine();
   e->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (dev::set_device(device) || dev::stream_create(&e->stream)) {
     delete e;
     return KP_EDEVICE;
   }
-  for (auto& ev : e->ev) (void)hipEventCreate(&ev);
-  int lds = 0;
-  if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && lds > 0)
-    e->max_lds = (size_t)lds;
+  for (auto& ev : e->ev) (void)dev::event_create(&ev);
+  e->max_lds = dev::max_lds_per_block(device);
   unsigned hc = std::thread::hardware_concurrency();
   e->n_threads = (int)std::max(1u, std::min(16u, hc));
   *out = e;
@@ -992,9 +988,10 @@ int kp_engine_create(int device, kp_engine** out) {
 
 void kp_engine_destroy(kp_engine* e) {
   if (!e) return;
-  (void)hipSetDevice(e->device);
-  for (auto& ev : e->ev) (void)hipEventDestroy(ev);
-  if (e->stream) (void)hipStreamDestroy(e->stream);
+  (void)dev::set_device(e->device);
+  for (auto& ev : e->ev)
+    if (ev) dev::event_destroy(ev);
+  if (e->stream) dev::stream_destroy(e->stream);
   delete e;
 }
 
@@ -1003,7 +1000,7 @@ const char* kp_last_error(const kp_engine* e) { return e ? e->err.c_str() : "nul
 int kp_snapshot_create(kp_engine* e, const kp_cluster* clusters, uint64_t n, const kp_options* opts,
                        kp_snapshot** out) {
   if (!e || !out || (n && !clusters)) return KP_EINVAL;
-  (void)hipSetDevice(e->device);
+  (void)dev::set_device(e->device);
   auto* s = new kp_snapshot();
   s->e = e;
   int rc = build_snapshot(e, clusters, n, opts, s);
@@ -1023,7 +1020,7 @@ int kp_snapshot_import(kp_engine*, const void*, uint64_t, kp_snapshot**) { retur
 int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindings, uint64_t n, kp_batch** out) {
   if (!e || !sc || !out || (n && !bindings)) return KP_EINVAL;
   if (n > (uint64_t)INT32_MAX) return KP_ENOTSUP;
-  (void)hipSetDevice(e->device);
+  (void)dev::set_device(e->device);
   kp_snapshot* s = const_cast<kp_snapshot*>(sc);
   auto* bt = new kp_batch();
   std::unique_ptr<kp_batch> guard(bt);
@@ -1114,7 +1111,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->slow_scratch, bt->slow_slot * bt->slow_grid);
   HIPCHK(a.alloc());
   auto up = [&](void* d, const void* h, size_t bytes) {
-    return bytes ? hipMemcpy(d, h, bytes, hipMemcpyHostToDevice) : hipSuccess;
+    return dev::h2d(d, h, bytes, e->stream);
   };
   HIPCHK(up(d_hdr, bt->hdr.data(), sizeof(BindHdr) * bt->hdr.size()));
   HIPCHK(up(d_ipool, bt->ipool.data(), 4 * bt->ipool.size()));
@@ -1126,7 +1123,8 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   HIPCHK(up(bt->d_cluster, bt->l_cluster.data(), 4 * bt->l_cluster.size()));
   HIPCHK(up(bt->d_region, bt->l_region.data(), 4 * bt->l_region.size()));
   HIPCHK(up(bt->d_slowlist, bt->l_slow.data(), 4 * bt->l_slow.size()));
-  HIPCHK(hipMemset(bt->slow, 0, 4 * (size_t)B));
+  HIPCHK(dev::fill(bt->slow, 0, 4 * (size_t)B, e->stream));
+  HIPCHK(dev::sync(e->stream));
   BatchView& v = bt->view;
   v.B = bt->B;
   v.hdr = d_hdr;
@@ -1143,19 +1141,19 @@ void kp_batch_destroy(kp_batch* b) { delete b; }
 
 int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   if (!e || !bt || !out) return KP_EINVAL;
-  (void)hipSetDevice(e->device);
+  (void)dev::set_device(e->device);
   kp_snapshot* s = bt->snap;
   const int B = bt->B;
   double t0 = now_ms();
   kp_stage_times tm{};
-  hipStream_t st = e->stream;
+  dev::stream_t st = e->stream;
   if (B == 0) {
     memset(out, 0, sizeof(*out));
     bt->h_offsets.assign(1, 0);
     out->offsets = bt->h_offsets.data();
     return KP_OK;
   }
-  HIPCHK(hipMemsetAsync(bt->counter, 0, sizeof(unsigned long long), st));
+  HIPCHK(dev::fill(bt->counter, 0, sizeof(unsigned long long), st));
   KArgs ka;
   ka.s = s->view;
   ka.bv = bt->view;
@@ -1170,9 +1168,9 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   ka.sink.start = bt->start;
   ka.sink.count = bt->count;
   ka.slow = bt->slow;
-  HIPCHK(hipEventRecord(e->ev[0], st));
-  HIPCHK(launch_pair(st, s->view, bt->view, 0, B, bt->fmask, bt->est, nullptr, 0, kMdCap, smem_pair(s, kMdCap)));
-  HIPCHK(hipEventRecord(e->ev[1], st));
+  HIPCHK(dev::event_record(e->ev[0], st));
+  HIPCHK(dev::pair(st, s->view, bt->view, 0, B, bt->fmask, bt->est, nullptr, 0, kMdCap, smem_pair(s, kMdCap)));
+  HIPCHK(dev::event_record(e->ev[1], st));
   SelectExtra sx;
   sx.rout = bt->rout;
   sx.rstat = bt->rstat;
@@ -1186,13 +1184,13 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     KArgs k = ka;
     k.list = bt->d_all;
     k.n = (int)bt->l_all.size();
-    HIPCHK(launch_select(st, SEL_LAUNCH_ALL, k, smem_all(s), cap, sx));
+    HIPCHK(dev::select(st, SEL_LAUNCH_ALL, k, smem_all(s), cap, sx));
   }
   if (!bt->l_cluster.empty()) {
     KArgs k = ka;
     k.list = bt->d_cluster;
     k.n = (int)bt->l_cluster.size();
-    HIPCHK(launch_select(st, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sx));
+    HIPCHK(dev::select(st, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sx));
   }
   double th0 = 0, th1 = 0;
   if (!bt->l_region.empty()) {
@@ -1200,13 +1198,12 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     KArgs k = ka;
     k.list = bt->d_region;
     k.n = nr;
-    HIPCHK(launch_select(st, SEL_LAUNCH_REGION_A, k, smem_region_a(s), cap, sx));
+    HIPCHK(dev::select(st, SEL_LAUNCH_REGION_A, k, smem_region_a(s), cap, sx));
     bt->h_rout.resize((size_t)nr * std::max(R, 1));
     bt->h_rstat.resize(nr);
-    HIPCHK(hipMemcpyAsync(bt->h_rout.data(), bt->rout, sizeof(RegionOut) * bt->h_rout.size(), hipMemcpyDeviceToHost,
-                          st));
-    HIPCHK(hipMemcpyAsync(bt->h_rstat.data(), bt->rstat, 4 * nr, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(dev::d2h(bt->h_rout.data(), bt->rout, sizeof(RegionOut) * bt->h_rout.size(), st));
+    HIPCHK(dev::d2h(bt->h_rstat.data(), bt->rstat, 4 * nr, st));
+    HIPCHK(dev::sync(st));
     th0 = now_ms();
     bt->h_rsel.assign((size_t)nr * std::max(R, 1), -1);
     bt->h_rnsel.assign(nr, 0);
@@ -1235,28 +1232,28 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
       bt->h_rnsel[j] = (int32_t)sel.size();
     });
     th1 = now_ms();
-    HIPCHK(hipMemcpyAsync(bt->rsel, bt->h_rsel.data(), 4 * bt->h_rsel.size(), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(bt->rnsel, bt->h_rnsel.data(), 4 * nr, hipMemcpyHostToDevice, st));
-    HIPCHK(launch_select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sx));
+    HIPCHK(dev::h2d(bt->rsel, bt->h_rsel.data(), 4 * bt->h_rsel.size(), st));
+    HIPCHK(dev::h2d(bt->rnsel, bt->h_rnsel.data(), 4 * nr, st));
+    HIPCHK(dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sx));
   }
   if (!bt->l_slow.empty()) {
     KArgs k = ka;
     k.list = bt->d_slowlist;
     k.n = (int)bt->l_slow.size();
-    HIPCHK(launch_select(st, SEL_LAUNCH_SLOW, k, 1024 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4), bt->slow_cap, sx));
+    HIPCHK(dev::select(st, SEL_LAUNCH_SLOW, k, 1024 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4), bt->slow_cap, sx));
   }
-  HIPCHK(hipEventRecord(e->ev[2], st));
+  HIPCHK(dev::event_record(e->ev[2], st));
   // results -> host, compacted to CSR
   bt->h_status.resize(B);
   bt->h_err.resize(B);
   bt->h_arg.resize(B);
   bt->h_start.resize(B);
   bt->h_count.resize(B);
-  HIPCHK(hipMemcpyAsync(bt->h_status.data(), bt->status, 4 * (size_t)B, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(bt->h_err.data(), bt->errc, 4 * (size_t)B, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(bt->h_arg.data(), bt->arg, 8 * (size_t)B, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(bt->h_count.data(), bt->count, 4 * (size_t)B, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(dev::d2h(bt->h_status.data(), bt->status, 4 * (size_t)B, st));
+  HIPCHK(dev::d2h(bt->h_err.data(), bt->errc, 4 * (size_t)B, st));
+  HIPCHK(dev::d2h(bt->h_arg.data(), bt->arg, 8 * (size_t)B, st));
+  HIPCHK(dev::d2h(bt->h_count.data(), bt->count, 4 * (size_t)B, st));
+  HIPCHK(dev::sync(st));
   double tc0 = now_ms();
   bt->h_offsets.resize(B + 1);
   uint64_t tot = 0;
@@ -1266,21 +1263,20 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     if (bt->h_status[i] != KP_STATUS_OK) bt->h_count[i] = 0;
   }
   bt->h_offsets[B] = tot;
-  HIPCHK(hipMemcpyAsync(bt->offsets_d, bt->h_offsets.data(), 8 * (size_t)(B + 1), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(bt->count, bt->h_count.data(), 4 * (size_t)B, hipMemcpyHostToDevice, st));
-  HIPCHK(launch_compact(st, bt->start, bt->count, bt->offsets_d, bt->out_idx, bt->out_rep, bt->cidx_d, bt->crep_d, B));
+  HIPCHK(dev::h2d(bt->offsets_d, bt->h_offsets.data(), 8 * (size_t)(B + 1), st));
+  HIPCHK(dev::h2d(bt->count, bt->h_count.data(), 4 * (size_t)B, st));
+  HIPCHK(dev::compact(st, bt->start, bt->count, bt->offsets_d, bt->out_idx, bt->out_rep, bt->cidx_d, bt->crep_d, B));
   bt->h_cidx.resize(std::max<uint64_t>(1, tot));
   bt->h_crep.resize(std::max<uint64_t>(1, tot));
   if (tot) {
-    HIPCHK(hipMemcpyAsync(bt->h_cidx.data(), bt->cidx_d, 4 * tot, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(bt->h_crep.data(), bt->crep_d, 4 * tot, hipMemcpyDeviceToHost, st));
+    HIPCHK(dev::d2h(bt->h_cidx.data(), bt->cidx_d, 4 * tot, st));
+    HIPCHK(dev::d2h(bt->h_crep.data(), bt->crep_d, 4 * tot, st));
   }
-  HIPCHK(hipStreamSynchronize(st));
-  HIPCHK(hipGetLastError());
+  HIPCHK(dev::sync(st));
   double t1 = now_ms();
   float ms_pair = 0, ms_sel = 0;
-  (void)hipEventElapsedTime(&ms_pair, e->ev[0], e->ev[1]);
-  (void)hipEventElapsedTime(&ms_sel, e->ev[1], e->ev[2]);
+  ms_pair = dev::event_ms(e->ev[0], e->ev[1]);
+  ms_sel = dev::event_ms(e->ev[1], e->ev[2]);
   tm.pair_kernel_ms = ms_pair;
   tm.select_kernel_ms = ms_sel;
   tm.pair_ms = ms_pair;
@@ -1303,21 +1299,22 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
 // Runs the pair kernel and returns the rank-ordered device row pointers.
 static int run_pair(kp_engine* e, kp_batch* bt, int64_t* score, int est_mode, int b0, int nb) {
   kp_snapshot* s = bt->snap;
-  HIPCHK(launch_pair(e->stream, s->view, bt->view, b0, nb, bt->fmask, bt->est, score, est_mode, kMdCap,
+  HIPCHK(dev::pair(e->stream, s->view, bt->view, b0, nb, bt->fmask, bt->est, score, est_mode, kMdCap,
                      smem_pair(s, kMdCap)));
-  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(dev::sync(e->stream));
   return KP_OK;
 }
 
 int kp_filter_batch(kp_engine* e, kp_batch* bt, uint64_t* out_mask) {
   if (!e || !bt || !out_mask) return KP_EINVAL;
-  (void)hipSetDevice(e->device);
+  (void)dev::set_device(e->device);
   kp_snapshot* s = bt->snap;
   if (bt->B == 0) return KP_OK;
   int rc = run_pair(e, bt, nullptr, 0, 0, bt->B);
   if (rc) return rc;
   std::vector<uint64_t> m((size_t)bt->B * s->W);
-  HIPCHK(hipMemcpy(m.data(), bt->fmask, 8 * m.size(), hipMemcpyDeviceToHost));
+  HIPCHK(dev::d2h(m.data(), bt->fmask, 8 * m.size(), e->stream));
+  HIPCHK(dev::sync(e->stream));
   const int Wc = (s->C + 63) / 64;
   memset(out_mask, 0, 8 * (size_t)bt->B * Wc);
   for (int b = 0; b < bt->B; b++)
@@ -1331,16 +1328,16 @@ int kp_filter_batch(kp_engine* e, kp_batch* bt, uint64_t* out_mask) {
 
 int kp_score_batch(kp_engine* e, kp_batch* bt, int64_t* out_scores) {
   if (!e || !bt || !out_scores) return KP_EINVAL;
-  (void)hipSetDevice(e->device);
+  (void)dev::set_device(e->device);
   kp_snapshot* s = bt->snap;
   if (bt->B == 0) return KP_OK;
   int64_t* d = nullptr;
   size_t n = (size_t)bt->B * std::max(1, s->C);
-  HIPCHK(hipMalloc(&d, 8 * n));
+  HIPCHK(dev::alloc((void**)&d, 8 * n));
   int rc = run_pair(e, bt, d, 0, 0, bt->B);
   std::vector<int64_t> h(n);
-  if (rc == KP_OK) rc = hipMemcpy(h.data(), d, 8 * n, hipMemcpyDeviceToHost) == hipSuccess ? KP_OK : KP_EDEVICE;
-  (void)hipFree(d);
+  if (rc == KP_OK) rc = (dev::d2h(h.data(), d, 8 * n, e->stream) || dev::sync(e->stream)) ? KP_EDEVICE : KP_OK;
+  dev::release(d);
   if (rc) return rc;
   for (int b = 0; b < bt->B; b++)
     for (int r = 0; r < s->C; r++) out_scores[(size_t)b * s->C + s->perm[r]] = h[(size_t)b * s->C + r];
@@ -1350,12 +1347,13 @@ int kp_score_batch(kp_engine* e, kp_batch* bt, int64_t* out_scores) {
 int kp_max_available_replicas(kp_engine* e, kp_batch* bt, uint64_t binding, const uint32_t* cluster_idx, uint64_t n,
                               int32_t* out) {
   if (!e || !bt || (n && (!cluster_idx || !out)) || binding >= (uint64_t)bt->B) return KP_EINVAL;
-  (void)hipSetDevice(e->device);
+  (void)dev::set_device(e->device);
   kp_snapshot* s = bt->snap;
   int rc = run_pair(e, bt, nullptr, 1, (int)binding, 1);
   if (rc) return rc;
   std::vector<int32_t> row(s->Cp);
-  HIPCHK(hipMemcpy(row.data(), bt->est + (size_t)binding * s->Cp, 4 * (size_t)s->Cp, hipMemcpyDeviceToHost));
+  HIPCHK(dev::d2h(row.data(), bt->est + (size_t)binding * s->Cp, 4 * (size_t)s->Cp, e->stream));
+  HIPCHK(dev::sync(e->stream));
   for (uint64_t i = 0; i < n; i++) {
     if (cluster_idx[i] >= (uint32_t)s->C) return KP_EINVAL;
     out[i] = row[s->inv[cluster_idx[i]]];

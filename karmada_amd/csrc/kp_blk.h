@@ -76,6 +76,11 @@ struct GpuBlk {
     *total = tot;
     return base + x - v;
   }
+  // Stores the feasibility bit of cluster c (c = wave base + lane) into its u64 word.
+  KP_INLINE void mask_store(uint64_t* row, int c, bool bit, int W) const {
+    const uint64_t m = __ballot(bit);
+    if (lane() == 0 && (c >> 6) < W) row[c >> 6] = m;
+  }
   // Value of thread 0 to every thread.
   template <class T>
   KP_INLINE T bcast(T v) const {
@@ -110,6 +115,11 @@ struct CpuBlk {
   T bcast(T v) const {
     return v;
   }
+  void mask_store(uint64_t* row, int c, bool bit, int W) const {
+    if ((c >> 6) >= W) return;
+    if ((c & 63) == 0) row[c >> 6] = 0;
+    if (bit) row[c >> 6] |= 1ull << (c & 63);
+  }
 };
 
 // Atomics on LDS/global memory, usable from both builds.
@@ -120,6 +130,15 @@ KP_HD inline T kp_atomic_add(T* p, T v) {
 #else
   T o = *p;
   *p = o + v;
+  return o;
+#endif
+}
+KP_HD inline uint32_t kp_atomic_or(uint32_t* p, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return atomicOr(p, v);
+#else
+  uint32_t o = *p;
+  *p = o | v;
   return o;
 #endif
 }

@@ -1,0 +1,46 @@
+// kp_dev.h — the device interface engine.cpp runs on.
+//
+// libkp.so implements it with HIP on gfx950 (kernels.hip). The test-only
+// libkp_cpusim.so implements it on the host (dev_cpu.cpp) by running the same
+// kernel bodies (kp_kernels.h) with a 1-thread block policy, so the engine's
+// orchestration and kernel logic can be checked without a GPU. The CPU build
+// is never linked into libkp.so.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "kp_launch.h"
+
+namespace kp {
+namespace dev {
+
+typedef void* stream_t;
+typedef void* event_t;
+
+int device_count();
+int set_device(int device);
+size_t max_lds_per_block(int device);
+const char* last_error();  // text of the last failing call
+
+int stream_create(stream_t* s);
+void stream_destroy(stream_t s);
+int sync(stream_t s);
+int event_create(event_t* e);
+void event_destroy(event_t e);
+int event_record(event_t e, stream_t s);
+float event_ms(event_t a, event_t b);
+
+int alloc(void** p, size_t bytes);
+void release(void* p);
+int h2d(void* dst, const void* src, size_t bytes, stream_t s);  // stream-ordered
+int d2h(void* dst, const void* src, size_t bytes, stream_t s);
+int fill(void* dst, int value, size_t bytes, stream_t s);
+
+int pair(stream_t st, const SnapView& s, const BatchView& bv, int b0, int nb, uint64_t* fmask, int32_t* est,
+         int64_t* score, int est_mode, int md_cap, size_t smem);
+int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x);
+int compact(stream_t st, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
+            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n);
+
+}  // namespace dev
+}  // namespace kp

@@ -1,0 +1,379 @@
+// kp_kernels.h — bodies of the engine's kernels, written once against a block
+// policy (kp_blk.h). kernels.hip instantiates them with GpuBlk as gfx950
+// kernels (one 256-thread workgroup per binding); the test-only CPU build
+// (dev_cpu.cpp -> libkp_cpusim.so) instantiates them with CpuBlk to check the
+// same code paths on the host.
+//
+// Per-block LDS layouts (dynamic shared memory; sizes computed in engine.cpp):
+//   pair      [512 red | tgt bits | evict bits | md table]
+//   sel_all   [512 red | tgt bits | cand r [Cp] | cand v [Cp]]
+//   sel_clus  [512 red | hist 1 KB | items 2*kSmallMax | keys 2*kSmallMax | tgt | cand/serial area]
+//   region_a  [512 red | 8x8R + 4x4R region accumulators | tgt | cand]
+//   region_b  [512 red | hist | items | keys | heads 8R | rsel 4R | tgt | cand/serial area]
+//   slow      [512 red | tgt]   (candidates/keys/serial scratch in a global slot)
+#pragma once
+#include "kp_launch.h"
+#include "kp_paths.h"
+
+namespace kp {
+
+KP_HD inline SelCtx make_ctx(const KArgs& a, int b, const uint32_t* tgt_bits) {
+  SelCtx x;
+  x.s = &a.s;
+  x.bv = &a.bv;
+  x.h = &a.bv.hdr[b];
+  x.b = b;
+  x.frow = a.fmask + (size_t)b * a.s.W;
+  x.erow = a.est + (size_t)b * a.s.Cp;
+  x.tgt_bits = tgt_bits;
+  x.sink = a.sink;
+  return x;
+}
+
+// Bitset (LDS) of the binding's spec.Clusters ranks (TargetContains, locality).
+template <class BLK>
+KP_HD void build_bits(const BLK& B, uint32_t* bits, int words, const int32_t* pool, int off, int cnt, int stride) {
+  for (int i = B.tid(); i < words; i += B.nth()) bits[i] = 0;
+  B.sync();
+  for (int j = B.tid(); j < cnt; j += B.nth()) {
+    int r = pool[off + stride * j];
+    kp_atomic_or(&bits[r >> 5], 1u << (r & 31));
+  }
+  B.sync();
+}
+
+// Status of bindings that never reach selection.
+template <class BLK>
+KP_HD bool pre_checks(const BLK& B, const SelCtx& x, int F) {
+  if (x.h->flags & BF_BAD) {
+    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, 0);
+    return true;
+  }
+  if (F == 0) {  // FitError (generic_scheduler.go:84-89)
+    if (B.tid() == 0) sink_error(x, KP_STATUS_FIT_ERROR, KP_ERR_FIT, x.s->C);
+    return true;
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------------------
+// Pair stage: each wave evaluates 64 consecutive clusters (coalesced SoA
+// columns), stores their feasibility as one u64 word and calAvailableReplicas
+// per cluster. est_mode 1: raw GeneralEstimator answers for every cluster.
+// ---------------------------------------------------------------------------
+template <class BLK>
+KP_HD void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView& s, const BatchView& bv, int b0,
+                     uint64_t* fmask, int32_t* est, int64_t* score, int est_mode, int md_cap) {
+  const int b = b0 + blk;
+  const BindHdr h = bv.hdr[b];
+  const int words = (s.Cp + 31) >> 5;
+  uint32_t* tgt = (uint32_t*)(smem + 512);
+  uint32_t* evict = tgt + words;
+  int32_t* md = (int32_t*)(evict + words);
+  build_bits(B, tgt, words, bv.ipool, h.tgt_off, h.tgt_cnt, 2);
+  build_bits(B, evict, words, bv.ipool, h.evict_off, h.evict_cnt, 1);
+  const bool use_md = s.n_tmpl <= md_cap && (h.flags & BF_HAS_RR);
+  if (use_md) {
+    for (int t = B.tid(); t < s.n_tmpl; t += B.nth()) md[t] = template_md(s, bv, h, t);
+    B.sync();
+  }
+  uint64_t* frow = fmask + (size_t)b * s.W;
+  int32_t* erow = est + (size_t)b * s.Cp;
+  for (int base = 0; base < s.Cp; base += B.nth()) {
+    const int c = base + B.tid();
+    bool fit = false;
+    int32_t e = 0;
+    if (est_mode == 0) {
+      fit = pair_feasible(s, bv, h, c, tgt, evict);
+      if (fit) e = cal_available(s, bv, h, c, use_md ? md : nullptr);
+    } else if (c < s.C) {
+      e = general_estimate(s, bv, h, c, use_md ? md : nullptr);
+      fit = true;
+    }
+    B.mask_store(frow, c, fit, s.W);
+    if (c < s.Cp) erow[c] = e;
+    if (score && c < s.C) {
+      int64_t sc = 0;
+      if ((h.enabled & KP_PLUGIN_CLUSTER_LOCALITY) && h.n_targets_all > 0 && h.tgt_cnt > 0 && bit_test(tgt, c)) sc = 100;
+      score[(size_t)b * s.C + c] = sc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Select stage: SEL_ALL (and spread-unsupported / FitError reporting)
+// ---------------------------------------------------------------------------
+template <class BLK>
+KP_HD void body_select_all(const BLK& B, int blk, unsigned char* smem, const KArgs& a) {
+  if (blk >= a.n) return;
+  const int b = a.list[blk];
+  const int words = (a.s.Cp + 31) >> 5;
+  uint32_t* tgt = (uint32_t*)(smem + 512);
+  Cands cd;
+  cd.r = tgt + words;
+  cd.v = (int32_t*)(cd.r + a.s.Cp);
+  const BindHdr* h = &a.bv.hdr[b];
+  build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
+  SelCtx x = make_ctx(a, b, tgt);
+  const bool weights = h->strategy == ST_STATIC && h->sel == SEL_ALL;
+  cd.F = gather(B, x, cd, weights);
+  if (pre_checks(B, x, cd.F)) return;
+  if (h->sel == SEL_ERR_UNSUPPORTED) {  // select_clusters.go:54
+    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_SPREAD_UNSUPPORTED, 0);
+    return;
+  }
+  if (!sel_all_fast(B, x, cd)) {
+    if (B.tid() == 0) {
+      a.slow[b] = 1;
+      a.sink.count[b] = 0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Select stage: SEL_CLUSTER
+// ---------------------------------------------------------------------------
+template <class BLK>
+KP_HD void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const KArgs& a, int scratch_cap) {
+  if (blk >= a.n) return;
+  const int b = a.list[blk];
+  const int words = (a.s.Cp + 31) >> 5;
+  uint32_t* hist = (uint32_t*)(smem + 512);
+  Item* items = (Item*)(smem + 512 + 1024);
+  uint64_t* keys = (uint64_t*)(items + 2 * kSmallMax);
+  uint32_t* tgt = (uint32_t*)(keys + 2 * kSmallMax);
+  unsigned char* area = (unsigned char*)(tgt + ((words + 3) & ~3));
+  Cands cd;
+  cd.r = (uint32_t*)area;
+  cd.v = (int32_t*)(cd.r + a.s.Cp);
+  const BindHdr* h = &a.bv.hdr[b];
+  build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
+  SelCtx x = make_ctx(a, b, tgt);
+  cd.F = gather(B, x, cd, false);
+  if (pre_checks(B, x, cd.F)) return;
+  if (!sel_cluster_fast(B, x, cd, hist, items, keys, area, scratch_cap)) {
+    if (B.tid() == 0) {
+      a.slow[b] = 1;
+      a.sink.count[b] = 0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Region stage A: per-region count and group score for the host selectGroups.
+// rout: [n][n_regions]; rstat[blk] = -1 when the final status is already written.
+// ---------------------------------------------------------------------------
+template <class BLK>
+KP_HD void body_region_a(const BLK& B, int blk, unsigned char* smem, const KArgs& a, RegionOut* rout, int32_t* rstat) {
+  if (blk >= a.n) return;
+  const int b = a.list[blk];
+  const int words = (a.s.Cp + 31) >> 5;
+  const int R = a.s.n_regions;
+  unsigned char* p = smem + 512;
+  RegionLds L;
+  L.minkey = (unsigned long long*)p;
+  p += 8 * R;
+  L.last = (unsigned long long*)p;
+  p += 8 * R;
+  L.sumAvail = (int64_t*)p;
+  p += 8 * R;
+  L.sumScore = (int64_t*)p;
+  p += 8 * R;
+  L.dscore = (int64_t*)p;
+  p += 8 * R;
+  L.wsum = (int64_t*)p;
+  p += 8 * R;
+  L.wscore = (int64_t*)p;
+  p += 8 * R;
+  L.amin = (int64_t*)p;
+  p += 8 * R;
+  L.cnt = (int32_t*)p;
+  p += 4 * R;
+  L.dvalid = (int32_t*)p;
+  p += 4 * R;
+  L.wcnt = (int32_t*)p;
+  p += 4 * R;
+  L.done = (int32_t*)p;
+  p += 4 * R;
+  uint32_t* tgt = (uint32_t*)p;
+  p += 4 * ((words + 3) & ~3);
+  Cands cd;
+  cd.r = (uint32_t*)p;
+  cd.v = (int32_t*)(cd.r + a.s.Cp);
+  const BindHdr* h = &a.bv.hdr[b];
+  build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
+  SelCtx x = make_ctx(a, b, tgt);
+  cd.F = gather(B, x, cd, false);
+  if (pre_checks(B, x, cd.F)) {
+    if (B.tid() == 0) rstat[blk] = -1;
+    return;
+  }
+  region_a(B, x, cd, L, rout + (size_t)blk * R);
+  if (B.tid() == 0) rstat[blk] = 0;
+}
+
+// Region stage B. rsel: [n][n_regions] selected region ids (path order); rnsel[n]:
+// count, -1000 when stage A already finalized, or -KP_ERR_* from the host step.
+template <class BLK>
+KP_HD void body_region_b(const BLK& B, int blk, unsigned char* smem, const KArgs& a, const int32_t* rsel,
+                         const int32_t* rnsel, int scratch_cap) {
+  if (blk >= a.n) return;
+  const int b = a.list[blk];
+  const int nsel = rnsel[blk];
+  if (nsel == -1000) return;
+  const int words = (a.s.Cp + 31) >> 5;
+  const int R = a.s.n_regions;
+  unsigned char* p = smem + 512;
+  uint32_t* hist = (uint32_t*)p;
+  p += 1024;
+  Item* items = (Item*)p;
+  p += sizeof(Item) * 2 * kSmallMax;
+  uint64_t* keys = (uint64_t*)p;
+  p += 8 * 2 * kSmallMax;
+  unsigned long long* heads = (unsigned long long*)p;
+  p += 8 * R;
+  int32_t* rs = (int32_t*)p;
+  p += 4 * ((R + 3) & ~3);
+  uint32_t* tgt = (uint32_t*)p;
+  p += 4 * ((words + 3) & ~3);
+  Cands cd;
+  cd.r = (uint32_t*)p;
+  cd.v = (int32_t*)(cd.r + a.s.Cp);
+  const BindHdr* h = &a.bv.hdr[b];
+  build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
+  SelCtx x = make_ctx(a, b, tgt);
+  if (nsel < 0) {
+    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, -nsel, 0);
+    return;
+  }
+  if ((h->flags & BF_DUP_TARGETS) && h->tgt_cnt > kTgtSmallMax) {  // engine limit (selected-list scratch)
+    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, -1);
+    return;
+  }
+  cd.F = gather(B, x, cd, false);
+  region_b(B, x, cd, rsel + (size_t)blk * R, nsel, hist, heads, rs, items, keys, p, scratch_cap);
+}
+
+// ---------------------------------------------------------------------------
+// Exact serial path: candidates fully sorted by the sortClusters key in a
+// global scratch slot, then the Go algorithm on thread 0 (Aggregated ties with
+// the pdqsort emulation, scale-down, overflow tiers, duplicates, wrap-around).
+// Persistent: block k handles list entries k, k+grid, ...
+// ---------------------------------------------------------------------------
+template <class BLK>
+KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const KArgs& a, unsigned char* scratch,
+                     size_t slot_bytes, int scratch_cap) {
+  const int words = (a.s.Cp + 31) >> 5;
+  uint32_t* tgt = (uint32_t*)(smem + 512);
+  unsigned char* mine = scratch + (size_t)blk * slot_bytes;
+  // slot layout: cand r/v [Cp] | keys [P] | items [Cp] | pos [Cp] | serial scratch
+  int P = 1;
+  while (P < a.s.Cp) P <<= 1;
+  Cands cd;
+  cd.r = (uint32_t*)mine;
+  cd.v = (int32_t*)(cd.r + a.s.Cp);
+  uint64_t* keys = (uint64_t*)(cd.v + a.s.Cp);
+  Item* items = (Item*)(keys + P);
+  int32_t* pos = (int32_t*)(items + a.s.Cp);
+  unsigned char* ser = (unsigned char*)(pos + a.s.Cp);
+  for (int i = B.tid(); i < a.s.Cp; i += B.nth()) pos[i] = -1;
+  B.sync();
+  for (int idx = blk; idx < a.n; idx += grid) {
+    const int b = a.list[idx];
+    if (!a.slow[b]) continue;
+    const BindHdr* h = &a.bv.hdr[b];
+    build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
+    SelCtx x = make_ctx(a, b, tgt);
+    cd.F = gather(B, x, cd, false);
+    const int F = cd.F;
+    for (int i = B.tid(); i < P; i += B.nth()) keys[i] = i < F ? cand_key(x, cd, i, cd.v[i]) : ~0ull;
+    B.sync();
+    for (int k = 2; k <= P; k <<= 1)  // bitonic sort (ascending)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = B.tid(); i < P; i += B.nth()) {
+          int l = i ^ j;
+          if (l > i) {
+            uint64_t ki = keys[i], kl = keys[l];
+            bool up = (i & k) == 0;
+            if ((ki > kl) == up) {
+              keys[i] = kl;
+              keys[l] = ki;
+            }
+          }
+        }
+        B.sync();
+      }
+    for (int i = B.tid(); i < F; i += B.nth()) items[i] = item_from_key(x, keys[i]);
+    B.sync();
+    if (B.tid() == 0) {
+      SerialScratch sc = serial_scratch_carve(ser, scratch_cap);
+      sc.pos = pos;
+      int n = F;
+      bool err = false;
+      if (h->sel == SEL_CLUSTER) {  // selectBestClustersByCluster on the sorted list
+        if ((int64_t)F < h->cluster_min) {
+          sink_error(x, KP_STATUS_ERROR, KP_ERR_CLUSTER_MIN_GROUPS, 0);
+          err = true;
+        } else {
+          int64_t needCnt = (int64_t)F < h->cluster_max ? (int64_t)F : h->cluster_max;
+          if (needCnt < 0) needCnt = 0;
+          if (h->need_replicas != -1) {
+            auto check = [&]() {
+              int64_t t = 0;
+              for (int i = 0; i < needCnt; i++) t += items[i].avail;
+              return t >= (int64_t)h->need_replicas;
+            };
+            int64_t upd = needCnt - 1;
+            while (!check() && upd >= 0) {  // selectClustersByAvailableResource
+              int64_t mv = items[upd].avail;
+              int64_t id = -1;
+              for (int64_t i = needCnt; i < F; i++)
+                if (mv < items[i].avail) {
+                  id = i;
+                  mv = items[i].avail;
+                }
+              if (id < 0) {
+                upd--;
+                continue;
+              }
+              Item t = items[upd];
+              items[upd] = items[id];
+              items[id] = t;
+              upd--;
+            }
+            if (!check() || needCnt == 0) {
+              sink_error(x, KP_STATUS_ERROR, KP_ERR_CLUSTER_RESOURCE, needCnt);
+              err = true;
+            }
+          } else if (needCnt == 0) {
+            sink_error(x, KP_STATUS_ERROR, KP_ERR_NO_CLUSTERS, 0);
+            err = true;
+          }
+          n = (int)needCnt;
+        }
+      }
+      if (!err) {
+        SerialAssign sa{x, sc, (h->flags & BF_UID_DESC) != 0};
+        SerialOut o = sa.run(items, n);
+        sink_serial(x, sc, o);
+      }
+      a.slow[b] = 0;
+    }
+    B.sync();
+  }
+}
+
+// Gathers per-binding results into CSR order (offsets computed on the host).
+template <class BLK>
+KP_HD void body_compact(const BLK& B, int blk, const uint64_t* start, const uint32_t* count, const uint64_t* offsets,
+                        const uint32_t* in_idx, const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n) {
+  if (blk >= n) return;
+  uint64_t s = start[blk], o = offsets[blk];
+  uint32_t c = count[blk];
+  for (uint32_t i = B.tid(); i < c; i += B.nth()) {
+    out_idx[o + i] = in_idx[s + i];
+    out_rep[o + i] = in_rep[s + i];
+  }
+}
+
+}  // namespace kp
