@@ -137,6 +137,7 @@ def main():
         pair_ms.append(st["pair_kernel_ms"])
         sel_ms.append(st["select_kernel_ms"])
         host_ms.append(st["host_ms"])
+        n_slow = st["n_slow"]
     barrier_sync()
     elapsed = time.perf_counter() - t0
     n_ok = sum(1 for i in range(r.n_bindings) if r.status[i] == 0)
@@ -176,6 +177,7 @@ def main():
         "setup_s": {"generate": round(gen_s, 2), "snapshot_pack_upload": round(snap_s, 3),
                     "binding_pack_upload": round(pack_s, 3)},
         "scheduled_ok": n_ok,
+        "slow_path_bindings": n_slow,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(u, opts, args.cpu_budget)

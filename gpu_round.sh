@@ -2,6 +2,7 @@
 # GPU-box driver for one gpurun call: smoke, GPU parity tests, short bench.
 # Stops at the first step that ends in a fault/abort/timeout (exit code >1).
 mkdir -p gpurun_out
+ROOT=$(pwd)
 step() {
   local name=$1 limit=$2; shift 2
   timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
@@ -16,5 +17,9 @@ for s in "$@"; do
     tests) step gpu_tests 900 python -m pytest tests -m gpu -q -rf ;;
     bench_small) step bench_small 300 python bench.py --steps 3 --warmup 1 --bindings 5000 --no-cpu ;;
     bench) step bench 600 python bench.py --steps 5 --warmup 1 ;;
+    prof_kt) step prof_kt 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/prof_kt -o kt -- python3 $ROOT/bench.py --steps 5 --warmup 1 --no-cpu" ;;
+    prof_fetch) step prof_fetch 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --pmc FETCH_SIZE --output-format csv -d $ROOT/gpurun_out/prof_fetch -o f -- python3 $ROOT/bench.py --steps 2 --warmup 0 --no-cpu" ;;
+    prof_write) step prof_write 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --pmc WRITE_SIZE --output-format csv -d $ROOT/gpurun_out/prof_write -o w -- python3 $ROOT/bench.py --steps 2 --warmup 0 --no-cpu" ;;
+    prof_l2) step prof_l2 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $ROOT/gpurun_out/prof_l2 -o l -- python3 $ROOT/bench.py --steps 2 --warmup 0 --no-cpu" ;;
   esac
 done

@@ -303,6 +303,7 @@ typedef struct kp_stage_times {
   double total_ms;
   float pair_kernel_ms; /* HIP event time of the pair kernel */
   float select_kernel_ms;
+  uint64_t n_slow; /* bindings that took the exact serial path */
 } kp_stage_times;
 
 /* ------------------------------------------------------------------------- */

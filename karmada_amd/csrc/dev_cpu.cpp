@@ -1,0 +1,137 @@
+// dev_cpu.cpp — TEST-ONLY host implementation of kp_dev.h (libkp_cpusim.so).
+//
+// Runs the kernel bodies of kp_kernels.h with the 1-thread CpuBlk policy, one
+// "workgroup" at a time per host thread, so tests/ can check the engine's
+// orchestration and kernel logic against the oracle without a GPU. It is never
+// linked into libkp.so and the product loader (karmada_amd/engine.py) never
+// loads it.
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "kp_dev.h"
+#include "kp_kernels.h"
+
+namespace kp {
+namespace dev {
+
+namespace {
+int threads() {
+  const char* e = getenv("KP_CPUSIM_THREADS");
+  int n = e ? atoi(e) : 1;
+  return n < 1 ? 1 : n;
+}
+// Runs fn(blk, smem) for blk in [0, n) on the configured host threads.
+template <class F>
+void grid(int n, size_t smem_bytes, F fn) {
+  int T = threads();
+  if (T > n) T = n;
+  std::atomic<int> next(0);
+  auto work = [&]() {
+    std::vector<int64_t> smem((smem_bytes + 512 + 7) / 8);
+    for (;;) {
+      int b = next.fetch_add(1);
+      if (b >= n) break;
+      fn(b, (unsigned char*)smem.data());
+    }
+  };
+  if (T <= 1) {
+    work();
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; t++) th.emplace_back(work);
+  for (auto& t : th) t.join();
+}
+struct Ev {
+  double ms;
+};
+}  // namespace
+
+int device_count() { return 1; }
+int set_device(int) { return 0; }
+size_t max_lds_per_block(int) { return 160 * 1024; }
+const char* last_error() { return "cpusim error"; }
+int stream_create(stream_t* s) {
+  *s = (void*)1;
+  return 0;
+}
+void stream_destroy(stream_t) {}
+int sync(stream_t) { return 0; }
+int event_create(event_t* e) {
+  *e = new Ev{0};
+  return 0;
+}
+void event_destroy(event_t e) { delete (Ev*)e; }
+int event_record(event_t e, stream_t) {
+  ((Ev*)e)->ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  return 0;
+}
+float event_ms(event_t a, event_t b) { return (float)(((Ev*)b)->ms - ((Ev*)a)->ms); }
+int alloc(void** p, size_t bytes) {
+  *p = calloc(1, bytes ? bytes : 1);
+  return *p ? 0 : -1;
+}
+void release(void* p) { free(p); }
+int h2d(void* dst, const void* src, size_t bytes, stream_t) {
+  if (bytes) memcpy(dst, src, bytes);
+  return 0;
+}
+int d2h(void* dst, const void* src, size_t bytes, stream_t) {
+  if (bytes) memcpy(dst, src, bytes);
+  return 0;
+}
+int fill(void* dst, int value, size_t bytes, stream_t) {
+  if (bytes) memset(dst, value, bytes);
+  return 0;
+}
+
+int pair(stream_t, const SnapView& s, const BatchView& bv, int b0, int nb, uint64_t* fmask, int32_t* est,
+         int64_t* score, int est_mode, int md_cap, size_t smem) {
+  grid(nb, smem, [&](int blk, unsigned char* sm) {
+    body_pair(CpuBlk{(int64_t*)sm}, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap);
+  });
+  return 0;
+}
+
+int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x) {
+  switch (which) {
+    case SEL_LAUNCH_ALL:
+      grid(a.n, smem, [&](int blk, unsigned char* sm) { body_select_all(CpuBlk{(int64_t*)sm}, blk, sm, a); });
+      break;
+    case SEL_LAUNCH_CLUSTER:
+      grid(a.n, smem,
+           [&](int blk, unsigned char* sm) { body_select_cluster(CpuBlk{(int64_t*)sm}, blk, sm, a, cap); });
+      break;
+    case SEL_LAUNCH_REGION_A:
+      grid(a.n, smem,
+           [&](int blk, unsigned char* sm) { body_region_a(CpuBlk{(int64_t*)sm}, blk, sm, a, x.rout, x.rstat); });
+      break;
+    case SEL_LAUNCH_REGION_B:
+      grid(a.n, smem, [&](int blk, unsigned char* sm) {
+        body_region_b(CpuBlk{(int64_t*)sm}, blk, sm, a, x.rsel, x.rnsel, cap);
+      });
+      break;
+    case SEL_LAUNCH_SLOW:
+      grid(x.grid, smem, [&](int blk, unsigned char* sm) {
+        body_slow(CpuBlk{(int64_t*)sm}, blk, x.grid, sm, a, x.scratch, x.slot_bytes, cap);
+      });
+      break;
+    default:
+      return -1;
+  }
+  return 0;
+}
+
+int compact(stream_t, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
+            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n) {
+  int64_t red[8];
+  for (int b = 0; b < n; b++) body_compact(CpuBlk{red}, b, start, count, offsets, in_idx, in_rep, out_idx, out_rep, n);
+  return 0;
+}
+
+}  // namespace dev
+}  // namespace kp

@@ -7,6 +7,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -139,6 +140,8 @@ struct kp_batch {
   uint64_t* start = nullptr;
   uint32_t* count = nullptr;
   unsigned long long* counter = nullptr;
+  uint32_t* stats = nullptr;
+  uint32_t h_stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t* out_idx = nullptr;
   int32_t* out_rep = nullptr;
   uint64_t* offsets_d = nullptr;
@@ -1099,6 +1102,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->start, B);
   a.add(&bt->count, B);
   a.add(&bt->counter, 1);
+  a.add(&bt->stats, 8);
   a.add(&bt->out_idx, std::max<uint64_t>(1, bt->out_cap));
   a.add(&bt->out_rep, std::max<uint64_t>(1, bt->out_cap));
   a.add(&bt->offsets_d, B + 1);
@@ -1154,6 +1158,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     return KP_OK;
   }
   HIPCHK(dev::fill(bt->counter, 0, sizeof(unsigned long long), st));
+  HIPCHK(dev::fill(bt->stats, 0, 8 * sizeof(uint32_t), st));
   KArgs ka;
   ka.s = s->view;
   ka.bv = bt->view;
@@ -1168,6 +1173,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   ka.sink.start = bt->start;
   ka.sink.count = bt->count;
   ka.slow = bt->slow;
+  ka.stats = bt->stats;
   HIPCHK(dev::event_record(e->ev[0], st));
   HIPCHK(dev::pair(st, s->view, bt->view, 0, B, bt->fmask, bt->est, nullptr, 0, kMdCap, smem_pair(s, kMdCap)));
   HIPCHK(dev::event_record(e->ev[1], st));
@@ -1253,6 +1259,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   HIPCHK(dev::d2h(bt->h_err.data(), bt->errc, 4 * (size_t)B, st));
   HIPCHK(dev::d2h(bt->h_arg.data(), bt->arg, 8 * (size_t)B, st));
   HIPCHK(dev::d2h(bt->h_count.data(), bt->count, 4 * (size_t)B, st));
+  HIPCHK(dev::d2h(bt->h_stats, bt->stats, sizeof(bt->h_stats), st));
   HIPCHK(dev::sync(st));
   double tc0 = now_ms();
   bt->h_offsets.resize(B + 1);
@@ -1279,6 +1286,11 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   ms_sel = dev::event_ms(e->ev[1], e->ev[2]);
   tm.pair_kernel_ms = ms_pair;
   tm.select_kernel_ms = ms_sel;
+  tm.n_slow = bt->h_stats[0];
+  if (getenv("KP_DEBUG_SLOW"))
+    fprintf(stderr, "kp slow: total %u overflow/dup %u scale-down %u wrap %u tie %u weight %u cluster %u\n",
+            bt->h_stats[0], bt->h_stats[1], bt->h_stats[2], bt->h_stats[3], bt->h_stats[4], bt->h_stats[5],
+            bt->h_stats[6]);
   tm.pair_ms = ms_pair;
   tm.select_ms = ms_sel;
   tm.host_ms = th1 - th0;

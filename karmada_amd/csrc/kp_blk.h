@@ -128,26 +128,23 @@ KP_HD inline T kp_atomic_add(T* p, T v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return atomicAdd(p, v);
 #else
-  T o = *p;
-  *p = o + v;
-  return o;
+  return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
 #endif
 }
 KP_HD inline uint32_t kp_atomic_or(uint32_t* p, uint32_t v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return atomicOr(p, v);
 #else
-  uint32_t o = *p;
-  *p = o | v;
-  return o;
+  return __atomic_fetch_or(p, v, __ATOMIC_RELAXED);
 #endif
 }
 KP_HD inline unsigned long long kp_atomic_min_u64(unsigned long long* p, unsigned long long v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return atomicMin(p, v);
 #else
-  unsigned long long o = *p;
-  if (v < o) *p = v;
+  unsigned long long o = __atomic_load_n(p, __ATOMIC_RELAXED);
+  while (v < o && !__atomic_compare_exchange_n(p, &o, v, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+  }
   return o;
 #endif
 }

@@ -122,10 +122,13 @@ KP_HD void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
     if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_SPREAD_UNSUPPORTED, 0);
     return;
   }
-  if (!sel_all_fast(B, x, cd)) {
+  const int why = sel_all_fast(B, x, cd);
+  if (why != SLOW_NONE) {
     if (B.tid() == 0) {
       a.slow[b] = 1;
       a.sink.count[b] = 0;
+      kp_atomic_add(&a.stats[0], 1u);
+      kp_atomic_add(&a.stats[why], 1u);
     }
   }
 }
@@ -155,6 +158,8 @@ KP_HD void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const
     if (B.tid() == 0) {
       a.slow[b] = 1;
       a.sink.count[b] = 0;
+      kp_atomic_add(&a.stats[0], 1u);
+      kp_atomic_add(&a.stats[SLOW_CLUSTER], 1u);
     }
   }
 }

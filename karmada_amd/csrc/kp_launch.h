@@ -17,6 +17,7 @@ struct KArgs {
   const int32_t* est;     // [B][Cp]
   Sink sink;
   int32_t* slow;          // [B] flag: needs the exact serial path
+  uint32_t* stats;        // [0]: bindings flagged for the serial path, [SLOW_*]: by reason
 };
 
 enum : int { SEL_LAUNCH_ALL = 0, SEL_LAUNCH_CLUSTER, SEL_LAUNCH_REGION_A, SEL_LAUNCH_REGION_B, SEL_LAUNCH_SLOW };

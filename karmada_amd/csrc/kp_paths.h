@@ -16,6 +16,10 @@ namespace kp {
 
 constexpr int kRegionMax = 256;
 
+// Reasons a binding leaves the fast paths for the exact serial path (stats[reason]).
+enum : int { SLOW_NONE = 0, SLOW_OVERFLOW_DUP = 1, SLOW_SCALE_DOWN = 2, SLOW_WRAP = 3, SLOW_TIE = 4, SLOW_WEIGHT = 5,
+             SLOW_CLUSTER = 6 };
+
 KP_HD inline uint64_t cand_key(const SelCtx& x, const Cands& cd, int i, int32_t est) {
   uint32_t rank = c_rank(cd, i);
   int64_t avail = (int64_t)est + (int64_t)assigned_of(*x.bv, *x.h, x.tgt_bits, rank);
@@ -85,24 +89,24 @@ KP_HD void emit_par(const BLK& B, const SelCtx& x, const Cands& cd, RepFn rep, b
 // Returns false when the binding needs the exact serial path (nothing written).
 // ----------------------------------------------------------------------------
 template <class BLK>
-KP_HD bool sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
+KP_HD int sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
   const BindHdr& h = *x.h;
   const bool desc = (h.flags & BF_UID_DESC) != 0;
   const bool prop = (h.flags & BF_EMPTY_PROP) != 0;
   if (!(h.flags & BF_WORKLOAD_ASSIGN)) {  // non-workload: all candidates, 0 replicas (common.go:72-82)
     emit_par(B, x, cd, [&](int) { return (int32_t)0; }, true);
-    return true;
+    return 0;
   }
-  if (h.flags & (BF_OVERFLOW | BF_DUP_TARGETS)) return false;
+  if (h.flags & (BF_OVERFLOW | BF_DUP_TARGETS)) return SLOW_OVERFLOW_DUP;
   const int st = h.strategy;
   if (st == ST_NONE) {
     if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_UNSUPPORTED_STRATEGY, 0);
-    return true;
+    return 0;
   }
   if (st == ST_DUPLICATED) {
     int32_t rep = h.replicas;
     emit_par(B, x, cd, [&](int) { return rep > 0 ? rep : (int32_t)0; }, prop);
-    return true;
+    return 0;
   }
   if (st == ST_STATIC) {
     int64_t wmax = 0, wsum = 0;
@@ -113,13 +117,13 @@ KP_HD bool sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
     }
     wmax = B.max64(wmax);
     wsum = B.sum64(wsum);
-    if (wmax >= kInt32Max) return false;
+    if (wmax >= kInt32Max) return SLOW_WEIGHT;
     bool all1 = wsum == 0;  // getStaticWeightInfoList: every candidate weight 1
     auto party = [&](int i) { return all1 || cd.v[i] > 0; };
     auto vote = [&](int i) { return all1 ? (int64_t)1 : (int64_t)cd.v[i]; };
     WebRes w = webster_par(B, cd, party, vote, h.replicas, desc);
     emit_par(B, x, cd, [&](int i) { return party(i) ? web_seats(w, vote(i), c_rank(cd, i)) : (int32_t)0; }, prop);
-    return true;
+    return 0;
   }
   // Dynamic / Aggregated (assignment.go:213-244)
   int32_t assigned = 0, ns = 0;
@@ -144,11 +148,37 @@ KP_HD bool sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
   else if (assigned > h.replicas) mode = 3;
   else if (assigned < h.replicas) mode = 1;
   else mode = 2;
-  if (mode == 3) return false;  // parties = scheduledClusters: exact serial path
+  if (mode == 3) {  // dynamicScaleDown: parties = scheduledClusters only, a small serial problem
+    if (prop) return SLOW_SCALE_DOWN;  // attachZeroReplicasCluster needs every candidate
+    const int nt = h.tgt_cnt;
+    const int cap = 2 * nt + 16;
+    if (sizeof(Item) * (size_t)nt + serial_scratch_bytes(cap) + 16 > 8 * (size_t)x.s->Cp) return SLOW_SCALE_DOWN;
+    B.sync();  // the candidate arrays are reused as scratch below
+    if (B.tid() == 0) {
+      Item* items = (Item*)cd.r;
+      int n = 0;
+      for (int j = 0; j < nt; j++) {
+        uint32_t r = (uint32_t)x.bv->ipool[h.tgt_off + 2 * j];
+        if (!mask_test(x.frow, (int)r)) continue;
+        items[n].rank = r;
+        items[n].alloc = x.erow[r];
+        items[n].avail = 0;
+        items[n].ovf = 0;
+        items[n].pad = 0;
+        n++;
+      }
+      SerialScratch sc = serial_scratch_carve(items + nt, cap);
+      SerialAssign sa{x, sc, desc};
+      SerialOut o = sa.run(items, n);
+      sink_serial(x, sc, o);
+    }
+    B.sync();
+    return 0;
+  }
   if (mode == 2) {              // unchanged: scheduledClusters, removeZero
     emit_par(B, x, cd, [&](int i) { return in_sched(x, c_rank(cd, i)) ? sched_rep_of(x, c_rank(cd, i)) : (int32_t)0; },
              prop);
-    return true;
+    return 0;
   }
   auto vote32 = [&](int i) -> int32_t {
     int32_t v = cd.v[i];
@@ -165,12 +195,12 @@ KP_HD bool sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
   sabs = B.sum64(sabs);
   vmin = B.min64(vmin);
   vtot = B.sum64(vtot);
-  if (vmin < 0 || sabs >= (int64_t)kInt32Max) return false;  // int32 wrap hazard
+  if (vmin < 0 || sabs >= (int64_t)kInt32Max) return SLOW_WRAP;  // int32 wrap hazard
   int32_t target = mode == 0 ? h.replicas : sub32(h.replicas, assigned);
   if ((int32_t)vtot < target) {
     if (B.tid() == 0)
       sink_error(x, KP_STATUS_UNSCHEDULABLE, mode == 0 ? KP_ERR_FRESH_NOT_ENOUGH : KP_ERR_SCALE_UP_NOT_ENOUGH, vtot);
-    return true;
+    return 0;
   }
   const bool merge = mode == 1;
   auto prior = [&](int i) { return merge && anyPriorPos && in_sched(x, c_rank(cd, i)) && sched_rep_of(x, c_rank(cd, i)) > 0; };
@@ -234,7 +264,7 @@ KP_HD bool sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
       ceq = B.sum64(ceq);
       int64_t need = tX - sgt;
       int64_t j = need <= 0 ? 1 : (vstar > 0 ? (need + vstar - 1) / vstar : ceq);
-      if (j < ceq) return false;  // tie group straddles the cut
+      if (j < ceq) return SLOW_TIE;  // tie group straddles the cut
       tie_all = true;
     }
   }
@@ -258,7 +288,7 @@ KP_HD bool sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
         return r;
       },
       prop);
-  return true;
+  return 0;
 }
 
 // ----------------------------------------------------------------------------

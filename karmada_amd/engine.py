@@ -27,7 +27,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libkp.so")
 KP_ABI_VERSION = 1
 
-_LIB = None
+_LIBS = {}
 
 # C-ABI entry points declared in include/kp/kp_api.h
 EXPORTS = (
@@ -45,9 +45,8 @@ class EngineError(RuntimeError):
 
 def load_library(path: str = LIB_PATH):
     """Loads libkp.so and declares the C-ABI signatures. Raises if it is absent."""
-    global _LIB
-    if _LIB is not None:
-        return _LIB
+    if path in _LIBS:
+        return _LIBS[path]
     if not os.path.exists(path):
         raise EngineError(f"{path} is missing: build it with `make -C karmada_amd/csrc` "
                           "(there is no CPU fallback)")
@@ -71,7 +70,7 @@ def load_library(path: str = LIB_PATH):
     L.kp_last_stage_times.argtypes = [vp, C.POINTER(api.kp_stage_times)]
     if L.kp_abi_version() != KP_ABI_VERSION:
         raise EngineError("libkp.so ABI version mismatch")
-    _LIB = L
+    _LIBS[path] = L
     return L
 
 
@@ -100,8 +99,8 @@ class ScheduleResult:
 class Engine:
     """One HIP device + stream (kp_engine)."""
 
-    def __init__(self, device: int = 0):
-        self.L = load_library()
+    def __init__(self, device: int = 0, lib_path: str = LIB_PATH):
+        self.L = load_library(lib_path)
         h = C.c_void_p()
         rc = self.L.kp_engine_create(device, C.byref(h))
         if rc != KP_OK:

@@ -1,0 +1,66 @@
+"""CPU parity of the engine's own code: libkp_cpusim.so runs engine.cpp and the
+kernel bodies of kp_kernels.h (1-thread block policy) on the host, checked
+against the oracle. The GPU build of the same bodies is checked in
+tests/test_gpu_parity.py; this file keeps the logic covered on every CPU run."""
+import os
+
+import pytest
+
+from karmada_amd import api, synth
+from karmada_amd.engine import Batch, Engine, Snapshot, PKG
+import oracle_lib as O
+
+CPUSIM = os.path.join(PKG, "libkp_cpusim.so")
+
+
+@pytest.fixture(scope="module")
+def engine():
+    os.environ.setdefault("KP_CPUSIM_THREADS", "8")
+    e = Engine(0, lib_path=CPUSIM)
+    yield e
+    e.close()
+
+
+def run(engine, u, opts, lo=0, hi=None):
+    hi = u.n_bindings if hi is None else hi
+    snap = Snapshot.from_structs(engine, u.clusters, u.n_clusters, u.names, opts)
+    b = Batch(snap, structs=u.binding_slice(lo, hi))
+    out = b.schedule()
+    b.close()
+    snap.close()
+    return out
+
+
+def compare(got, want, label):
+    bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert len(got) == len(want)
+    if bad:
+        msg = [f"{label}: {len(bad)}/{len(want)} differ"]
+        for i in bad[:4]:
+            msg += [f"  {i}: sim={got[i]}", f"  {i}: ref={want[i]}"]
+        pytest.fail("\n".join(msg))
+
+
+@pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
+    (1, 1, 10, 1000), (2, 2, 300, 400), (3, 3, 200, 300), (4, 4, 400, 500),
+    (6, 6, 120, 1500), (6, 7, 40, 1500), (6, 8, 1, 200), (6, 9, 257, 600),
+])
+def test_cpusim_schedule_parity(engine, config, seed, n_clusters, n_bindings):
+    u = synth.Universe(config, seed, n_clusters, 0, n_bindings)
+    opts = api.options()
+    ba, n = u.binding_slice(0, n_bindings)
+    want = O.schedule_c(u.clusters, u.n_clusters, ba, n, opts, O.FAST, 8)
+    compare(run(engine, u, opts), want, f"config {config} seed {seed}")
+
+
+@pytest.mark.parametrize("prop,plugins,gate", [
+    (True, api.PLUGIN_ALL, True),
+    (False, api.PLUGIN_ALL & ~api.PLUGIN_TAINT_TOLERATION, False),
+    (False, 0, True),
+])
+def test_cpusim_options(engine, prop, plugins, gate):
+    u = synth.Universe(6, 21, 90, 0, 800)
+    opts = api.options(empty_workload_propagation=prop, models_gate=gate, plugins=plugins)
+    ba, n = u.binding_slice(0, u.n_bindings)
+    want = O.schedule_c(u.clusters, u.n_clusters, ba, n, opts, O.FAST, 8)
+    compare(run(engine, u, opts), want, f"options {prop} {plugins} {gate}")
