@@ -135,3 +135,47 @@ int compact(stream_t, const uint64_t* start, const uint32_t* count, const uint64
 
 }  // namespace dev
 }  // namespace kp
+
+// ---------------------------------------------------------------------------
+// Test-only entry points into single kernel helpers (tests/test_cpusim_units.py)
+// ---------------------------------------------------------------------------
+extern "C" {
+
+// webster_par over n parties with the given votes (>= 0, < 2^31) and ranks
+// (name order); seats per party into out. ecap: enumeration capacity (0 =
+// bisection only).
+int kpsim_webster(const int32_t* votes, const uint32_t* ranks, int n, int32_t N, int desc, int ecap, int32_t* out) {
+  using namespace kp;
+  std::vector<uint32_t> r(n);
+  std::vector<int32_t> v(n);
+  for (int i = 0; i < n; i++) {
+    r[i] = ranks[i];
+    v[i] = votes[i];
+  }
+  Cands cd;
+  cd.r = r.data();
+  cd.v = v.data();
+  cd.F = n;
+  std::vector<uint32_t> hist(256);
+  std::vector<unsigned long long> wh(256);
+  std::vector<uint64_t> buf(ecap > 0 ? ecap : 1);
+  SelScratch ss{hist.data(), wh.data(), buf.data(), ecap};
+  int64_t red[8];
+  CpuBlk B{red};
+  auto party = [&](int) { return true; };
+  auto vote = [&](int i) { return (int64_t)v[i]; };
+  WebRes w = webster_par(B, cd, party, vote, N, desc != 0, ss);
+  for (int i = 0; i < n; i++) out[i] = web_seats(w, v[i], r[i]);
+  return w.mode;
+}
+
+// wsel_max over values (>= 0): largest v* with sum{v_i >= v*} >= target.
+int64_t kpsim_wsel_max(const int32_t* vals, int n, int64_t target) {
+  using namespace kp;
+  std::vector<unsigned long long> wh(256);
+  int64_t red[8];
+  CpuBlk B{red};
+  return wsel_max(B, wh.data(), n, [](int) { return true; }, [&](int i) { return (int64_t)vals[i]; }, target);
+}
+
+}  // extern "C"

@@ -942,7 +942,7 @@ size_t smem_pair(const kp_snapshot* s, int md_cap) {
 }
 size_t smem_all(const kp_snapshot* s) {
   int words = (s->Cp + 31) >> 5;
-  return 512 + 4 * (size_t)words + 8 * (size_t)s->Cp + 64;
+  return 512 + 4 * (size_t)words + 8 * (size_t)s->Cp + 2048 + 1024 + 8 * (size_t)sel_all_ecap(s->Cp) + 64;
 }
 size_t smem_cluster(const kp_snapshot* s, int cap) {
   int words = (s->Cp + 31) >> 5;
@@ -1075,7 +1075,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   bt->slow_slot = (size_t)s->Cp * 8 + (size_t)P * 8 + sizeof(Item) * s->Cp + 4 * (size_t)s->Cp +
                   serial_scratch_bytes(bt->slow_cap) + 1024;
   bt->slow_slot = (bt->slow_slot + 255) & ~(size_t)255;
-  bt->slow_grid = 256;
+  bt->slow_grid = (int)std::max<size_t>(1, std::min<size_t>(1024, bt->l_slow.size()));
   Arena& a = bt->dev;
   BindHdr* d_hdr;
   int32_t* d_ipool;

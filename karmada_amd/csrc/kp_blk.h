@@ -17,6 +17,9 @@
 #define KP_DEV
 #define KP_INLINE inline
 #endif
+// Forced inlining for the block-parallel helpers: an outlined call in a kernel
+// costs a stack frame (scratch) and spills around every call site.
+#define KP_FI KP_HD __attribute__((always_inline)) inline
 
 namespace kp {
 

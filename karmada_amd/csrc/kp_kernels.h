@@ -6,7 +6,7 @@
 //
 // Per-block LDS layouts (dynamic shared memory; sizes computed in engine.cpp):
 //   pair      [512 red | tgt bits | evict bits | md table]
-//   sel_all   [512 red | tgt bits | cand r [Cp] | cand v [Cp]]
+//   sel_all   [512 red | tgt bits | cand r [Cp] | cand v [Cp] | whist 2 KB | hist 1 KB | buf ecap*8]
 //   sel_clus  [512 red | hist 1 KB | items 2*kSmallMax | keys 2*kSmallMax | tgt | cand/serial area]
 //   region_a  [512 red | 8x8R + 4x4R region accumulators | tgt | cand]
 //   region_b  [512 red | hist | items | keys | heads 8R | rsel 4R | tgt | cand/serial area]
@@ -32,7 +32,7 @@ KP_HD inline SelCtx make_ctx(const KArgs& a, int b, const uint32_t* tgt_bits) {
 
 // Bitset (LDS) of the binding's spec.Clusters ranks (TargetContains, locality).
 template <class BLK>
-KP_HD void build_bits(const BLK& B, uint32_t* bits, int words, const int32_t* pool, int off, int cnt, int stride) {
+KP_FI void build_bits(const BLK& B, uint32_t* bits, int words, const int32_t* pool, int off, int cnt, int stride) {
   for (int i = B.tid(); i < words; i += B.nth()) bits[i] = 0;
   B.sync();
   for (int j = B.tid(); j < cnt; j += B.nth()) {
@@ -44,7 +44,7 @@ KP_HD void build_bits(const BLK& B, uint32_t* bits, int words, const int32_t* po
 
 // Status of bindings that never reach selection.
 template <class BLK>
-KP_HD bool pre_checks(const BLK& B, const SelCtx& x, int F) {
+KP_FI bool pre_checks(const BLK& B, const SelCtx& x, int F) {
   if (x.h->flags & BF_BAD) {
     if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, 0);
     return true;
@@ -62,7 +62,7 @@ KP_HD bool pre_checks(const BLK& B, const SelCtx& x, int F) {
 // per cluster. est_mode 1: raw GeneralEstimator answers for every cluster.
 // ---------------------------------------------------------------------------
 template <class BLK>
-KP_HD void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView& s, const BatchView& bv, int b0,
+KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView& s, const BatchView& bv, int b0,
                      uint64_t* fmask, int32_t* est, int64_t* score, int est_mode, int md_cap) {
   const int b = b0 + blk;
   const BindHdr h = bv.hdr[b];
@@ -104,7 +104,7 @@ KP_HD void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
 // Select stage: SEL_ALL (and spread-unsupported / FitError reporting)
 // ---------------------------------------------------------------------------
 template <class BLK>
-KP_HD void body_select_all(const BLK& B, int blk, unsigned char* smem, const KArgs& a) {
+KP_FI void body_select_all(const BLK& B, int blk, unsigned char* smem, const KArgs& a) {
   if (blk >= a.n) return;
   const int b = a.list[blk];
   const int words = (a.s.Cp + 31) >> 5;
@@ -112,6 +112,11 @@ KP_HD void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
   Cands cd;
   cd.r = tgt + words;
   cd.v = (int32_t*)(cd.r + a.s.Cp);
+  SelScratch ss;
+  ss.whist = (unsigned long long*)(cd.v + a.s.Cp);
+  ss.hist = (uint32_t*)(ss.whist + 256);
+  ss.buf = (uint64_t*)(ss.hist + 256);
+  ss.cap = sel_all_ecap(a.s.Cp);
   const BindHdr* h = &a.bv.hdr[b];
   build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
   SelCtx x = make_ctx(a, b, tgt);
@@ -122,7 +127,7 @@ KP_HD void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
     if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_SPREAD_UNSUPPORTED, 0);
     return;
   }
-  const int why = sel_all_fast(B, x, cd);
+  const int why = sel_all_fast(B, x, cd, ss);
   if (why != SLOW_NONE) {
     if (B.tid() == 0) {
       a.slow[b] = 1;
@@ -137,7 +142,7 @@ KP_HD void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
 // Select stage: SEL_CLUSTER
 // ---------------------------------------------------------------------------
 template <class BLK>
-KP_HD void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const KArgs& a, int scratch_cap) {
+KP_FI void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const KArgs& a, int scratch_cap) {
   if (blk >= a.n) return;
   const int b = a.list[blk];
   const int words = (a.s.Cp + 31) >> 5;
@@ -169,7 +174,7 @@ KP_HD void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const
 // rout: [n][n_regions]; rstat[blk] = -1 when the final status is already written.
 // ---------------------------------------------------------------------------
 template <class BLK>
-KP_HD void body_region_a(const BLK& B, int blk, unsigned char* smem, const KArgs& a, RegionOut* rout, int32_t* rstat) {
+KP_FI void body_region_a(const BLK& B, int blk, unsigned char* smem, const KArgs& a, RegionOut* rout, int32_t* rstat) {
   if (blk >= a.n) return;
   const int b = a.list[blk];
   const int words = (a.s.Cp + 31) >> 5;
@@ -220,7 +225,7 @@ KP_HD void body_region_a(const BLK& B, int blk, unsigned char* smem, const KArgs
 // Region stage B. rsel: [n][n_regions] selected region ids (path order); rnsel[n]:
 // count, -1000 when stage A already finalized, or -KP_ERR_* from the host step.
 template <class BLK>
-KP_HD void body_region_b(const BLK& B, int blk, unsigned char* smem, const KArgs& a, const int32_t* rsel,
+KP_FI void body_region_b(const BLK& B, int blk, unsigned char* smem, const KArgs& a, const int32_t* rsel,
                          const int32_t* rnsel, int scratch_cap) {
   if (blk >= a.n) return;
   const int b = a.list[blk];
@@ -289,6 +294,12 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
     const BindHdr* h = &a.bv.hdr[b];
     build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
     SelCtx x = make_ctx(a, b, tgt);
+    int done = 0;
+    if (B.tid() == 0 && scale_down_targets(x, ser, (size_t)serial_scratch_bytes(scratch_cap))) {
+      a.slow[b] = 0;
+      done = 1;
+    }
+    if (B.bcast(done)) continue;
     cd.F = gather(B, x, cd, false);
     const int F = cd.F;
     for (int i = B.tid(); i < P; i += B.nth()) keys[i] = i < F ? cand_key(x, cd, i, cd.v[i]) : ~0ull;
@@ -370,7 +381,7 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
 
 // Gathers per-binding results into CSR order (offsets computed on the host).
 template <class BLK>
-KP_HD void body_compact(const BLK& B, int blk, const uint64_t* start, const uint32_t* count, const uint64_t* offsets,
+KP_FI void body_compact(const BLK& B, int blk, const uint64_t* start, const uint32_t* count, const uint64_t* offsets,
                         const uint32_t* in_idx, const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n) {
   if (blk >= n) return;
   uint64_t s = start[blk], o = offsets[blk];

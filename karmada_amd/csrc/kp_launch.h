@@ -34,4 +34,7 @@ struct SelectExtra {
 
 constexpr int kBlock = 256;
 
+// Enumeration capacity (u64 entries) of the SEL_ALL selection buffer.
+KP_HD inline int sel_all_ecap(int Cp) { return Cp / 2 > 64 ? Cp / 2 : 64; }
+
 }  // namespace kp

@@ -48,7 +48,7 @@ KP_HD inline bool in_sched(const SelCtx& x, uint32_t rank) {
 // of candidate i in the result; `keep_all` emits every candidate (non-workload /
 // EnableEmptyWorkloadPropagation), otherwise only rep > 0 (removeZeroReplicasCluster).
 template <class BLK, class RepFn>
-KP_HD void emit_par(const BLK& B, const SelCtx& x, const Cands& cd, RepFn rep, bool keep_all) {
+KP_FI void emit_par(const BLK& B, const SelCtx& x, const Cands& cd, RepFn rep, bool keep_all) {
   int64_t cnt = 0;
   for (int i = B.tid(); i < cd.F; i += B.nth())
     if (keep_all || rep(i) > 0) cnt++;
@@ -84,12 +84,46 @@ KP_HD void emit_par(const BLK& B, const SelCtx& x, const Cands& cd, RepFn rep, b
   }
 }
 
+// dynamicScaleDown (division_algorithm.go:103-119) for SEL_ALL bindings: the
+// parties are the scheduled clusters only, so the serial answer needs no
+// candidate sort. Thread 0; `mem` holds Items[tgt_cnt] + serial scratch.
+// Returns false when the binding needs the general serial path instead.
+KP_HD inline bool scale_down_targets(const SelCtx& x, unsigned char* mem, size_t mem_bytes) {
+  const BindHdr& h = *x.h;
+  if (h.sel != SEL_ALL || !(h.flags & BF_WORKLOAD_ASSIGN)) return false;
+  if (h.flags & (BF_OVERFLOW | BF_DUP_TARGETS | BF_EMPTY_PROP | BF_FRESH)) return false;
+  if (h.strategy != ST_DYNAMIC && h.strategy != ST_AGGREGATED) return false;
+  const int nt = h.tgt_cnt;
+  const int cap = 2 * nt + 16;
+  if (sizeof(Item) * (size_t)nt + serial_scratch_bytes(cap) + 16 > mem_bytes) return false;
+  Item* items = (Item*)mem;
+  int n = 0;
+  int32_t assigned = 0;
+  for (int j = 0; j < nt; j++) {
+    uint32_t r = (uint32_t)x.bv->ipool[h.tgt_off + 2 * j];
+    if (!mask_test(x.frow, (int)r)) continue;
+    assigned = add32(assigned, x.bv->ipool[h.tgt_off + 2 * j + 1]);
+    items[n].rank = r;
+    items[n].alloc = x.erow[r];
+    items[n].avail = 0;
+    items[n].ovf = 0;
+    items[n].pad = 0;
+    n++;
+  }
+  if (!(assigned > h.replicas)) return false;
+  SerialScratch sc = serial_scratch_carve(items + nt, cap);
+  SerialAssign sa{x, sc, (h.flags & BF_UID_DESC) != 0};
+  SerialOut o = sa.run(items, n);
+  sink_serial(x, sc, o);
+  return true;
+}
+
 // ----------------------------------------------------------------------------
 // SEL_ALL: every feasible cluster is selected (select_clusters.go:29-32).
 // Returns false when the binding needs the exact serial path (nothing written).
 // ----------------------------------------------------------------------------
 template <class BLK>
-KP_HD int sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
+KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd, const SelScratch& ss) {
   const BindHdr& h = *x.h;
   const bool desc = (h.flags & BF_UID_DESC) != 0;
   const bool prop = (h.flags & BF_EMPTY_PROP) != 0;
@@ -121,7 +155,7 @@ KP_HD int sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
     bool all1 = wsum == 0;  // getStaticWeightInfoList: every candidate weight 1
     auto party = [&](int i) { return all1 || cd.v[i] > 0; };
     auto vote = [&](int i) { return all1 ? (int64_t)1 : (int64_t)cd.v[i]; };
-    WebRes w = webster_par(B, cd, party, vote, h.replicas, desc);
+    WebRes w = webster_par(B, cd, party, vote, h.replicas, desc, ss);
     emit_par(B, x, cd, [&](int i) { return party(i) ? web_seats(w, vote(i), c_rank(cd, i)) : (int32_t)0; }, prop);
     return 0;
   }
@@ -148,33 +182,7 @@ KP_HD int sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
   else if (assigned > h.replicas) mode = 3;
   else if (assigned < h.replicas) mode = 1;
   else mode = 2;
-  if (mode == 3) {  // dynamicScaleDown: parties = scheduledClusters only, a small serial problem
-    if (prop) return SLOW_SCALE_DOWN;  // attachZeroReplicasCluster needs every candidate
-    const int nt = h.tgt_cnt;
-    const int cap = 2 * nt + 16;
-    if (sizeof(Item) * (size_t)nt + serial_scratch_bytes(cap) + 16 > 8 * (size_t)x.s->Cp) return SLOW_SCALE_DOWN;
-    B.sync();  // the candidate arrays are reused as scratch below
-    if (B.tid() == 0) {
-      Item* items = (Item*)cd.r;
-      int n = 0;
-      for (int j = 0; j < nt; j++) {
-        uint32_t r = (uint32_t)x.bv->ipool[h.tgt_off + 2 * j];
-        if (!mask_test(x.frow, (int)r)) continue;
-        items[n].rank = r;
-        items[n].alloc = x.erow[r];
-        items[n].avail = 0;
-        items[n].ovf = 0;
-        items[n].pad = 0;
-        n++;
-      }
-      SerialScratch sc = serial_scratch_carve(items + nt, cap);
-      SerialAssign sa{x, sc, desc};
-      SerialOut o = sa.run(items, n);
-      sink_serial(x, sc, o);
-    }
-    B.sync();
-    return 0;
-  }
+  if (mode == 3) return SLOW_SCALE_DOWN;  // parties = scheduledClusters: serial kernel (k_slow)
   if (mode == 2) {              // unchanged: scheduledClusters, removeZero
     emit_par(B, x, cd, [&](int i) { return in_sched(x, c_rank(cd, i)) ? sched_rep_of(x, c_rank(cd, i)) : (int32_t)0; },
              prop);
@@ -233,25 +241,10 @@ KP_HD int sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
     if (xmax < 0 || xsum < tX) {
       noCut = true;  // every element of X is taken
     } else {
-      auto sge = [&](int64_t v0) {
-        int64_t s = 0;
-        for (int i = B.tid(); i < cd.F; i += B.nth())
-          if (inX(i)) {
-            int64_t v = vote32(i);
-            if (v >= v0) s += v;
-          }
-        return B.sum64(s);
-      };
       if (tX <= 0) {
         vstar = xmax;  // the first element alone reaches the target
-      } else {
-        int64_t lo = 0, hi = xmax;  // largest v with sge(v) >= tX
-        while (lo < hi) {
-          int64_t mid = lo + (hi - lo + 1) / 2;
-          if (sge(mid) >= tX) lo = mid;
-          else hi = mid - 1;
-        }
-        vstar = lo;
+      } else {  // largest v with sum{v_i >= v} >= tX
+        vstar = wsel_max(B, ss.whist, cd.F, inX, [&](int i) { return (int64_t)vote32(i); }, tX);
       }
       int64_t sgt = 0, ceq = 0;
       for (int i = B.tid(); i < cd.F; i += B.nth())
@@ -278,7 +271,7 @@ KP_HD int sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
     return v > vstar || (v == vstar && tie_all);
   };
   auto vote = [&](int i) { return (int64_t)vote32(i); };
-  WebRes w = webster_par(B, cd, member, vote, target, desc);
+  WebRes w = webster_par(B, cd, member, vote, target, desc, ss);
   emit_par(
       B, x, cd,
       [&](int i) {
@@ -295,7 +288,7 @@ KP_HD int sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd) {
 // Small selected list -> serial AssignReplicas (thread 0) -> sink.
 // ----------------------------------------------------------------------------
 template <class BLK>
-KP_HD void assign_small(const BLK& B, const SelCtx& x, const Item* items, int n, void* scratch, int cap) {
+KP_FI void assign_small(const BLK& B, const SelCtx& x, const Item* items, int n, void* scratch, int cap) {
   if (B.tid() == 0) {
     SerialScratch sc = serial_scratch_carve(scratch, cap);
     SerialAssign sa{x, sc, (x.h->flags & BF_UID_DESC) != 0};
@@ -310,7 +303,7 @@ KP_HD void assign_small(const BLK& B, const SelCtx& x, const Item* items, int n,
 // items: LDS buffer of kSmallMax*2 Items. Returns false -> slow path.
 // ----------------------------------------------------------------------------
 template <class BLK>
-KP_HD bool sel_cluster_fast(const BLK& B, const SelCtx& x, const Cands& cd, uint32_t* hist, Item* items,
+KP_FI bool sel_cluster_fast(const BLK& B, const SelCtx& x, const Cands& cd, uint32_t* hist, Item* items,
                             uint64_t* keys, void* scratch, int cap) {
   const BindHdr& h = *x.h;
   const int F = cd.F;
@@ -477,7 +470,7 @@ KP_HD inline int64_t go_ceil_div_i64(int32_t a, int64_t b) {
   return (int64_t)q;
 }
 template <class BLK>
-KP_HD void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L, RegionOut* out) {
+KP_FI void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L, RegionOut* out) {
   const BindHdr& h = *x.h;
   const int R = x.s->n_regions;
   for (int r = B.tid(); r < R; r += B.nth()) {
@@ -587,7 +580,7 @@ KP_HD void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L,
 // (select_clusters_by_region.go:41-63). sel: selected region ids in path order.
 // ----------------------------------------------------------------------------
 template <class BLK>
-KP_HD void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_t* sel, int nsel, uint32_t* hist,
+KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_t* sel, int nsel, uint32_t* hist,
                     unsigned long long* heads, int32_t* rsel, Item* items, uint64_t* keys, void* scratch, int cap) {
   const BindHdr& h = *x.h;
   const int R = x.s->n_regions;

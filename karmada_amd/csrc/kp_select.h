@@ -485,7 +485,7 @@ KP_HD inline void sink_error(const SelCtx& x, int status, int err, int64_t arg) 
 // Candidate gather: feasible clusters of the binding in rank order.
 // ----------------------------------------------------------------------------
 template <class BLK>
-KP_HD int gather(const BLK& B, const SelCtx& x, Cands cd, bool weights) {
+KP_FI int gather(const BLK& B, const SelCtx& x, Cands cd, bool weights) {
   const SnapView& s = *x.s;
   const BindHdr& h = *x.h;
   int F = 0;
@@ -544,22 +544,46 @@ KP_HD inline int32_t web_seats(const WebRes& w, int64_t v, uint32_t rank) {
   return (int32_t)base;
 }
 
+// Scratch for the exact selection steps (LDS): a 256-bin histogram and a key
+// buffer of `cap` u64 entries. cap == 0 -> bisection only.
+struct SelScratch {
+  uint32_t* hist;
+  unsigned long long* whist;  // 256 u64 bins (weighted selection); may alias hist storage
+  uint64_t* buf;
+  int cap;
+};
+
+template <class BLK, class Pred, class Key>
+KP_FI uint64_t radix_select(const BLK& B, uint32_t* hist, int F, Pred pred, Key key, int64_t k);
+
+// AllocateWebsterSeats (webstermethod.go:112-161) for parties with int32 votes
+// >= 0 and no initial seats, block-parallel. The N-th largest seat priority
+// t* = max{t : cnt_ge(t) >= N} is bracketed by the divisor-method bounds
+//   V/(2N+P) <= t* < V/(2N-P)   (P = parties with votes > 0)
+// verified with exact counts, narrowed by bisection over the double's bit
+// pattern only while more than sc.cap priorities lie in the bracket, then the
+// bracketed priorities are enumerated into LDS and t* is radix-selected. Seats
+// strictly above t* are exact per party; the tie group at t* is ordered by
+// (seats asc, name) as the heap's tie-breaker orders it (tie_key).
 template <class BLK, class Pred, class Vote>
-KP_HD WebRes webster_par(const BLK& B, const Cands& cd, Pred party, Vote vote, int32_t N, bool desc) {
+KP_FI WebRes webster_par(const BLK& B, const Cands& cd, Pred party, Vote vote, int32_t N, bool desc,
+                         const SelScratch& sc) {
   WebRes r;
   r.N = N;
   r.desc = desc;
   r.t = 0;
   r.tie = 0;
-  int64_t V = 0, vmax = 0;
+  int64_t V = 0, vmax = 0, P = 0;
   for (int i = B.tid(); i < cd.F; i += B.nth())
     if (party(i)) {
       int64_t v = vote(i);
       V += v;
       if (v > vmax) vmax = v;
+      if (v > 0) P++;
     }
   V = B.sum64(V);
   vmax = B.max64(vmax);
+  P = B.sum64(P);
   if (V == 0) {
     r.mode = 0;
     return r;
@@ -569,24 +593,83 @@ KP_HD WebRes webster_par(const BLK& B, const Cands& cd, Pred party, Vote vote, i
     return r;
   }
   r.mode = 2;
-  auto cnt_ge = [&](double t) {
+  const int64_t capN = (int64_t)N;
+  // two thresholds per pass
+  auto cnt2 = [&](double ta, double tb, int64_t* ca, int64_t* cb) {
+    int64_t a = 0, b = 0;
+    for (int i = B.tid(); i < cd.F; i += B.nth())
+      if (party(i)) {
+        int64_t v = vote(i);
+        a += w_count(v, ta, capN, true);
+        b += w_count(v, tb, capN, true);
+      }
+    *ca = B.sum64(a);
+    *cb = B.sum64(b);
+  };
+  auto cnt1 = [&](double t) {
     int64_t c = 0;
     for (int i = B.tid(); i < cd.F; i += B.nth())
-      if (party(i)) c += w_count(vote(i), t, (int64_t)N, true);
+      if (party(i)) c += w_count(vote(i), t, capN, true);
     return B.sum64(c);
   };
-  double tmax = (double)vmax;
-  double tstar;
-  if (cnt_ge(tmax) >= N) {
-    tstar = tmax;
-  } else {
-    uint64_t lo = 1, hi = dbits(tmax);  // cnt_ge(lo) >= N, cnt_ge(hi) < N
-    while (hi - lo > 1) {
-      uint64_t mid = lo + (hi - lo) / 2;
-      if (cnt_ge(bitsd(mid)) >= N) lo = mid;
-      else hi = mid;
+  // invariant: cnt_ge(lo) >= N > cnt_ge(hi), lo < hi (as bit patterns)
+  uint64_t lo = 1, hi = dbits((double)vmax) + 1;
+  int64_t clo = -1, chi = 0;
+  {
+    double l0 = (double)V / (double)(2 * (int64_t)N + P);
+    l0 = bitsd(dbits(l0) > 64 ? dbits(l0) - 64 : 1);  // a few ulps below the bound
+    double h0 = 2 * (int64_t)N - P - 1 > 0 ? (double)V / (double)(2 * (int64_t)N - P - 1) : (double)vmax;
+    uint64_t hb = dbits(h0) + 64;
+    if (hb > hi) hb = hi;
+    int64_t cl, ch;
+    cnt2(bitsd(dbits(l0)), bitsd(hb), &cl, &ch);
+    if (cl >= N) {
+      lo = dbits(l0);
+      clo = cl;
     }
+    if (ch < N) {
+      hi = hb;
+      chi = ch;
+    }
+    if (clo < 0) clo = cnt1(bitsd(lo));
+  }
+  // narrow while too many priorities lie in [lo, hi)
+  while (hi - lo > 1 && clo - chi > (int64_t)sc.cap) {
+    uint64_t mid = lo + (hi - lo) / 2;
+    int64_t c = cnt1(bitsd(mid));
+    if (c >= N) {
+      lo = mid;
+      clo = c;
+    } else {
+      hi = mid;
+      chi = c;
+    }
+  }
+  double tstar;
+  if (hi - lo <= 1) {
     tstar = bitsd(lo);
+  } else {
+    // enumerate every priority in [lo, hi) and select the (N - chi)-th largest
+    const double tl = bitsd(lo), th = bitsd(hi);
+    int E = 0;
+    for (int t0 = 0; t0 < cd.F; t0 += B.nth()) {
+      int i = t0 + B.tid();
+      int64_t k0 = 0, k1 = 0, v = 0;
+      if (i < cd.F && party(i)) {
+        v = vote(i);
+        k0 = w_count(v, th, capN, true);
+        k1 = w_count(v, tl, capN, true);
+      }
+      int32_t tot;
+      int32_t off = B.excl_scan((int32_t)(k1 - k0), &tot);
+      for (int64_t k = k0; k < k1; k++) sc.buf[E + off + (k - k0)] = dbits(w_prio(v, k));
+      E += tot;
+    }
+    B.sync();
+    const int64_t kth_small = (int64_t)E - ((int64_t)N - chi) + 1;
+    auto all = [&](int) { return true; };
+    auto key = [&](int i) { return (uint64_t)sc.buf[i]; };
+    tstar = bitsd(radix_select(B, sc.hist, E, all, key, kth_small));
   }
   r.t = tstar;
   // seats strictly above t*, then the tie group at t* ordered by (k asc, name)
@@ -601,33 +684,89 @@ KP_HD WebRes webster_par(const BLK& B, const Cands& cd, Pred party, Vote vote, i
   S = B.sum64(S);
   T = B.sum64(T);
   int64_t M = (int64_t)N - S;
+  auto is_tie = [&](int i, int64_t* base) {
+    int64_t v = vote(i);
+    *base = w_count(v, tstar, (int64_t)N + 1, false);
+    return w_prio(v, *base) == tstar;
+  };
   if (M >= T) {
     r.tie = ~0ull;
-  } else {
-    uint64_t lo = 0, hi = (uint64_t)1 << 62;  // smallest x with count(tk <= x) >= M
-    while (lo < hi) {
-      uint64_t mid = lo + (hi - lo) / 2;
-      int64_t c = 0;
-      for (int i = B.tid(); i < cd.F; i += B.nth())
-        if (party(i)) {
-          int64_t v = vote(i);
-          int64_t base = w_count(v, tstar, (int64_t)N + 1, false);
-          if (w_prio(v, base) == tstar && tie_key(base, c_rank(cd, i), desc) <= mid) c++;
-        }
-      c = B.sum64(c);
-      if (c >= M) hi = mid;
-      else lo = mid + 1;
+  } else if (T <= (int64_t)sc.cap) {
+    int n = 0;
+    for (int t0 = 0; t0 < cd.F; t0 += B.nth()) {
+      int i = t0 + B.tid();
+      int64_t base = 0;
+      bool e = i < cd.F && party(i) && is_tie(i, &base);
+      int32_t tot;
+      int32_t off = B.excl_scan(e ? 1 : 0, &tot);
+      if (e) sc.buf[n + off] = tie_key(base, c_rank(cd, i), desc);
+      n += tot;
     }
-    r.tie = lo;
+    B.sync();
+    auto all = [&](int) { return true; };
+    auto key = [&](int i) { return (uint64_t)sc.buf[i]; };
+    r.tie = radix_select(B, sc.hist, n, all, key, M);
+  } else {
+    uint64_t tlo = 0, thi = (uint64_t)1 << 62;  // smallest x with count(tk <= x) >= M
+    while (tlo < thi) {
+      uint64_t mid = tlo + (thi - tlo) / 2;
+      int64_t c = 0;
+      for (int i = B.tid(); i < cd.F; i += B.nth()) {
+        int64_t base;
+        if (party(i) && is_tie(i, &base) && tie_key(base, c_rank(cd, i), desc) <= mid) c++;
+      }
+      c = B.sum64(c);
+      if (c >= M) thi = mid;
+      else tlo = mid + 1;
+    }
+    r.tie = tlo;
   }
   return r;
+}
+
+// Largest value v* over the predicate set (values in [0, 2^31)) such that the
+// values >= v* sum to at least `target` (>= 1; the caller guarantees the total
+// reaches it): an 8-bit radix descent with value-weighted bins.
+template <class BLK, class Pred, class Val>
+KP_FI int64_t wsel_max(const BLK& B, unsigned long long* wh, int F, Pred pred, Val val, int64_t target) {
+  uint32_t prefix = 0;
+  int64_t above = 0;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = B.tid(); i < 256; i += B.nth()) wh[i] = 0;
+    B.sync();
+    const uint32_t hm = shift == 24 ? 0u : (~0u << (shift + 8));
+    for (int i = B.tid(); i < F; i += B.nth())
+      if (pred(i)) {
+        uint32_t v = (uint32_t)val(i);
+        if ((v & hm) == (prefix & hm) && v) kp_atomic_add(&wh[(v >> shift) & 255], (unsigned long long)v);
+      }
+    B.sync();
+    int64_t sel = 0, ab = above;
+    if (B.tid() == 0) {
+      int64_t cum = above;
+      int bin = 0;
+      for (int b = 255; b >= 0; b--) {
+        if (cum + (int64_t)wh[b] >= target) {
+          bin = b;
+          break;
+        }
+        cum += (int64_t)wh[b];
+      }
+      sel = bin;
+      ab = cum;
+    }
+    sel = B.bcast(sel);
+    above = B.bcast(ab);
+    prefix |= (uint32_t)sel << shift;
+  }
+  return (int64_t)prefix;
 }
 
 // ----------------------------------------------------------------------------
 // k-th smallest (1-based) 64-bit key over a predicate set: 8-bit radix select.
 // ----------------------------------------------------------------------------
 template <class BLK, class Pred, class Key>
-KP_HD uint64_t radix_select(const BLK& B, uint32_t* hist, int F, Pred pred, Key key, int64_t k) {
+KP_FI uint64_t radix_select(const BLK& B, uint32_t* hist, int F, Pred pred, Key key, int64_t k) {
   uint64_t prefix = 0;
   for (int shift = 56; shift >= 0; shift -= 8) {
     for (int i = B.tid(); i < 256; i += B.nth()) hist[i] = 0;

@@ -1,0 +1,91 @@
+"""Kernel helpers of kp_select.h, run on the host through libkp_cpusim.so
+(test-only), against the oracle's restatement of the reference:
+
+  webster_par  vs AllocateWebsterSeats (pkg/util/helper/webstermethod.go:112-161)
+  wsel_max     vs the Aggregated prefix cut's value threshold
+               (pkg/scheduler/core/division_algorithm.go:81-89), brute force.
+"""
+import ctypes as C
+import os
+import random
+
+import pytest
+
+from karmada_amd import api
+from karmada_amd.engine import PKG
+import oracle_lib as O
+
+SIM = C.CDLL(os.path.join(PKG, "libkp_cpusim.so"))
+SIM.kpsim_webster.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_uint32), C.c_int, C.c_int32, C.c_int, C.c_int,
+                              C.POINTER(C.c_int32)]
+SIM.kpsim_wsel_max.restype = C.c_int64
+SIM.kpsim_wsel_max.argtypes = [C.POINTER(C.c_int32), C.c_int, C.c_int64]
+
+
+def oracle_webster(votes, N, desc):
+    L = O.lib()
+    w = api.World()
+    n = len(votes)
+    names, _ = w.arr(api.kp_str, [w.s(f"c{i:06d}") for i in range(n)])
+    vv = (C.c_int64 * max(1, n))(*votes)
+    out = (C.c_int32 * max(1, n))()
+    k = L.kpo_allocate_webster(N, names, vv, n, None, None, 0, 2 if desc else 1, api.kp_str(None, 0), out, n)
+    assert k == n
+    return [out[i] for i in range(n)]
+
+
+def sim_webster(votes, N, desc, ecap):
+    n = len(votes)
+    vv = (C.c_int32 * max(1, n))(*votes)
+    rr = (C.c_uint32 * max(1, n))(*range(n))
+    out = (C.c_int32 * max(1, n))()
+    SIM.kpsim_webster(vv, rr, n, N, 1 if desc else 0, ecap, out)
+    return [out[i] for i in range(n)]
+
+
+def vote_sets(rng):
+    for _ in range(60):
+        n = rng.choice([1, 2, 3, 7, 12, 13, 50, 200, 700])
+        kind = rng.choice(["uniform", "ties", "zeros", "huge", "powers", "one-big"])
+        if kind == "uniform":
+            v = [rng.randint(0, 1000) for _ in range(n)]
+        elif kind == "ties":
+            v = [rng.choice([3, 5, 15, 45]) for _ in range(n)]
+        elif kind == "zeros":
+            v = [rng.choice([0, 0, 0, 1, 2]) for _ in range(n)]
+        elif kind == "huge":
+            v = [rng.randint(0, 2**31 - 1) for _ in range(n)]
+        elif kind == "powers":
+            v = [3 ** rng.randint(0, 12) for _ in range(n)]
+        else:
+            v = [1] * n
+            v[rng.randrange(n)] = 100000
+        yield v
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_webster_par_matches_reference_heap(seed):
+    rng = random.Random(seed)
+    for votes in vote_sets(rng):
+        if sum(votes) == 0:
+            continue
+        N = rng.choice([1, 2, 5, 17, 100, 999, 4000, 65536])
+        desc = rng.random() < 0.5
+        want = oracle_webster(votes, N, desc)
+        for ecap in (0, 4, 64, 4096):
+            got = sim_webster(votes, N, desc, ecap)
+            assert got == want, (votes[:20], N, desc, ecap)
+
+
+def test_wsel_max_brute_force():
+    rng = random.Random(7)
+    for _ in range(300):
+        n = rng.randint(1, 60)
+        vals = [rng.choice([0, 1, 2, 5, 255, 256, 257, 65535, 65536, rng.randint(0, 2**31 - 1)]) for _ in range(n)]
+        tot = sum(vals)
+        if tot == 0:
+            continue
+        target = rng.randint(1, tot)
+        want = max(v for v in set(vals) if v > 0 and sum(x for x in vals if x >= v) >= target)
+        arr = (C.c_int32 * n)(*vals)
+        assert SIM.kpsim_wsel_max(arr, n, target) == want, (vals, target)
