@@ -111,7 +111,7 @@ struct kp_snapshot {
   // host copies
   std::vector<uint32_t> flags;
   std::vector<int32_t> provider, region, region_idx, zone_off, zone_ids, label_val, taint_off, taint_key, taint_val,
-      taint_eff, mgrp_off, mgrp_tid;
+      taint_eff, mgrp_off, mgrp_tid, mg_tid, mg_cnt;
   std::vector<int64_t> provider_int, region_int, allowed, avail, mgrp_cnt, tmpl;
   std::vector<uint64_t> api_bits;
   Arena dev;
@@ -379,8 +379,17 @@ int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_opti
   pad1(s->taint_key);
   pad1(s->taint_val);
   pad1(s->taint_eff);
-  pad1(s->mgrp_tid);
-  pad1(s->mgrp_cnt);
+  // model groups transposed to [kmax][Cp] so a wave reads 64 clusters' k-th group coalesced
+  int kmax = 0;
+  for (int r = 0; r < C; r++) kmax = std::max(kmax, s->mgrp_off[r + 1] - s->mgrp_off[r]);
+  s->mg_tid.assign((size_t)std::max(kmax, 1) * Cp, 0);
+  s->mg_cnt.assign((size_t)std::max(kmax, 1) * Cp, 0);
+  for (int r = 0; r < C; r++)
+    for (int g = s->mgrp_off[r]; g < s->mgrp_off[r + 1]; g++) {
+      size_t k = (size_t)(g - s->mgrp_off[r]);
+      s->mg_tid[k * Cp + r] = s->mgrp_tid[g];
+      s->mg_cnt[k * Cp + r] = (int32_t)std::min<int64_t>(s->mgrp_cnt[g], kInt32Max);
+    }
   // upload
   SnapView& v = s->view;
   v.C = C;
@@ -393,8 +402,8 @@ int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_opti
   v.n_regions = (int)s->regions.names.size();
   Arena& a = s->dev;
   uint32_t *d_flags, *d_perm;
-  int32_t *d_prov, *d_reg, *d_regidx, *d_zoff, *d_zid, *d_lbl, *d_toff, *d_tk, *d_tv, *d_te, *d_moff, *d_mtid;
-  int64_t *d_pint, *d_rint, *d_allowed, *d_avail, *d_mcnt, *d_tmpl;
+  int32_t *d_prov, *d_reg, *d_regidx, *d_zoff, *d_zid, *d_lbl, *d_toff, *d_tk, *d_tv, *d_te, *d_mtid, *d_mcnt;
+  int64_t *d_pint, *d_rint, *d_allowed, *d_avail, *d_tmpl;
   uint64_t* d_api;
   a.add(&d_flags, Cp);
   a.add(&d_perm, Cp);
@@ -408,13 +417,12 @@ int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_opti
   a.add(&d_tk, s->taint_key.size());
   a.add(&d_tv, s->taint_val.size());
   a.add(&d_te, s->taint_eff.size());
-  a.add(&d_moff, C + 1);
-  a.add(&d_mtid, s->mgrp_tid.size());
+  a.add(&d_mtid, s->mg_tid.size());
+  a.add(&d_mcnt, s->mg_cnt.size());
   a.add(&d_pint, Cp);
   a.add(&d_rint, Cp);
   a.add(&d_allowed, Cp);
   a.add(&d_avail, s->avail.size());
-  a.add(&d_mcnt, s->mgrp_cnt.size());
   a.add(&d_tmpl, s->tmpl.size());
   a.add(&d_api, s->api_bits.size());
   HIPCHK(a.alloc());
@@ -433,13 +441,12 @@ int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_opti
   HIPCHK(up(d_tk, s->taint_key.data(), 4 * s->taint_key.size()));
   HIPCHK(up(d_tv, s->taint_val.data(), 4 * s->taint_val.size()));
   HIPCHK(up(d_te, s->taint_eff.data(), 4 * s->taint_eff.size()));
-  HIPCHK(up(d_moff, s->mgrp_off.data(), 4 * (C + 1)));
-  HIPCHK(up(d_mtid, s->mgrp_tid.data(), 4 * s->mgrp_tid.size()));
+  HIPCHK(up(d_mtid, s->mg_tid.data(), 4 * s->mg_tid.size()));
+  HIPCHK(up(d_mcnt, s->mg_cnt.data(), 4 * s->mg_cnt.size()));
   HIPCHK(up(d_pint, s->provider_int.data(), 8 * Cp));
   HIPCHK(up(d_rint, s->region_int.data(), 8 * Cp));
   HIPCHK(up(d_allowed, s->allowed.data(), 8 * Cp));
   HIPCHK(up(d_avail, s->avail.data(), 8 * s->avail.size()));
-  HIPCHK(up(d_mcnt, s->mgrp_cnt.data(), 8 * s->mgrp_cnt.size()));
   HIPCHK(up(d_tmpl, s->tmpl.data(), 8 * s->tmpl.size()));
   HIPCHK(up(d_api, s->api_bits.data(), 8 * s->api_bits.size()));
   HIPCHK(dev::sync(e->stream));
@@ -460,9 +467,9 @@ int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_opti
   v.api_bits = d_api;
   v.allowed = d_allowed;
   v.avail = d_avail;
-  v.mgrp_off = d_moff;
-  v.mgrp_tid = d_mtid;
-  v.mgrp_cnt = d_mcnt;
+  v.kmax = kmax;
+  v.mg_tid = d_mtid;
+  v.mg_cnt = d_mcnt;
   v.tmpl = d_tmpl;
   return KP_OK;
 }

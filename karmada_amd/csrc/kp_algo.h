@@ -250,9 +250,11 @@ KP_HD inline int32_t general_estimate(const SnapView& s, const BatchView& bv, co
     // getMaximumReplicasBasedOnResourceModels: each identical model node absorbs
     // exactly its initial MaxDivided, capped at MaxInt32.
     int64_t total = 0;
-    for (int g = s.mgrp_off[c]; g < s.mgrp_off[c + 1]; g++) {
-      int64_t d = md ? md[s.mgrp_tid[g]] : template_md(s, bv, h, s.mgrp_tid[g]);
-      int64_t cnt = s.mgrp_cnt[g];
+    for (int k = 0; k < s.kmax; k++) {
+      const int64_t cnt = s.mg_cnt[(size_t)k * s.Cp + c];
+      if (cnt == 0) continue;
+      const int32_t tid = s.mg_tid[(size_t)k * s.Cp + c];
+      int64_t d = md ? md[tid] : template_md(s, bv, h, tid);
       if (d > 0 && cnt > (int64_t)kInt32Max / d) {
         total = kInt32Max;
         break;

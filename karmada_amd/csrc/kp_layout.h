@@ -129,6 +129,7 @@ struct alignas(16) BindHdr {
 struct SnapView {
   int32_t C, Cp, W;              // clusters, padded clusters, ceil(C/64)
   int32_t n_label_keys, api_words, n_res, n_tmpl, n_regions;
+  int32_t kmax;                  // model node groups per cluster (max over the snapshot)
   const uint32_t* flags;         // [Cp]
   const int32_t* provider;       // [Cp] string id or -1
   const int32_t* region;         // [Cp] string id or -1
@@ -145,9 +146,8 @@ struct SnapView {
   const uint64_t* api_bits;      // [api_words][Cp]
   const int64_t* allowed;        // [Cp] getAllowedPodNumber
   const int64_t* avail;          // [n_res][Cp] summary path available (milli for cpu), <=0 -> 0
-  const int32_t* mgrp_off;       // [C+1] model node groups (grade ascending)
-  const int32_t* mgrp_tid;
-  const int64_t* mgrp_cnt;
+  const int32_t* mg_tid;         // [kmax][Cp] model node group: template id (grade ascending)
+  const int32_t* mg_cnt;         // [kmax][Cp] node count, clamped to MaxInt32 (0 = no group)
   const int64_t* tmpl;           // [n_tmpl][n_res] model template values
   const uint32_t* perm;          // rank -> caller index
 };
