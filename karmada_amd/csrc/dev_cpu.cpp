@@ -100,8 +100,13 @@ int pair(stream_t, const SnapView& s, const BatchView& bv, int b0, int nb, uint6
 int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x) {
   switch (which) {
     case SEL_LAUNCH_ALL:
-      grid(a.n, smem, [&](int blk, unsigned char* sm) { body_select_all(CpuBlk{(int64_t*)sm}, blk, sm, a); });
+    case SEL_LAUNCH_ALL_REG: {  // the host runs the LDS form; size its scratch here
+      const size_t need = 512 + 4 * (size_t)((((a.s.Cp + 31) >> 5) + 3) & ~3) + 8 * (size_t)a.s.Cp + 3072 +
+                          8 * (size_t)sel_all_ecap(a.s.Cp) + 64;
+      grid(a.n, need > smem ? need : smem,
+           [&](int blk, unsigned char* sm) { body_select_all(CpuBlk{(int64_t*)sm}, blk, sm, a); });
       break;
+    }
     case SEL_LAUNCH_CLUSTER:
       grid(a.n, smem,
            [&](int blk, unsigned char* sm) { body_select_cluster(CpuBlk{(int64_t*)sm}, blk, sm, a, cap); });
@@ -152,19 +157,16 @@ int kpsim_webster(const int32_t* votes, const uint32_t* ranks, int n, int32_t N,
     r[i] = ranks[i];
     v[i] = votes[i];
   }
-  Cands cd;
-  cd.r = r.data();
-  cd.v = v.data();
-  cd.F = n;
   std::vector<uint32_t> hist(256);
   std::vector<unsigned long long> wh(256);
   std::vector<uint64_t> buf(ecap > 0 ? ecap : 1);
   SelScratch ss{hist.data(), wh.data(), buf.data(), ecap};
   int64_t red[8];
   CpuBlk B{red};
-  auto party = [&](int) { return true; };
-  auto vote = [&](int i) { return (int64_t)v[i]; };
-  WebRes w = webster_par(B, cd, party, vote, N, desc != 0, ss);
+  auto parties = [&](auto fn) {
+    for (int i = 0; i < n; i++) fn(r[i], (int64_t)v[i]);
+  };
+  WebRes w = webster_par(B, parties, N, desc != 0, ss);
   for (int i = 0; i < n; i++) out[i] = web_seats(w, v[i], r[i]);
   return w.mode;
 }
@@ -175,7 +177,10 @@ int64_t kpsim_wsel_max(const int32_t* vals, int n, int64_t target) {
   std::vector<unsigned long long> wh(256);
   int64_t red[8];
   CpuBlk B{red};
-  return wsel_max(B, wh.data(), n, [](int) { return true; }, [&](int i) { return (int64_t)vals[i]; }, target);
+  auto vs = [&](auto fn) {
+    for (int i = 0; i < n; i++) fn((int64_t)vals[i]);
+  };
+  return wsel_max(B, wh.data(), vs, target);
 }
 
 }  // extern "C"

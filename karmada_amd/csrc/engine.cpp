@@ -949,7 +949,7 @@ size_t smem_pair(const kp_snapshot* s, int md_cap) {
 }
 size_t smem_all(const kp_snapshot* s) {
   int words = (s->Cp + 31) >> 5;
-  return 512 + 4 * (size_t)words + 8 * (size_t)s->Cp + 2048 + 1024 + 8 * (size_t)sel_all_ecap(s->Cp) + 64;
+  return 512 + 4 * (size_t)((words + 3) & ~3) + 8 * (size_t)s->Cp + 3072 + 8 * (size_t)sel_all_ecap(s->Cp) + 64;
 }
 size_t smem_cluster(const kp_snapshot* s, int cap) {
   int words = (s->Cp + 31) >> 5;

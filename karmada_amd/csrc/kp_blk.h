@@ -20,6 +20,11 @@
 // Forced inlining for the block-parallel helpers: an outlined call in a kernel
 // costs a stack frame (scratch) and spills around every call site.
 #define KP_FI KP_HD __attribute__((always_inline)) inline
+#if defined(__HIPCC__) || defined(__HIP__)
+#define KP_UNROLL _Pragma("unroll")
+#else
+#define KP_UNROLL
+#endif
 
 namespace kp {
 

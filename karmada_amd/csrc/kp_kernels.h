@@ -7,6 +7,7 @@
 // Per-block LDS layouts (dynamic shared memory; sizes computed in engine.cpp):
 //   pair      [512 red | tgt bits | evict bits | md table]
 //   sel_all   [512 red | tgt bits | cand r [Cp] | cand v [Cp] | whist 2 KB | hist 1 KB | buf ecap*8]
+//   sel_all_reg [512 red | tgt bits | whist 2 KB | hist 1 KB | buf ecap*8]  (candidates in registers)
 //   sel_clus  [512 red | hist 1 KB | items 2*kSmallMax | keys 2*kSmallMax | tgt | cand/serial area]
 //   region_a  [512 red | 8x8R + 4x4R region accumulators | tgt | cand]
 //   region_b  [512 red | hist | items | keys | heads 8R | rsel 4R | tgt | cand/serial area]
@@ -103,6 +104,34 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
 // ---------------------------------------------------------------------------
 // Select stage: SEL_ALL (and spread-unsupported / FitError reporting)
 // ---------------------------------------------------------------------------
+template <class BLK, class CS>
+KP_FI void select_all_common(const BLK& B, const KArgs& a, const SelCtx& x, const CS& cs, int F,
+                             const SelScratch& ss) {
+  const int b = x.b;
+  if (pre_checks(B, x, F)) return;
+  if (x.h->sel == SEL_ERR_UNSUPPORTED) {  // select_clusters.go:54
+    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_SPREAD_UNSUPPORTED, 0);
+    return;
+  }
+  const int why = sel_all_fast(B, x, cs, ss);
+  if (why != SLOW_NONE && B.tid() == 0) {
+    a.slow[b] = 1;
+    a.sink.count[b] = 0;
+    kp_atomic_add(&a.stats[0], 1u);
+    kp_atomic_add(&a.stats[why], 1u);
+  }
+}
+
+KP_HD inline SelScratch carve_sel_scratch(unsigned char* p, int Cp) {
+  SelScratch ss;
+  ss.whist = (unsigned long long*)p;
+  ss.hist = (uint32_t*)(ss.whist + 256);
+  ss.buf = (uint64_t*)(ss.hist + 256);
+  ss.cap = sel_all_ecap(Cp);
+  return ss;
+}
+
+// Candidates compacted in LDS (any block policy; the only form for CpuBlk).
 template <class BLK>
 KP_FI void body_select_all(const BLK& B, int blk, unsigned char* smem, const KArgs& a) {
   if (blk >= a.n) return;
@@ -110,32 +139,45 @@ KP_FI void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
   const int words = (a.s.Cp + 31) >> 5;
   uint32_t* tgt = (uint32_t*)(smem + 512);
   Cands cd;
-  cd.r = tgt + words;
+  cd.r = tgt + ((words + 3) & ~3);
   cd.v = (int32_t*)(cd.r + a.s.Cp);
-  SelScratch ss;
-  ss.whist = (unsigned long long*)(cd.v + a.s.Cp);
-  ss.hist = (uint32_t*)(ss.whist + 256);
-  ss.buf = (uint64_t*)(ss.hist + 256);
-  ss.cap = sel_all_ecap(a.s.Cp);
+  const SelScratch ss = carve_sel_scratch((unsigned char*)(cd.v + a.s.Cp), a.s.Cp);
   const BindHdr* h = &a.bv.hdr[b];
   build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
   SelCtx x = make_ctx(a, b, tgt);
   const bool weights = h->strategy == ST_STATIC && h->sel == SEL_ALL;
   cd.F = gather(B, x, cd, weights);
-  if (pre_checks(B, x, cd.F)) return;
-  if (h->sel == SEL_ERR_UNSUPPORTED) {  // select_clusters.go:54
-    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_SPREAD_UNSUPPORTED, 0);
-    return;
-  }
-  const int why = sel_all_fast(B, x, cd, ss);
-  if (why != SLOW_NONE) {
-    if (B.tid() == 0) {
-      a.slow[b] = 1;
-      a.sink.count[b] = 0;
-      kp_atomic_add(&a.stats[0], 1u);
-      kp_atomic_add(&a.stats[why], 1u);
+  LdsCands cs{&cd, B.tid(), B.nth()};
+  select_all_common(B, a, x, cs, cd.F, ss);
+}
+
+// Candidates in registers: thread t owns clusters t + nth*j, j < J (C <= nth*J).
+template <int J, class BLK>
+KP_FI void body_select_all_reg(const BLK& B, int blk, unsigned char* smem, const KArgs& a) {
+  if (blk >= a.n) return;
+  const int b = a.list[blk];
+  const int words = (a.s.Cp + 31) >> 5;
+  uint32_t* tgt = (uint32_t*)(smem + 512);
+  const SelScratch ss = carve_sel_scratch((unsigned char*)(tgt + ((words + 3) & ~3)), a.s.Cp);
+  const BindHdr* h = &a.bv.hdr[b];
+  build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
+  SelCtx x = make_ctx(a, b, tgt);
+  const bool weights = h->strategy == ST_STATIC && h->sel == SEL_ALL;
+  RegCands<J> cs;
+  cs.tid = B.tid();
+  cs.nth = B.nth();
+  cs.fm = 0;
+KP_UNROLL
+  for (int j = 0; j < J; j++) {
+    const int c = cs.tid + cs.nth * j;
+    cs.v[j] = 0;
+    if (c < a.s.C && mask_test(x.frow, c)) {
+      cs.fm |= 1ull << j;
+      cs.v[j] = weights ? static_vote(x, c) : x.erow[c];
     }
   }
+  const int F = (int)B.sum64(popc64(cs.fm));
+  select_all_common(B, a, x, cs, F, ss);
 }
 
 // ---------------------------------------------------------------------------

@@ -20,7 +20,14 @@ struct KArgs {
   uint32_t* stats;        // [0]: bindings flagged for the serial path, [SLOW_*]: by reason
 };
 
-enum : int { SEL_LAUNCH_ALL = 0, SEL_LAUNCH_CLUSTER, SEL_LAUNCH_REGION_A, SEL_LAUNCH_REGION_B, SEL_LAUNCH_SLOW };
+enum : int {
+  SEL_LAUNCH_ALL = 0,
+  SEL_LAUNCH_CLUSTER,
+  SEL_LAUNCH_REGION_A,
+  SEL_LAUNCH_REGION_B,
+  SEL_LAUNCH_SLOW,
+  SEL_LAUNCH_ALL_REG  // SEL_LAUNCH_ALL with candidates in registers (GPU)
+};
 
 struct SelectExtra {
   RegionOut* rout = nullptr;         // region A output [n][n_regions]
@@ -35,6 +42,12 @@ struct SelectExtra {
 constexpr int kBlock = 256;
 
 // Enumeration capacity (u64 entries) of the SEL_ALL selection buffer.
-KP_HD inline int sel_all_ecap(int Cp) { return Cp / 2 > 64 ? Cp / 2 : 64; }
+KP_HD inline int sel_all_ecap(int Cp) { return Cp / 2 < 64 ? 64 : (Cp / 2 > 2048 ? 2048 : Cp / 2); }
+// Register-resident SEL_ALL: slots per thread for C clusters (0 = use the LDS form).
+KP_HD inline int sel_all_slots(int C) {
+  for (int J = 4; J <= 64; J *= 2)
+    if (C <= kBlock * J) return J;
+  return 0;
+}
 
 }  // namespace kp

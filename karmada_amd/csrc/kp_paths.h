@@ -44,44 +44,58 @@ KP_HD inline bool in_sched(const SelCtx& x, uint32_t rank) {
   return x.h->tgt_cnt > 0 && bit_test(x.tgt_bits, (int)rank) && mask_test(x.frow, (int)rank);
 }
 
-// Block-parallel emission of per-candidate results. rep(i) returns the replicas
-// of candidate i in the result; `keep_all` emits every candidate (non-workload /
+// Candidate sets for the SEL_ALL path. each(fn) calls fn(rank, v) for every
+// candidate the calling thread owns, always in the same per-thread order.
+struct LdsCands {  // candidates compacted in LDS (gather)
+  const Cands* cd;
+  int tid, nth;
+  template <class Fn>
+  KP_FI void each(Fn fn) const {
+    for (int i = tid; i < cd->F; i += nth) fn(c_rank(*cd, i), cd->v[i]);
+  }
+};
+template <int J>
+struct RegCands {  // slot j of thread t is cluster t + nth*j; votes live in registers
+  int32_t v[J];
+  uint64_t fm;  // bit j: slot j is a candidate
+  int tid, nth;
+  template <class Fn>
+  KP_FI void each(Fn fn) const {
+KP_UNROLL
+    for (int j = 0; j < J; j++)
+      if ((fm >> j) & 1ull) fn((uint32_t)(tid + nth * j), v[j]);
+  }
+};
+
+// Block-parallel emission of per-candidate results. rep(rank, v) gives the
+// replicas of a candidate; `keep_all` emits every candidate (non-workload /
 // EnableEmptyWorkloadPropagation), otherwise only rep > 0 (removeZeroReplicasCluster).
-template <class BLK, class RepFn>
-KP_FI void emit_par(const BLK& B, const SelCtx& x, const Cands& cd, RepFn rep, bool keep_all) {
-  int64_t cnt = 0;
-  for (int i = B.tid(); i < cd.F; i += B.nth())
-    if (keep_all || rep(i) > 0) cnt++;
-  cnt = B.sum64(cnt);
+template <class BLK, class CS, class RepFn>
+KP_FI void emit_each(const BLK& B, const SelCtx& x, const CS& cs, RepFn rep, bool keep_all) {
+  int32_t mine = 0;
+  cs.each([&](uint32_t rk, int32_t v) {
+    if (keep_all || rep(rk, v) > 0) mine++;
+  });
+  int32_t tot;
+  const int32_t off = B.excl_scan(mine, &tot);
   unsigned long long base = 0;
   if (B.tid() == 0) {
-    base = cnt > 0 ? kp_atomic_add(x.sink.counter, (unsigned long long)cnt) : 0ull;
+    base = tot > 0 ? kp_atomic_add(x.sink.counter, (unsigned long long)tot) : 0ull;
     x.sink.status[x.b] = KP_STATUS_OK;
     x.sink.err[x.b] = KP_ERR_NONE;
     x.sink.arg[x.b] = 0;
     x.sink.start[x.b] = base;
-    x.sink.count[x.b] = (uint32_t)cnt;
+    x.sink.count[x.b] = (uint32_t)tot;
   }
-  base = B.bcast(base);
-  int64_t run = 0;
-  for (int t0 = 0; t0 < cd.F; t0 += B.nth()) {
-    int i = t0 + B.tid();
-    int32_t r = 0;
-    bool e = false;
-    if (i < cd.F) {
-      r = rep(i);
-      e = keep_all || r > 0;
-      if (keep_all && r < 0) r = 0;
+  uint64_t o = (uint64_t)B.bcast(base) + (uint64_t)off;
+  cs.each([&](uint32_t rk, int32_t v) {
+    int32_t r = rep(rk, v);
+    if (keep_all || r > 0) {
+      x.sink.out_idx[o] = x.s->perm[rk];
+      x.sink.out_rep[o] = r < 0 ? 0 : r;
+      o++;
     }
-    int32_t tot;
-    int32_t off = B.excl_scan(e ? 1 : 0, &tot);
-    if (e) {
-      uint64_t o = base + (uint64_t)run + (uint64_t)off;
-      x.sink.out_idx[o] = x.s->perm[c_rank(cd, i)];
-      x.sink.out_rep[o] = r;
-    }
-    run += tot;
-  }
+  });
 }
 
 // dynamicScaleDown (division_algorithm.go:103-119) for SEL_ALL bindings: the
@@ -119,48 +133,57 @@ KP_HD inline bool scale_down_targets(const SelCtx& x, unsigned char* mem, size_t
 }
 
 // ----------------------------------------------------------------------------
-// SEL_ALL: every feasible cluster is selected (select_clusters.go:29-32).
-// Returns false when the binding needs the exact serial path (nothing written).
+// SEL_ALL: every feasible cluster is selected (select_clusters.go:29-32) and
+// AssignReplicas runs block-parallel over the candidate set `cs` (F members).
+// Returns SLOW_NONE when the result (or error) is written, else the reason the
+// binding needs the exact serial path (nothing written).
 // ----------------------------------------------------------------------------
-template <class BLK>
-KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd, const SelScratch& ss) {
+template <class BLK, class CS>
+KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScratch& ss) {
   const BindHdr& h = *x.h;
   const bool desc = (h.flags & BF_UID_DESC) != 0;
   const bool prop = (h.flags & BF_EMPTY_PROP) != 0;
   if (!(h.flags & BF_WORKLOAD_ASSIGN)) {  // non-workload: all candidates, 0 replicas (common.go:72-82)
-    emit_par(B, x, cd, [&](int) { return (int32_t)0; }, true);
-    return 0;
+    emit_each(B, x, cs, [&](uint32_t, int32_t) { return (int32_t)0; }, true);
+    return SLOW_NONE;
   }
   if (h.flags & (BF_OVERFLOW | BF_DUP_TARGETS)) return SLOW_OVERFLOW_DUP;
   const int st = h.strategy;
   if (st == ST_NONE) {
     if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_UNSUPPORTED_STRATEGY, 0);
-    return 0;
+    return SLOW_NONE;
   }
   if (st == ST_DUPLICATED) {
-    int32_t rep = h.replicas;
-    emit_par(B, x, cd, [&](int) { return rep > 0 ? rep : (int32_t)0; }, prop);
-    return 0;
+    const int32_t rep = h.replicas > 0 ? h.replicas : 0;
+    emit_each(B, x, cs, [&](uint32_t, int32_t) { return rep; }, prop);
+    return SLOW_NONE;
   }
-  if (st == ST_STATIC) {
+  if (st == ST_STATIC) {  // v = max matching rule weight (gather)
     int64_t wmax = 0, wsum = 0;
-    for (int i = B.tid(); i < cd.F; i += B.nth()) {
-      int64_t w = cd.v[i];
+    cs.each([&](uint32_t, int32_t w) {
       if (w > wmax) wmax = w;
       wsum += w > 0 ? w : 0;
-    }
+    });
     wmax = B.max64(wmax);
     wsum = B.sum64(wsum);
     if (wmax >= kInt32Max) return SLOW_WEIGHT;
-    bool all1 = wsum == 0;  // getStaticWeightInfoList: every candidate weight 1
-    auto party = [&](int i) { return all1 || cd.v[i] > 0; };
-    auto vote = [&](int i) { return all1 ? (int64_t)1 : (int64_t)cd.v[i]; };
-    WebRes w = webster_par(B, cd, party, vote, h.replicas, desc, ss);
-    emit_par(B, x, cd, [&](int i) { return party(i) ? web_seats(w, vote(i), c_rank(cd, i)) : (int32_t)0; }, prop);
-    return 0;
+    const bool all1 = wsum == 0;  // getStaticWeightInfoList: every candidate weight 1
+    auto parties = [&](auto fn) {
+      cs.each([&](uint32_t rk, int32_t w) {
+        if (all1 || w > 0) fn(rk, all1 ? (int64_t)1 : (int64_t)w);
+      });
+    };
+    WebRes w = webster_par(B, parties, h.replicas, desc, ss);
+    emit_each(
+        B, x, cs,
+        [&](uint32_t rk, int32_t wt) {
+          return (all1 || wt > 0) ? web_seats(w, all1 ? (int64_t)1 : (int64_t)wt, rk) : (int32_t)0;
+        },
+        prop);
+    return SLOW_NONE;
   }
   // Dynamic / Aggregated (assignment.go:213-244)
-  int32_t assigned = 0, ns = 0;
+  int32_t assigned = 0;
   bool anyPriorPos = false;
   if (B.tid() == 0) {
     for (int j = 0; j < h.tgt_cnt; j++) {
@@ -168,13 +191,11 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd, const Sel
       if (mask_test(x.frow, (int)r)) {
         int32_t v = x.bv->ipool[h.tgt_off + 2 * j + 1];
         assigned = add32(assigned, v);
-        ns++;
         if (v > 0) anyPriorPos = true;
       }
     }
   }
   assigned = B.bcast(assigned);
-  ns = B.bcast(ns);
   anyPriorPos = B.bcast(anyPriorPos ? 1 : 0) != 0;
   const bool fresh = (h.flags & BF_FRESH) != 0;
   int mode;  // 0 fresh, 1 scale up, 2 unchanged, 3 scale down
@@ -183,105 +204,105 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const Cands& cd, const Sel
   else if (assigned < h.replicas) mode = 1;
   else mode = 2;
   if (mode == 3) return SLOW_SCALE_DOWN;  // parties = scheduledClusters: serial kernel (k_slow)
-  if (mode == 2) {              // unchanged: scheduledClusters, removeZero
-    emit_par(B, x, cd, [&](int i) { return in_sched(x, c_rank(cd, i)) ? sched_rep_of(x, c_rank(cd, i)) : (int32_t)0; },
-             prop);
-    return 0;
+  // spec.Clusters membership of a candidate (candidates are feasible)
+  auto tgt = [&](uint32_t rk) { return h.tgt_cnt > 0 && bit_test(x.tgt_bits, (int)rk); };
+  if (mode == 2) {  // unchanged: scheduledClusters, removeZero
+    emit_each(B, x, cs, [&](uint32_t rk, int32_t) { return tgt(rk) ? sched_rep_of(x, rk) : (int32_t)0; }, prop);
+    return SLOW_NONE;
   }
-  auto vote32 = [&](int i) -> int32_t {
-    int32_t v = cd.v[i];
-    if (mode == 0 && in_sched(x, c_rank(cd, i))) v = add32(v, sched_rep_of(x, c_rank(cd, i)));
+  auto vote32 = [&](uint32_t rk, int32_t v) -> int32_t {
+    if (mode == 0 && tgt(rk)) v = add32(v, sched_rep_of(x, rk));
     return v;
   };
   int64_t sabs = 0, vmin = 0, vtot = 0;
-  for (int i = B.tid(); i < cd.F; i += B.nth()) {
-    int64_t v = vote32(i);
+  cs.each([&](uint32_t rk, int32_t v0) {
+    int64_t v = vote32(rk, v0);
     sabs += v < 0 ? -v : v;
     if (v < vmin) vmin = v;
     vtot += v;
-  }
+  });
   sabs = B.sum64(sabs);
   vmin = B.min64(vmin);
   vtot = B.sum64(vtot);
   if (vmin < 0 || sabs >= (int64_t)kInt32Max) return SLOW_WRAP;  // int32 wrap hazard
-  int32_t target = mode == 0 ? h.replicas : sub32(h.replicas, assigned);
+  const int32_t target = mode == 0 ? h.replicas : sub32(h.replicas, assigned);
   if ((int32_t)vtot < target) {
     if (B.tid() == 0)
       sink_error(x, KP_STATUS_UNSCHEDULABLE, mode == 0 ? KP_ERR_FRESH_NOT_ENOUGH : KP_ERR_SCALE_UP_NOT_ENOUGH, vtot);
-    return 0;
+    return SLOW_NONE;
   }
   const bool merge = mode == 1;
-  auto prior = [&](int i) { return merge && anyPriorPos && in_sched(x, c_rank(cd, i)) && sched_rep_of(x, c_rank(cd, i)) > 0; };
+  auto prior = [&](uint32_t rk) { return merge && anyPriorPos && tgt(rk) && sched_rep_of(x, rk) > 0; };
   // Aggregated prefix cut (division_algorithm.go:81-89) over sort.Sort order
   // (Replicas desc) with prior clusters first: membership is exact unless a
   // tie group straddles the cut (then the pdqsort permutation matters).
-  int64_t vstar = -1;   // members: X elements with v > vstar, plus the whole tie group when tie_all
-  bool xIsPrior = false, tie_all = true, noCut = false;
+  int64_t vstar = -1;  // members: X elements with v > vstar, plus the whole tie group
+  bool xIsPrior = false, noCut = false;
   if (st == ST_AGGREGATED) {
     int64_t SP = 0, nP = 0;
-    for (int i = B.tid(); i < cd.F; i += B.nth())
-      if (prior(i)) {
-        SP += vote32(i);
+    cs.each([&](uint32_t rk, int32_t v0) {
+      if (prior(rk)) {
+        SP += vote32(rk, v0);
         nP++;
       }
+    });
     SP = B.sum64(SP);
     nP = B.sum64(nP);
     xIsPrior = nP > 0 && SP >= target;
-    int64_t tX = xIsPrior ? (int64_t)target : (int64_t)target - SP;
-    auto inX = [&](int i) { return prior(i) == xIsPrior; };
+    const int64_t tX = xIsPrior ? (int64_t)target : (int64_t)target - SP;
+    auto xvals = [&](auto fn) {
+      cs.each([&](uint32_t rk, int32_t v0) {
+        if (prior(rk) == xIsPrior) fn((int64_t)vote32(rk, v0));
+      });
+    };
     int64_t xmax = -1, xsum = 0;
-    for (int i = B.tid(); i < cd.F; i += B.nth())
-      if (inX(i)) {
-        int64_t v = vote32(i);
-        if (v > xmax) xmax = v;
-        xsum += v;
-      }
+    xvals([&](int64_t v) {
+      if (v > xmax) xmax = v;
+      xsum += v;
+    });
     xmax = B.max64(xmax);
     xsum = B.sum64(xsum);
     if (xmax < 0 || xsum < tX) {
       noCut = true;  // every element of X is taken
     } else {
-      if (tX <= 0) {
-        vstar = xmax;  // the first element alone reaches the target
-      } else {  // largest v with sum{v_i >= v} >= tX
-        vstar = wsel_max(B, ss.whist, cd.F, inX, [&](int i) { return (int64_t)vote32(i); }, tX);
-      }
+      if (tX <= 0) vstar = xmax;  // the first element alone reaches the target
+      else vstar = wsel_max(B, ss.whist, xvals, tX);  // largest v with sum{v_i >= v} >= tX
       int64_t sgt = 0, ceq = 0;
-      for (int i = B.tid(); i < cd.F; i += B.nth())
-        if (inX(i)) {
-          int64_t v = vote32(i);
-          if (v > vstar) sgt += v;
-          if (v == vstar) ceq++;
-        }
+      xvals([&](int64_t v) {
+        if (v > vstar) sgt += v;
+        if (v == vstar) ceq++;
+      });
       sgt = B.sum64(sgt);
       ceq = B.sum64(ceq);
-      int64_t need = tX - sgt;
-      int64_t j = need <= 0 ? 1 : (vstar > 0 ? (need + vstar - 1) / vstar : ceq);
+      const int64_t need = tX - sgt;
+      const int64_t j = need <= 0 ? 1 : (vstar > 0 ? (need + vstar - 1) / vstar : ceq);
       if (j < ceq) return SLOW_TIE;  // tie group straddles the cut
-      tie_all = true;
     }
   }
-  auto member = [&](int i) {
+  auto member = [&](uint32_t rk, int64_t v) {
     if (st != ST_AGGREGATED) return true;
-    bool p = prior(i);
+    const bool p = prior(rk);
     if (!xIsPrior && p) return true;  // X = non-prior: every prior cluster precedes the cut
     if (p != xIsPrior) return false;
-    if (noCut) return true;
-    int64_t v = vote32(i);
-    return v > vstar || (v == vstar && tie_all);
+    return noCut || v >= vstar;
   };
-  auto vote = [&](int i) { return (int64_t)vote32(i); };
-  WebRes w = webster_par(B, cd, member, vote, target, desc, ss);
-  emit_par(
-      B, x, cd,
-      [&](int i) {
-        uint32_t rk = c_rank(cd, i);
-        int32_t r = member(i) ? web_seats(w, vote32(i), rk) : 0;
-        if (merge && in_sched(x, rk)) r = add32(r, sched_rep_of(x, rk));
+  auto parties = [&](auto fn) {
+    cs.each([&](uint32_t rk, int32_t v0) {
+      const int64_t v = vote32(rk, v0);
+      if (member(rk, v)) fn(rk, v);
+    });
+  };
+  WebRes w = webster_par(B, parties, target, desc, ss);
+  emit_each(
+      B, x, cs,
+      [&](uint32_t rk, int32_t v0) {
+        const int64_t v = vote32(rk, v0);
+        int32_t r = member(rk, v) ? web_seats(w, v, rk) : 0;
+        if (merge && tgt(rk)) r = add32(r, sched_rep_of(x, rk));
         return r;
       },
       prop);
-  return 0;
+  return SLOW_NONE;
 }
 
 // ----------------------------------------------------------------------------

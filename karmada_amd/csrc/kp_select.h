@@ -481,42 +481,47 @@ KP_HD inline void sink_error(const SelCtx& x, int status, int err, int64_t arg) 
   k.count[x.b] = 0;
 }
 
+// StaticWeight vote of cluster c: the largest matching rule weight, saturated at
+// MaxInt32 (getStaticWeightInfoList, division_algorithm.go:41-48).
+KP_HD inline int32_t static_vote(const SelCtx& x, int c) {
+  const BindHdr& h = *x.h;
+  int64_t wt = 0;
+  if (!(h.flags & BF_HAS_WP)) {
+    wt = 1;
+  } else {
+    for (int j = 0; j < h.sw_cnt; j++)
+      if (prog_match(*x.s, *x.bv, x.bv->ipool[h.sw_off + j], c)) {
+        int64_t rw = x.bv->lpool[h.sw_w_off + j];
+        if (rw > wt) wt = rw;
+      }
+  }
+  return (int32_t)(wt > kInt32Max ? kInt32Max : wt);
+}
+
 // ----------------------------------------------------------------------------
 // Candidate gather: feasible clusters of the binding in rank order.
 // ----------------------------------------------------------------------------
 template <class BLK>
 KP_FI int gather(const BLK& B, const SelCtx& x, Cands cd, bool weights) {
+  // Thread t reads cluster base + t of each block-wide step: the feasibility
+  // word is one broadcast load per wave and erow is read fully coalesced.
   const SnapView& s = *x.s;
   const BindHdr& h = *x.h;
   int F = 0;
-  for (int w0 = 0; w0 < s.W; w0 += B.nth()) {
-    int w = w0 + B.tid();
-    uint64_t m = w < s.W ? x.frow[w] : 0ull;
+  for (int base = 0; base < s.C; base += B.nth()) {
+    const int c = base + B.tid();
+    const bool f = c < s.C && mask_test(x.frow, c);
+    uint32_t r = 0;
+    int32_t v = 0;
+    if (f) {
+      r = (uint32_t)c | ((uint32_t)overflow_order(s, *x.bv, h, c) << kRankBits);
+      v = weights ? static_vote(x, c) : x.erow[c];
+    }
     int32_t tot;
-    int32_t off = B.excl_scan(popc64(m), &tot);
-    int pos = F + off;
-    while (m) {
-      int bit = ctz64(m);
-      m &= m - 1;
-      int c = w * 64 + bit;
-      uint32_t ovf = (uint32_t)overflow_order(s, *x.bv, h, c);
-      cd.r[pos] = (uint32_t)c | (ovf << kRankBits);
-      int32_t v = x.erow[c];
-      if (weights) {  // StaticWeight votes: max matching rule weight (division_algorithm.go:41-48)
-        int64_t wt = 0;
-        if (!(h.flags & BF_HAS_WP)) {
-          wt = 1;
-        } else {
-          for (int j = 0; j < h.sw_cnt; j++)
-            if (prog_match(s, *x.bv, x.bv->ipool[h.sw_off + j], c)) {
-              int64_t rw = x.bv->lpool[h.sw_w_off + j];
-              if (rw > wt) wt = rw;
-            }
-        }
-        v = (int32_t)(wt > kInt32Max ? kInt32Max : wt);
-      }
-      cd.v[pos] = v;
-      pos++;
+    const int32_t off = B.excl_scan(f ? 1 : 0, &tot);
+    if (f) {
+      cd.r[F + off] = r;
+      cd.v[F + off] = v;
     }
     F += tot;
   }
@@ -557,30 +562,28 @@ template <class BLK, class Pred, class Key>
 KP_FI uint64_t radix_select(const BLK& B, uint32_t* hist, int F, Pred pred, Key key, int64_t k);
 
 // AllocateWebsterSeats (webstermethod.go:112-161) for parties with int32 votes
-// >= 0 and no initial seats, block-parallel. The N-th largest seat priority
+// >= 0 and no initial seats, block-parallel. `parties(fn)` calls fn(rank, votes)
+// for every party the calling thread owns. The N-th largest seat priority
 // t* = max{t : cnt_ge(t) >= N} is bracketed by the divisor-method bounds
-//   V/(2N+P) <= t* < V/(2N-P)   (P = parties with votes > 0)
+//   V/(2N+P) <= t* < V/(2N-P-1)   (P = parties with votes > 0)
 // verified with exact counts, narrowed by bisection over the double's bit
-// pattern only while more than sc.cap priorities lie in the bracket, then the
-// bracketed priorities are enumerated into LDS and t* is radix-selected. Seats
-// strictly above t* are exact per party; the tie group at t* is ordered by
-// (seats asc, name) as the heap's tie-breaker orders it (tie_key).
-template <class BLK, class Pred, class Vote>
-KP_FI WebRes webster_par(const BLK& B, const Cands& cd, Pred party, Vote vote, int32_t N, bool desc,
-                         const SelScratch& sc) {
+// pattern only while more than sc.cap priorities lie in the bracket; the
+// bracketed priorities are then enumerated into LDS and t* is radix-selected.
+// Seats strictly above t* are exact per party; the tie group at t* is ordered
+// by (seats asc, name) as the heap's tie-breaker orders it (tie_key).
+template <class BLK, class Parties>
+KP_FI WebRes webster_par(const BLK& B, Parties parties, int32_t N, bool desc, const SelScratch& sc) {
   WebRes r;
   r.N = N;
   r.desc = desc;
   r.t = 0;
   r.tie = 0;
   int64_t V = 0, vmax = 0, P = 0;
-  for (int i = B.tid(); i < cd.F; i += B.nth())
-    if (party(i)) {
-      int64_t v = vote(i);
-      V += v;
-      if (v > vmax) vmax = v;
-      if (v > 0) P++;
-    }
+  parties([&](uint32_t, int64_t v) {
+    V += v;
+    if (v > vmax) vmax = v;
+    if (v > 0) P++;
+  });
   V = B.sum64(V);
   vmax = B.max64(vmax);
   P = B.sum64(P);
@@ -594,22 +597,18 @@ KP_FI WebRes webster_par(const BLK& B, const Cands& cd, Pred party, Vote vote, i
   }
   r.mode = 2;
   const int64_t capN = (int64_t)N;
-  // two thresholds per pass
   auto cnt2 = [&](double ta, double tb, int64_t* ca, int64_t* cb) {
     int64_t a = 0, b = 0;
-    for (int i = B.tid(); i < cd.F; i += B.nth())
-      if (party(i)) {
-        int64_t v = vote(i);
-        a += w_count(v, ta, capN, true);
-        b += w_count(v, tb, capN, true);
-      }
+    parties([&](uint32_t, int64_t v) {
+      a += w_count(v, ta, capN, true);
+      b += w_count(v, tb, capN, true);
+    });
     *ca = B.sum64(a);
     *cb = B.sum64(b);
   };
   auto cnt1 = [&](double t) {
     int64_t c = 0;
-    for (int i = B.tid(); i < cd.F; i += B.nth())
-      if (party(i)) c += w_count(vote(i), t, capN, true);
+    parties([&](uint32_t, int64_t v) { c += w_count(v, t, capN, true); });
     return B.sum64(c);
   };
   // invariant: cnt_ge(lo) >= N > cnt_ge(hi), lo < hi (as bit patterns)
@@ -617,14 +616,14 @@ KP_FI WebRes webster_par(const BLK& B, const Cands& cd, Pred party, Vote vote, i
   int64_t clo = -1, chi = 0;
   {
     double l0 = (double)V / (double)(2 * (int64_t)N + P);
-    l0 = bitsd(dbits(l0) > 64 ? dbits(l0) - 64 : 1);  // a few ulps below the bound
+    uint64_t lb = dbits(l0) > 64 ? dbits(l0) - 64 : 1;  // a few ulps below the bound
     double h0 = 2 * (int64_t)N - P - 1 > 0 ? (double)V / (double)(2 * (int64_t)N - P - 1) : (double)vmax;
     uint64_t hb = dbits(h0) + 64;
     if (hb > hi) hb = hi;
     int64_t cl, ch;
-    cnt2(bitsd(dbits(l0)), bitsd(hb), &cl, &ch);
+    cnt2(bitsd(lb), bitsd(hb), &cl, &ch);
     if (cl >= N) {
-      lo = dbits(l0);
+      lo = lb;
       clo = cl;
     }
     if (ch < N) {
@@ -633,7 +632,6 @@ KP_FI WebRes webster_par(const BLK& B, const Cands& cd, Pred party, Vote vote, i
     }
     if (clo < 0) clo = cnt1(bitsd(lo));
   }
-  // narrow while too many priorities lie in [lo, hi)
   while (hi - lo > 1 && clo - chi > (int64_t)sc.cap) {
     uint64_t mid = lo + (hi - lo) / 2;
     int64_t c = cnt1(bitsd(mid));
@@ -651,20 +649,16 @@ KP_FI WebRes webster_par(const BLK& B, const Cands& cd, Pred party, Vote vote, i
   } else {
     // enumerate every priority in [lo, hi) and select the (N - chi)-th largest
     const double tl = bitsd(lo), th = bitsd(hi);
-    int E = 0;
-    for (int t0 = 0; t0 < cd.F; t0 += B.nth()) {
-      int i = t0 + B.tid();
-      int64_t k0 = 0, k1 = 0, v = 0;
-      if (i < cd.F && party(i)) {
-        v = vote(i);
-        k0 = w_count(v, th, capN, true);
-        k1 = w_count(v, tl, capN, true);
-      }
-      int32_t tot;
-      int32_t off = B.excl_scan((int32_t)(k1 - k0), &tot);
-      for (int64_t k = k0; k < k1; k++) sc.buf[E + off + (k - k0)] = dbits(w_prio(v, k));
-      E += tot;
-    }
+    int32_t mine = 0;
+    parties([&](uint32_t, int64_t v) {
+      mine += (int32_t)(w_count(v, tl, capN, true) - w_count(v, th, capN, true));
+    });
+    int32_t E;
+    int32_t pos = B.excl_scan(mine, &E);
+    parties([&](uint32_t, int64_t v) {
+      int64_t k0 = w_count(v, th, capN, true), k1 = w_count(v, tl, capN, true);
+      for (int64_t k = k0; k < k1; k++) sc.buf[pos++] = dbits(w_prio(v, k));
+    });
     B.sync();
     const int64_t kth_small = (int64_t)E - ((int64_t)N - chi) + 1;
     auto all = [&](int) { return true; };
@@ -674,34 +668,28 @@ KP_FI WebRes webster_par(const BLK& B, const Cands& cd, Pred party, Vote vote, i
   r.t = tstar;
   // seats strictly above t*, then the tie group at t* ordered by (k asc, name)
   int64_t S = 0, T = 0;
-  for (int i = B.tid(); i < cd.F; i += B.nth())
-    if (party(i)) {
-      int64_t v = vote(i);
-      int64_t base = w_count(v, tstar, (int64_t)N + 1, false);
-      S += base;
-      if (w_prio(v, base) == tstar) T++;
-    }
+  parties([&](uint32_t, int64_t v) {
+    int64_t base = w_count(v, tstar, (int64_t)N + 1, false);
+    S += base;
+    if (w_prio(v, base) == tstar) T++;
+  });
   S = B.sum64(S);
   T = B.sum64(T);
-  int64_t M = (int64_t)N - S;
-  auto is_tie = [&](int i, int64_t* base) {
-    int64_t v = vote(i);
-    *base = w_count(v, tstar, (int64_t)N + 1, false);
-    return w_prio(v, *base) == tstar;
-  };
+  const int64_t M = (int64_t)N - S;
   if (M >= T) {
     r.tie = ~0ull;
   } else if (T <= (int64_t)sc.cap) {
-    int n = 0;
-    for (int t0 = 0; t0 < cd.F; t0 += B.nth()) {
-      int i = t0 + B.tid();
-      int64_t base = 0;
-      bool e = i < cd.F && party(i) && is_tie(i, &base);
-      int32_t tot;
-      int32_t off = B.excl_scan(e ? 1 : 0, &tot);
-      if (e) sc.buf[n + off] = tie_key(base, c_rank(cd, i), desc);
-      n += tot;
-    }
+    int32_t mine = 0;
+    parties([&](uint32_t, int64_t v) {
+      int64_t base = w_count(v, tstar, (int64_t)N + 1, false);
+      if (w_prio(v, base) == tstar) mine++;
+    });
+    int32_t n;
+    int32_t pos = B.excl_scan(mine, &n);
+    parties([&](uint32_t rk, int64_t v) {
+      int64_t base = w_count(v, tstar, (int64_t)N + 1, false);
+      if (w_prio(v, base) == tstar) sc.buf[pos++] = tie_key(base, rk, desc);
+    });
     B.sync();
     auto all = [&](int) { return true; };
     auto key = [&](int i) { return (uint64_t)sc.buf[i]; };
@@ -711,10 +699,10 @@ KP_FI WebRes webster_par(const BLK& B, const Cands& cd, Pred party, Vote vote, i
     while (tlo < thi) {
       uint64_t mid = tlo + (thi - tlo) / 2;
       int64_t c = 0;
-      for (int i = B.tid(); i < cd.F; i += B.nth()) {
-        int64_t base;
-        if (party(i) && is_tie(i, &base) && tie_key(base, c_rank(cd, i), desc) <= mid) c++;
-      }
+      parties([&](uint32_t rk, int64_t v) {
+        int64_t base = w_count(v, tstar, (int64_t)N + 1, false);
+        if (w_prio(v, base) == tstar && tie_key(base, rk, desc) <= mid) c++;
+      });
       c = B.sum64(c);
       if (c >= M) thi = mid;
       else tlo = mid + 1;
@@ -724,22 +712,22 @@ KP_FI WebRes webster_par(const BLK& B, const Cands& cd, Pred party, Vote vote, i
   return r;
 }
 
-// Largest value v* over the predicate set (values in [0, 2^31)) such that the
-// values >= v* sum to at least `target` (>= 1; the caller guarantees the total
-// reaches it): an 8-bit radix descent with value-weighted bins.
-template <class BLK, class Pred, class Val>
-KP_FI int64_t wsel_max(const BLK& B, unsigned long long* wh, int F, Pred pred, Val val, int64_t target) {
+// Largest value v* over a value set (values in [0, 2^31)) such that the values
+// >= v* sum to at least `target` (>= 1; the caller guarantees the total reaches
+// it): an 8-bit radix descent with value-weighted bins. `vals(fn)` calls fn(v)
+// for every value the calling thread owns.
+template <class BLK, class Vals>
+KP_FI int64_t wsel_max(const BLK& B, unsigned long long* wh, Vals vals, int64_t target) {
   uint32_t prefix = 0;
   int64_t above = 0;
   for (int shift = 24; shift >= 0; shift -= 8) {
     for (int i = B.tid(); i < 256; i += B.nth()) wh[i] = 0;
     B.sync();
     const uint32_t hm = shift == 24 ? 0u : (~0u << (shift + 8));
-    for (int i = B.tid(); i < F; i += B.nth())
-      if (pred(i)) {
-        uint32_t v = (uint32_t)val(i);
-        if ((v & hm) == (prefix & hm) && v) kp_atomic_add(&wh[(v >> shift) & 255], (unsigned long long)v);
-      }
+    vals([&](int64_t v64) {
+      uint32_t v = (uint32_t)v64;
+      if ((v & hm) == (prefix & hm) && v) kp_atomic_add(&wh[(v >> shift) & 255], (unsigned long long)v);
+    });
     B.sync();
     int64_t sel = 0, ab = above;
     if (B.tid() == 0) {
