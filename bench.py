@@ -86,6 +86,7 @@ def main():
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--lib", default=None, help="engine library (default karmada_amd/libkp.so)")
     args = ap.parse_args()
 
     from karmada_amd import api, synth
@@ -112,7 +113,7 @@ def main():
     u = synth.Universe(cfg, seed, C_, lo, hi)
     gen_s = time.perf_counter() - t0
     opts = api.options()
-    eng = Engine(local)
+    eng = Engine(local, lib_path=os.path.join(ROOT, args.lib)) if args.lib else Engine(local)
     t0 = time.perf_counter()
     snap = Snapshot.from_structs(eng, u.clusters, u.n_clusters, u.names, opts)
     snap_s = time.perf_counter() - t0

@@ -141,6 +141,7 @@ struct kp_batch {
   uint32_t* count = nullptr;
   unsigned long long* counter = nullptr;
   uint32_t* stats = nullptr;
+  unsigned long long* dbg = nullptr;
   uint32_t h_stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t* out_idx = nullptr;
   int32_t* out_rep = nullptr;
@@ -1110,6 +1111,9 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->count, B);
   a.add(&bt->counter, 1);
   a.add(&bt->stats, 8);
+#ifdef KP_STAMPS
+  a.add(&bt->dbg, 32);
+#endif
   a.add(&bt->out_idx, std::max<uint64_t>(1, bt->out_cap));
   a.add(&bt->out_rep, std::max<uint64_t>(1, bt->out_cap));
   a.add(&bt->offsets_d, B + 1);
@@ -1181,6 +1185,10 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   ka.sink.count = bt->count;
   ka.slow = bt->slow;
   ka.stats = bt->stats;
+  ka.dbg = bt->dbg;
+#ifdef KP_STAMPS
+  HIPCHK(dev::fill(bt->dbg, 0, 32 * 8, st));
+#endif
   HIPCHK(dev::event_record(e->ev[0], st));
   HIPCHK(dev::pair(st, s->view, bt->view, 0, B, bt->fmask, bt->est, nullptr, 0, kMdCap, smem_pair(s, kMdCap)));
   HIPCHK(dev::event_record(e->ev[1], st));
@@ -1294,6 +1302,16 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   tm.pair_kernel_ms = ms_pair;
   tm.select_kernel_ms = ms_sel;
   tm.n_slow = bt->h_stats[0];
+#ifdef KP_STAMPS
+  {
+    unsigned long long h[32];
+    HIPCHK(dev::d2h(h, bt->dbg, sizeof(h), st));
+    HIPCHK(dev::sync(st));
+    fprintf(stderr, "kp stamps (s_memtime ticks, summed over workgroups):");
+    for (int i = 0; i < 8; i++) fprintf(stderr, " [%d]=%llu", i, h[i]);
+    fprintf(stderr, "\n");
+  }
+#endif
   if (getenv("KP_DEBUG_SLOW"))
     fprintf(stderr, "kp slow: total %u overflow/dup %u scale-down %u wrap %u tie %u weight %u cluster %u\n",
             bt->h_stats[0], bt->h_stats[1], bt->h_stats[2], bt->h_stats[3], bt->h_stats[4], bt->h_stats[5],

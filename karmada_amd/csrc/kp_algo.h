@@ -237,6 +237,24 @@ KP_HD inline int32_t template_md(const SnapView& s, const BatchView& bv, const B
   return (int32_t)res;
 }
 
+// min(a / q, lim) for a >= 0, q >= 1, lim >= 0 without a 64-bit integer divide:
+// a double estimate decides "quotient >= lim" when it is far from the limit,
+// otherwise the quotient (< lim + 2 <= 2^31 + 2) is corrected exactly.
+KP_HD inline int64_t floor_div_below(int64_t a, int64_t q, int64_t lim) {
+  if (a < q) return 0;
+  if (q > ((int64_t)1 << 60)) {  // enormous request: the quotient is tiny, divide exactly
+    const int64_t d = a / q;
+    return d < lim ? d : lim;
+  }
+  const double est = kp_floor((double)a / (double)q);
+  if (est >= (double)lim + 2.0) return lim;
+  uint64_t e = (uint64_t)est;
+  const uint64_t ua = (uint64_t)a, uq = (uint64_t)q;  // e*uq <= a + uq < 2^64
+  while (e > 0 && e * uq > ua) e--;
+  while ((e + 1) * uq <= ua) e++;
+  return (int64_t)e < lim ? (int64_t)e : lim;
+}
+
 // GeneralEstimator.maxAvailableReplicas (general.go:66-108), assumed workloads empty.
 // md: per-template MaxDivided table (LDS) or nullptr to compute per pair.
 KP_HD inline int32_t general_estimate(const SnapView& s, const BatchView& bv, const BindHdr& h, int c,
@@ -254,11 +272,9 @@ KP_HD inline int32_t general_estimate(const SnapView& s, const BatchView& bv, co
       const int64_t cnt = s.mg_cnt[(size_t)k * s.Cp + c];
       if (cnt == 0) continue;
       const int32_t tid = s.mg_tid[(size_t)k * s.Cp + c];
-      int64_t d = md ? md[tid] : template_md(s, bv, h, tid);
-      if (d > 0 && cnt > (int64_t)kInt32Max / d) {
-        total = kInt32Max;
-        break;
-      }
+      // d <= 110 (MaxPodsPerNode) and cnt <= MaxInt32: d*cnt < 2^38, and the sum
+      // stops at MaxInt32, so int64 cannot overflow.
+      const int64_t d = md ? md[tid] : template_md(s, bv, h, tid);
       total += d * cnt;
       if (total >= kInt32Max) {
         total = kInt32Max;
@@ -275,7 +291,8 @@ KP_HD inline int32_t general_estimate(const SnapView& s, const BatchView& bv, co
     if (rid < 0) return 0;
     int64_t a = s.avail[(size_t)rid * s.Cp + c];
     if (a <= 0) return 0;
-    int64_t d = a / bv.lpool[h.sreq_q_off + j];
+    const int64_t lim = num < m ? num : m;  // only quotients below min(num, allowed) matter
+    const int64_t d = floor_div_below(a, bv.lpool[h.sreq_q_off + j], lim);
     if (d < num) num = d;
   }
   if (num < m) m = num;

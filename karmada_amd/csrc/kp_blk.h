@@ -84,6 +84,52 @@ struct GpuBlk {
     *total = tot;
     return base + x - v;
   }
+  // Histogram search: the first bin i (in ascending index order, or descending
+  // when `rev`) whose running sum reaches k (k >= 1); *before = the running sum
+  // before it. Wave 0 scans 4 bins per lane. Not found -> the last bin.
+  template <class T>
+  KP_INLINE int find_bin(const T* hist, int64_t k, int64_t* before, bool rev) const {
+    sync();
+    if (wid() == 0) {
+      const int l = lane();
+      int64_t v[4], s = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int idx = rev ? 255 - (4 * l + q) : 4 * l + q;
+        v[q] = (int64_t)hist[idx];
+        s += v[q];
+      }
+      int64_t incl = s;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        int64_t y = __shfl_up(incl, o, 64);
+        if (l >= o) incl += y;
+      }
+      const uint64_t m = __ballot(incl >= k);
+      const int first = m ? (int)__builtin_ctzll(m) : 63;
+      if (l == first) {
+        int64_t c = incl - s;
+        int q = 0;
+        for (; q < 3; q++) {
+          if (c + v[q] >= k) break;
+          c += v[q];
+        }
+        red[0] = rev ? 255 - (4 * l + q) : 4 * l + q;
+        red[1] = c;
+      }
+    }
+    sync();
+    const int bin = (int)red[0];
+    *before = red[1];
+    sync();
+    return bin;
+  }
+  KP_INLINE uint64_t and64(uint64_t v) const {
+    return (uint64_t)reduce((int64_t)v, [](int64_t a, int64_t b) { return (int64_t)((uint64_t)a & (uint64_t)b); });
+  }
+  KP_INLINE uint64_t or64(uint64_t v) const {
+    return (uint64_t)reduce((int64_t)v, [](int64_t a, int64_t b) { return (int64_t)((uint64_t)a | (uint64_t)b); });
+  }
   // Stores the feasibility bit of cluster c (c = wave base + lane) into its u64 word.
   KP_INLINE void mask_store(uint64_t* row, int c, bool bit, int W) const {
     const uint64_t m = __ballot(bit);
@@ -123,6 +169,21 @@ struct CpuBlk {
   T bcast(T v) const {
     return v;
   }
+  template <class T>
+  int find_bin(const T* hist, int64_t k, int64_t* before, bool rev) const {
+    int64_t c = 0;
+    for (int i = 0; i < 256; i++) {
+      const int idx = rev ? 255 - i : i;
+      if (c + (int64_t)hist[idx] >= k || i == 255) {
+        *before = c;
+        return idx;
+      }
+      c += (int64_t)hist[idx];
+    }
+    return 0;
+  }
+  uint64_t and64(uint64_t v) const { return v; }
+  uint64_t or64(uint64_t v) const { return v; }
   void mask_store(uint64_t* row, int c, bool bit, int W) const {
     if ((c >> 6) >= W) return;
     if ((c & 63) == 0) row[c >> 6] = 0;

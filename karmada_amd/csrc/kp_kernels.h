@@ -28,6 +28,7 @@ KP_HD inline SelCtx make_ctx(const KArgs& a, int b, const uint32_t* tgt_bits) {
   x.erow = a.est + (size_t)b * a.s.Cp;
   x.tgt_bits = tgt_bits;
   x.sink = a.sink;
+  x.dbg = a.dbg;
   return x;
 }
 
@@ -135,6 +136,7 @@ KP_HD inline SelScratch carve_sel_scratch(unsigned char* p, int Cp) {
 template <class BLK>
 KP_FI void body_select_all(const BLK& B, int blk, unsigned char* smem, const KArgs& a) {
   if (blk >= a.n) return;
+  KP_STAMP_INIT
   const int b = a.list[blk];
   const int words = (a.s.Cp + 31) >> 5;
   uint32_t* tgt = (uint32_t*)(smem + 512);
@@ -145,8 +147,10 @@ KP_FI void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
   const BindHdr* h = &a.bv.hdr[b];
   build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
   SelCtx x = make_ctx(a, b, tgt);
+  KP_STAMP(x, 0);
   const bool weights = h->strategy == ST_STATIC && h->sel == SEL_ALL;
   cd.F = gather(B, x, cd, weights);
+  KP_STAMP(x, 1);
   LdsCands cs{&cd, B.tid(), B.nth()};
   select_all_common(B, a, x, cs, cd.F, ss);
 }

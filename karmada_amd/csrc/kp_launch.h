@@ -18,6 +18,7 @@ struct KArgs {
   Sink sink;
   int32_t* slow;          // [B] flag: needs the exact serial path
   uint32_t* stats;        // [0]: bindings flagged for the serial path, [SLOW_*]: by reason
+  unsigned long long* dbg;  // diagnostic build only: phase cycle sums (nullptr otherwise)
 };
 
 enum : int {

@@ -140,6 +140,7 @@ KP_HD inline bool scale_down_targets(const SelCtx& x, unsigned char* mem, size_t
 // ----------------------------------------------------------------------------
 template <class BLK, class CS>
 KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScratch& ss) {
+  KP_STAMP_INIT
   const BindHdr& h = *x.h;
   const bool desc = (h.flags & BF_UID_DESC) != 0;
   const bool prop = (h.flags & BF_EMPTY_PROP) != 0;
@@ -225,6 +226,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
   vmin = B.min64(vmin);
   vtot = B.sum64(vtot);
   if (vmin < 0 || sabs >= (int64_t)kInt32Max) return SLOW_WRAP;  // int32 wrap hazard
+  KP_STAMP(x, 2);
   const int32_t target = mode == 0 ? h.replicas : sub32(h.replicas, assigned);
   if ((int32_t)vtot < target) {
     if (B.tid() == 0)
@@ -279,6 +281,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
       if (j < ceq) return SLOW_TIE;  // tie group straddles the cut
     }
   }
+  KP_STAMP(x, 3);
   auto member = [&](uint32_t rk, int64_t v) {
     if (st != ST_AGGREGATED) return true;
     const bool p = prior(rk);
@@ -293,6 +296,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
     });
   };
   WebRes w = webster_par(B, parties, target, desc, ss);
+  KP_STAMP(x, 4);
   emit_each(
       B, x, cs,
       [&](uint32_t rk, int32_t v0) {
@@ -302,6 +306,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
         return r;
       },
       prop);
+  KP_STAMP(x, 5);
   return SLOW_NONE;
 }
 

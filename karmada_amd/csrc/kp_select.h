@@ -72,7 +72,26 @@ struct SelCtx {
   const int32_t* erow;
   const uint32_t* tgt_bits;
   Sink sink;
+  unsigned long long* dbg;  // diagnostic build only (KP_STAMPS): per-phase cycle sums
 };
+
+// Diagnostic phase stamps (a separate -DKP_STAMPS build; never in libkp.so).
+#if defined(KP_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+#define KP_STAMP_INIT unsigned long long kp_t0 = __builtin_amdgcn_s_memtime();
+#define KP_STAMP(x, i)                                                   \
+  do {                                                                   \
+    if (threadIdx.x == 0 && (x).dbg) {                                   \
+      unsigned long long t = __builtin_amdgcn_s_memtime();               \
+      atomicAdd(&(x).dbg[i], t - kp_t0);                                 \
+      kp_t0 = t;                                                         \
+    }                                                                    \
+  } while (0)
+#else
+#define KP_STAMP_INIT
+#define KP_STAMP(x, i) \
+  do {                 \
+  } while (0)
+#endif
 
 struct SerialOut {
   int status = 0;
@@ -718,9 +737,14 @@ KP_FI WebRes webster_par(const BLK& B, Parties parties, int32_t N, bool desc, co
 // for every value the calling thread owns.
 template <class BLK, class Vals>
 KP_FI int64_t wsel_max(const BLK& B, unsigned long long* wh, Vals vals, int64_t target) {
+  uint64_t on = 0;
+  vals([&](int64_t v) { on |= (uint64_t)v; });
+  on = B.or64(on);
+  int start = 24;
+  while (start > 0 && !(on >> start)) start -= 8;
   uint32_t prefix = 0;
   int64_t above = 0;
-  for (int shift = 24; shift >= 0; shift -= 8) {
+  for (int shift = start; shift >= 0; shift -= 8) {
     for (int i = B.tid(); i < 256; i += B.nth()) wh[i] = 0;
     B.sync();
     const uint32_t hm = shift == 24 ? 0u : (~0u << (shift + 8));
@@ -728,24 +752,10 @@ KP_FI int64_t wsel_max(const BLK& B, unsigned long long* wh, Vals vals, int64_t 
       uint32_t v = (uint32_t)v64;
       if ((v & hm) == (prefix & hm) && v) kp_atomic_add(&wh[(v >> shift) & 255], (unsigned long long)v);
     });
-    B.sync();
-    int64_t sel = 0, ab = above;
-    if (B.tid() == 0) {
-      int64_t cum = above;
-      int bin = 0;
-      for (int b = 255; b >= 0; b--) {
-        if (cum + (int64_t)wh[b] >= target) {
-          bin = b;
-          break;
-        }
-        cum += (int64_t)wh[b];
-      }
-      sel = bin;
-      ab = cum;
-    }
-    sel = B.bcast(sel);
-    above = B.bcast(ab);
-    prefix |= (uint32_t)sel << shift;
+    int64_t before;
+    const int bin = B.find_bin(wh, target - above, &before, true);
+    above += before;
+    prefix |= (uint32_t)bin << shift;
   }
   return (int64_t)prefix;
 }
@@ -755,34 +765,35 @@ KP_FI int64_t wsel_max(const BLK& B, unsigned long long* wh, Vals vals, int64_t 
 // ----------------------------------------------------------------------------
 template <class BLK, class Pred, class Key>
 KP_FI uint64_t radix_select(const BLK& B, uint32_t* hist, int F, Pred pred, Key key, int64_t k) {
-  uint64_t prefix = 0;
-  for (int shift = 56; shift >= 0; shift -= 8) {
+  // bytes shared by every key are skipped: start at the highest differing byte
+  uint64_t an = ~0ull, on = 0;
+  for (int i = B.tid(); i < F; i += B.nth())
+    if (pred(i)) {
+      const uint64_t kk = key(i);
+      an &= kk;
+      on |= kk;
+    }
+  an = B.and64(an);
+  on = B.or64(on);
+  const uint64_t diff = an ^ on;
+  if (diff == 0) return an;  // all keys equal
+  int top = 63;
+  while (!((diff >> top) & 1)) top--;
+  const int start = (top / 8) * 8;
+  uint64_t prefix = start == 56 ? 0ull : (an & (~0ull << (start + 8)));
+  for (int shift = start; shift >= 0; shift -= 8) {
     for (int i = B.tid(); i < 256; i += B.nth()) hist[i] = 0;
     B.sync();
-    uint64_t hm = shift == 56 ? 0ull : (~0ull << (shift + 8));
+    const uint64_t hm = shift == 56 ? 0ull : (~0ull << (shift + 8));
     for (int i = B.tid(); i < F; i += B.nth())
       if (pred(i)) {
-        uint64_t kk = key(i);
+        const uint64_t kk = key(i);
         if ((kk & hm) == (prefix & hm)) kp_atomic_add(&hist[(kk >> shift) & 255], 1u);
       }
-    B.sync();
-    int64_t sel = 0, kk2 = k;
-    if (B.tid() == 0) {
-      int64_t cum = 0;
-      int bin = 255;
-      for (int i = 0; i < 256; i++) {
-        if (cum + hist[i] >= k) {
-          bin = i;
-          break;
-        }
-        cum += hist[i];
-      }
-      sel = bin;
-      kk2 = k - cum;
-    }
-    sel = B.bcast(sel);
-    k = B.bcast(kk2);
-    prefix |= (uint64_t)sel << shift;
+    int64_t before;
+    const int bin = B.find_bin(hist, k, &before, false);
+    k -= before;
+    prefix |= (uint64_t)bin << shift;
   }
   return prefix;
 }
