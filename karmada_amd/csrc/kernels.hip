@@ -11,6 +11,8 @@
 // k_compact       per-binding results gathered into CSR order.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kp_dev.h"
 #include "kp_kernels.h"
 
@@ -23,7 +25,7 @@ extern "C" __global__ void __launch_bounds__(kBlock) k_pair(SnapView s, BatchVie
   KP_SMEM;
   body_pair(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, b0, fmask, est, score, est_mode, md_cap);
 }
-extern "C" __global__ void __launch_bounds__(kBlock) k_select_all(KArgs a) {
+extern "C" __global__ void __launch_bounds__(1024) k_select_all(KArgs a) {
   KP_SMEM;
   body_select_all(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a);
 }
@@ -61,6 +63,16 @@ namespace dev {
 
 namespace {
 thread_local hipError_t g_err = hipSuccess;
+// Threads per SEL_ALL workgroup (LDS, not threads, bounds the workgroups per CU,
+// so wider workgroups add latency hiding). KP_SEL_THREADS overrides for tuning.
+int sel_threads() {
+  static int n = [] {
+    const char* e = getenv("KP_SEL_THREADS");
+    int v = e ? atoi(e) : 512;
+    return (v == 256 || v == 512 || v == 1024) ? v : 512;
+  }();
+  return n;
+}
 int chk(hipError_t e) {
   if (e != hipSuccess) {
     g_err = e;
@@ -129,7 +141,7 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
   hipStream_t h = (hipStream_t)st;
   switch (which) {
     case SEL_LAUNCH_ALL:
-      hipLaunchKernelGGL(k_select_all, dim3(a.n), dim3(kBlock), smem, h, a);
+      hipLaunchKernelGGL(k_select_all, dim3(a.n), dim3(sel_threads()), smem, h, a);
       break;
     case SEL_LAUNCH_CLUSTER:
       hipLaunchKernelGGL(k_select_cluster, dim3(a.n), dim3(kBlock), smem, h, a, cap);

@@ -522,28 +522,23 @@ KP_HD inline int32_t static_vote(const SelCtx& x, int c) {
 // ----------------------------------------------------------------------------
 template <class BLK>
 KP_FI int gather(const BLK& B, const SelCtx& x, Cands cd, bool weights) {
-  // Thread t reads cluster base + t of each block-wide step: the feasibility
-  // word is one broadcast load per wave and erow is read fully coalesced.
+  // Thread t owns clusters t + nth*j: one pass counts them (the feasibility word
+  // is a broadcast load per wave), one scan places them, and the second pass
+  // reads erow fully coalesced with no barrier between iterations. Candidate
+  // order is thread-major; nothing downstream depends on it (keys carry ranks).
   const SnapView& s = *x.s;
   const BindHdr& h = *x.h;
-  int F = 0;
-  for (int base = 0; base < s.C; base += B.nth()) {
-    const int c = base + B.tid();
-    const bool f = c < s.C && mask_test(x.frow, c);
-    uint32_t r = 0;
-    int32_t v = 0;
-    if (f) {
-      r = (uint32_t)c | ((uint32_t)overflow_order(s, *x.bv, h, c) << kRankBits);
-      v = weights ? static_vote(x, c) : x.erow[c];
+  const int tid = B.tid(), nth = B.nth();
+  int32_t mine = 0;
+  for (int c = tid; c < s.C; c += nth) mine += mask_test(x.frow, c) ? 1 : 0;
+  int32_t F;
+  int32_t pos = B.excl_scan(mine, &F);
+  for (int c = tid; c < s.C; c += nth)
+    if (mask_test(x.frow, c)) {
+      cd.r[pos] = (uint32_t)c | ((uint32_t)overflow_order(s, *x.bv, h, c) << kRankBits);
+      cd.v[pos] = weights ? static_vote(x, c) : x.erow[c];
+      pos++;
     }
-    int32_t tot;
-    const int32_t off = B.excl_scan(f ? 1 : 0, &tot);
-    if (f) {
-      cd.r[F + off] = r;
-      cd.v[F + off] = v;
-    }
-    F += tot;
-  }
   B.sync();
   return F;
 }
