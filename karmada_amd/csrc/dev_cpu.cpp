@@ -122,7 +122,7 @@ int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const Sele
       break;
     case SEL_LAUNCH_SLOW:
       grid(x.grid, smem, [&](int blk, unsigned char* sm) {
-        body_slow(CpuBlk{(int64_t*)sm}, blk, x.grid, sm, a, x.scratch, x.slot_bytes, cap);
+        body_slow(CpuBlk{(int64_t*)sm}, blk, x.grid, sm, a, x.scratch, x.slot_bytes, cap, x.lds_area);
       });
       break;
     default:

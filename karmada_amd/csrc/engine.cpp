@@ -152,7 +152,7 @@ struct kp_batch {
   int32_t *rstat = nullptr, *rsel = nullptr, *rnsel = nullptr;
   unsigned char* slow_scratch = nullptr;
   size_t slow_slot = 0;
-  int slow_grid = 0, slow_cap = 0;
+  int slow_grid = 0, slow_cap = 0, slow_lds = 0;
   // host results
   std::vector<int32_t> h_status, h_err, h_rstat, h_rsel, h_rnsel;
   std::vector<int64_t> h_arg;
@@ -640,6 +640,9 @@ struct Packer {
 
   void pack(const kp_binding& b, BindHdr& h) {
     memset(&h, 0, sizeof(h));
+    h.ip_beg = (int32_t)bt->ipool.size();
+    h.pr_beg = (int32_t)bt->progs.size();
+    h.in_beg = (int32_t)bt->instrs.size();
     const kp_options& o = s->opts;
     h.replicas = b.replicas;
     h.enabled = (int32_t)o.enabled_plugins;
@@ -845,6 +848,9 @@ struct Packer {
     bool big = !(f & BF_WORKLOAD_ASSIGN) || h.strategy == ST_DUPLICATED || (f & BF_EMPTY_PROP);
     uint64_t rep = b.replicas > 0 ? (uint64_t)b.replicas : 0;
     h.out_cap = (big ? C : std::min<uint64_t>(C, rep)) + (uint64_t)h.tgt_cnt;
+    h.ip_end = (int32_t)bt->ipool.size();
+    h.pr_end = (int32_t)bt->progs.size();
+    h.in_end = (int32_t)bt->instrs.size();
   }
 };
 
@@ -946,7 +952,7 @@ void parallel_for(int n, int threads, F fn) {
 
 size_t smem_pair(const kp_snapshot* s, int md_cap) {
   int words = (s->Cp + 31) >> 5;
-  return 512 + 8 * (size_t)words + 4 * (size_t)md_cap + 64;
+  return 512 + 8 * (size_t)words + 4 * (size_t)((md_cap + 3) & ~3) + kPairStage + 64;
 }
 size_t smem_all(const kp_snapshot* s) {
   int words = (s->Cp + 31) >> 5;
@@ -970,6 +976,8 @@ size_t smem_region_b(const kp_snapshot* s, int cap) {
          4 * (size_t)((words + 3) & ~3) + area + 64;
 }
 const int kMdCap = 4096;
+// MaxDivided table entries staged per workgroup: the snapshot's template count.
+int md_cap_of(const kp_snapshot* s) { return s->n_tmpl <= kMdCap ? std::max(4, s->n_tmpl) : 0; }
 
 }  // namespace
 
@@ -1055,7 +1063,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   }
   {
     const int cap = kSmallMax + kTgtSmallMax + 16;
-    size_t need = smem_pair(s, kMdCap);
+    size_t need = smem_pair(s, md_cap_of(s));
     if (!bt->l_all.empty()) need = std::max(need, smem_all(s));
     if (!bt->l_cluster.empty()) need = std::max(need, smem_cluster(s, cap));
     if (!bt->l_region.empty()) need = std::max({need, smem_region_a(s), smem_region_b(s, cap)});
@@ -1078,6 +1086,10 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   int max_tgt = 0;
   for (auto& h : bt->hdr) max_tgt = std::max(max_tgt, (int)h.tgt_cnt);
   bt->slow_cap = s->Cp + max_tgt + 64;
+  {  // LDS for the targets-only serial problems (scale-down), if small
+    size_t b = sizeof(Item) * (size_t)max_tgt + serial_scratch_bytes(2 * max_tgt + 16) + 64;
+    bt->slow_lds = b <= 32768 ? (int)((b + 15) & ~(size_t)15) : 0;
+  }
   int P = 1;
   while (P < s->Cp) P <<= 1;
   bt->slow_slot = (size_t)s->Cp * 8 + (size_t)P * 8 + sizeof(Item) * s->Cp + 4 * (size_t)s->Cp +
@@ -1190,7 +1202,8 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   HIPCHK(dev::fill(bt->dbg, 0, 32 * 8, st));
 #endif
   HIPCHK(dev::event_record(e->ev[0], st));
-  HIPCHK(dev::pair(st, s->view, bt->view, 0, B, bt->fmask, bt->est, nullptr, 0, kMdCap, smem_pair(s, kMdCap)));
+  HIPCHK(dev::pair(st, s->view, bt->view, 0, B, bt->fmask, bt->est, nullptr, 0, md_cap_of(s),
+                   smem_pair(s, md_cap_of(s))));
   HIPCHK(dev::event_record(e->ev[1], st));
   SelectExtra sx;
   sx.rout = bt->rout;
@@ -1200,6 +1213,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   sx.scratch = bt->slow_scratch;
   sx.slot_bytes = bt->slow_slot;
   sx.grid = bt->slow_grid;
+  sx.lds_area = bt->slow_lds;
   const int cap = kSmallMax + kTgtSmallMax + 16;
   if (!bt->l_all.empty()) {
     KArgs k = ka;
@@ -1261,7 +1275,8 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     KArgs k = ka;
     k.list = bt->d_slowlist;
     k.n = (int)bt->l_slow.size();
-    HIPCHK(dev::select(st, SEL_LAUNCH_SLOW, k, 1024 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4), bt->slow_cap, sx));
+    HIPCHK(dev::select(st, SEL_LAUNCH_SLOW, k, 1024 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area,
+                       bt->slow_cap, sx));
   }
   HIPCHK(dev::event_record(e->ev[2], st));
   // results -> host, compacted to CSR
@@ -1336,8 +1351,8 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
 // Runs the pair kernel and returns the rank-ordered device row pointers.
 static int run_pair(kp_engine* e, kp_batch* bt, int64_t* score, int est_mode, int b0, int nb) {
   kp_snapshot* s = bt->snap;
-  HIPCHK(dev::pair(e->stream, s->view, bt->view, b0, nb, bt->fmask, bt->est, score, est_mode, kMdCap,
-                     smem_pair(s, kMdCap)));
+  HIPCHK(dev::pair(e->stream, s->view, bt->view, b0, nb, bt->fmask, bt->est, score, est_mode, md_cap_of(s),
+                     smem_pair(s, md_cap_of(s))));
   HIPCHK(dev::sync(e->stream));
   return KP_OK;
 }

@@ -5,7 +5,7 @@
 // same code paths on the host.
 //
 // Per-block LDS layouts (dynamic shared memory; sizes computed in engine.cpp):
-//   pair      [512 red | tgt bits | evict bits | md table]
+//   pair      [512 red | tgt bits | evict bits | md table | predicate stage kPairStage]
 //   sel_all   [512 red | tgt bits | cand r [Cp] | cand v [Cp] | whist 2 KB | hist 1 KB | buf ecap*8]
 //   sel_all_reg [512 red | tgt bits | whist 2 KB | hist 1 KB | buf ecap*8]  (candidates in registers)
 //   sel_clus  [512 red | hist 1 KB | items 2*kSmallMax | keys 2*kSmallMax | tgt | cand/serial area]
@@ -79,6 +79,29 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
     for (int t = B.tid(); t < s.n_tmpl; t += B.nth()) md[t] = template_md(s, bv, h, t);
     B.sync();
   }
+  // Stage this binding's predicate data (programs, value lists, tolerations) in
+  // LDS: every lane reads it for every cluster, uniformly.
+  BatchView lv = bv;
+  {
+    unsigned char* st = (unsigned char*)(md + ((md_cap + 3) & ~3));
+    const int nin = h.in_end - h.in_beg, npr = h.pr_end - h.pr_beg, nip = h.ip_end - h.ip_beg, nto = h.tol_cnt;
+    const size_t need = sizeof(Instr) * nin + sizeof(Prog) * npr + sizeof(Tol) * nto + 4 * (size_t)nip;
+    if (need <= (size_t)kPairStage) {
+      Instr* si = (Instr*)st;
+      Prog* sp = (Prog*)(si + nin);
+      Tol* so = (Tol*)(sp + npr);
+      int32_t* sv = (int32_t*)(so + nto);
+      for (int i = B.tid(); i < nin; i += B.nth()) si[i] = bv.instrs[h.in_beg + i];
+      for (int i = B.tid(); i < npr; i += B.nth()) sp[i] = bv.progs[h.pr_beg + i];
+      for (int i = B.tid(); i < nto; i += B.nth()) so[i] = bv.tols[h.tol_off + i];
+      for (int i = B.tid(); i < nip; i += B.nth()) sv[i] = bv.ipool[h.ip_beg + i];
+      B.sync();
+      lv.instrs = si - h.in_beg;  // absolute pool indices keep working
+      lv.progs = sp - h.pr_beg;
+      lv.tols = so - h.tol_off;
+      lv.ipool = sv - h.ip_beg;
+    }
+  }
   uint64_t* frow = fmask + (size_t)b * s.W;
   int32_t* erow = est + (size_t)b * s.Cp;
   for (int base = 0; base < s.Cp; base += B.nth()) {
@@ -86,10 +109,10 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
     bool fit = false;
     int32_t e = 0;
     if (est_mode == 0) {
-      fit = pair_feasible(s, bv, h, c, tgt, evict);
-      if (fit) e = cal_available(s, bv, h, c, use_md ? md : nullptr);
+      fit = pair_feasible(s, lv, h, c, tgt, evict);
+      if (fit) e = cal_available(s, lv, h, c, use_md ? md : nullptr);
     } else if (c < s.C) {
-      e = general_estimate(s, bv, h, c, use_md ? md : nullptr);
+      e = general_estimate(s, lv, h, c, use_md ? md : nullptr);
       fit = true;
     }
     B.mask_store(frow, c, fit, s.W);
@@ -318,9 +341,10 @@ KP_FI void body_region_b(const BLK& B, int blk, unsigned char* smem, const KArgs
 // ---------------------------------------------------------------------------
 template <class BLK>
 KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const KArgs& a, unsigned char* scratch,
-                     size_t slot_bytes, int scratch_cap) {
+                     size_t slot_bytes, int scratch_cap, int lds_area) {
   const int words = (a.s.Cp + 31) >> 5;
   uint32_t* tgt = (uint32_t*)(smem + 512);
+  unsigned char* larea = (unsigned char*)(tgt + ((words + 3) & ~3));  // lds_area bytes
   unsigned char* mine = scratch + (size_t)blk * slot_bytes;
   // slot layout: cand r/v [Cp] | keys [P] | items [Cp] | pos [Cp] | serial scratch
   int P = 1;
@@ -341,7 +365,8 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
     build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
     SelCtx x = make_ctx(a, b, tgt);
     int done = 0;
-    if (B.tid() == 0 && scale_down_targets(x, ser, (size_t)serial_scratch_bytes(scratch_cap))) {
+    if (B.tid() == 0 && ((lds_area > 0 && scale_down_targets(x, larea, (size_t)lds_area)) ||
+                         scale_down_targets(x, ser, (size_t)serial_scratch_bytes(scratch_cap)))) {
       a.slow[b] = 0;
       done = 1;
     }

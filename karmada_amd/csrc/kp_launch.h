@@ -38,9 +38,11 @@ struct SelectExtra {
   unsigned char* scratch = nullptr;  // slow path global scratch
   size_t slot_bytes = 0;
   int grid = 0;                      // slow path persistent grid
+  int lds_area = 0;                  // slow path: LDS bytes for the small serial problems
 };
 
 constexpr int kBlock = 256;
+constexpr int kPairStage = 4096;  // bytes of per-binding predicate data staged in LDS
 
 // Enumeration capacity (u64 entries) of the SEL_ALL selection buffer.
 KP_HD inline int sel_all_ecap(int Cp) { return Cp / 2 < 64 ? 64 : (Cp / 2 > 2048 ? 2048 : Cp / 2); }

@@ -123,6 +123,8 @@ struct alignas(16) BindHdr {
   int32_t need_replicas;         // SelectBestClusters needReplicas (-1 = ignore resources)
   int32_t pad0;
   uint64_t out_cap;
+  // this binding's slices of the pools (staged into LDS by the pair kernel)
+  int32_t ip_beg, ip_end, pr_beg, pr_end, in_beg, in_end;
 };
 
 // ---- snapshot device view -----------------------------------------------------
