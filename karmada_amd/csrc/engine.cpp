@@ -107,7 +107,9 @@ struct kp_snapshot {
   std::vector<uint32_t> perm;                        // rank -> caller index
   std::vector<int32_t> inv;                          // caller index -> rank
   int32_t rid_cpu = -1, rid_mem = -1, rid_eph = -1;
-  int n_tmpl = 0;
+  int n_tmpl = 0, kmax = 0;
+  std::vector<std::string> names;  // cluster names in rank order
+  std::vector<unsigned char> blob;  // kp_snapshot_export buffer
   // host copies
   std::vector<uint32_t> flags;
   std::vector<int32_t> provider, region, region_idx, zone_off, zone_ids, label_val, taint_off, taint_key, taint_val,
@@ -177,6 +179,8 @@ bool qmap(const kp_resource* r, uint32_t n, QtyMap* m) {
   }
   return ok;
 }
+
+int upload_snapshot(kp_engine* e, kp_snapshot* s);
 
 int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_options* o, kp_snapshot* s) {
   s->opts = o ? *o : kp_options{0, 1, KP_PLUGIN_ALL};
@@ -381,7 +385,7 @@ int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_opti
   pad1(s->taint_val);
   pad1(s->taint_eff);
   // model groups transposed to [kmax][Cp] so a wave reads 64 clusters' k-th group coalesced
-  int kmax = 0;
+  int& kmax = s->kmax;
   for (int r = 0; r < C; r++) kmax = std::max(kmax, s->mgrp_off[r + 1] - s->mgrp_off[r]);
   s->mg_tid.assign((size_t)std::max(kmax, 1) * Cp, 0);
   s->mg_cnt.assign((size_t)std::max(kmax, 1) * Cp, 0);
@@ -391,7 +395,16 @@ int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_opti
       s->mg_tid[k * Cp + r] = s->mgrp_tid[g];
       s->mg_cnt[k * Cp + r] = (int32_t)std::min<int64_t>(s->mgrp_cnt[g], kInt32Max);
     }
-  // upload
+  s->names.resize(C);
+  for (int r = 0; r < C; r++) s->names[r] = names[order[r]];
+  return upload_snapshot(e, s);
+}
+
+// Device copy of a packed snapshot (kp_snapshot_create and kp_snapshot_import).
+int upload_snapshot(kp_engine* e, kp_snapshot* s) {
+  const int C = s->C, Cp = s->Cp, kmax = s->kmax;
+  const int K = (int)s->keys.names.size(), AW = ((int)s->gvk.names.size() + 63) / 64,
+            R = (int)s->res.names.size();
   SnapView& v = s->view;
   v.C = C;
   v.Cp = Cp;
@@ -981,6 +994,78 @@ int md_cap_of(const kp_snapshot* s) { return s->n_tmpl <= kMdCap ? std::max(4, s
 
 }  // namespace
 
+// Packed-snapshot bytes: pack once on one rank, broadcast the bytes, import on
+// the others. Host-endian; same engine build on every rank.
+namespace {
+const char kSnapMagic[8] = {'K', 'P', 'S', 'N', 'A', 'P', '0', '1'};
+struct Wr {
+  std::vector<unsigned char>& b;
+  void raw(const void* p, size_t n) { b.insert(b.end(), (const unsigned char*)p, (const unsigned char*)p + n); }
+  void u64(uint64_t x) { raw(&x, 8); }
+  void str(const std::string& x) {
+    u64(x.size());
+    raw(x.data(), x.size());
+  }
+  void strs(const std::vector<std::string>& v) {
+    u64(v.size());
+    for (auto& x : v) str(x);
+  }
+  template <class T>
+  void vec(const std::vector<T>& v) {
+    u64(v.size());
+    raw(v.data(), v.size() * sizeof(T));
+  }
+};
+struct Rd {
+  const unsigned char* p;
+  const unsigned char* end;
+  bool ok = true;
+  bool raw(void* d, size_t n) {
+    if ((size_t)(end - p) < n) return ok = false;
+    memcpy(d, p, n);
+    p += n;
+    return true;
+  }
+  uint64_t u64() {
+    uint64_t x = 0;
+    raw(&x, 8);
+    return x;
+  }
+  std::string str() {
+    uint64_t n = u64();
+    if (!ok || (size_t)(end - p) < n) {
+      ok = false;
+      return {};
+    }
+    std::string x((const char*)p, n);
+    p += n;
+    return x;
+  }
+  std::vector<std::string> strs() {
+    uint64_t n = u64();
+    std::vector<std::string> v;
+    for (uint64_t i = 0; ok && i < n; i++) v.push_back(str());
+    return v;
+  }
+  template <class T>
+  std::vector<T> vec() {
+    uint64_t n = u64();
+    std::vector<T> v;
+    if (!ok || n > (uint64_t)(end - p) / sizeof(T)) {
+      ok = false;
+      return v;
+    }
+    v.resize(n);
+    raw(v.data(), n * sizeof(T));
+    return v;
+  }
+};
+void dict_from(Dict& d, const std::vector<std::string>& names) {
+  for (auto& n : names) d.add(n);
+}
+}  // namespace
+
+
 // ============================================================================
 // C ABI
 // ============================================================================
@@ -1033,8 +1118,118 @@ int kp_snapshot_create(kp_engine* e, const kp_cluster* clusters, uint64_t n, con
 
 void kp_snapshot_destroy(kp_snapshot* s) { delete s; }
 
-int kp_snapshot_export(const kp_snapshot*, const void**, uint64_t*) { return KP_ENOTSUP; }
-int kp_snapshot_import(kp_engine*, const void*, uint64_t, kp_snapshot**) { return KP_ENOTSUP; }
+int kp_snapshot_export(const kp_snapshot* cs, const void** bytes, uint64_t* n_bytes) {
+  if (!cs || !bytes || !n_bytes) return KP_EINVAL;
+  kp_snapshot* s = const_cast<kp_snapshot*>(cs);
+  s->blob.clear();
+  Wr w{s->blob};
+  w.raw(kSnapMagic, 8);
+  w.u64((uint64_t)s->C);
+  w.u64(s->opts.enable_empty_workload_propagation);
+  w.u64(s->opts.customized_cluster_resource_modeling);
+  w.u64(s->opts.enabled_plugins);
+  w.u64((uint64_t)(int64_t)s->rid_cpu);
+  w.u64((uint64_t)(int64_t)s->rid_mem);
+  w.u64((uint64_t)(int64_t)s->rid_eph);
+  w.u64((uint64_t)s->n_tmpl);
+  w.u64((uint64_t)s->kmax);
+  w.strs(s->str.names);
+  w.strs(s->keys.names);
+  w.strs(s->gvk.names);
+  w.strs(s->res.names);
+  w.strs(s->regions.names);
+  w.strs(s->names);
+  w.vec(s->perm);
+  w.vec(s->flags);
+  w.vec(s->provider);
+  w.vec(s->region);
+  w.vec(s->region_idx);
+  w.vec(s->zone_off);
+  w.vec(s->zone_ids);
+  w.vec(s->label_val);
+  w.vec(s->taint_off);
+  w.vec(s->taint_key);
+  w.vec(s->taint_val);
+  w.vec(s->taint_eff);
+  w.vec(s->mg_tid);
+  w.vec(s->mg_cnt);
+  w.vec(s->provider_int);
+  w.vec(s->region_int);
+  w.vec(s->allowed);
+  w.vec(s->avail);
+  w.vec(s->tmpl);
+  w.vec(s->api_bits);
+  *bytes = s->blob.data();
+  *n_bytes = s->blob.size();
+  return KP_OK;
+}
+
+int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_snapshot** out) {
+  if (!e || !bytes || !out) return KP_EINVAL;
+  Rd r{(const unsigned char*)bytes, (const unsigned char*)bytes + n_bytes};
+  char magic[8];
+  if (!r.raw(magic, 8) || memcmp(magic, kSnapMagic, 8) != 0) {
+    e->err = "not a kp snapshot";
+    return KP_EINVAL;
+  }
+  (void)dev::set_device(e->device);
+  auto* s = new kp_snapshot();
+  std::unique_ptr<kp_snapshot> guard(s);
+  s->e = e;
+  s->C = (int)r.u64();
+  s->Cp = s->C ? ((s->C + 63) / 64) * 64 : 64;
+  s->W = s->Cp / 64;
+  s->opts.enable_empty_workload_propagation = (uint8_t)r.u64();
+  s->opts.customized_cluster_resource_modeling = (uint8_t)r.u64();
+  s->opts.enabled_plugins = (uint32_t)r.u64();
+  s->rid_cpu = (int32_t)(int64_t)r.u64();
+  s->rid_mem = (int32_t)(int64_t)r.u64();
+  s->rid_eph = (int32_t)(int64_t)r.u64();
+  s->n_tmpl = (int)r.u64();
+  s->kmax = (int)r.u64();
+  dict_from(s->str, r.strs());
+  dict_from(s->keys, r.strs());
+  dict_from(s->gvk, r.strs());
+  dict_from(s->res, r.strs());
+  dict_from(s->regions, r.strs());
+  s->names = r.strs();
+  s->perm = r.vec<uint32_t>();
+  s->flags = r.vec<uint32_t>();
+  s->provider = r.vec<int32_t>();
+  s->region = r.vec<int32_t>();
+  s->region_idx = r.vec<int32_t>();
+  s->zone_off = r.vec<int32_t>();
+  s->zone_ids = r.vec<int32_t>();
+  s->label_val = r.vec<int32_t>();
+  s->taint_off = r.vec<int32_t>();
+  s->taint_key = r.vec<int32_t>();
+  s->taint_val = r.vec<int32_t>();
+  s->taint_eff = r.vec<int32_t>();
+  s->mg_tid = r.vec<int32_t>();
+  s->mg_cnt = r.vec<int32_t>();
+  s->provider_int = r.vec<int64_t>();
+  s->region_int = r.vec<int64_t>();
+  s->allowed = r.vec<int64_t>();
+  s->avail = r.vec<int64_t>();
+  s->tmpl = r.vec<int64_t>();
+  s->api_bits = r.vec<uint64_t>();
+  const size_t Cp = (size_t)s->Cp;
+  if (!r.ok || s->C > kMaxClusters || (int)s->names.size() != s->C || s->perm.size() != (size_t)s->C ||
+      s->flags.size() != Cp || s->allowed.size() != Cp || s->zone_off.size() != (size_t)s->C + 1 ||
+      s->taint_off.size() != (size_t)s->C + 1 || s->mg_tid.size() != s->mg_cnt.size()) {
+    e->err = "truncated or inconsistent snapshot bytes";
+    return KP_EINVAL;
+  }
+  s->inv.assign(s->C, -1);
+  for (int rk = 0; rk < s->C; rk++) {
+    s->rank_of[s->names[rk]] = rk;
+    if (s->perm[rk] < (uint32_t)s->C) s->inv[s->perm[rk]] = rk;
+  }
+  int rc = upload_snapshot(e, s);
+  if (rc != KP_OK) return rc;
+  *out = guard.release();
+  return KP_OK;
+}
 
 int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindings, uint64_t n, kp_batch** out) {
   if (!e || !sc || !out || (n && !bindings)) return KP_EINVAL;

@@ -68,6 +68,8 @@ def load_library(path: str = LIB_PATH):
     L.kp_max_available_replicas.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint32), C.c_uint64,
                                             C.POINTER(C.c_int32)]
     L.kp_last_stage_times.argtypes = [vp, C.POINTER(api.kp_stage_times)]
+    L.kp_snapshot_export.argtypes = [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
+    L.kp_snapshot_import.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(vp)]
     if L.kp_abi_version() != KP_ABI_VERSION:
         raise EngineError("libkp.so ABI version mismatch")
     _LIBS[path] = L
@@ -148,6 +150,22 @@ class Snapshot:
         self.engine, self.names, self.opts = engine, names, opts
         h = C.c_void_p()
         engine._check(engine.L.kp_snapshot_create(engine.h, ca, n, C.byref(opts), C.byref(h)), "kp_snapshot_create")
+        self.h = h
+        return self
+
+    def to_bytes(self) -> bytes:
+        """Packed snapshot bytes (kp_snapshot_export) for broadcast to other ranks."""
+        p, n = C.c_void_p(), C.c_uint64()
+        self.engine._check(self.engine.L.kp_snapshot_export(self.h, C.byref(p), C.byref(n)), "kp_snapshot_export")
+        return C.string_at(p, n.value)
+
+    @classmethod
+    def from_bytes(cls, engine: Engine, data: bytes, names: List[str]):
+        """kp_snapshot_import: the packed snapshot of another rank, uploaded to this engine's device."""
+        self = cls.__new__(cls)
+        self.engine, self.names, self.opts = engine, names, None
+        h = C.c_void_p()
+        engine._check(engine.L.kp_snapshot_import(engine.h, data, len(data), C.byref(h)), "kp_snapshot_import")
         self.h = h
         return self
 
