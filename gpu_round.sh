@@ -9,12 +9,12 @@ step() {
   local rc=$?
   echo "$name rc=$rc"
   tail -5 "gpurun_out/$name.log"
-  if [ $rc -gt 1 ]; then exit $rc; fi
+  if [ $rc -ne 0 ]; then exit $rc; fi
 }
 for s in "$@"; do
   case $s in
     smoke) step smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
-    tests) step gpu_tests 900 python -m pytest tests -m gpu -q -rf ;;
+    tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     bench_small) step bench_small 300 python bench.py --steps 3 --warmup 1 --bindings 5000 --no-cpu ;;
     bench) step bench 600 python bench.py --steps 5 --warmup 1 ;;
     sweep) for t in 256 512 1024; do KP_SEL_THREADS=$t step sweep_$t 300 python bench.py --steps 3 --warmup 1 --no-cpu; done ;;

@@ -44,6 +44,16 @@ KP_FI void build_bits(const BLK& B, uint32_t* bits, int words, const int32_t* po
   B.sync();
 }
 
+// p - bias as a flat (64-bit) address. Biasing the LDS pointer itself would be
+// done in the 32-bit local address space, where a bias larger than the offset
+// wraps; the wrapped offset, cast to flat and indexed again, then lands past
+// the LDS aperture (HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION). The integer
+// round trip keeps the arithmetic in 64 bits.
+template <class T>
+KP_FI const T* rebase(const T* p, int64_t bias) {
+  return (const T*)((uintptr_t)p - (uintptr_t)bias * sizeof(T));
+}
+
 // Status of bindings that never reach selection.
 template <class BLK>
 KP_FI bool pre_checks(const BLK& B, const SelCtx& x, int F) {
@@ -96,10 +106,10 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
       for (int i = B.tid(); i < nto; i += B.nth()) so[i] = bv.tols[h.tol_off + i];
       for (int i = B.tid(); i < nip; i += B.nth()) sv[i] = bv.ipool[h.ip_beg + i];
       B.sync();
-      lv.instrs = si - h.in_beg;  // absolute pool indices keep working
-      lv.progs = sp - h.pr_beg;
-      lv.tols = so - h.tol_off;
-      lv.ipool = sv - h.ip_beg;
+      lv.instrs = rebase(si, h.in_beg);  // absolute pool indices keep working
+      lv.progs = rebase(sp, h.pr_beg);
+      lv.tols = rebase(so, h.tol_off);
+      lv.ipool = rebase(sv, h.ip_beg);
     }
   }
   uint64_t* frow = fmask + (size_t)b * s.W;
