@@ -17,6 +17,7 @@ for s in "$@"; do
     tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     bench_small) step bench_small 300 python bench.py --steps 3 --warmup 1 --bindings 5000 --no-cpu ;;
     bench) step bench 600 python bench.py --steps 5 --warmup 1 ;;
+    benchq) step benchq 300 python bench.py --steps 5 --warmup 1 --no-cpu ;;
     sweep) for t in 256 512 1024; do KP_SEL_THREADS=$t step sweep_$t 300 python bench.py --steps 3 --warmup 1 --no-cpu; done ;;
     configs) for c in 2 4 6; do step bench_config$c 300 python bench.py --config $c --steps 3 --warmup 1 --no-cpu; done ;;
     stamps) step stamps 300 python bench.py --lib karmada_amd/libkp_stamps.so --steps 2 --warmup 1 --no-cpu ;;

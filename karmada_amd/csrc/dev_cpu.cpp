@@ -31,7 +31,7 @@ void grid(int n, size_t smem_bytes, F fn) {
   if (T > n) T = n;
   std::atomic<int> next(0);
   auto work = [&]() {
-    std::vector<int64_t> smem((smem_bytes + 512 + 7) / 8);
+    std::vector<int64_t> smem((smem_bytes + kRedBytes + 7) / 8);
     for (;;) {
       int b = next.fetch_add(1);
       if (b >= n) break;
@@ -101,7 +101,7 @@ int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const Sele
   switch (which) {
     case SEL_LAUNCH_ALL:
     case SEL_LAUNCH_ALL_REG: {  // the host runs the LDS form; size its scratch here
-      const size_t need = 512 + 4 * (size_t)((((a.s.Cp + 31) >> 5) + 3) & ~3) + 8 * (size_t)a.s.Cp + 3072 +
+      const size_t need = kRedBytes + 4 * (size_t)((((a.s.Cp + 31) >> 5) + 3) & ~3) + 8 * (size_t)a.s.Cp + 3072 +
                           8 * (size_t)sel_all_ecap(a.s.Cp) + 64;
       grid(a.n, need > smem ? need : smem,
            [&](int blk, unsigned char* sm) { body_select_all(CpuBlk{(int64_t*)sm}, blk, sm, a); });

@@ -965,27 +965,27 @@ void parallel_for(int n, int threads, F fn) {
 
 size_t smem_pair(const kp_snapshot* s, int md_cap) {
   int words = (s->Cp + 31) >> 5;
-  return 512 + 8 * (size_t)words + 4 * (size_t)((md_cap + 3) & ~3) + kPairStage + 64;
+  return kRedBytes + 8 * (size_t)words + 4 * (size_t)((md_cap + 3) & ~3) + kPairStage + 64;
 }
 size_t smem_all(const kp_snapshot* s) {
   int words = (s->Cp + 31) >> 5;
-  return 512 + 4 * (size_t)((words + 3) & ~3) + 8 * (size_t)s->Cp + 3072 + 8 * (size_t)sel_all_ecap(s->Cp) + 64;
+  return kRedBytes + 4 * (size_t)((words + 3) & ~3) + 8 * (size_t)s->Cp + 3072 + 8 * (size_t)sel_all_ecap(s->Cp) + 64;
 }
 size_t smem_cluster(const kp_snapshot* s, int cap) {
   int words = (s->Cp + 31) >> 5;
   size_t area = std::max(8 * (size_t)s->Cp, serial_scratch_bytes(cap));
-  return 512 + 1024 + sizeof(Item) * 2 * kSmallMax + 16 * kSmallMax + 4 * (size_t)((words + 3) & ~3) + area + 64;
+  return kRedBytes + 1024 + sizeof(Item) * 2 * kSmallMax + 16 * kSmallMax + 4 * (size_t)((words + 3) & ~3) + area + 64;
 }
 size_t smem_region_a(const kp_snapshot* s) {
   int words = (s->Cp + 31) >> 5;
   size_t R = s->view.n_regions;
-  return 512 + 80 * R + 4 * (size_t)((words + 3) & ~3) + 8 * (size_t)s->Cp + 64;
+  return kRedBytes + 80 * R + 4 * (size_t)((words + 3) & ~3) + 8 * (size_t)s->Cp + 64;
 }
 size_t smem_region_b(const kp_snapshot* s, int cap) {
   int words = (s->Cp + 31) >> 5;
   size_t R = s->view.n_regions;
   size_t area = std::max(8 * (size_t)s->Cp, serial_scratch_bytes(cap));
-  return 512 + 1024 + sizeof(Item) * 2 * kSmallMax + 16 * kSmallMax + 8 * R + 4 * ((R + 3) & ~3) +
+  return kRedBytes + 1024 + sizeof(Item) * 2 * kSmallMax + 16 * kSmallMax + 8 * R + 4 * ((R + 3) & ~3) +
          4 * (size_t)((words + 3) & ~3) + area + 64;
 }
 const int kMdCap = 4096;
@@ -1470,7 +1470,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     KArgs k = ka;
     k.list = bt->d_slowlist;
     k.n = (int)bt->l_slow.size();
-    HIPCHK(dev::select(st, SEL_LAUNCH_SLOW, k, 1024 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area,
+    HIPCHK(dev::select(st, SEL_LAUNCH_SLOW, k, kRedBytes + 512 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area,
                        bt->slow_cap, sx));
   }
   HIPCHK(dev::event_record(e->ev[2], st));

@@ -28,9 +28,47 @@
 
 namespace kp {
 
+// Bytes of LDS at the start of every workgroup's dynamic shared memory reserved
+// for the block primitives' cross-wave scratch (two alternating 64-slot areas).
+constexpr int kRedBytes = 1024;
+
 #if defined(__HIPCC__) || defined(__HIP__)
+// DPP lane exchange (GFX9 encodings): quad_perm [1,0,3,2] / [2,3,0,1], row
+// half-mirror, row mirror, row_shr:n (0x110+n), row_bcast:15 / :31.
+template <int CTRL, int ROWS = 0xF, bool BOUND0 = false, class T>
+KP_INLINE T kp_dpp(T old, T v) {
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t u = (uint64_t)v, o = (uint64_t)old;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)o, (int)(uint32_t)u, CTRL, ROWS, 0xF, BOUND0);
+    const uint32_t hi =
+        (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(o >> 32), (int)(uint32_t)(u >> 32), CTRL, ROWS, 0xF, BOUND0);
+    return (T)(((uint64_t)hi << 32) | lo);
+  } else {
+    return (T)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWS, 0xF, BOUND0);
+  }
+}
+template <class T>
+KP_INLINE T kp_readlane(T v, int l) {
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t u = (uint64_t)v;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return (T)(((uint64_t)hi << 32) | lo);
+  } else {
+    return (T)__builtin_amdgcn_readlane((int)v, l);
+  }
+}
+
+// Block policy of one HIP workgroup (wave64 x N waves, N <= 16). Wave-level
+// reductions and scans run on DPP (no LDS round trips); the cross-wave step
+// writes one slot per wave into one of two alternating scratch areas, so each
+// primitive needs a single barrier: a thread can only write an area again after
+// passing the next primitive's barrier, which every thread reaches only once it
+// has read the previous contents. Every primitive must be called in block-
+// uniform control flow, in the same sequence by all threads.
 struct GpuBlk {
-  int64_t* red;  // >= 32 int64 of LDS
+  int64_t* red;  // kRedBytes of LDS
+  mutable int ph = 0;
 
   KP_INLINE int tid() const { return (int)threadIdx.x; }
   KP_INLINE int nth() const { return (int)blockDim.x; }
@@ -38,49 +76,100 @@ struct GpuBlk {
   KP_INLINE int wid() const { return (int)(threadIdx.x >> 6); }
   KP_INLINE int nwaves() const { return (int)(blockDim.x >> 6); }
   KP_INLINE void sync() const { __syncthreads(); }
+  KP_INLINE int64_t* area() const {
+    int64_t* a = red + (ph ? 64 : 0);
+    ph ^= 1;
+    return a;
+  }
 
+  // Every lane's v combined over the wave (op associative and commutative,
+  // id its identity); the result is wave-uniform.
   template <class T, class Op>
-  KP_INLINE T wave_reduce(T v, Op op) const {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = op(v, (T)__shfl_xor(v, o, 64));
-    return v;
+  KP_INLINE T wave_reduce(T v, Op op, T id) const {
+    v = op(v, kp_dpp<0xB1>(id, v));
+    v = op(v, kp_dpp<0x4E>(id, v));
+    v = op(v, kp_dpp<0x141>(id, v));
+    v = op(v, kp_dpp<0x140>(id, v));
+    return op(op(kp_readlane(v, 0), kp_readlane(v, 16)), op(kp_readlane(v, 32), kp_readlane(v, 48)));
+  }
+  // Inclusive prefix sum over the wave's lanes.
+  template <class T>
+  KP_INLINE T wave_incl_scan(T x) const {
+    x += kp_dpp<0x111, 0xF, true>((T)0, x);
+    x += kp_dpp<0x112, 0xF, true>((T)0, x);
+    x += kp_dpp<0x114, 0xF, true>((T)0, x);
+    x += kp_dpp<0x118, 0xF, true>((T)0, x);
+    x += kp_dpp<0x142, 0xA>((T)0, x);
+    x += kp_dpp<0x143, 0xC>((T)0, x);
+    return x;
   }
   template <class T, class Op>
-  KP_INLINE T reduce(T v, Op op) const {
-    v = wave_reduce(v, op);
+  KP_INLINE T reduce(T v, Op op, T id) const {
+    v = wave_reduce(v, op, id);
+    int64_t* a = area();
+    if (lane() == 0) a[wid()] = (int64_t)v;
     sync();
-    if (lane() == 0) red[wid()] = (int64_t)v;
-    sync();
-    T r = (T)red[0];
-    for (int w = 1; w < nwaves(); w++) r = op(r, (T)red[w]);
-    sync();
+    T r = (T)a[0];
+    for (int w = 1; w < nwaves(); w++) r = op(r, (T)a[w]);
     return r;
   }
-  KP_INLINE int64_t sum64(int64_t v) const { return reduce(v, [](int64_t a, int64_t b) { return a + b; }); }
-  KP_INLINE uint64_t minu64(uint64_t v) const {
-    return reduce(v, [](uint64_t a, uint64_t b) { return a < b ? a : b; });
-  }
-  KP_INLINE int64_t max64(int64_t v) const { return reduce(v, [](int64_t a, int64_t b) { return a > b ? a : b; }); }
-  KP_INLINE int64_t min64(int64_t v) const { return reduce(v, [](int64_t a, int64_t b) { return a < b ? a : b; }); }
-  KP_INLINE bool any(bool p) const { return sum64(p ? 1 : 0) != 0; }
-  // Exclusive prefix sum of per-thread counts in thread order; *total = sum.
-  KP_INLINE int32_t excl_scan(int32_t v, int32_t* total) const {
-    int32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      int32_t y = __shfl_up(x, o, 64);
-      if (lane() >= o) x += y;
+  // Two reductions for one barrier.
+  template <class OpA, class OpB>
+  KP_INLINE void reduce2(int64_t& x, OpA opa, int64_t ida, int64_t& y, OpB opb, int64_t idb) const {
+    x = wave_reduce(x, opa, ida);
+    y = wave_reduce(y, opb, idb);
+    int64_t* a = area();
+    if (lane() == 0) {
+      a[wid()] = x;
+      a[16 + wid()] = y;
     }
     sync();
-    if (lane() == 63) red[wid()] = x;
+    x = a[0];
+    y = a[16];
+    for (int w = 1; w < nwaves(); w++) {
+      x = opa(x, a[w]);
+      y = opb(y, a[16 + w]);
+    }
+  }
+  KP_INLINE int64_t sum64(int64_t v) const { return reduce(v, [](int64_t a, int64_t b) { return a + b; }, (int64_t)0); }
+  KP_INLINE uint64_t minu64(uint64_t v) const {
+    return reduce(v, [](uint64_t a, uint64_t b) { return a < b ? a : b; }, (uint64_t)~0ull);
+  }
+  KP_INLINE int64_t max64(int64_t v) const {
+    return reduce(v, [](int64_t a, int64_t b) { return a > b ? a : b; }, (int64_t)INT64_MIN);
+  }
+  KP_INLINE int64_t min64(int64_t v) const {
+    return reduce(v, [](int64_t a, int64_t b) { return a < b ? a : b; }, (int64_t)INT64_MAX);
+  }
+  KP_INLINE void sum2(int64_t& x, int64_t& y) const {
+    auto add = [](int64_t a, int64_t b) { return a + b; };
+    reduce2(x, add, 0, y, add, 0);
+  }
+  KP_INLINE void maxsum(int64_t& mx, int64_t& sm) const {
+    reduce2(mx, [](int64_t a, int64_t b) { return a > b ? a : b; }, INT64_MIN, sm,
+            [](int64_t a, int64_t b) { return a + b; }, 0);
+  }
+  KP_INLINE bool any(bool p) const {
+    const bool w = __ballot(p) != 0;
+    int64_t* a = area();
+    if (lane() == 0) a[wid()] = w ? 1 : 0;
+    sync();
+    int64_t r = 0;
+    for (int i = 0; i < nwaves(); i++) r |= a[i];
+    return r != 0;
+  }
+  // Exclusive prefix sum of per-thread counts in thread order; *total = sum.
+  KP_INLINE int32_t excl_scan(int32_t v, int32_t* total) const {
+    const int32_t x = wave_incl_scan(v);
+    int64_t* a = area();
+    if (lane() == 63) a[wid()] = x;
     sync();
     int32_t base = 0, tot = 0;
     for (int w = 0; w < nwaves(); w++) {
-      int32_t s = (int32_t)red[w];
+      int32_t s = (int32_t)a[w];
       if (w < wid()) base += s;
       tot += s;
     }
-    sync();
     *total = tot;
     return base + x - v;
   }
@@ -90,6 +179,7 @@ struct GpuBlk {
   template <class T>
   KP_INLINE int find_bin(const T* hist, int64_t k, int64_t* before, bool rev) const {
     sync();
+    int64_t* a = area();
     if (wid() == 0) {
       const int l = lane();
       int64_t v[4], s = 0;
@@ -99,12 +189,7 @@ struct GpuBlk {
         v[q] = (int64_t)hist[idx];
         s += v[q];
       }
-      int64_t incl = s;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        int64_t y = __shfl_up(incl, o, 64);
-        if (l >= o) incl += y;
-      }
+      const int64_t incl = wave_incl_scan(s);
       const uint64_t m = __ballot(incl >= k);
       const int first = m ? (int)__builtin_ctzll(m) : 63;
       if (l == first) {
@@ -114,21 +199,26 @@ struct GpuBlk {
           if (c + v[q] >= k) break;
           c += v[q];
         }
-        red[0] = rev ? 255 - (4 * l + q) : 4 * l + q;
-        red[1] = c;
+        a[0] = rev ? 255 - (4 * l + q) : 4 * l + q;
+        a[1] = c;
       }
     }
     sync();
-    const int bin = (int)red[0];
-    *before = red[1];
-    sync();
-    return bin;
+    *before = a[1];
+    return (int)a[0];
   }
   KP_INLINE uint64_t and64(uint64_t v) const {
-    return (uint64_t)reduce((int64_t)v, [](int64_t a, int64_t b) { return (int64_t)((uint64_t)a & (uint64_t)b); });
+    return reduce(v, [](uint64_t a, uint64_t b) { return a & b; }, (uint64_t)~0ull);
   }
   KP_INLINE uint64_t or64(uint64_t v) const {
-    return (uint64_t)reduce((int64_t)v, [](int64_t a, int64_t b) { return (int64_t)((uint64_t)a | (uint64_t)b); });
+    return reduce(v, [](uint64_t a, uint64_t b) { return a | b; }, (uint64_t)0);
+  }
+  KP_INLINE void andor(uint64_t& an, uint64_t& on) const {
+    int64_t x = (int64_t)an, y = (int64_t)on;
+    reduce2(x, [](int64_t a, int64_t b) { return a & b; }, (int64_t)-1, y, [](int64_t a, int64_t b) { return a | b; },
+            (int64_t)0);
+    an = (uint64_t)x;
+    on = (uint64_t)y;
   }
   // Stores the feasibility bit of cluster c (c = wave base + lane) into its u64 word.
   KP_INLINE void mask_store(uint64_t* row, int c, bool bit, int W) const {
@@ -138,12 +228,10 @@ struct GpuBlk {
   // Value of thread 0 to every thread.
   template <class T>
   KP_INLINE T bcast(T v) const {
+    int64_t* a = area();
+    if (tid() == 0) a[0] = (int64_t)v;
     sync();
-    if (tid() == 0) red[0] = (int64_t)v;
-    sync();
-    T r = (T)red[0];
-    sync();
-    return r;
+    return (T)a[0];
   }
 };
 #endif
@@ -157,6 +245,9 @@ struct CpuBlk {
   int nwaves() const { return 1; }
   void sync() const {}
   int64_t sum64(int64_t v) const { return v; }
+  void sum2(int64_t&, int64_t&) const {}
+  void maxsum(int64_t&, int64_t&) const {}
+  void andor(uint64_t&, uint64_t&) const {}
   uint64_t minu64(uint64_t v) const { return v; }
   int64_t max64(int64_t v) const { return v; }
   int64_t min64(int64_t v) const { return v; }

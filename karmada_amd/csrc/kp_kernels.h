@@ -79,7 +79,7 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
   const int b = b0 + blk;
   const BindHdr h = bv.hdr[b];
   const int words = (s.Cp + 31) >> 5;
-  uint32_t* tgt = (uint32_t*)(smem + 512);
+  uint32_t* tgt = (uint32_t*)(smem + kRedBytes);
   uint32_t* evict = tgt + words;
   int32_t* md = (int32_t*)(evict + words);
   build_bits(B, tgt, words, bv.ipool, h.tgt_off, h.tgt_cnt, 2);
@@ -172,7 +172,7 @@ KP_FI void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
   KP_STAMP_INIT
   const int b = a.list[blk];
   const int words = (a.s.Cp + 31) >> 5;
-  uint32_t* tgt = (uint32_t*)(smem + 512);
+  uint32_t* tgt = (uint32_t*)(smem + kRedBytes);
   Cands cd;
   cd.r = tgt + ((words + 3) & ~3);
   cd.v = (int32_t*)(cd.r + a.s.Cp);
@@ -194,7 +194,7 @@ KP_FI void body_select_all_reg(const BLK& B, int blk, unsigned char* smem, const
   if (blk >= a.n) return;
   const int b = a.list[blk];
   const int words = (a.s.Cp + 31) >> 5;
-  uint32_t* tgt = (uint32_t*)(smem + 512);
+  uint32_t* tgt = (uint32_t*)(smem + kRedBytes);
   const SelScratch ss = carve_sel_scratch((unsigned char*)(tgt + ((words + 3) & ~3)), a.s.Cp);
   const BindHdr* h = &a.bv.hdr[b];
   build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
@@ -225,8 +225,8 @@ KP_FI void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const
   if (blk >= a.n) return;
   const int b = a.list[blk];
   const int words = (a.s.Cp + 31) >> 5;
-  uint32_t* hist = (uint32_t*)(smem + 512);
-  Item* items = (Item*)(smem + 512 + 1024);
+  uint32_t* hist = (uint32_t*)(smem + kRedBytes);
+  Item* items = (Item*)(smem + kRedBytes + 1024);
   uint64_t* keys = (uint64_t*)(items + 2 * kSmallMax);
   uint32_t* tgt = (uint32_t*)(keys + 2 * kSmallMax);
   unsigned char* area = (unsigned char*)(tgt + ((words + 3) & ~3));
@@ -258,7 +258,7 @@ KP_FI void body_region_a(const BLK& B, int blk, unsigned char* smem, const KArgs
   const int b = a.list[blk];
   const int words = (a.s.Cp + 31) >> 5;
   const int R = a.s.n_regions;
-  unsigned char* p = smem + 512;
+  unsigned char* p = smem + kRedBytes;
   RegionLds L;
   L.minkey = (unsigned long long*)p;
   p += 8 * R;
@@ -312,7 +312,7 @@ KP_FI void body_region_b(const BLK& B, int blk, unsigned char* smem, const KArgs
   if (nsel == -1000) return;
   const int words = (a.s.Cp + 31) >> 5;
   const int R = a.s.n_regions;
-  unsigned char* p = smem + 512;
+  unsigned char* p = smem + kRedBytes;
   uint32_t* hist = (uint32_t*)p;
   p += 1024;
   Item* items = (Item*)p;
@@ -353,7 +353,7 @@ template <class BLK>
 KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const KArgs& a, unsigned char* scratch,
                      size_t slot_bytes, int scratch_cap, int lds_area) {
   const int words = (a.s.Cp + 31) >> 5;
-  uint32_t* tgt = (uint32_t*)(smem + 512);
+  uint32_t* tgt = (uint32_t*)(smem + kRedBytes);
   unsigned char* larea = (unsigned char*)(tgt + ((words + 3) & ~3));  // lds_area bytes
   unsigned char* mine = scratch + (size_t)blk * slot_bytes;
   // slot layout: cand r/v [Cp] | keys [P] | items [Cp] | pos [Cp] | serial scratch

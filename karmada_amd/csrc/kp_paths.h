@@ -165,8 +165,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
       if (w > wmax) wmax = w;
       wsum += w > 0 ? w : 0;
     });
-    wmax = B.max64(wmax);
-    wsum = B.sum64(wsum);
+    B.maxsum(wmax, wsum);
     if (wmax >= kInt32Max) return SLOW_WEIGHT;
     const bool all1 = wsum == 0;  // getStaticWeightInfoList: every candidate weight 1
     auto parties = [&](auto fn) {
@@ -222,9 +221,8 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
     if (v < vmin) vmin = v;
     vtot += v;
   });
-  sabs = B.sum64(sabs);
+  B.sum2(sabs, vtot);
   vmin = B.min64(vmin);
-  vtot = B.sum64(vtot);
   if (vmin < 0 || sabs >= (int64_t)kInt32Max) return SLOW_WRAP;  // int32 wrap hazard
   KP_STAMP(x, 2);
   const int32_t target = mode == 0 ? h.replicas : sub32(h.replicas, assigned);
@@ -248,8 +246,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
         nP++;
       }
     });
-    SP = B.sum64(SP);
-    nP = B.sum64(nP);
+    B.sum2(SP, nP);
     xIsPrior = nP > 0 && SP >= target;
     const int64_t tX = xIsPrior ? (int64_t)target : (int64_t)target - SP;
     auto xvals = [&](auto fn) {
@@ -262,8 +259,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
       if (v > xmax) xmax = v;
       xsum += v;
     });
-    xmax = B.max64(xmax);
-    xsum = B.sum64(xsum);
+    B.maxsum(xmax, xsum);
     if (xmax < 0 || xsum < tX) {
       noCut = true;  // every element of X is taken
     } else {
@@ -274,8 +270,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
         if (v > vstar) sgt += v;
         if (v == vstar) ceq++;
       });
-      sgt = B.sum64(sgt);
-      ceq = B.sum64(ceq);
+      B.sum2(sgt, ceq);
       const int64_t need = tX - sgt;
       const int64_t j = need <= 0 ? 1 : (vstar > 0 ? (need + vstar - 1) / vstar : ceq);
       if (j < ceq) return SLOW_TIE;  // tie group straddles the cut

@@ -575,6 +575,41 @@ struct SelScratch {
 template <class BLK, class Pred, class Key>
 KP_FI uint64_t radix_select(const BLK& B, uint32_t* hist, int F, Pred pred, Key key, int64_t k);
 
+// k-th largest (1-based) vote over the parties with votes in [1, 2^31), counted
+// with multiplicity (k <= #parties with v > 0): 8-bit radix descent over the
+// bytes in which the votes differ.
+template <class BLK, class Parties>
+KP_FI int64_t kth_largest_vote(const BLK& B, uint32_t* hist, Parties parties, int64_t k) {
+  uint64_t an = ~0ull, on = 0;
+  parties([&](uint32_t, int64_t v) {
+    if (v > 0) {
+      an &= (uint64_t)v;
+      on |= (uint64_t)v;
+    }
+  });
+  B.andor(an, on);
+  const uint64_t diff = an ^ on;
+  if (diff == 0) return (int64_t)an;
+  int top = 31;
+  while (!((diff >> top) & 1)) top--;
+  const int start = (top / 8) * 8;
+  uint32_t prefix = start >= 24 ? 0u : (uint32_t)(an & (~0ull << (start + 8)));
+  for (int shift = start; shift >= 0; shift -= 8) {
+    for (int i = B.tid(); i < 256; i += B.nth()) hist[i] = 0;
+    B.sync();
+    const uint32_t hm = shift >= 24 ? 0u : (~0u << (shift + 8));
+    parties([&](uint32_t, int64_t v64) {
+      const uint32_t v = (uint32_t)v64;
+      if (v64 > 0 && (v & hm) == (prefix & hm)) kp_atomic_add(&hist[(v >> shift) & 255], 1u);
+    });
+    int64_t before;
+    const int bin = B.find_bin(hist, k, &before, true);
+    k -= before;
+    prefix |= (uint32_t)bin << shift;
+  }
+  return (int64_t)prefix;
+}
+
 // AllocateWebsterSeats (webstermethod.go:112-161) for parties with int32 votes
 // >= 0 and no initial seats, block-parallel. `parties(fn)` calls fn(rank, votes)
 // for every party the calling thread owns. The N-th largest seat priority
@@ -598,9 +633,8 @@ KP_FI WebRes webster_par(const BLK& B, Parties parties, int32_t N, bool desc, co
     if (v > vmax) vmax = v;
     if (v > 0) P++;
   });
-  V = B.sum64(V);
+  B.sum2(V, P);
   vmax = B.max64(vmax);
-  P = B.sum64(P);
   if (V == 0) {
     r.mode = 0;
     return r;
@@ -617,8 +651,9 @@ KP_FI WebRes webster_par(const BLK& B, Parties parties, int32_t N, bool desc, co
       a += w_count(v, ta, capN, true);
       b += w_count(v, tb, capN, true);
     });
-    *ca = B.sum64(a);
-    *cb = B.sum64(b);
+    B.sum2(a, b);
+    *ca = a;
+    *cb = b;
   };
   auto cnt1 = [&](double t) {
     int64_t c = 0;
@@ -634,6 +669,14 @@ KP_FI WebRes webster_par(const BLK& B, Parties parties, int32_t N, bool desc, co
     double h0 = 2 * (int64_t)N - P - 1 > 0 ? (double)V / (double)(2 * (int64_t)N - P - 1) : (double)vmax;
     uint64_t hb = dbits(h0) + 64;
     if (hb > hi) hb = hi;
+    if (P > (int64_t)N) {
+      // Every party's first priority is its vote, so t* >= L = the N-th largest
+      // vote and cnt_ge(L) >= N. When P >> N this bound is far above the
+      // divisor bound and leaves few priorities to enumerate.
+      const int64_t L = kth_largest_vote(B, sc.hist, parties, (int64_t)N);
+      const uint64_t lL = dbits((double)L);
+      if (lL > lb && lL < hb) lb = lL;
+    }
     int64_t cl, ch;
     cnt2(bitsd(lb), bitsd(hb), &cl, &ch);
     if (cl >= N) {
@@ -687,8 +730,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties parties, int32_t N, bool desc, co
     S += base;
     if (w_prio(v, base) == tstar) T++;
   });
-  S = B.sum64(S);
-  T = B.sum64(T);
+  B.sum2(S, T);
   const int64_t M = (int64_t)N - S;
   if (M >= T) {
     r.tie = ~0ull;
@@ -768,8 +810,7 @@ KP_FI uint64_t radix_select(const BLK& B, uint32_t* hist, int F, Pred pred, Key 
       an &= kk;
       on |= kk;
     }
-  an = B.and64(an);
-  on = B.or64(on);
+  B.andor(an, on);
   const uint64_t diff = an ^ on;
   if (diff == 0) return an;  // all keys equal
   int top = 63;
