@@ -245,6 +245,8 @@ struct CpuBlk {
   int nwaves() const { return 1; }
   void sync() const {}
   int64_t sum64(int64_t v) const { return v; }
+  template <class OpA, class OpB>
+  void reduce2(int64_t&, OpA, int64_t, int64_t&, OpB, int64_t) const {}
   void sum2(int64_t&, int64_t&) const {}
   void maxsum(int64_t&, int64_t&) const {}
   void andor(uint64_t&, uint64_t&) const {}

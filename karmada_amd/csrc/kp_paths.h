@@ -44,6 +44,12 @@ KP_HD inline bool in_sched(const SelCtx& x, uint32_t rank) {
   return x.h->tgt_cnt > 0 && bit_test(x.tgt_bits, (int)rank) && mask_test(x.frow, (int)rank);
 }
 
+// sortClusters key of a SEL_ALL candidate (no overflow tiers on the fast path).
+KP_HD inline uint64_t cand_order_key(const SelCtx& x, uint32_t rk, int32_t est) {
+  const int64_t avail = (int64_t)est + (int64_t)assigned_of(*x.bv, *x.h, x.tgt_bits, rk);
+  return sort_key(0, locality_score(*x.h, x.tgt_bits, rk), avail, rk);
+}
+
 // Candidate sets for the SEL_ALL path. each(fn) calls fn(rank, v) for every
 // candidate the calling thread owns, always in the same per-thread order.
 struct LdsCands {  // candidates compacted in LDS (gather)
@@ -53,6 +59,8 @@ struct LdsCands {  // candidates compacted in LDS (gather)
   KP_FI void each(Fn fn) const {
     for (int i = tid; i < cd->F; i += nth) fn(c_rank(*cd, i), cd->v[i]);
   }
+  // Position key of a candidate in the sort.Sort input (sortClusters order).
+  KP_FI uint64_t okey(const SelCtx& x, uint32_t rk, int32_t v0) const { return cand_order_key(x, rk, v0); }
 };
 template <int J>
 struct RegCands {  // slot j of thread t is cluster t + nth*j; votes live in registers
@@ -64,6 +72,30 @@ struct RegCands {  // slot j of thread t is cluster t + nth*j; votes live in reg
 KP_UNROLL
     for (int j = 0; j < J; j++)
       if ((fm >> j) & 1ull) fn((uint32_t)(tid + nth * j), v[j]);
+  }
+  KP_FI uint64_t okey(const SelCtx& x, uint32_t rk, int32_t v0) const { return cand_order_key(x, rk, v0); }
+};
+
+// The binding's spec.Clusters entries that are candidates (scheduledClusters,
+// assignment.go:125-142), v = their scheduled replicas: the parties of
+// dynamicScaleDown (division_algorithm.go:103-119).
+struct TgtCands {
+  const SelCtx* x;
+  int tid, nth;
+  template <class Fn>
+  KP_FI void each(Fn fn) const {
+    const BindHdr& h = *x->h;
+    for (int j = tid; j < h.tgt_cnt; j += nth) {
+      const uint32_t r = (uint32_t)x->bv->ipool[h.tgt_off + 2 * j];
+      if (mask_test(x->frow, (int)r)) fn(r, x->bv->ipool[h.tgt_off + 2 * j + 1]);
+    }
+  }
+  // Position in scheduledClusters = position in spec.Clusters (targets unique).
+  KP_FI uint64_t okey(const SelCtx&, uint32_t rk, int32_t) const {
+    const BindHdr& h = *x->h;
+    for (int j = 0; j < h.tgt_cnt; j++)
+      if ((uint32_t)x->bv->ipool[h.tgt_off + 2 * j] == rk) return (uint64_t)j;
+    return ~0ull;
   }
 };
 
@@ -183,61 +215,80 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
     return SLOW_NONE;
   }
   // Dynamic / Aggregated (assignment.go:213-244)
-  int32_t assigned = 0;
-  bool anyPriorPos = false;
-  if (B.tid() == 0) {
-    for (int j = 0; j < h.tgt_cnt; j++) {
-      uint32_t r = (uint32_t)x.bv->ipool[h.tgt_off + 2 * j];
-      if (mask_test(x.frow, (int)r)) {
-        int32_t v = x.bv->ipool[h.tgt_off + 2 * j + 1];
-        assigned = add32(assigned, v);
-        if (v > 0) anyPriorPos = true;
-      }
-    }
-  }
-  assigned = B.bcast(assigned);
-  anyPriorPos = B.bcast(anyPriorPos ? 1 : 0) != 0;
+  // GetSumOfReplicas(scheduledClusters) wraps in int32; the int64 sum taken
+  // mod 2^32 is the same value.
+  int64_t asum = 0, apos = 0;
+  TgtCands{&x, B.tid(), B.nth()}.each([&](uint32_t, int32_t v) {
+    asum += v;
+    apos |= v > 0 ? 1 : 0;
+  });
+  B.reduce2(asum, [](int64_t p, int64_t q) { return p + q; }, (int64_t)0, apos,
+            [](int64_t p, int64_t q) { return p | q; }, (int64_t)0);
+  const int32_t assigned = wrap32(asum);
+  const bool anyPriorPos = apos != 0;
   const bool fresh = (h.flags & BF_FRESH) != 0;
   int mode;  // 0 fresh, 1 scale up, 2 unchanged, 3 scale down
   if (fresh) mode = 0;
   else if (assigned > h.replicas) mode = 3;
   else if (assigned < h.replicas) mode = 1;
   else mode = 2;
-  if (mode == 3) return SLOW_SCALE_DOWN;  // parties = scheduledClusters: serial kernel (k_slow)
+  if (mode == 3) {  // dynamicScaleDown: parties = scheduledClusters, no merge
+    if (prop) return SLOW_SCALE_DOWN;  // attachZeroReplicasCluster over all candidates: serial
+    TgtCands tc{&x, B.tid(), B.nth()};
+    return divide_par(B, x, tc, h.replicas, false, false, false, KP_ERR_SCALE_DOWN_NOT_ENOUGH, ss);
+  }
   // spec.Clusters membership of a candidate (candidates are feasible)
   auto tgt = [&](uint32_t rk) { return h.tgt_cnt > 0 && bit_test(x.tgt_bits, (int)rk); };
   if (mode == 2) {  // unchanged: scheduledClusters, removeZero
     emit_each(B, x, cs, [&](uint32_t rk, int32_t) { return tgt(rk) ? sched_rep_of(x, rk) : (int32_t)0; }, prop);
     return SLOW_NONE;
   }
+  const int32_t target = mode == 0 ? h.replicas : sub32(h.replicas, assigned);
+  return divide_par(B, x, cs, target, mode == 0, mode == 1, anyPriorPos,
+                    mode == 0 ? KP_ERR_FRESH_NOT_ENOUGH : KP_ERR_SCALE_UP_NOT_ENOUGH, ss);
+}
+
+// dynamicDivideReplicas (division_algorithm.go:75-101) for DynamicWeight and
+// Aggregated, block-parallel over the candidate set: votes (fresh: + scheduled
+// replicas), the availability check, the Aggregated prefix cut, Webster
+// (SpreadReplicasByTargetClusters) and MergeTargetClusters (scale-up).
+template <class BLK, class CS>
+KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target, bool fresh, bool merge,
+                     bool anyPriorPos, int not_enough, const SelScratch& ss) {
+  KP_STAMP_INIT
+  const BindHdr& h = *x.h;
+  const int st = h.strategy;
+  const bool desc = (h.flags & BF_UID_DESC) != 0;
+  const bool prop = (h.flags & BF_EMPTY_PROP) != 0;
+  auto tgt = [&](uint32_t rk) { return h.tgt_cnt > 0 && bit_test(x.tgt_bits, (int)rk); };
   auto vote32 = [&](uint32_t rk, int32_t v) -> int32_t {
-    if (mode == 0 && tgt(rk)) v = add32(v, sched_rep_of(x, rk));
+    if (fresh && tgt(rk)) v = add32(v, sched_rep_of(x, rk));
     return v;
   };
-  int64_t sabs = 0, vmin = 0, vtot = 0;
+  int64_t sabs = 0, vmin = 0, vtot = 0, nparty = 0;
   cs.each([&](uint32_t rk, int32_t v0) {
     int64_t v = vote32(rk, v0);
     sabs += v < 0 ? -v : v;
     if (v < vmin) vmin = v;
     vtot += v;
+    nparty++;
   });
   B.sum2(sabs, vtot);
-  vmin = B.min64(vmin);
+  B.reduce2(vmin, [](int64_t p, int64_t q) { return p < q ? p : q; }, (int64_t)0, nparty,
+            [](int64_t p, int64_t q) { return p + q; }, (int64_t)0);
   if (vmin < 0 || sabs >= (int64_t)kInt32Max) return SLOW_WRAP;  // int32 wrap hazard
   KP_STAMP(x, 2);
-  const int32_t target = mode == 0 ? h.replicas : sub32(h.replicas, assigned);
   if ((int32_t)vtot < target) {
-    if (B.tid() == 0)
-      sink_error(x, KP_STATUS_UNSCHEDULABLE, mode == 0 ? KP_ERR_FRESH_NOT_ENOUGH : KP_ERR_SCALE_UP_NOT_ENOUGH, vtot);
+    if (B.tid() == 0) sink_error(x, KP_STATUS_UNSCHEDULABLE, not_enough, vtot);
     return SLOW_NONE;
   }
-  const bool merge = mode == 1;
   auto prior = [&](uint32_t rk) { return merge && anyPriorPos && tgt(rk) && sched_rep_of(x, rk) > 0; };
   // Aggregated prefix cut (division_algorithm.go:81-89) over sort.Sort order
   // (Replicas desc) with prior clusters first: membership is exact unless a
   // tie group straddles the cut (then the pdqsort permutation matters).
   int64_t vstar = -1;  // members: X elements with v > vstar, plus the whole tie group
-  bool xIsPrior = false, noCut = false;
+  bool xIsPrior = false, noCut = false, straddle = false;
+  uint64_t tieCut = 0;  // straddle: tie-group members with okey <= tieCut are taken
   if (st == ST_AGGREGATED) {
     int64_t SP = 0, nP = 0;
     cs.each([&](uint32_t rk, int32_t v0) {
@@ -273,21 +324,41 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
       B.sum2(sgt, ceq);
       const int64_t need = tX - sgt;
       const int64_t j = need <= 0 ? 1 : (vstar > 0 ? (need + vstar - 1) / vstar : ceq);
-      if (j < ceq) return SLOW_TIE;  // tie group straddles the cut
+      if (j < ceq) {  // the tie group straddles the cut
+        // Only sort.Sort's permutation of equal keys decides. For lists of at
+        // most 12 Go runs insertion sort, which is stable: the tie group keeps
+        // input order and its first j members are taken. Longer lists: serial.
+        if (nparty > 12) return SLOW_TIE;
+        uint64_t prev = 0;
+        bool first = true;
+        for (int64_t q = 0; q < j; q++) {
+          uint64_t m = ~0ull;
+          cs.each([&](uint32_t rk, int32_t v0) {
+            if (prior(rk) != xIsPrior || (int64_t)vote32(rk, v0) != vstar) return;
+            const uint64_t k = cs.okey(x, rk, v0);
+            if ((first || k > prev) && k < m) m = k;
+          });
+          prev = B.minu64(m);
+          first = false;
+        }
+        tieCut = prev;
+        straddle = true;
+      }
     }
   }
   KP_STAMP(x, 3);
-  auto member = [&](uint32_t rk, int64_t v) {
+  auto member = [&](uint32_t rk, int64_t v, int32_t v0) {
     if (st != ST_AGGREGATED) return true;
     const bool p = prior(rk);
     if (!xIsPrior && p) return true;  // X = non-prior: every prior cluster precedes the cut
     if (p != xIsPrior) return false;
-    return noCut || v >= vstar;
+    if (noCut || v > vstar) return true;
+    return v == vstar && (!straddle || cs.okey(x, rk, v0) <= tieCut);
   };
   auto parties = [&](auto fn) {
     cs.each([&](uint32_t rk, int32_t v0) {
       const int64_t v = vote32(rk, v0);
-      if (member(rk, v)) fn(rk, v);
+      if (member(rk, v, v0)) fn(rk, v);
     });
   };
   WebRes w = webster_par(B, parties, target, desc, ss);
@@ -296,7 +367,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
       B, x, cs,
       [&](uint32_t rk, int32_t v0) {
         const int64_t v = vote32(rk, v0);
-        int32_t r = member(rk, v) ? web_seats(w, v, rk) : 0;
+        int32_t r = member(rk, v, v0) ? web_seats(w, v, rk) : 0;
         if (merge && tgt(rk)) r = add32(r, sched_rep_of(x, rk));
         return r;
       },

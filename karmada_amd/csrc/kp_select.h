@@ -557,7 +557,7 @@ KP_HD inline uint64_t tie_key(int64_t base, uint32_t rank, bool desc) {
   return ((uint64_t)base << kRankBits) | (desc ? (uint64_t)(kRankMask - rank) : (uint64_t)rank);
 }
 KP_HD inline int32_t web_seats(const WebRes& w, int64_t v, uint32_t rank) {
-  if (w.mode != 2) return 0;
+  if (w.mode != 2 || (double)v < w.t) return 0;  // every priority of v is below t*
   int64_t base = w_count(v, w.t, (int64_t)w.N + 1, false);
   if (base < w.N && w_prio(v, base) == w.t && tie_key(base, rank, w.desc) <= w.tie) base++;
   return (int32_t)base;
@@ -621,14 +621,14 @@ KP_FI int64_t kth_largest_vote(const BLK& B, uint32_t* hist, Parties parties, in
 // Seats strictly above t* are exact per party; the tie group at t* is ordered
 // by (seats asc, name) as the heap's tie-breaker orders it (tie_key).
 template <class BLK, class Parties>
-KP_FI WebRes webster_par(const BLK& B, Parties parties, int32_t N, bool desc, const SelScratch& sc) {
+KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc, const SelScratch& sc) {
   WebRes r;
   r.N = N;
   r.desc = desc;
   r.t = 0;
   r.tie = 0;
   int64_t V = 0, vmax = 0, P = 0;
-  parties([&](uint32_t, int64_t v) {
+  all_parties([&](uint32_t, int64_t v) {
     V += v;
     if (v > vmax) vmax = v;
     if (v > 0) P++;
@@ -644,6 +644,16 @@ KP_FI WebRes webster_par(const BLK& B, Parties parties, int32_t N, bool desc, co
     return r;
   }
   r.mode = 2;
+  // Every party's first priority is its vote, so t* >= L = the N-th largest
+  // vote (cnt_ge(L) >= N). Parties with v < L have every priority below t*:
+  // they take no seat and no part in any count below, so the passes skip
+  // their fp64 work. When P >> N this leaves about N parties.
+  const int64_t L = P > (int64_t)N ? kth_largest_vote(B, sc.hist, all_parties, (int64_t)N) : 0;
+  auto parties = [&](auto fn) {
+    all_parties([&](uint32_t rk, int64_t v) {
+      if (v >= L) fn(rk, v);
+    });
+  };
   const int64_t capN = (int64_t)N;
   auto cnt2 = [&](double ta, double tb, int64_t* ca, int64_t* cb) {
     int64_t a = 0, b = 0;
@@ -669,13 +679,11 @@ KP_FI WebRes webster_par(const BLK& B, Parties parties, int32_t N, bool desc, co
     double h0 = 2 * (int64_t)N - P - 1 > 0 ? (double)V / (double)(2 * (int64_t)N - P - 1) : (double)vmax;
     uint64_t hb = dbits(h0) + 64;
     if (hb > hi) hb = hi;
-    if (P > (int64_t)N) {
-      // Every party's first priority is its vote, so t* >= L = the N-th largest
-      // vote and cnt_ge(L) >= N. When P >> N this bound is far above the
-      // divisor bound and leaves few priorities to enumerate.
-      const int64_t L = kth_largest_vote(B, sc.hist, parties, (int64_t)N);
+    if (L > 0) {  // t* >= L: usually far above the divisor bound when P >> N
+      // (and every count below must be taken at t >= L, where it is exact)
       const uint64_t lL = dbits((double)L);
-      if (lL > lb && lL < hb) lb = lL;
+      if (lL > lb) lb = lL;
+      if (hb <= lb) hb = lb + 1;
     }
     int64_t cl, ch;
     cnt2(bitsd(lb), bitsd(hb), &cl, &ch);
