@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "kp_blk.h"
+#include "kp_pdq.h"
 
 using namespace kp;
 
@@ -185,4 +186,62 @@ extern "C" int kp_blk_selftest(int nth, int nblocks, uint64_t seed, char* msg, i
     }
   }
   return bad;
+}
+
+// ---------------------------------------------------------------------------
+// sort.Sort wave emulation (kp_pdq.h) on the device: wave 0 of each block
+// sorts its own list in LDS; the host compares with the serial emulation.
+// ---------------------------------------------------------------------------
+extern "C" __global__ void k_pdq_test(const int32_t* reps, const int32_t* offs, uint32_t* out_names,
+                                      int32_t* out_ok) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  GpuBlk B{(int64_t*)smem};
+  const int a = offs[blockIdx.x], n = offs[blockIdx.x + 1] - a;
+  PdqWave<GpuBlk> pw = pdq_carve(B, smem + kRedBytes, n);
+  for (int i = B.tid(); i < n; i += B.nth()) {
+    pw.name[i] = (uint32_t)i;
+    pw.rep[i] = reps[a + i];
+  }
+  B.sync();
+  int ok = 1;
+  if (B.wid() == 0) ok = pw.run(n) ? 1 : 0;
+  ok = B.bcast(ok);
+  for (int i = B.tid(); i < n; i += B.nth()) out_names[a + i] = pw.name[i];
+  if (B.tid() == 0) out_ok[blockIdx.x] = ok;
+}
+
+// Sorts nl lists (concatenated in reps, list j = [offs[j], offs[j+1])) on the
+// device; out_names gets each list's permutation (indices into the list).
+// Returns the number of lists the wave form declined, or -1 on a HIP error.
+extern "C" int kp_pdq_selftest(const int32_t* reps, const int32_t* offs, int nl, int nth, uint32_t* out_names,
+                               char* msg, int msg_len) {
+  const int total = offs[nl];
+  int maxn = 0;
+  for (int j = 0; j < nl; j++) maxn = offs[j + 1] - offs[j] > maxn ? offs[j + 1] - offs[j] : maxn;
+  int32_t *dr, *doffs, *dok;
+  uint32_t* dn;
+  if (hipMalloc(&dr, 4 * (size_t)(total + 1)) || hipMalloc(&doffs, 4 * (size_t)(nl + 1)) ||
+      hipMalloc(&dn, 4 * (size_t)(total + 1)) || hipMalloc(&dok, 4 * (size_t)nl)) {
+    snprintf(msg, msg_len, "hipMalloc failed");
+    return -1;
+  }
+  (void)hipMemcpy(dr, reps, 4 * (size_t)total, hipMemcpyHostToDevice);
+  (void)hipMemcpy(doffs, offs, 4 * (size_t)(nl + 1), hipMemcpyHostToDevice);
+  const size_t smem = kRedBytes + pdq_wave_bytes(maxn);
+  if (smem > 65536) (void)hipFuncSetAttribute((const void*)k_pdq_test, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(k_pdq_test, dim3(nl), dim3(nth), smem, 0, dr, doffs, dn, dok);
+  if (hipDeviceSynchronize() != hipSuccess) {
+    snprintf(msg, msg_len, "kernel failed: %s", hipGetErrorString(hipGetLastError()));
+    return -1;
+  }
+  std::vector<int32_t> ok(nl);
+  (void)hipMemcpy(out_names, dn, 4 * (size_t)total, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(ok.data(), dok, 4 * (size_t)nl, hipMemcpyDeviceToHost);
+  (void)hipFree(dr);
+  (void)hipFree(doffs);
+  (void)hipFree(dn);
+  (void)hipFree(dok);
+  int declined = 0;
+  for (int j = 0; j < nl; j++) declined += ok[j] ? 0 : 1;
+  return declined;
 }

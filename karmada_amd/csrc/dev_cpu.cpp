@@ -122,7 +122,7 @@ int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const Sele
       break;
     case SEL_LAUNCH_SLOW:
       grid(x.grid, smem, [&](int blk, unsigned char* sm) {
-        body_slow(CpuBlk{(int64_t*)sm}, blk, x.grid, sm, a, x.scratch, x.slot_bytes, cap, x.lds_area);
+        body_slow(CpuBlk{(int64_t*)sm}, blk, x.grid, sm, a, x.scratch, x.slot_bytes, cap, x.lds_area, x.lds_sort);
       });
       break;
     default:
@@ -181,6 +181,31 @@ int64_t kpsim_wsel_max(const int32_t* vals, int n, int64_t target) {
     for (int i = 0; i < n; i++) fn((int64_t)vals[i]);
   };
   return wsel_max(B, wh.data(), vs, target);
+}
+
+// Go sort.Sort over (name, rep)[0, n): mode 0 = the serial emulation
+// (pdqsort_go), mode 1 = the wave form (PdqWave, one lane). Returns 1 if the
+// wave form emulated it (0: it declined), in place.
+int kpsim_sort_tcl(uint32_t* name, int32_t* rep, int n, int mode) {
+  using namespace kp;
+  if (mode == 0) {
+    sort_tcl(name, rep, n);
+    return 1;
+  }
+  std::vector<unsigned char> lds(pdq_wave_bytes(n));
+  int64_t red[8];
+  CpuBlk B{red};
+  PdqWave<CpuBlk> pw = pdq_carve(B, lds.data(), n);
+  for (int i = 0; i < n; i++) {
+    pw.name[i] = name[i];
+    pw.rep[i] = rep[i];
+  }
+  if (!pw.run(n)) return 0;
+  for (int i = 0; i < n; i++) {
+    name[i] = pw.name[i];
+    rep[i] = pw.rep[i];
+  }
+  return 1;
 }
 
 }  // extern "C"

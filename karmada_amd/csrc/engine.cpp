@@ -22,6 +22,7 @@
 #include "kp_layout.h"
 #include "kp_launch.h"
 #include "kp_paths.h"
+#include "kp_pdq.h"
 
 using namespace kp;
 
@@ -154,7 +155,7 @@ struct kp_batch {
   int32_t *rstat = nullptr, *rsel = nullptr, *rnsel = nullptr;
   unsigned char* slow_scratch = nullptr;
   size_t slow_slot = 0;
-  int slow_grid = 0, slow_cap = 0, slow_lds = 0;
+  int slow_grid = 0, slow_cap = 0, slow_lds = 0, slow_sort = 0;
   // host results
   std::vector<int32_t> h_status, h_err, h_rstat, h_rsel, h_rnsel;
   std::vector<int64_t> h_arg;
@@ -1287,10 +1288,18 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   }
   int P = 1;
   while (P < s->Cp) P <<= 1;
+  {  // LDS for the candidate sorts (bitonic keys, then the sort.Sort emulation)
+    const size_t base = kRedBytes + 512 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + bt->slow_lds;
+    const size_t sel = 3072 + 8 * (size_t)sel_all_ecap(s->Cp) + 64;  // SelScratch of the tie route
+    const size_t pdq = (std::max(pdq_wave_bytes(s->Cp), sel) + 15) & ~(size_t)15;
+    const size_t both = std::max(8 * (size_t)P, pdq);
+    bt->slow_sort = base + both <= e->max_lds ? (int)both : (base + pdq <= e->max_lds ? (int)pdq : 0);
+  }
   bt->slow_slot = (size_t)s->Cp * 8 + (size_t)P * 8 + sizeof(Item) * s->Cp + 4 * (size_t)s->Cp +
                   serial_scratch_bytes(bt->slow_cap) + 1024;
   bt->slow_slot = (bt->slow_slot + 255) & ~(size_t)255;
-  bt->slow_grid = (int)std::max<size_t>(1, std::min<size_t>(1024, bt->l_slow.size()));
+  // k_slow: one workgroup per CU pass over the flagged bindings (appended on device)
+  bt->slow_grid = (int)std::max<size_t>(1, std::min<size_t>(256, bt->l_slow.size()));
   Arena& a = bt->dev;
   BindHdr* d_hdr;
   int32_t* d_ipool;
@@ -1344,7 +1353,6 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   HIPCHK(up(bt->d_all, bt->l_all.data(), 4 * bt->l_all.size()));
   HIPCHK(up(bt->d_cluster, bt->l_cluster.data(), 4 * bt->l_cluster.size()));
   HIPCHK(up(bt->d_region, bt->l_region.data(), 4 * bt->l_region.size()));
-  HIPCHK(up(bt->d_slowlist, bt->l_slow.data(), 4 * bt->l_slow.size()));
   HIPCHK(dev::fill(bt->slow, 0, 4 * (size_t)B, e->stream));
   HIPCHK(dev::sync(e->stream));
   BatchView& v = bt->view;
@@ -1392,6 +1400,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   ka.sink.count = bt->count;
   ka.slow = bt->slow;
   ka.stats = bt->stats;
+  ka.slow_ids = bt->d_slowlist;
   ka.dbg = bt->dbg;
 #ifdef KP_STAMPS
   HIPCHK(dev::fill(bt->dbg, 0, 32 * 8, st));
@@ -1409,6 +1418,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   sx.slot_bytes = bt->slow_slot;
   sx.grid = bt->slow_grid;
   sx.lds_area = bt->slow_lds;
+  sx.lds_sort = bt->slow_sort;
   const int cap = kSmallMax + kTgtSmallMax + 16;
   if (!bt->l_all.empty()) {
     KArgs k = ka;
@@ -1470,7 +1480,8 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     KArgs k = ka;
     k.list = bt->d_slowlist;
     k.n = (int)bt->l_slow.size();
-    HIPCHK(dev::select(st, SEL_LAUNCH_SLOW, k, kRedBytes + 512 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area,
+    HIPCHK(dev::select(st, SEL_LAUNCH_SLOW, k, kRedBytes + 512 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area +
+                                                      sx.lds_sort,
                        bt->slow_cap, sx));
   }
   HIPCHK(dev::event_record(e->ev[2], st));
@@ -1518,14 +1529,16 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     HIPCHK(dev::d2h(h, bt->dbg, sizeof(h), st));
     HIPCHK(dev::sync(st));
     fprintf(stderr, "kp stamps (s_memtime ticks, summed over workgroups):");
-    for (int i = 0; i < 8; i++) fprintf(stderr, " [%d]=%llu", i, h[i]);
+    for (int i = 0; i < 9; i++) fprintf(stderr, " [%d]=%llu", i, h[i]);
     fprintf(stderr, "\n");
   }
 #endif
   if (getenv("KP_DEBUG_SLOW"))
-    fprintf(stderr, "kp slow: total %u overflow/dup %u scale-down %u wrap %u tie %u weight %u cluster %u\n",
+    fprintf(stderr,
+            "kp slow: total %u overflow/dup %u scale-down %u wrap %u tie %u weight %u cluster %u "
+            "(ties resolved block-parallel %u)\n",
             bt->h_stats[0], bt->h_stats[1], bt->h_stats[2], bt->h_stats[3], bt->h_stats[4], bt->h_stats[5],
-            bt->h_stats[6]);
+            bt->h_stats[6], bt->h_stats[7]);
   tm.pair_ms = ms_pair;
   tm.select_ms = ms_sel;
   tm.host_ms = th1 - th0;

@@ -42,10 +42,10 @@ extern "C" __global__ void __launch_bounds__(kBlock) k_region_b(KArgs a, const i
   KP_SMEM;
   body_region_b(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, rsel, rnsel, cap);
 }
-extern "C" __global__ void __launch_bounds__(kBlock) k_slow(KArgs a, unsigned char* scratch, size_t slot_bytes,
-                                                            int cap, int lds_area) {
+extern "C" __global__ void __launch_bounds__(kSlowBlock) k_slow(KArgs a, unsigned char* scratch, size_t slot_bytes,
+                                                                int cap, int lds_area, int lds_sort) {
   KP_SMEM;
-  body_slow(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, (int)gridDim.x, smem, a, scratch, slot_bytes, cap, lds_area);
+  body_slow(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, (int)gridDim.x, smem, a, scratch, slot_bytes, cap, lds_area, lds_sort);
 }
 extern "C" __global__ void __launch_bounds__(64) k_compact(const uint64_t* start, const uint32_t* count,
                                                            const uint64_t* offsets, const uint32_t* in_idx,
@@ -153,7 +153,11 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
       hipLaunchKernelGGL(k_region_b, dim3(a.n), dim3(kBlock), smem, h, a, x.rsel, x.rnsel, cap);
       break;
     case SEL_LAUNCH_SLOW:
-      hipLaunchKernelGGL(k_slow, dim3(x.grid), dim3(kBlock), smem, h, a, x.scratch, x.slot_bytes, cap, x.lds_area);
+      if (smem > 65536 &&
+          chk(hipFuncSetAttribute((const void*)k_slow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)))
+        return -1;
+      hipLaunchKernelGGL(k_slow, dim3(x.grid), dim3(kSlowBlock), smem, h, a, x.scratch, x.slot_bytes, cap, x.lds_area,
+                         x.lds_sort);
       break;
     default:
       return chk(hipErrorInvalidValue);

@@ -429,9 +429,46 @@ KP_HD int pdq_median(const D& d, int a, int b, int c, int& swaps) {
   }
   return b;
 }
+// breakPatterns: three xorshift-chosen swaps around the middle.
 template <class D>
-KP_HD void pdqsort_go(const D& d, int a, int b, int limit) {
-  bool wasBalanced = true, wasPartitioned = true;
+KP_HD void pdq_break_patterns(const D& d, int a, int b) {
+  const int length = b - a;
+  if (length >= 8) {
+    uint64_t r = (uint64_t)length;
+    uint64_t modulus = 1ull << bits_len((uint64_t)length);
+    int idx = a + (length / 4) * 2 - 1;
+    for (int i = 0; i < 3; i++) {
+      r ^= r << 13;
+      r ^= r >> 7;
+      r ^= r << 17;
+      int other = (int)((unsigned)r & (modulus - 1));
+      if (other >= length) other -= length;
+      d.Swap(idx - 1 + i, a + other);
+    }
+  }
+}
+// choosePivot (read-only): median of three, Tukey ninther from 50 elements.
+// *hint: 0 unknown, 1 increasing, 2 decreasing.
+template <class D>
+KP_HD int pdq_choose_pivot(const D& d, int a, int b, int* hint) {
+  const int length = b - a;
+  int swaps = 0;
+  int pi = a + length / 4 * 1, pj = a + length / 4 * 2, pk = a + length / 4 * 3;
+  if (length >= 8) {
+    if (length >= 50) {
+      pi = pdq_median(d, pi - 1, pi, pi + 1, swaps);
+      pj = pdq_median(d, pj - 1, pj, pj + 1, swaps);
+      pk = pdq_median(d, pk - 1, pk, pk + 1, swaps);
+    }
+    pj = pdq_median(d, pi, pj, pk, swaps);
+  }
+  *hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
+  return pj;
+}
+// The loop state (wasBalanced, wasPartitioned) is a parameter so that a
+// segment handed over mid-loop (pdq_wave) resumes exactly where Go would.
+template <class D>
+KP_HD void pdqsort_go(const D& d, int a, int b, int limit, bool wasBalanced = true, bool wasPartitioned = true) {
   for (;;) {
     int length = b - a;
     if (length <= 12) {
@@ -442,35 +479,12 @@ KP_HD void pdqsort_go(const D& d, int a, int b, int limit) {
       pdq_heapsort(d, a, b);
       return;
     }
-    if (!wasBalanced) {  // breakPatterns
-      if (length >= 8) {
-        uint64_t r = (uint64_t)length;
-        uint64_t modulus = 1ull << bits_len((uint64_t)length);
-        int idx = a + (length / 4) * 2 - 1;
-        for (int i = 0; i < 3; i++) {
-          r ^= r << 13;
-          r ^= r >> 7;
-          r ^= r << 17;
-          int other = (int)((unsigned)r & (modulus - 1));
-          if (other >= length) other -= length;
-          d.Swap(idx - 1 + i, a + other);
-        }
-      }
+    if (!wasBalanced) {
+      pdq_break_patterns(d, a, b);
       limit--;
     }
-    // choosePivot
-    int swaps = 0;
-    int pi = a + length / 4 * 1, pj = a + length / 4 * 2, pk = a + length / 4 * 3;
-    if (length >= 8) {
-      if (length >= 50) {
-        pi = pdq_median(d, pi - 1, pi, pi + 1, swaps);
-        pj = pdq_median(d, pj - 1, pj, pj + 1, swaps);
-        pk = pdq_median(d, pk - 1, pk, pk + 1, swaps);
-      }
-      pj = pdq_median(d, pi, pj, pk, swaps);
-    }
-    int hint = swaps == 0 ? 1 : (swaps == 12 ? 2 : 0);
-    int pivot = pj;
+    int hint;
+    int pivot = pdq_choose_pivot(d, a, b, &hint);
     if (hint == 2) {
       int i = a, j = b - 1;
       while (i < j) {

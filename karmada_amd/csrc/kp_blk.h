@@ -225,6 +225,16 @@ struct GpuBlk {
     const uint64_t m = __ballot(bit);
     if (lane() == 0 && (c >> 6) < W) row[c >> 6] = m;
   }
+  // Wave-level primitives (the calling wave only; no workgroup barrier).
+  KP_INLINE int wwidth() const { return 64; }
+  KP_INLINE uint64_t wballot(bool p) const { return __ballot(p); }
+  KP_INLINE uint64_t wlt() const { return (1ull << lane()) - 1; }  // lanes below this one
+  // Orders this wave's LDS/global accesses: writes made by one lane before it
+  // are visible to every lane of the wave after it.
+  KP_INLINE void wsync() const {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
   // Value of thread 0 to every thread.
   template <class T>
   KP_INLINE T bcast(T v) const {
@@ -262,6 +272,10 @@ struct CpuBlk {
   T bcast(T v) const {
     return v;
   }
+  int wwidth() const { return 1; }
+  uint64_t wballot(bool p) const { return p ? 1ull : 0ull; }
+  uint64_t wlt() const { return 0; }
+  void wsync() const {}
   template <class T>
   int find_bin(const T* hist, int64_t k, int64_t* before, bool rev) const {
     int64_t c = 0;

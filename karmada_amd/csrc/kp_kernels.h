@@ -15,6 +15,7 @@
 #pragma once
 #include "kp_launch.h"
 #include "kp_paths.h"
+#include "kp_pdq.h"
 
 namespace kp {
 
@@ -138,6 +139,15 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
 // ---------------------------------------------------------------------------
 // Select stage: SEL_ALL (and spread-unsupported / FitError reporting)
 // ---------------------------------------------------------------------------
+// Hands binding b to k_slow for reason `why` (one thread).
+KP_HD inline void flag_slow(const KArgs& a, int b, int why) {
+  a.slow[b] = why;
+  a.sink.count[b] = 0;
+  const uint32_t i = kp_atomic_add(&a.stats[0], 1u);
+  a.slow_ids[i] = b;
+  kp_atomic_add(&a.stats[why], 1u);
+}
+
 template <class BLK, class CS>
 KP_FI void select_all_common(const BLK& B, const KArgs& a, const SelCtx& x, const CS& cs, int F,
                              const SelScratch& ss) {
@@ -148,12 +158,7 @@ KP_FI void select_all_common(const BLK& B, const KArgs& a, const SelCtx& x, cons
     return;
   }
   const int why = sel_all_fast(B, x, cs, ss);
-  if (why != SLOW_NONE && B.tid() == 0) {
-    a.slow[b] = 1;
-    a.sink.count[b] = 0;
-    kp_atomic_add(&a.stats[0], 1u);
-    kp_atomic_add(&a.stats[why], 1u);
-  }
+  if (why != SLOW_NONE && B.tid() == 0) flag_slow(a, b, why);
 }
 
 KP_HD inline SelScratch carve_sel_scratch(unsigned char* p, int Cp) {
@@ -239,12 +244,7 @@ KP_FI void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const
   cd.F = gather(B, x, cd, false);
   if (pre_checks(B, x, cd.F)) return;
   if (!sel_cluster_fast(B, x, cd, hist, items, keys, area, scratch_cap)) {
-    if (B.tid() == 0) {
-      a.slow[b] = 1;
-      a.sink.count[b] = 0;
-      kp_atomic_add(&a.stats[0], 1u);
-      kp_atomic_add(&a.stats[SLOW_CLUSTER], 1u);
-    }
+    if (B.tid() == 0) flag_slow(a, b, SLOW_CLUSTER);
   }
 }
 
@@ -349,12 +349,64 @@ KP_FI void body_region_b(const BLK& B, int blk, unsigned char* smem, const KArgs
 // the pdqsort emulation, scale-down, overflow tiers, duplicates, wrap-around).
 // Persistent: block k handles list entries k, k+grid, ...
 // ---------------------------------------------------------------------------
+// The dynamic-strategy TargetClustersList of a fresh or scale-up binding
+// (dynamicFreshScale / dynamicScaleUp, division_algorithm.go:121-166) built in
+// LDS and sorted there by sort.Sort's wave emulation (kp_pdq.h), then handed
+// to the serial assignment (SerialScratch::presorted). Returns false when the
+// binding takes another route (the serial code then builds and sorts itself).
+template <class BLK>
+KP_FI bool presort_dynamic(const BLK& B, const SelCtx& x, const Item* items, int n, unsigned char* area,
+                           int32_t* pos, SerialScratch& sc) {
+  const BindHdr& h = *x.h;
+  if (!(h.flags & BF_WORKLOAD_ASSIGN) || (h.flags & BF_OVERFLOW) || h.sel != SEL_ALL) return false;
+  if (h.strategy != ST_DYNAMIC && h.strategy != ST_AGGREGATED) return false;
+  PdqWave<BLK> pw = pdq_carve(B, area, n);
+  for (int i = B.tid(); i < n; i += B.nth()) {
+    pw.name[i] = items[i].rank;
+    pw.rep[i] = items[i].alloc;
+    pos[items[i].rank] = i;
+  }
+  B.sync();
+  int go = 0;
+  if (B.tid() == 0) {  // buildScheduledClusters over spec.Clusters order (assignment.go:125-142)
+    const bool fresh = (h.flags & BF_FRESH) != 0;
+    int32_t assigned = 0;
+    for (int j = 0; j < h.tgt_cnt; j++) {
+      const int32_t i = pos[x.bv->ipool[h.tgt_off + 2 * j]];
+      if (i < 0) continue;
+      const int32_t r = x.bv->ipool[h.tgt_off + 2 * j + 1];
+      assigned = add32(assigned, r);
+      if (fresh) pw.rep[i] = add32(pw.rep[i], r);  // first (only) occurrence of the name
+    }
+    go = fresh || assigned < h.replicas;
+  }
+  go = B.bcast(go);
+  for (int i = B.tid(); i < n; i += B.nth()) pos[items[i].rank] = -1;
+  if (!go) {
+    B.sync();
+    return false;
+  }
+  int ok = 1;
+  if (B.wid() == 0) ok = pw.run(n) ? 1 : 0;
+  ok = B.bcast(ok);
+  if (!ok) return false;
+  for (int i = B.tid(); i < n; i += B.nth()) {
+    sc.an[i] = pw.name[i];
+    sc.ar[i] = pw.rep[i];
+  }
+  B.sync();
+  sc.presorted = 1;
+  return true;
+}
+
 template <class BLK>
 KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const KArgs& a, unsigned char* scratch,
-                     size_t slot_bytes, int scratch_cap, int lds_area) {
+                     size_t slot_bytes, int scratch_cap, int lds_area, int lds_sort) {
+  KP_STAMP_INIT
   const int words = (a.s.Cp + 31) >> 5;
   uint32_t* tgt = (uint32_t*)(smem + kRedBytes);
   unsigned char* larea = (unsigned char*)(tgt + ((words + 3) & ~3));  // lds_area bytes
+  unsigned char* sarea = larea + lds_area;                             // lds_sort bytes
   unsigned char* mine = scratch + (size_t)blk * slot_bytes;
   // slot layout: cand r/v [Cp] | keys [P] | items [Cp] | pos [Cp] | serial scratch
   int P = 1;
@@ -362,15 +414,20 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
   Cands cd;
   cd.r = (uint32_t*)mine;
   cd.v = (int32_t*)(cd.r + a.s.Cp);
-  uint64_t* keys = (uint64_t*)(cd.v + a.s.Cp);
-  Item* items = (Item*)(keys + P);
+  // the candidates' sortClusters keys are sorted in LDS when they fit
+  uint64_t* keys = (size_t)lds_sort >= 8 * (size_t)P ? (uint64_t*)sarea : (uint64_t*)(cd.v + a.s.Cp);
+  const bool pdq_lds = (size_t)lds_sort >= pdq_wave_bytes(a.s.Cp);
+  Item* items = (Item*)((uint64_t*)(cd.v + a.s.Cp) + P);
   int32_t* pos = (int32_t*)(items + a.s.Cp);
   unsigned char* ser = (unsigned char*)(pos + a.s.Cp);
   for (int i = B.tid(); i < a.s.Cp; i += B.nth()) pos[i] = -1;
   B.sync();
-  for (int idx = blk; idx < a.n; idx += grid) {
+  const bool tie_lds = (size_t)lds_sort >= 3072 + 8 * (size_t)sel_all_ecap(a.s.Cp) + 64;
+  // the select kernels appended the flagged bindings to slow_ids (same stream: complete)
+  const int nslow = (int)*(volatile uint32_t*)&a.stats[0];
+  for (int idx = blk; idx < nslow && idx < a.n; idx += grid) {
     const int b = a.list[idx];
-    if (!a.slow[b]) continue;
+    const int why = a.slow[b];
     const BindHdr* h = &a.bv.hdr[b];
     build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
     SelCtx x = make_ctx(a, b, tgt);
@@ -383,11 +440,13 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
     if (B.bcast(done)) continue;
     cd.F = gather(B, x, cd, false);
     const int F = cd.F;
-    for (int i = B.tid(); i < P; i += B.nth()) keys[i] = i < F ? cand_key(x, cd, i, cd.v[i]) : ~0ull;
+    int PF = 1;
+    while (PF < F) PF <<= 1;
+    for (int i = B.tid(); i < PF; i += B.nth()) keys[i] = i < F ? cand_key(x, cd, i, cd.v[i]) : ~0ull;
     B.sync();
-    for (int k = 2; k <= P; k <<= 1)  // bitonic sort (ascending)
+    for (int k = 2; k <= PF; k <<= 1)  // bitonic sort (ascending)
       for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = B.tid(); i < P; i += B.nth()) {
+        for (int i = B.tid(); i < PF; i += B.nth()) {
           int l = i ^ j;
           if (l > i) {
             uint64_t ki = keys[i], kl = keys[l];
@@ -402,8 +461,29 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
       }
     for (int i = B.tid(); i < F; i += B.nth()) items[i] = item_from_key(x, keys[i]);
     B.sync();
+    KP_STAMP(x, 6);
+    SerialScratch sc = serial_scratch_carve(ser, scratch_cap);
+    if (pdq_lds && presort_dynamic(B, x, items, F, sarea, pos, sc) && why == SLOW_TIE && tie_lds) {
+      // The Aggregated tie group straddled the cut: with sort.Sort's output
+      // order known, the block-parallel path decides it exactly.
+      for (int i = B.tid(); i < F; i += B.nth()) pos[sc.an[i]] = i;
+      B.sync();
+      const SelScratch ss = carve_sel_scratch(sarea, a.s.Cp);
+      const int w2 = sel_all_fast(B, x, PosCands{&cd, pos, B.tid(), B.nth()}, ss);
+      B.sync();  // every thread's last read of pos (emit) precedes the reset
+      for (int i = B.tid(); i < F; i += B.nth()) pos[sc.an[i]] = -1;
+      B.sync();
+      if (w2 == SLOW_NONE) {
+        if (B.tid() == 0) {
+          a.slow[b] = 0;
+          kp_atomic_add(&a.stats[7], 1u);  // resolved block-parallel
+        }
+        KP_STAMP(x, 7);
+        continue;
+      }
+    }
+    KP_STAMP(x, 7);
     if (B.tid() == 0) {
-      SerialScratch sc = serial_scratch_carve(ser, scratch_cap);
       sc.pos = pos;
       int n = F;
       bool err = false;
@@ -457,6 +537,7 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
       a.slow[b] = 0;
     }
     B.sync();
+    KP_STAMP(x, 8);
   }
 }
 

@@ -16,7 +16,8 @@ struct KArgs {
   const uint64_t* fmask;  // [B][W]
   const int32_t* est;     // [B][Cp]
   Sink sink;
-  int32_t* slow;          // [B] flag: needs the exact serial path
+  int32_t* slow;          // [B] SLOW_* reason the binding needs k_slow for (0: none)
+  int32_t* slow_ids;      // bindings flagged for k_slow, [0, stats[0]) (append order)
   uint32_t* stats;        // [0]: bindings flagged for the serial path, [SLOW_*]: by reason
   unsigned long long* dbg;  // diagnostic build only: phase cycle sums (nullptr otherwise)
 };
@@ -39,9 +40,11 @@ struct SelectExtra {
   size_t slot_bytes = 0;
   int grid = 0;                      // slow path persistent grid
   int lds_area = 0;                  // slow path: LDS bytes for the small serial problems
+  int lds_sort = 0;                  // slow path: LDS bytes for the candidate sorts (0: global slot)
 };
 
 constexpr int kBlock = 256;
+constexpr int kSlowBlock = 512;  // k_slow: wider for the LDS bitonic sort
 constexpr int kPairStage = 4096;  // bytes of per-binding predicate data staged in LDS
 
 // Enumeration capacity (u64 entries) of the SEL_ALL selection buffer.

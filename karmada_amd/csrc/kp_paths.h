@@ -61,6 +61,7 @@ struct LdsCands {  // candidates compacted in LDS (gather)
   }
   // Position key of a candidate in the sort.Sort input (sortClusters order).
   KP_FI uint64_t okey(const SelCtx& x, uint32_t rk, int32_t v0) const { return cand_order_key(x, rk, v0); }
+  static constexpr bool kExact = false;  // okey is sort.Sort's output order only for <= 12 (stable insertion)
 };
 template <int J>
 struct RegCands {  // slot j of thread t is cluster t + nth*j; votes live in registers
@@ -74,6 +75,21 @@ KP_UNROLL
       if ((fm >> j) & 1ull) fn((uint32_t)(tid + nth * j), v[j]);
   }
   KP_FI uint64_t okey(const SelCtx& x, uint32_t rk, int32_t v0) const { return cand_order_key(x, rk, v0); }
+  static constexpr bool kExact = false;
+};
+
+// Gathered candidates (any memory) whose sort.Sort output order is known:
+// pos[rank] = position after the emulated sort (k_slow, kp_pdq.h).
+struct PosCands {
+  const Cands* cd;
+  const int32_t* pos;
+  int tid, nth;
+  template <class Fn>
+  KP_FI void each(Fn fn) const {
+    for (int i = tid; i < cd->F; i += nth) fn(c_rank(*cd, i), cd->v[i]);
+  }
+  KP_FI uint64_t okey(const SelCtx&, uint32_t rk, int32_t) const { return (uint64_t)(uint32_t)pos[rk]; }
+  static constexpr bool kExact = true;
 };
 
 // The binding's spec.Clusters entries that are candidates (scheduledClusters,
@@ -97,6 +113,7 @@ struct TgtCands {
       if ((uint32_t)x->bv->ipool[h.tgt_off + 2 * j] == rk) return (uint64_t)j;
     return ~0ull;
   }
+  static constexpr bool kExact = false;
 };
 
 // Block-parallel emission of per-candidate results. rep(rank, v) gives the
@@ -325,23 +342,19 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
       const int64_t need = tX - sgt;
       const int64_t j = need <= 0 ? 1 : (vstar > 0 ? (need + vstar - 1) / vstar : ceq);
       if (j < ceq) {  // the tie group straddles the cut
-        // Only sort.Sort's permutation of equal keys decides. For lists of at
-        // most 12 Go runs insertion sort, which is stable: the tie group keeps
-        // input order and its first j members are taken. Longer lists: serial.
-        if (nparty > 12) return SLOW_TIE;
-        uint64_t prev = 0;
-        bool first = true;
-        for (int64_t q = 0; q < j; q++) {
-          uint64_t m = ~0ull;
-          cs.each([&](uint32_t rk, int32_t v0) {
-            if (prior(rk) != xIsPrior || (int64_t)vote32(rk, v0) != vstar) return;
-            const uint64_t k = cs.okey(x, rk, v0);
-            if ((first || k > prev) && k < m) m = k;
-          });
-          prev = B.minu64(m);
-          first = false;
-        }
-        tieCut = prev;
+        // Only sort.Sort's permutation of equal keys decides: the first j tie
+        // members in its output order are taken. Lists of at most 12 are
+        // insertion-sorted (stable), so input order is output order; longer
+        // lists need the emulated permutation (CS::kExact, k_slow).
+        if (!CS::kExact && nparty > 12) return SLOW_TIE;
+        tieCut = radix_select_each(
+            B, ss.hist,
+            [&](auto fn) {
+              cs.each([&](uint32_t rk, int32_t v0) {
+                if (prior(rk) == xIsPrior && (int64_t)vote32(rk, v0) == vstar) fn(cs.okey(x, rk, v0));
+              });
+            },
+            j);
         straddle = true;
       }
     }

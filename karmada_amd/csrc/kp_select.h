@@ -28,6 +28,7 @@ struct SerialScratch {
   uint32_t* sn;  int32_t* sr;    // scheduledClusters
   uint32_t* rn;  int32_t* rr;    // final result
   int32_t* pos;                  // optional rank-indexed scratch (all -1 between uses)
+  int presorted;                 // an/ar already hold the sorted TargetClustersList (body_slow)
 };
 KP_HD inline size_t serial_scratch_bytes(int cap) {
   return (size_t)cap * (sizeof(Item) + 2 * sizeof(int64_t) + 14 * sizeof(uint32_t)) + 256;
@@ -60,6 +61,7 @@ KP_HD inline SerialScratch serial_scratch_carve(void* mem, int cap) {
   s.rn = (uint32_t*)take((size_t)cap * 4);
   s.rr = (int32_t*)take((size_t)cap * 4);
   s.pos = nullptr;
+  s.presorted = 0;
   return s;
 }
 
@@ -338,6 +340,7 @@ struct SerialAssign {
       for (int i = 0; i < m; i++) sc.pos[list[i].rank] = -1;
     int32_t assigned = 0;
     for (int j = 0; j < ns; j++) assigned = add32(assigned, sc.sr[j]);
+    if ((h.flags & BF_FRESH) && sc.presorted) return divide(m, rep, 0, KP_ERR_FRESH_NOT_ENOUGH, o, nt);
     if (h.flags & BF_FRESH) {  // dynamicFreshScale (division_algorithm.go:139-166)
       for (int i = 0; i < m; i++) {
         sc.an[i] = list[i].rank;
@@ -369,6 +372,7 @@ struct SerialAssign {
       sort_tcl(sc.an, sc.ar, ns);
       return divide(ns, rep, 0, KP_ERR_SCALE_DOWN_NOT_ENOUGH, o, nt);
     }
+    if (assigned < rep && sc.presorted) return divide(m, sub32(rep, assigned), ns, KP_ERR_SCALE_UP_NOT_ENOUGH, o, nt);
     if (assigned < rep) {  // dynamicScaleUp (:121-136)
       for (int i = 0; i < m; i++) {
         sc.an[i] = list[i].rank;
@@ -808,16 +812,15 @@ KP_FI int64_t wsel_max(const BLK& B, unsigned long long* wh, Vals vals, int64_t 
 // ----------------------------------------------------------------------------
 // k-th smallest (1-based) 64-bit key over a predicate set: 8-bit radix select.
 // ----------------------------------------------------------------------------
-template <class BLK, class Pred, class Key>
-KP_FI uint64_t radix_select(const BLK& B, uint32_t* hist, int F, Pred pred, Key key, int64_t k) {
+// keys(fn) calls fn(key) for every key of the set the calling thread owns.
+template <class BLK, class Keys>
+KP_FI uint64_t radix_select_each(const BLK& B, uint32_t* hist, Keys keys, int64_t k) {
   // bytes shared by every key are skipped: start at the highest differing byte
   uint64_t an = ~0ull, on = 0;
-  for (int i = B.tid(); i < F; i += B.nth())
-    if (pred(i)) {
-      const uint64_t kk = key(i);
-      an &= kk;
-      on |= kk;
-    }
+  keys([&](uint64_t kk) {
+    an &= kk;
+    on |= kk;
+  });
   B.andor(an, on);
   const uint64_t diff = an ^ on;
   if (diff == 0) return an;  // all keys equal
@@ -829,17 +832,25 @@ KP_FI uint64_t radix_select(const BLK& B, uint32_t* hist, int F, Pred pred, Key 
     for (int i = B.tid(); i < 256; i += B.nth()) hist[i] = 0;
     B.sync();
     const uint64_t hm = shift == 56 ? 0ull : (~0ull << (shift + 8));
-    for (int i = B.tid(); i < F; i += B.nth())
-      if (pred(i)) {
-        const uint64_t kk = key(i);
-        if ((kk & hm) == (prefix & hm)) kp_atomic_add(&hist[(kk >> shift) & 255], 1u);
-      }
+    keys([&](uint64_t kk) {
+      if ((kk & hm) == (prefix & hm)) kp_atomic_add(&hist[(kk >> shift) & 255], 1u);
+    });
     int64_t before;
     const int bin = B.find_bin(hist, k, &before, false);
     k -= before;
     prefix |= (uint64_t)bin << shift;
   }
   return prefix;
+}
+template <class BLK, class Pred, class Key>
+KP_FI uint64_t radix_select(const BLK& B, uint32_t* hist, int F, Pred pred, Key key, int64_t k) {
+  return radix_select_each(
+      B, hist,
+      [&](auto fn) {
+        for (int i = B.tid(); i < F; i += B.nth())
+          if (pred(i)) fn(key(i));
+      },
+      k);
 }
 
 }  // namespace kp

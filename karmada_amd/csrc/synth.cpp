@@ -13,6 +13,9 @@
 //   5  C=10k,  B=1M:  mix of 2-4 by binding index
 //   6  "edge": every branch of the path (overflow tiers, multi-term affinities,
 //      reschedule, scale-down, duplicates, non-workloads, odd strategies) at small C.
+//   7  "ties": clusters in three identical capacity classes, mostly Aggregated,
+//      so equal AvailableReplicas straddle the Aggregated cut (sort.Sort's
+//      permutation of equal keys decides; SURVEY hazard H2), parity only.
 #include <stdint.h>
 
 #include <cmath>
@@ -187,6 +190,13 @@ void gen_cluster(kps_world& w, uint32_t i, kp_cluster& c) {
           eph = r.range(10, 100), gpus = r.range(0, 64);
   double f = 0.7 * r.unit();
   if (cfg == 6 && r.p(0.2)) f = 0.999;  // nearly full clusters
+  if (cfg == 7) {  // three capacity classes, nothing allocated: estimates tie in large groups
+    cpu = 1000 * (1 + (int64_t)r.below(3));
+    memg = 16384;
+    pods = 11000;
+    eph = 100;
+    f = 0;
+  }
   al[0] = {w.s("cpu"), w.s(std::to_string(cpu))};
   al[1] = {w.s("memory"), w.s(std::to_string(memg) + "Gi")};
   al[2] = {w.s("pods"), w.s(std::to_string(pods))};
@@ -345,6 +355,21 @@ void gen_binding(kps_world& w, uint64_t i, kp_binding& b) {
     ev[0] = w.s(w.cname((uint32_t)r.below(C)));
     b.eviction_from = ev;
     b.n_eviction_from = 1;
+  }
+  if (cfg == 7) {
+    b.replica_division_preference = w.s(r.p(0.8) ? "Aggregated" : "Weighted");
+    if (r.p(0.7)) b.has_cluster_affinity = 0;  // keep most clusters feasible
+    b.replicas = (int32_t)r.range(1, 400000);
+    if (r.p(0.1)) {  // reschedule triggered: fresh with prior placement
+      b.has_reschedule_triggered_at = 1;
+      b.has_last_scheduled_time = 1;
+      b.reschedule_triggered_at_ns = 2000;
+      b.last_scheduled_time_ns = 1000;
+    }
+    if (b.n_clusters > 0)
+      for (uint32_t k = 0; k < b.n_clusters; k++)
+        const_cast<kp_target_cluster*>(b.clusters)[k].replicas = (int32_t)r.range(0, b.replicas / 4 + 1);
+    return;
   }
   if (cfg != 6) return;
   // ---- edge workload: perturb everything the path branches on ----

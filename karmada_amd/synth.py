@@ -18,6 +18,7 @@ CONFIGS = {
     4: (5_000, 100_000),
     5: (10_000, 1_000_000),
     6: (300, 5_000),   # edge workload (every branch), parity only
+    7: (2_000, 5_000),  # Aggregated tie straddles (sort.Sort permutation), parity only
 }
 
 

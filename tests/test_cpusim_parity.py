@@ -44,6 +44,7 @@ def compare(got, want, label):
 @pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
     (1, 1, 10, 1000), (2, 2, 300, 400), (3, 3, 200, 300), (4, 4, 400, 500),
     (6, 6, 120, 1500), (6, 7, 40, 1500), (6, 8, 1, 200), (6, 9, 257, 600),
+    (7, 17, 300, 400), (7, 18, 13, 300),
 ])
 def test_cpusim_schedule_parity(engine, config, seed, n_clusters, n_bindings):
     u = synth.Universe(config, seed, n_clusters, 0, n_bindings)

@@ -89,3 +89,36 @@ def test_wsel_max_brute_force():
         want = max(v for v in set(vals) if v > 0 and sum(x for x in vals if x >= v) >= target)
         arr = (C.c_int32 * n)(*vals)
         assert SIM.kpsim_wsel_max(arr, n, target) == want, (vals, target)
+
+
+SIM.kpsim_sort_tcl.restype = C.c_int
+SIM.kpsim_sort_tcl.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.c_int, C.c_int]
+
+
+def _sort(reps, mode):
+    n = len(reps)
+    names = (C.c_uint32 * max(1, n))(*range(n))
+    rr = (C.c_int32 * max(1, n))(*reps)
+    ok = SIM.kpsim_sort_tcl(names, rr, n, mode)
+    return ok, [names[i] for i in range(n)], [rr[i] for i in range(n)]
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_sort_tcl_wave_form_matches_serial_and_oracle(seed):
+    """sort.Sort(TargetClustersList) (division_algorithm.go:31-36): the wave
+    emulation (kp_pdq.h, one lane here) and the serial emulation (kp_algo.h)
+    give the oracle's permutation (unstable: equal replicas keep Go's order)."""
+    import pdq_cases
+    L = O.lib()
+    L.kpo_sort_target_clusters.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_uint32), C.c_uint32]
+    for n, kind, reps in pdq_cases.cases(seed):
+        ids = (C.c_uint32 * max(1, n))(*range(n))
+        rr = (C.c_int32 * max(1, n))(*reps)
+        L.kpo_sort_target_clusters(rr, ids, n)
+        want = [ids[i] for i in range(n)]
+        _, serial, _ = _sort(reps, 0)
+        ok, wave, wrep = _sort(reps, 1)
+        assert serial == want, (n, kind)
+        assert ok == 1, (n, kind)
+        assert wave == want, (n, kind)
+        assert wrep == [reps[i] for i in want]

@@ -63,6 +63,12 @@ CASES = [
     (6, 7, 64, 3000),
     (6, 8, 1, 500),
     (6, 9, 700, 2000),
+    # Aggregated ties straddling the cut at every list length: k_slow's
+    # sort.Sort wave emulation + block-parallel cut (kp_pdq.h)
+    (7, 17, 2000, 3000),
+    (7, 18, 13, 2000),
+    (7, 19, 100, 2000),
+    (7, 20, 5000, 1000),
 ]
 
 
