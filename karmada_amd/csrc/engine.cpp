@@ -420,7 +420,31 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
   int32_t *d_prov, *d_reg, *d_regidx, *d_zoff, *d_zid, *d_lbl, *d_toff, *d_tk, *d_tv, *d_te, *d_mtid, *d_mcnt;
   int64_t *d_pint, *d_rint, *d_allowed, *d_avail, *d_tmpl;
   uint64_t* d_api;
+  // taint lists deduplicated: one TaintToleration answer per distinct list and binding
+  std::vector<int32_t> tset(Cp, 0), trep;
+  {
+    std::map<std::vector<int32_t>, int32_t> ids;
+    std::vector<int32_t> key;
+    for (int r = 0; r < C; r++) {
+      key.clear();
+      for (int t = s->taint_off[r]; t < s->taint_off[r + 1]; t++) {
+        key.push_back(s->taint_key[t]);
+        key.push_back(s->taint_val[t]);
+        key.push_back(s->taint_eff[t]);
+      }
+      auto it = ids.find(key);
+      if (it == ids.end()) {
+        it = ids.emplace(key, (int32_t)trep.size()).first;
+        trep.push_back(r);
+      }
+      tset[r] = it->second;
+    }
+    if (trep.empty()) trep.push_back(0);
+  }
+  int32_t *d_tset, *d_trep;
   a.add(&d_flags, Cp);
+  a.add(&d_tset, Cp);
+  a.add(&d_trep, trep.size());
   a.add(&d_perm, Cp);
   a.add(&d_prov, Cp);
   a.add(&d_reg, Cp);
@@ -445,6 +469,8 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
   for (int r = 0; r < C; r++) permp[r] = s->perm[r];
   auto up = [&](void* d, const void* h, size_t bytes) { return dev::h2d(d, h, bytes, e->stream); };
   HIPCHK(up(d_flags, s->flags.data(), 4 * Cp));
+  HIPCHK(up(d_tset, tset.data(), 4 * Cp));
+  HIPCHK(up(d_trep, trep.data(), 4 * trep.size()));
   HIPCHK(up(d_perm, permp.data(), 4 * Cp));
   HIPCHK(up(d_prov, s->provider.data(), 4 * Cp));
   HIPCHK(up(d_reg, s->region.data(), 4 * Cp));
@@ -479,6 +505,9 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
   v.taint_key = d_tk;
   v.taint_val = d_tv;
   v.taint_eff = d_te;
+  v.taint_set = d_tset;
+  v.tset_rep = d_trep;
+  v.n_tsets = (int32_t)trep.size();
   v.api_bits = d_api;
   v.allowed = d_allowed;
   v.avail = d_avail;
@@ -966,7 +995,7 @@ void parallel_for(int n, int threads, F fn) {
 
 size_t smem_pair(const kp_snapshot* s, int md_cap) {
   int words = (s->Cp + 31) >> 5;
-  return kRedBytes + 8 * (size_t)words + 4 * (size_t)((md_cap + 3) & ~3) + kPairStage + 64;
+  return kRedBytes + 8 * (size_t)words + 4 * (size_t)((md_cap + 3) & ~3) + kPairStage + kTsetMax / 8 + 64;
 }
 size_t smem_all(const kp_snapshot* s) {
   int words = (s->Cp + 31) >> 5;
@@ -1529,7 +1558,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     HIPCHK(dev::d2h(h, bt->dbg, sizeof(h), st));
     HIPCHK(dev::sync(st));
     fprintf(stderr, "kp stamps (s_memtime ticks, summed over workgroups):");
-    for (int i = 0; i < 9; i++) fprintf(stderr, " [%d]=%llu", i, h[i]);
+    for (int i = 0; i < 16; i++) fprintf(stderr, " [%d]=%llu", i, h[i]);
     fprintf(stderr, "\n");
   }
 #endif

@@ -255,59 +255,161 @@ KP_HD inline int64_t floor_div_below(int64_t a, int64_t q, int64_t lim) {
   return (int64_t)e < lim ? (int64_t)e : lim;
 }
 
+// Per-cluster operands of the GeneralEstimator, loaded before any is used: the
+// grade walk and the per-resource minimum then cost one memory latency per
+// cluster, not one per grade or resource (the loads are independent; only the
+// uniform binding fields decide which are issued).
+constexpr int kEstUnroll = 8;
+struct EstOps {
+  uint32_t f;
+  int64_t allowed;
+  int32_t gc[kEstUnroll], gt[kEstUnroll];  // model node groups k < kEstUnroll
+  int64_t av[kEstUnroll];                  // summary available of request j < kEstUnroll
+};
+KP_HD inline EstOps est_load(const SnapView& s, const BatchView& bv, const BindHdr& h, int c, uint32_t f) {
+  EstOps o;
+  o.f = f;
+  o.allowed = s.allowed[c];
+  const bool rr = (h.flags & BF_HAS_RR) != 0;
+  const int kh = rr && !(h.flags & BF_MODEL_ERR) ? (s.kmax < kEstUnroll ? s.kmax : kEstUnroll) : 0;
+  const int jh = rr ? (h.sreq_cnt < kEstUnroll ? h.sreq_cnt : kEstUnroll) : 0;
+KP_UNROLL
+  for (int k = 0; k < kEstUnroll; k++) {
+    o.gc[k] = 0;
+    o.gt[k] = 0;
+    if (k < kh) {
+      o.gc[k] = s.mg_cnt[(size_t)k * s.Cp + c];
+      o.gt[k] = s.mg_tid[(size_t)k * s.Cp + c];
+    }
+  }
+KP_UNROLL
+  for (int j = 0; j < kEstUnroll; j++) {
+    o.av[j] = 0;
+    if (j < jh) {
+      const int32_t rid = bv.ipool[h.sreq_off + j];
+      if (rid >= 0) o.av[j] = s.avail[(size_t)rid * s.Cp + c];
+    }
+  }
+  return o;
+}
+
 // GeneralEstimator.maxAvailableReplicas (general.go:66-108), assumed workloads empty.
 // md: per-template MaxDivided table (LDS) or nullptr to compute per pair.
-KP_HD inline int32_t general_estimate(const SnapView& s, const BatchView& bv, const BindHdr& h, int c,
-                                      const int32_t* md) {
-  uint32_t f = s.flags[c];
+KP_HD inline int32_t est_compute(const SnapView& s, const BatchView& bv, const BindHdr& h, int c, const int32_t* md,
+                                 const EstOps& o) {
+  const uint32_t f = o.f;
   if (!(f & CF_HAS_SUMMARY)) return 0;
-  int64_t m = s.allowed[c];
+  int64_t m = o.allowed;
   if (m <= 0) return 0;
   if (!(h.flags & BF_HAS_RR)) return (int32_t)m;
   if ((f & CF_MODEL_OK) && !(h.flags & BF_MODEL_ERR)) {
     // getMaximumReplicasBasedOnResourceModels: each identical model node absorbs
     // exactly its initial MaxDivided, capped at MaxInt32.
+    // d <= 110 (MaxPodsPerNode) and cnt <= MaxInt32: d*cnt < 2^38, and the
+    // sum stops growing at MaxInt32 (Go's break), so int64 cannot overflow.
     int64_t total = 0;
-    for (int k = 0; k < s.kmax; k++) {
+KP_UNROLL
+    for (int k = 0; k < kEstUnroll; k++)
+      if (k < s.kmax && o.gc[k] != 0 && total < kInt32Max)
+        total += (int64_t)(md ? md[o.gt[k]] : template_md(s, bv, h, o.gt[k])) * o.gc[k];
+    for (int k = kEstUnroll; k < s.kmax && total < kInt32Max; k++) {
       const int64_t cnt = s.mg_cnt[(size_t)k * s.Cp + c];
       if (cnt == 0) continue;
       const int32_t tid = s.mg_tid[(size_t)k * s.Cp + c];
-      // d <= 110 (MaxPodsPerNode) and cnt <= MaxInt32: d*cnt < 2^38, and the sum
-      // stops at MaxInt32, so int64 cannot overflow.
-      const int64_t d = md ? md[tid] : template_md(s, bv, h, tid);
-      total += d * cnt;
-      if (total >= kInt32Max) {
-        total = kInt32Max;
-        break;
-      }
+      total += (int64_t)(md ? md[tid] : template_md(s, bv, h, tid)) * cnt;
     }
+    if (total >= kInt32Max) total = kInt32Max;
     if (total < m) m = total;
     return (int32_t)m;
   }
   // getMaximumReplicasBasedOnClusterSummary (general.go:465-505)
   int64_t num = INT64_MAX;
-  for (int j = 0; j < h.sreq_cnt; j++) {
+  bool zero = false;
+KP_UNROLL
+  for (int j = 0; j < kEstUnroll; j++) {
+    if (j < h.sreq_cnt && !zero) {
+      if (bv.ipool[h.sreq_off + j] < 0 || o.av[j] <= 0) {
+        zero = true;
+      } else {
+        const int64_t lim = num < m ? num : m;  // only quotients below min(num, allowed) matter
+        const int64_t d = floor_div_below(o.av[j], bv.lpool[h.sreq_q_off + j], lim);
+        if (d < num) num = d;
+      }
+    }
+  }
+  if (zero) return 0;
+  for (int j = kEstUnroll; j < h.sreq_cnt; j++) {
     int32_t rid = bv.ipool[h.sreq_off + j];
     if (rid < 0) return 0;
     int64_t a = s.avail[(size_t)rid * s.Cp + c];
     if (a <= 0) return 0;
-    const int64_t lim = num < m ? num : m;  // only quotients below min(num, allowed) matter
+    const int64_t lim = num < m ? num : m;
     const int64_t d = floor_div_below(a, bv.lpool[h.sreq_q_off + j], lim);
     if (d < num) num = d;
   }
   if (num < m) m = num;
   return (int32_t)m;
 }
+KP_HD inline int32_t general_estimate(const SnapView& s, const BatchView& bv, const BindHdr& h, int c,
+                                      const int32_t* md) {
+  return est_compute(s, bv, h, c, md, est_load(s, bv, h, c, s.flags[c]));
+}
+
+// calAvailableReplicas over an estimate: MaxInt32 init, min with the
+// GeneralEstimator answer (-1 = UnauthenticReplica is skipped, core/util.go:86-99),
+// leftover MaxInt32 -> spec.Replicas.
+KP_HD inline int32_t cal_merge(const BindHdr& h, int32_t r) {
+  int32_t v = kInt32Max;
+  if (r != -1 && v > r) v = r;
+  if (v == kInt32Max) v = h.replicas;
+  return v;
+}
 
 // calAvailableReplicas (core/util.go:57-110) with the GeneralEstimator only.
 KP_HD inline int32_t cal_available(const SnapView& s, const BatchView& bv, const BindHdr& h, int c,
                                    const int32_t* md) {
   if (h.flags & BF_NONWORKLOAD_EST) return kInt32Max;
-  int32_t r = general_estimate(s, bv, h, c, md);
-  int32_t v = kInt32Max;
-  if (r != -1 && v > r) v = r;  // mergeReplicaResults skips UnauthenticReplica (-1)
-  if (v == kInt32Max) v = h.replicas;
-  return v;
+  return cal_merge(h, general_estimate(s, bv, h, c, md));
+}
+
+// Filter + calAvailableReplicas of one (binding, cluster) pair for the pair
+// kernel: every snapshot column the pair can need is loaded first, so the
+// filter's and the estimator's memory latencies overlap. tol_bits: per taint
+// set "tolerated" bits of this binding (LDS), or nullptr for the per-taint
+// loop. Returns the estimate (0 when infeasible); *fit = feasibility.
+KP_HD inline int32_t pair_eval(const SnapView& s, const BatchView& bv, const BindHdr& h, int c,
+                               const uint32_t* tgt_bits, const uint32_t* evict_bits, const uint32_t* tol_bits,
+                               const int32_t* md, bool* fit) {
+  const int en = h.enabled;
+  const uint32_t f = s.flags[c];
+  const bool api_on = (en & 1) && h.gvk >= 0;
+  uint64_t aw = 0;
+  if (api_on) aw = s.api_bits[(size_t)(h.gvk >> 6) * s.Cp + c];
+  const bool tset_on = (en & 2) && tol_bits != nullptr;
+  int32_t ts = 0;
+  if (tset_on) ts = s.taint_set[c];
+  const bool est_on = !(h.flags & BF_NONWORKLOAD_EST);
+  EstOps o;
+  if (est_on) o = est_load(s, bv, h, c, f);
+  // findClustersThatFit skip-deleting + RunFilterPlugins (same predicates as pair_feasible)
+  bool ok = c < s.C && !(f & CF_DELETING);
+  const bool in_t = h.tgt_cnt > 0 && bit_test(tgt_bits, c);
+  if ((en & 1) && !in_t) ok = ok && api_on && ((aw >> (h.gvk & 63)) & 1ull);
+  if ((en & 2) && !in_t) ok = ok && (tset_on ? bit_test(tol_bits, ts) : taints_tolerated(s, bv, h, c));
+  if ((en & 4) && !(h.flags & BF_AFF_ALL) && ok) {
+    bool m = false;
+    for (int j = 0; j < h.filt_cnt && !m; j++) m = prog_match(s, bv, bv.ipool[h.filt_off + j], c);
+    ok = m;
+  }
+  if (en & 8) {
+    if ((h.flags & BF_NEED_PROVIDER) && !(f & CF_HAS_PROVIDER)) ok = false;
+    if ((h.flags & BF_NEED_REGION) && !(f & CF_HAS_REGION)) ok = false;
+    if ((h.flags & BF_NEED_ZONES) && !(f & CF_HAS_ZONES)) ok = false;
+  }
+  if ((en & 32) && h.evict_cnt > 0 && bit_test(evict_bits, c)) ok = false;
+  *fit = ok;
+  if (!ok) return 0;
+  return est_on ? cal_merge(h, est_compute(s, bv, h, c, md, o)) : kInt32Max;
 }
 
 // getClusterOverflowOrder (group_clusters.go:517-543)

@@ -5,7 +5,7 @@
 // same code paths on the host.
 //
 // Per-block LDS layouts (dynamic shared memory; sizes computed in engine.cpp):
-//   pair      [512 red | tgt bits | evict bits | md table | predicate stage kPairStage]
+//   pair      [512 red | tgt bits | evict bits | md table | predicate stage kPairStage | taint-set bits]
 //   sel_all   [512 red | tgt bits | cand r [Cp] | cand v [Cp] | whist 2 KB | hist 1 KB | buf ecap*8]
 //   sel_all_reg [512 red | tgt bits | whist 2 KB | hist 1 KB | buf ecap*8]  (candidates in registers)
 //   sel_clus  [512 red | hist 1 KB | items 2*kSmallMax | keys 2*kSmallMax | tgt | cand/serial area]
@@ -93,8 +93,8 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
   // Stage this binding's predicate data (programs, value lists, tolerations) in
   // LDS: every lane reads it for every cluster, uniformly.
   BatchView lv = bv;
+  unsigned char* st = (unsigned char*)(md + ((md_cap + 3) & ~3));
   {
-    unsigned char* st = (unsigned char*)(md + ((md_cap + 3) & ~3));
     const int nin = h.in_end - h.in_beg, npr = h.pr_end - h.pr_beg, nip = h.ip_end - h.ip_beg, nto = h.tol_cnt;
     const size_t need = sizeof(Instr) * nin + sizeof(Prog) * npr + sizeof(Tol) * nto + 4 * (size_t)nip;
     if (need <= (size_t)kPairStage) {
@@ -113,6 +113,17 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
       lv.ipool = rebase(sv, h.ip_beg);
     }
   }
+  // TaintToleration once per distinct taint list of the snapshot, not per cluster
+  uint32_t* tolb = (uint32_t*)(st + kPairStage);
+  const bool use_ts = est_mode == 0 && (h.enabled & 2) && s.n_tsets <= kTsetMax;
+  if (use_ts) {
+    const int tw = (s.n_tsets + 31) >> 5;
+    for (int i = B.tid(); i < tw; i += B.nth()) tolb[i] = 0;
+    B.sync();
+    for (int t = B.tid(); t < s.n_tsets; t += B.nth())
+      if (taints_tolerated(s, lv, h, s.tset_rep[t])) kp_atomic_or(&tolb[t >> 5], 1u << (t & 31));
+    B.sync();
+  }
   uint64_t* frow = fmask + (size_t)b * s.W;
   int32_t* erow = est + (size_t)b * s.Cp;
   for (int base = 0; base < s.Cp; base += B.nth()) {
@@ -120,8 +131,7 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
     bool fit = false;
     int32_t e = 0;
     if (est_mode == 0) {
-      fit = pair_feasible(s, lv, h, c, tgt, evict);
-      if (fit) e = cal_available(s, lv, h, c, use_md ? md : nullptr);
+      e = pair_eval(s, lv, h, c, tgt, evict, use_ts ? tolb : nullptr, use_md ? md : nullptr, &fit);
     } else if (c < s.C) {
       e = general_estimate(s, lv, h, c, use_md ? md : nullptr);
       fit = true;
@@ -181,7 +191,8 @@ KP_FI void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
   Cands cd;
   cd.r = tgt + ((words + 3) & ~3);
   cd.v = (int32_t*)(cd.r + a.s.Cp);
-  const SelScratch ss = carve_sel_scratch((unsigned char*)(cd.v + a.s.Cp), a.s.Cp);
+  SelScratch ss = carve_sel_scratch((unsigned char*)(cd.v + a.s.Cp), a.s.Cp);
+  ss.dbg = a.dbg;
   const BindHdr* h = &a.bv.hdr[b];
   build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
   SelCtx x = make_ctx(a, b, tgt);

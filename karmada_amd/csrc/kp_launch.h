@@ -46,6 +46,7 @@ struct SelectExtra {
 constexpr int kBlock = 256;
 constexpr int kSlowBlock = 512;  // k_slow: wider for the LDS bitonic sort
 constexpr int kPairStage = 4096;  // bytes of per-binding predicate data staged in LDS
+constexpr int kTsetMax = 4096;    // distinct taint lists answered once per binding (LDS bits)
 
 // Enumeration capacity (u64 entries) of the SEL_ALL selection buffer.
 KP_HD inline int sel_all_ecap(int Cp) { return Cp / 2 < 64 ? 64 : (Cp / 2 > 2048 ? 2048 : Cp / 2); }

@@ -145,6 +145,9 @@ struct SnapView {
   const int32_t* taint_key;
   const int32_t* taint_val;
   const int32_t* taint_eff;
+  const int32_t* taint_set;      // [Cp] id of the cluster's taint list (identical lists share an id)
+  const int32_t* tset_rep;       // [n_tsets] a cluster holding that list
+  int32_t n_tsets;
   const uint64_t* api_bits;      // [api_words][Cp]
   const int64_t* allowed;        // [Cp] getAllowedPodNumber
   const int64_t* avail;          // [n_res][Cp] summary path available (milli for cpu), <=0 -> 0

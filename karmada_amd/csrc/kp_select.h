@@ -88,10 +88,21 @@ struct SelCtx {
       kp_t0 = t;                                                         \
     }                                                                    \
   } while (0)
+#define KP_STAMPD(dbg, i)                                                \
+  do {                                                                   \
+    if (threadIdx.x == 0 && (dbg)) {                                     \
+      unsigned long long t = __builtin_amdgcn_s_memtime();               \
+      atomicAdd(&(dbg)[i], t - kp_t0);                                   \
+      kp_t0 = t;                                                         \
+    }                                                                    \
+  } while (0)
 #else
 #define KP_STAMP_INIT
 #define KP_STAMP(x, i) \
   do {                 \
+  } while (0)
+#define KP_STAMPD(dbg, i) \
+  do {                    \
   } while (0)
 #endif
 
@@ -524,8 +535,42 @@ KP_HD inline int32_t static_vote(const SelCtx& x, int c) {
 // ----------------------------------------------------------------------------
 // Candidate gather: feasible clusters of the binding in rank order.
 // ----------------------------------------------------------------------------
+struct alignas(16) I32x4 {
+  int32_t v[4];
+};
 template <class BLK>
 KP_FI int gather(const BLK& B, const SelCtx& x, Cands cd, bool weights) {
+  // Vector form (no overflow tiers, AllocatableReplicas votes): thread t owns
+  // the 4-cluster units t + nth*j and issues every 16-B row load before the
+  // first use, so a binding's row costs one memory latency, not one per unit.
+  constexpr int kJ = 8;
+  const int nu = (x.s->Cp + 3) >> 2;
+  if (!weights && x.h->ovf_mode == OVF_ZERO && nu <= kJ * B.nth()) {
+    const int tid = B.tid(), nth = B.nth();
+    const I32x4* e4 = (const I32x4*)x.erow;
+    uint32_t fm[kJ];
+    I32x4 ev[kJ];
+    int32_t mine = 0;
+KP_UNROLL
+    for (int j = 0; j < kJ; j++) {
+      const int u = tid + nth * j;
+      fm[j] = u < nu ? (uint32_t)(x.frow[u >> 4] >> ((u & 15) * 4)) & 0xFu : 0u;
+      if (fm[j]) ev[j] = e4[u];
+      mine += popc64(fm[j]);
+    }
+    int32_t F;
+    int32_t pos = B.excl_scan(mine, &F);
+KP_UNROLL
+    for (int j = 0; j < kJ; j++)
+      for (int q = 0; q < 4; q++)
+        if ((fm[j] >> q) & 1u) {
+          cd.r[pos] = (uint32_t)(4 * (tid + nth * j) + q);
+          cd.v[pos] = ev[j].v[q];
+          pos++;
+        }
+    B.sync();
+    return F;
+  }
   // Thread t owns clusters t + nth*j: one pass counts them (the feasibility word
   // is a broadcast load per wave), one scan places them, and the second pass
   // reads erow fully coalesced with no barrier between iterations. Candidate
@@ -574,6 +619,7 @@ struct SelScratch {
   unsigned long long* whist;  // 256 u64 bins (weighted selection); may alias hist storage
   uint64_t* buf;
   int cap;
+  unsigned long long* dbg = nullptr;  // diagnostic build only (KP_STAMPS)
 };
 
 template <class BLK, class Pred, class Key>
@@ -652,7 +698,9 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   // vote (cnt_ge(L) >= N). Parties with v < L have every priority below t*:
   // they take no seat and no part in any count below, so the passes skip
   // their fp64 work. When P >> N this leaves about N parties.
+  KP_STAMP_INIT
   const int64_t L = P > (int64_t)N ? kth_largest_vote(B, sc.hist, all_parties, (int64_t)N) : 0;
+  KP_STAMPD(sc.dbg, 9);
   auto parties = [&](auto fn) {
     all_parties([&](uint32_t rk, int64_t v) {
       if (v >= L) fn(rk, v);
@@ -701,6 +749,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     }
     if (clo < 0) clo = cnt1(bitsd(lo));
   }
+  KP_STAMPD(sc.dbg, 10);
   while (hi - lo > 1 && clo - chi > (int64_t)sc.cap) {
     uint64_t mid = lo + (hi - lo) / 2;
     int64_t c = cnt1(bitsd(mid));
@@ -712,6 +761,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
       chi = c;
     }
   }
+  KP_STAMPD(sc.dbg, 11);
   double tstar;
   if (hi - lo <= 1) {
     tstar = bitsd(lo);
@@ -735,6 +785,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     tstar = bitsd(radix_select(B, sc.hist, E, all, key, kth_small));
   }
   r.t = tstar;
+  KP_STAMPD(sc.dbg, 12);
   // seats strictly above t*, then the tie group at t* ordered by (k asc, name)
   int64_t S = 0, T = 0;
   parties([&](uint32_t, int64_t v) {
@@ -744,6 +795,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   });
   B.sum2(S, T);
   const int64_t M = (int64_t)N - S;
+  KP_STAMPD(sc.dbg, 13);
   if (M >= T) {
     r.tie = ~0ull;
   } else if (T <= (int64_t)sc.cap) {
@@ -777,6 +829,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     }
     r.tie = tlo;
   }
+  KP_STAMPD(sc.dbg, 14);
   return r;
 }
 
