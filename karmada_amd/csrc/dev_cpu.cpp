@@ -90,9 +90,10 @@ int fill(void* dst, int value, size_t bytes, stream_t) {
 }
 
 int pair(stream_t, const SnapView& s, const BatchView& bv, int b0, int nb, uint64_t* fmask, int32_t* est,
-         int64_t* score, int est_mode, int md_cap, size_t smem) {
+         int64_t* score, int est_mode, int md_cap, size_t smem, int fast) {
   grid(nb, smem, [&](int blk, unsigned char* sm) {
-    body_pair(CpuBlk{(int64_t*)sm}, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap);
+    if (fast) body_pair<true>(CpuBlk{(int64_t*)sm}, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap);
+    else body_pair<false>(CpuBlk{(int64_t*)sm}, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap);
   });
   return 0;
 }

@@ -156,6 +156,7 @@ struct kp_batch {
   unsigned char* slow_scratch = nullptr;
   size_t slow_slot = 0;
   int slow_grid = 0, slow_cap = 0, slow_lds = 0, slow_sort = 0;
+  bool pair_fast = false;
   // host results
   std::vector<int32_t> h_status, h_err, h_rstat, h_rsel, h_rnsel;
   std::vector<int64_t> h_arg;
@@ -441,10 +442,27 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
     }
     if (trep.empty()) trep.push_back(0);
   }
-  int32_t *d_tset, *d_trep;
+  int32_t *d_tset, *d_trep, *d_mt = nullptr;
+  // model node counts per (template, cluster): the fast estimator's dense form
+  std::vector<int32_t> mt;
+  {
+    bool dense = s->n_tmpl > 0 && s->n_tmpl <= kTmplDense;
+    for (int64_t x : s->tmpl) dense = dense && x >= 0;
+    if (dense) {
+      std::vector<int64_t> acc((size_t)s->n_tmpl * Cp, 0);
+      for (int k = 0; k < kmax; k++)
+        for (int r = 0; r < C; r++) {
+          const int32_t cnt = s->mg_cnt[(size_t)k * Cp + r];
+          if (cnt) acc[(size_t)s->mg_tid[(size_t)k * Cp + r] * Cp + r] += cnt;
+        }
+      mt.resize(acc.size());
+      for (size_t i = 0; i < acc.size(); i++) mt[i] = (int32_t)std::min<int64_t>(acc[i], kInt32Max);
+    }
+  }
   a.add(&d_flags, Cp);
   a.add(&d_tset, Cp);
   a.add(&d_trep, trep.size());
+  if (!mt.empty()) a.add(&d_mt, mt.size());
   a.add(&d_perm, Cp);
   a.add(&d_prov, Cp);
   a.add(&d_reg, Cp);
@@ -471,6 +489,7 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
   HIPCHK(up(d_flags, s->flags.data(), 4 * Cp));
   HIPCHK(up(d_tset, tset.data(), 4 * Cp));
   HIPCHK(up(d_trep, trep.data(), 4 * trep.size()));
+  if (!mt.empty()) HIPCHK(up(d_mt, mt.data(), 4 * mt.size()));
   HIPCHK(up(d_perm, permp.data(), 4 * Cp));
   HIPCHK(up(d_prov, s->provider.data(), 4 * Cp));
   HIPCHK(up(d_reg, s->region.data(), 4 * Cp));
@@ -515,6 +534,7 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
   v.mg_tid = d_mtid;
   v.mg_cnt = d_mcnt;
   v.tmpl = d_tmpl;
+  v.mt_cnt = d_mt;
   return KP_OK;
 }
 
@@ -1021,6 +1041,19 @@ size_t smem_region_b(const kp_snapshot* s, int cap) {
 const int kMdCap = 4096;
 // MaxDivided table entries staged per workgroup: the snapshot's template count.
 int md_cap_of(const kp_snapshot* s) { return s->n_tmpl <= kMdCap ? std::max(4, s->n_tmpl) : 0; }
+// Whether the specialised pair kernel (est_compute<true>) covers every binding of
+// the batch: MaxDivided and taint-set tables fit in LDS, the dense node-count
+// matrix exists (or no cluster has models), at most kReqUnroll resource requests
+// per binding, divisors <= 2^60.
+bool pair_fast_ok(const kp_snapshot* s, const kp_batch* bt) {
+  if (md_cap_of(s) == 0 || s->view.n_tsets > kTsetMax || (s->n_tmpl > 0 && !s->view.mt_cnt)) return false;
+  for (const BindHdr& h : bt->hdr) {
+    if (h.sreq_cnt > kReqUnroll) return false;
+    for (int j = 0; j < h.sreq_cnt; j++)
+      if (bt->lpool[h.sreq_q_off + j] > ((int64_t)1 << 60)) return false;
+  }
+  return true;
+}
 
 }  // namespace
 
@@ -1329,6 +1362,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   bt->slow_slot = (bt->slow_slot + 255) & ~(size_t)255;
   // k_slow: one workgroup per CU pass over the flagged bindings (appended on device)
   bt->slow_grid = (int)std::max<size_t>(1, std::min<size_t>(256, bt->l_slow.size()));
+  bt->pair_fast = pair_fast_ok(s, bt);
   Arena& a = bt->dev;
   BindHdr* d_hdr;
   int32_t* d_ipool;
@@ -1436,7 +1470,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
 #endif
   HIPCHK(dev::event_record(e->ev[0], st));
   HIPCHK(dev::pair(st, s->view, bt->view, 0, B, bt->fmask, bt->est, nullptr, 0, md_cap_of(s),
-                   smem_pair(s, md_cap_of(s))));
+                   smem_pair(s, md_cap_of(s)), bt->pair_fast && !getenv("KP_PAIR_GENERIC")));
   HIPCHK(dev::event_record(e->ev[1], st));
   SelectExtra sx;
   sx.rout = bt->rout;

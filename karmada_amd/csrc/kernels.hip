@@ -23,7 +23,12 @@ using namespace kp;
 extern "C" __global__ void __launch_bounds__(kBlock) k_pair(SnapView s, BatchView bv, int b0, uint64_t* fmask,
                                                             int32_t* est, int64_t* score, int est_mode, int md_cap) {
   KP_SMEM;
-  body_pair(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, b0, fmask, est, score, est_mode, md_cap);
+  body_pair<false>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, b0, fmask, est, score, est_mode, md_cap);
+}
+extern "C" __global__ void __launch_bounds__(kBlock) k_pair_fast(SnapView s, BatchView bv, int b0, uint64_t* fmask,
+                                                                 int32_t* est, int md_cap) {
+  KP_SMEM;
+  body_pair<true>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, b0, fmask, est, nullptr, 0, md_cap);
 }
 extern "C" __global__ void __launch_bounds__(1024) k_select_all(KArgs a) {
   KP_SMEM;
@@ -129,10 +134,13 @@ int fill(void* dst, int value, size_t bytes, stream_t s) {
 }
 
 int pair(stream_t st, const SnapView& s, const BatchView& bv, int b0, int nb, uint64_t* fmask, int32_t* est,
-         int64_t* score, int est_mode, int md_cap, size_t smem) {
+         int64_t* score, int est_mode, int md_cap, size_t smem, int fast) {
   if (nb <= 0) return 0;
-  hipLaunchKernelGGL(k_pair, dim3(nb), dim3(kBlock), smem, (hipStream_t)st, s, bv, b0, fmask, est, score, est_mode,
-                     md_cap);
+  if (fast)
+    hipLaunchKernelGGL(k_pair_fast, dim3(nb), dim3(kBlock), smem, (hipStream_t)st, s, bv, b0, fmask, est, md_cap);
+  else
+    hipLaunchKernelGGL(k_pair, dim3(nb), dim3(kBlock), smem, (hipStream_t)st, s, bv, b0, fmask, est, score, est_mode,
+                       md_cap);
   return chk(hipGetLastError());
 }
 

@@ -240,9 +240,10 @@ KP_HD inline int32_t template_md(const SnapView& s, const BatchView& bv, const B
 // min(a / q, lim) for a >= 0, q >= 1, lim >= 0 without a 64-bit integer divide:
 // a double estimate decides "quotient >= lim" when it is far from the limit,
 // otherwise the quotient (< lim + 2 <= 2^31 + 2) is corrected exactly.
+template <bool Fast = false>
 KP_HD inline int64_t floor_div_below(int64_t a, int64_t q, int64_t lim) {
   if (a < q) return 0;
-  if (q > ((int64_t)1 << 60)) {  // enormous request: the quotient is tiny, divide exactly
+  if (!Fast && q > ((int64_t)1 << 60)) {  // enormous request: the quotient is tiny, divide exactly
     const int64_t d = a / q;
     return d < lim ? d : lim;
   }
@@ -259,31 +260,45 @@ KP_HD inline int64_t floor_div_below(int64_t a, int64_t q, int64_t lim) {
 // grade walk and the per-resource minimum then cost one memory latency per
 // cluster, not one per grade or resource (the loads are independent; only the
 // uniform binding fields decide which are issued).
-constexpr int kEstUnroll = 8;
+constexpr int kEstUnroll = 8;   // model node groups per cluster (generic path)
+constexpr int kReqUnroll = 4;   // summary-path resource requests per binding
+constexpr int kTmplDense = 16;  // templates of the dense node-count matrix (fast path)
 struct EstOps {
   uint32_t f;
   int64_t allowed;
-  int32_t gc[kEstUnroll], gt[kEstUnroll];  // model node groups k < kEstUnroll
-  int64_t av[kEstUnroll];                  // summary available of request j < kEstUnroll
+  int32_t gc[kEstUnroll], gt[kEstUnroll];  // generic: model node groups k < kEstUnroll
+  int32_t mt[kTmplDense];                  // fast: nodes of template t (SnapView::mt_cnt)
+  int64_t av[kReqUnroll];                  // summary available of request j < kReqUnroll
 };
+template <bool Fast = false>
 KP_HD inline EstOps est_load(const SnapView& s, const BatchView& bv, const BindHdr& h, int c, uint32_t f) {
   EstOps o;
   o.f = f;
   o.allowed = s.allowed[c];
   const bool rr = (h.flags & BF_HAS_RR) != 0;
-  const int kh = rr && !(h.flags & BF_MODEL_ERR) ? (s.kmax < kEstUnroll ? s.kmax : kEstUnroll) : 0;
-  const int jh = rr ? (h.sreq_cnt < kEstUnroll ? h.sreq_cnt : kEstUnroll) : 0;
+  const bool model = rr && !(h.flags & BF_MODEL_ERR);
+  const int jh = rr ? (h.sreq_cnt < kReqUnroll ? h.sreq_cnt : kReqUnroll) : 0;
+  if (Fast) {
+    const int th = model ? s.n_tmpl : 0;
 KP_UNROLL
-  for (int k = 0; k < kEstUnroll; k++) {
-    o.gc[k] = 0;
-    o.gt[k] = 0;
-    if (k < kh) {
-      o.gc[k] = s.mg_cnt[(size_t)k * s.Cp + c];
-      o.gt[k] = s.mg_tid[(size_t)k * s.Cp + c];
+    for (int t = 0; t < kTmplDense; t++) {
+      o.mt[t] = 0;
+      if (t < th) o.mt[t] = s.mt_cnt[(size_t)t * s.Cp + c];
+    }
+  } else {
+    const int kh = model ? (s.kmax < kEstUnroll ? s.kmax : kEstUnroll) : 0;
+KP_UNROLL
+    for (int k = 0; k < kEstUnroll; k++) {
+      o.gc[k] = 0;
+      o.gt[k] = 0;
+      if (k < kh) {
+        o.gc[k] = s.mg_cnt[(size_t)k * s.Cp + c];
+        o.gt[k] = s.mg_tid[(size_t)k * s.Cp + c];
+      }
     }
   }
 KP_UNROLL
-  for (int j = 0; j < kEstUnroll; j++) {
+  for (int j = 0; j < kReqUnroll; j++) {
     o.av[j] = 0;
     if (j < jh) {
       const int32_t rid = bv.ipool[h.sreq_off + j];
@@ -295,6 +310,11 @@ KP_UNROLL
 
 // GeneralEstimator.maxAvailableReplicas (general.go:66-108), assumed workloads empty.
 // md: per-template MaxDivided table (LDS) or nullptr to compute per pair.
+// Fast: the launch guarantees md != nullptr, the dense node-count matrix
+// (n_tmpl <= kTmplDense, every template value >= 0 so every MaxDivided is >= 0),
+// every sreq_cnt <= kReqUnroll and every divisor <= 2^60 (pair_fast_ok,
+// engine.cpp), so the cold fallbacks are compiled out of the pair kernel.
+template <bool Fast = false>
 KP_HD inline int32_t est_compute(const SnapView& s, const BatchView& bv, const BindHdr& h, int c, const int32_t* md,
                                  const EstOps& o) {
   const uint32_t f = o.f;
@@ -308,11 +328,20 @@ KP_HD inline int32_t est_compute(const SnapView& s, const BatchView& bv, const B
     // d <= 110 (MaxPodsPerNode) and cnt <= MaxInt32: d*cnt < 2^38, and the
     // sum stops growing at MaxInt32 (Go's break), so int64 cannot overflow.
     int64_t total = 0;
+    if (Fast) {
+      // Groups of one template merged: sum_t MaxDivided_t * nodes_t, each term
+      // >= 0, so Go's stop at MaxInt32 is the clamp below; a node count
+      // clamped at MaxInt32 only matters when its MaxDivided >= 1, where the
+      // sum saturates either way.
 KP_UNROLL
-    for (int k = 0; k < kEstUnroll; k++)
+      for (int t = 0; t < kTmplDense; t++)
+        if (t < s.n_tmpl) total += (int64_t)md[t] * (int64_t)o.mt[t];
+    }
+KP_UNROLL
+    for (int k = 0; !Fast && k < kEstUnroll; k++)
       if (k < s.kmax && o.gc[k] != 0 && total < kInt32Max)
         total += (int64_t)(md ? md[o.gt[k]] : template_md(s, bv, h, o.gt[k])) * o.gc[k];
-    for (int k = kEstUnroll; k < s.kmax && total < kInt32Max; k++) {
+    for (int k = kEstUnroll; !Fast && k < s.kmax && total < kInt32Max; k++) {
       const int64_t cnt = s.mg_cnt[(size_t)k * s.Cp + c];
       if (cnt == 0) continue;
       const int32_t tid = s.mg_tid[(size_t)k * s.Cp + c];
@@ -326,19 +355,19 @@ KP_UNROLL
   int64_t num = INT64_MAX;
   bool zero = false;
 KP_UNROLL
-  for (int j = 0; j < kEstUnroll; j++) {
+  for (int j = 0; j < kReqUnroll; j++) {
     if (j < h.sreq_cnt && !zero) {
       if (bv.ipool[h.sreq_off + j] < 0 || o.av[j] <= 0) {
         zero = true;
       } else {
         const int64_t lim = num < m ? num : m;  // only quotients below min(num, allowed) matter
-        const int64_t d = floor_div_below(o.av[j], bv.lpool[h.sreq_q_off + j], lim);
+        const int64_t d = floor_div_below<Fast>(o.av[j], bv.lpool[h.sreq_q_off + j], lim);
         if (d < num) num = d;
       }
     }
   }
   if (zero) return 0;
-  for (int j = kEstUnroll; j < h.sreq_cnt; j++) {
+  for (int j = kReqUnroll; !Fast && j < h.sreq_cnt; j++) {
     int32_t rid = bv.ipool[h.sreq_off + j];
     if (rid < 0) return 0;
     int64_t a = s.avail[(size_t)rid * s.Cp + c];
@@ -377,6 +406,7 @@ KP_HD inline int32_t cal_available(const SnapView& s, const BatchView& bv, const
 // filter's and the estimator's memory latencies overlap. tol_bits: per taint
 // set "tolerated" bits of this binding (LDS), or nullptr for the per-taint
 // loop. Returns the estimate (0 when infeasible); *fit = feasibility.
+template <bool Fast = false>
 KP_HD inline int32_t pair_eval(const SnapView& s, const BatchView& bv, const BindHdr& h, int c,
                                const uint32_t* tgt_bits, const uint32_t* evict_bits, const uint32_t* tol_bits,
                                const int32_t* md, bool* fit) {
@@ -385,22 +415,24 @@ KP_HD inline int32_t pair_eval(const SnapView& s, const BatchView& bv, const Bin
   const bool api_on = (en & 1) && h.gvk >= 0;
   uint64_t aw = 0;
   if (api_on) aw = s.api_bits[(size_t)(h.gvk >> 6) * s.Cp + c];
-  const bool tset_on = (en & 2) && tol_bits != nullptr;
+  const bool tset_on = (en & 2) && (Fast || tol_bits != nullptr);
   int32_t ts = 0;
   if (tset_on) ts = s.taint_set[c];
   const bool est_on = !(h.flags & BF_NONWORKLOAD_EST);
   EstOps o;
-  if (est_on) o = est_load(s, bv, h, c, f);
+  if (est_on) o = est_load<Fast>(s, bv, h, c, f);
+  // ClusterAffinity first: its selector loads then issue while the loads above
+  // are still in flight (it reads none of them).
+  bool aff = true;
+  if ((en & 4) && !(h.flags & BF_AFF_ALL) && c < s.C) {  // (zone lists are [C+1])
+    aff = false;
+    for (int j = 0; j < h.filt_cnt && !aff; j++) aff = prog_match(s, bv, bv.ipool[h.filt_off + j], c);
+  }
   // findClustersThatFit skip-deleting + RunFilterPlugins (same predicates as pair_feasible)
-  bool ok = c < s.C && !(f & CF_DELETING);
+  bool ok = c < s.C && !(f & CF_DELETING) && aff;
   const bool in_t = h.tgt_cnt > 0 && bit_test(tgt_bits, c);
   if ((en & 1) && !in_t) ok = ok && api_on && ((aw >> (h.gvk & 63)) & 1ull);
-  if ((en & 2) && !in_t) ok = ok && (tset_on ? bit_test(tol_bits, ts) : taints_tolerated(s, bv, h, c));
-  if ((en & 4) && !(h.flags & BF_AFF_ALL) && ok) {
-    bool m = false;
-    for (int j = 0; j < h.filt_cnt && !m; j++) m = prog_match(s, bv, bv.ipool[h.filt_off + j], c);
-    ok = m;
-  }
+  if ((en & 2) && !in_t) ok = ok && ((Fast || tset_on) ? bit_test(tol_bits, ts) : taints_tolerated(s, bv, h, c));
   if (en & 8) {
     if ((h.flags & BF_NEED_PROVIDER) && !(f & CF_HAS_PROVIDER)) ok = false;
     if ((h.flags & BF_NEED_REGION) && !(f & CF_HAS_REGION)) ok = false;
@@ -409,7 +441,7 @@ KP_HD inline int32_t pair_eval(const SnapView& s, const BatchView& bv, const Bin
   if ((en & 32) && h.evict_cnt > 0 && bit_test(evict_bits, c)) ok = false;
   *fit = ok;
   if (!ok) return 0;
-  return est_on ? cal_merge(h, est_compute(s, bv, h, c, md, o)) : kInt32Max;
+  return est_on ? cal_merge(h, est_compute<Fast>(s, bv, h, c, md, o)) : kInt32Max;
 }
 
 // getClusterOverflowOrder (group_clusters.go:517-543)

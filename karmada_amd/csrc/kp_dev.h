@@ -36,8 +36,9 @@ int h2d(void* dst, const void* src, size_t bytes, stream_t s);  // stream-ordere
 int d2h(void* dst, const void* src, size_t bytes, stream_t s);
 int fill(void* dst, int value, size_t bytes, stream_t s);
 
+// fast: launch the specialised pair kernel (the batch meets pair_fast_ok).
 int pair(stream_t st, const SnapView& s, const BatchView& bv, int b0, int nb, uint64_t* fmask, int32_t* est,
-         int64_t* score, int est_mode, int md_cap, size_t smem);
+         int64_t* score, int est_mode, int md_cap, size_t smem, int fast = 0);
 int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x);
 int compact(stream_t st, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
             const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n);

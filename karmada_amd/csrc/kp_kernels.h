@@ -74,7 +74,9 @@ KP_FI bool pre_checks(const BLK& B, const SelCtx& x, int F) {
 // columns), stores their feasibility as one u64 word and calAvailableReplicas
 // per cluster. est_mode 1: raw GeneralEstimator answers for every cluster.
 // ---------------------------------------------------------------------------
-template <class BLK>
+// Fast: the specialised instance for batches that meet pair_fast_ok (engine.cpp):
+// est_mode 0, the MaxDivided and taint-set tables in LDS, no cold fallbacks.
+template <bool Fast, class BLK>
 KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView& s, const BatchView& bv, int b0,
                      uint64_t* fmask, int32_t* est, int64_t* score, int est_mode, int md_cap) {
   const int b = b0 + blk;
@@ -130,7 +132,9 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
     const int c = base + B.tid();
     bool fit = false;
     int32_t e = 0;
-    if (est_mode == 0) {
+    if (Fast) {
+      e = pair_eval<true>(s, lv, h, c, tgt, evict, tolb, md, &fit);
+    } else if (est_mode == 0) {
       e = pair_eval(s, lv, h, c, tgt, evict, use_ts ? tolb : nullptr, use_md ? md : nullptr, &fit);
     } else if (c < s.C) {
       e = general_estimate(s, lv, h, c, use_md ? md : nullptr);

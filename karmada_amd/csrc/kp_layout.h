@@ -154,6 +154,8 @@ struct SnapView {
   const int32_t* mg_tid;         // [kmax][Cp] model node group: template id (grade ascending)
   const int32_t* mg_cnt;         // [kmax][Cp] node count, clamped to MaxInt32 (0 = no group)
   const int64_t* tmpl;           // [n_tmpl][n_res] model template values
+  const int32_t* mt_cnt;         // [n_tmpl][Cp] model nodes per template, clamped to MaxInt32, or
+                                 // nullptr (n_tmpl > kTmplDense or a negative template value)
   const uint32_t* perm;          // rank -> caller index
 };
 
