@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 1
+#define KP_ABI_VERSION 2
 
 /* ------------------------------------------------------------------------- */
 /* Object model                                                              */
@@ -301,9 +301,11 @@ typedef struct kp_stage_times {
   double host_ms;      /* host group-combination (region DFS) */
   double copy_ms;      /* device -> host result copies */
   double total_ms;
-  float pair_kernel_ms; /* HIP event time of the pair kernel */
-  float select_kernel_ms;
-  uint64_t n_slow; /* bindings that took the exact serial path */
+  float pair_kernel_ms;   /* sum of the pair kernel launches' HIP event times */
+  float select_kernel_ms; /* select kernels after the last pair launch (HIP events) */
+  uint64_t n_slow;        /* bindings that took the exact serial path */
+  uint32_t pair_launches; /* pair kernel launches (chunks) in the batch */
+  uint32_t pad;
 } kp_stage_times;
 
 /* ------------------------------------------------------------------------- */

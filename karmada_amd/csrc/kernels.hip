@@ -115,6 +115,7 @@ int event_create(event_t* e) {
 }
 void event_destroy(event_t e) { (void)hipEventDestroy((hipEvent_t)e); }
 int event_record(event_t e, stream_t s) { return chk(hipEventRecord((hipEvent_t)e, (hipStream_t)s)); }
+int stream_wait(stream_t s, event_t e) { return chk(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)e, 0)); }
 float event_ms(event_t a, event_t b) {
   float ms = 0;
   if (hipEventElapsedTime(&ms, (hipEvent_t)a, (hipEvent_t)b) != hipSuccess) return -1.f;

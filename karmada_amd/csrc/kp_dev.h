@@ -28,6 +28,7 @@ int sync(stream_t s);
 int event_create(event_t* e);
 void event_destroy(event_t e);
 int event_record(event_t e, stream_t s);
+int stream_wait(stream_t s, event_t e);  // s waits for e (no host block)
 float event_ms(event_t a, event_t b);
 
 int alloc(void** p, size_t bytes);

@@ -33,7 +33,7 @@ def test_abi_version_and_struct_sizes():
     # ctypes mirrors must match the C layout (x86-64 SysV)
     assert C.sizeof(api.kp_str) == 16
     assert C.sizeof(api.kp_results) == 64
-    assert C.sizeof(api.kp_stage_times) == 56
+    assert C.sizeof(api.kp_stage_times) == 64
 
 
 def test_engine_create_fails_loudly_without_gpu():
