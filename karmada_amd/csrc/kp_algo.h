@@ -725,7 +725,17 @@ KP_HD inline double w_prio(int64_t v, int64_t k) { return (double)v / (double)(2
 KP_HD inline int64_t w_count(int64_t v, double t, int64_t cap, bool ge) {
   if (v <= 0) return 0;
   double r = (double)v / t;
-  double kf = r < 1.0 ? 0.0 : kp_floor((r - 1.0) * 0.5) + 1.0;
+  const double y = (r - 1.0) * 0.5;
+  double kf = r < 1.0 ? 0.0 : kp_floor(y) + 1.0;
+  // Exact without further divisions when y = (v/t - 1)/2 is far from every
+  // integer: y's error is below r*2^-51, and fl(v/(2k+1)) can only compare
+  // with t differently from the real v/(2k+1) when v/t lies within a relative
+  // 2^-52 of 2k+1 (|y - k| < r*2^-52). Outside tol = r*2^-44 neither happens,
+  // so the count is floor(y)+1 for >= and > alike.
+  if (r >= 1.0) {
+    const double fr = y - kp_floor(y), tol = r * 0x1p-44;
+    if (fr > tol && fr < 1.0 - tol) return kf > (double)cap ? cap : (int64_t)kf;
+  }
   int64_t k = kf > (double)cap ? cap : (int64_t)kf;
   while (k > 0) {
     double p = w_prio(v, k - 1);

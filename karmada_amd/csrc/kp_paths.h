@@ -59,6 +59,12 @@ struct LdsCands {  // candidates compacted in LDS (gather)
   KP_FI void each(Fn fn) const {
     for (int i = tid; i < cd->F; i += nth) fn(c_rank(*cd, i), cd->v[i]);
   }
+  // v := fn(rank, v) for every candidate the thread owns (same order as each).
+  template <class Fn>
+  KP_FI void each_set(Fn fn) const {
+    for (int i = tid; i < cd->F; i += nth) cd->v[i] = fn(c_rank(*cd, i), cd->v[i]);
+  }
+  static constexpr bool kSettable = true;
   // Position key of a candidate in the sort.Sort input (sortClusters order).
   KP_FI uint64_t okey(const SelCtx& x, uint32_t rk, int32_t v0) const { return cand_order_key(x, rk, v0); }
   static constexpr bool kExact = false;  // okey is sort.Sort's output order only for <= 12 (stable insertion)
@@ -76,6 +82,7 @@ KP_UNROLL
   }
   KP_FI uint64_t okey(const SelCtx& x, uint32_t rk, int32_t v0) const { return cand_order_key(x, rk, v0); }
   static constexpr bool kExact = false;
+  static constexpr bool kSettable = false;
 };
 
 // Gathered candidates (any memory) whose sort.Sort output order is known:
@@ -88,6 +95,11 @@ struct PosCands {
   KP_FI void each(Fn fn) const {
     for (int i = tid; i < cd->F; i += nth) fn(c_rank(*cd, i), cd->v[i]);
   }
+  template <class Fn>
+  KP_FI void each_set(Fn fn) const {
+    for (int i = tid; i < cd->F; i += nth) cd->v[i] = fn(c_rank(*cd, i), cd->v[i]);
+  }
+  static constexpr bool kSettable = true;
   KP_FI uint64_t okey(const SelCtx&, uint32_t rk, int32_t) const { return (uint64_t)(uint32_t)pos[rk]; }
   static constexpr bool kExact = true;
 };
@@ -114,17 +126,29 @@ struct TgtCands {
     return ~0ull;
   }
   static constexpr bool kExact = false;
+  static constexpr bool kSettable = false;
 };
 
 // Block-parallel emission of per-candidate results. rep(rank, v) gives the
 // replicas of a candidate; `keep_all` emits every candidate (non-workload /
 // EnableEmptyWorkloadPropagation), otherwise only rep > 0 (removeZeroReplicasCluster).
+// Candidate sets that can store a value per candidate (CS::kSettable) keep the
+// replicas from the counting pass, so rep runs once per candidate; the votes
+// are dead after this.
 template <class BLK, class CS, class RepFn>
 KP_FI void emit_each(const BLK& B, const SelCtx& x, const CS& cs, RepFn rep, bool keep_all) {
   int32_t mine = 0;
-  cs.each([&](uint32_t rk, int32_t v) {
-    if (keep_all || rep(rk, v) > 0) mine++;
-  });
+  if constexpr (CS::kSettable) {
+    cs.each_set([&](uint32_t rk, int32_t v) {
+      const int32_t r = rep(rk, v);
+      if (keep_all || r > 0) mine++;
+      return r;
+    });
+  } else {
+    cs.each([&](uint32_t rk, int32_t v) {
+      if (keep_all || rep(rk, v) > 0) mine++;
+    });
+  }
   int32_t tot;
   const int32_t off = B.excl_scan(mine, &tot);
   unsigned long long base = 0;
@@ -138,7 +162,7 @@ KP_FI void emit_each(const BLK& B, const SelCtx& x, const CS& cs, RepFn rep, boo
   }
   uint64_t o = (uint64_t)B.bcast(base) + (uint64_t)off;
   cs.each([&](uint32_t rk, int32_t v) {
-    int32_t r = rep(rk, v);
+    const int32_t r = CS::kSettable ? v : rep(rk, v);
     if (keep_all || r > 0) {
       x.sink.out_idx[o] = x.s->perm[rk];
       x.sink.out_rep[o] = r < 0 ? 0 : r;

@@ -660,18 +660,63 @@ KP_FI int64_t kth_largest_vote(const BLK& B, uint32_t* hist, Parties parties, in
   return (int64_t)prefix;
 }
 
+// Lower bound of the k-th largest vote (votes in [1, 2^31), k <= #votes > 0):
+// one 256-bin histogram over (octave, next 3 bits) and the lower edge of the
+// bin holding the k-th largest. Every vote >= the bound lies in that bin or
+// above it, so the bound also caps how many parties pass it.
+KP_HD inline int vote_bin(uint32_t v) {
+  const int e = 31 - __builtin_clz(v);
+  const uint32_t m = e >= 3 ? (v >> (e - 3)) & 7u : (v << (3 - e)) & 7u;
+  return e * 8 + (int)m;
+}
+KP_HD inline int64_t vote_bin_floor(int b) { return ((int64_t)(8 + (b & 7)) << (b >> 3)) >> 3; }
+template <class BLK, class Parties>
+KP_FI int64_t kth_vote_floor(const BLK& B, uint32_t* hist, Parties parties, int64_t k) {
+  for (int i = B.tid(); i < 256; i += B.nth()) hist[i] = 0;
+  B.sync();
+  parties([&](uint32_t, int64_t v) {
+    if (v > 0) kp_atomic_add(&hist[vote_bin((uint32_t)v)], 1u);
+  });
+  int64_t before;
+  const int bin = B.find_bin(hist, k, &before, true);
+  return vote_bin_floor(bin);
+}
+
+// k-th largest (1-based) of E <= 64 * (waves) u64 keys in LDS by rank counting:
+// the key x with #(> x) < k <= #(>= x). desc = false selects the k-th smallest.
+// Every thread gets the answer (one barrier).
+template <class BLK>
+KP_FI uint64_t rank_select(const BLK& B, const uint64_t* keys, int E, int64_t k, bool largest, uint64_t* slot) {
+  for (int i = B.tid(); i < E; i += B.nth()) {
+    const uint64_t x = keys[i];
+    int64_t before = 0, upto = 0;
+    for (int j = 0; j < E; j++) {
+      const uint64_t y = keys[j];
+      before += largest ? (y > x) : (y < x);
+      upto += y == x ? 1 : 0;
+    }
+    upto += before;
+    if (before < k && k <= upto) *slot = x;  // every writer writes the same value
+  }
+  B.sync();
+  return *slot;
+}
+
 // AllocateWebsterSeats (webstermethod.go:112-161) for parties with int32 votes
 // >= 0 and no initial seats, block-parallel. `parties(fn)` calls fn(rank, votes)
 // for every party the calling thread owns. The N-th largest seat priority
 // t* = max{t : cnt_ge(t) >= N} is bracketed by the divisor-method bounds
 //   V/(2N+P) <= t* < V/(2N-P-1)   (P = parties with votes > 0)
-// verified with exact counts, narrowed by bisection over the double's bit
-// pattern only while more than sc.cap priorities lie in the bracket; the
-// bracketed priorities are then enumerated into LDS and t* is radix-selected.
+// and by t* >= the N-th largest vote >= Lb (every party's first priority is its
+// vote). Parties below Lb take no seat: the rest are compacted into LDS (when
+// they fit) so every later pass walks only them. The bracket is verified with
+// exact counts and bisected over the double's bit pattern until at most 64
+// priorities remain, which are enumerated and rank-selected.
 // Seats strictly above t* are exact per party; the tie group at t* is ordered
 // by (seats asc, name) as the heap's tie-breaker orders it (tie_key).
 template <class BLK, class Parties>
 KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc, const SelScratch& sc) {
+  KP_STAMP_INIT
   WebRes r;
   r.N = N;
   r.desc = desc;
@@ -694,18 +739,43 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     return r;
   }
   r.mode = 2;
-  // Every party's first priority is its vote, so t* >= L = the N-th largest
-  // vote (cnt_ge(L) >= N). Parties with v < L have every priority below t*:
-  // they take no seat and no part in any count below, so the passes skip
-  // their fp64 work. When P >> N this leaves about N parties.
-  KP_STAMP_INIT
-  const int64_t L = P > (int64_t)N ? kth_largest_vote(B, sc.hist, all_parties, (int64_t)N) : 0;
-  KP_STAMPD(sc.dbg, 9);
+  // LDS areas of sc.buf: [0, ecap) enumeration / rank selection, [64, cap) parties
+  const int ecap = sc.cap < 64 ? sc.cap : 64;
+  const int pcap = sc.cap > 64 ? sc.cap - 64 : 0;
+  uint64_t* pl = sc.buf + 64;
+  int64_t Lb = P > (int64_t)N ? kth_vote_floor(B, sc.hist, all_parties, (int64_t)N) : 1;
+  int32_t np = 0;
+  bool compact = false;
+  for (int attempt = 0; attempt < 2 && pcap > 0; attempt++) {
+    int32_t mine = 0;
+    all_parties([&](uint32_t, int64_t v) { mine += v >= Lb ? 1 : 0; });
+    const int32_t pos0 = B.excl_scan(mine, &np);
+    if (np <= pcap) {
+      int32_t pos = pos0;
+      all_parties([&](uint32_t rk, int64_t v) {
+        if (v >= Lb) pl[pos++] = ((uint64_t)rk << 32) | (uint64_t)(uint32_t)v;
+      });
+      B.sync();
+      compact = true;
+      break;
+    }
+    // the octave bin was crowded: the exact N-th largest vote, then retry once
+    if (attempt == 0 && P > (int64_t)N) Lb = kth_largest_vote(B, sc.hist, all_parties, (int64_t)N);
+    else break;
+  }
   auto parties = [&](auto fn) {
-    all_parties([&](uint32_t rk, int64_t v) {
-      if (v >= L) fn(rk, v);
-    });
+    if (compact) {
+      for (int i = B.tid(); i < np; i += B.nth()) {
+        const uint64_t e = pl[i];
+        fn((uint32_t)(e >> 32), (int64_t)(uint32_t)e);
+      }
+    } else {
+      all_parties([&](uint32_t rk, int64_t v) {
+        if (v >= Lb) fn(rk, v);
+      });
+    }
   };
+  KP_STAMPD(sc.dbg, 9);
   const int64_t capN = (int64_t)N;
   auto cnt2 = [&](double ta, double tb, int64_t* ca, int64_t* cb) {
     int64_t a = 0, b = 0;
@@ -731,9 +801,8 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     double h0 = 2 * (int64_t)N - P - 1 > 0 ? (double)V / (double)(2 * (int64_t)N - P - 1) : (double)vmax;
     uint64_t hb = dbits(h0) + 64;
     if (hb > hi) hb = hi;
-    if (L > 0) {  // t* >= L: usually far above the divisor bound when P >> N
-      // (and every count below must be taken at t >= L, where it is exact)
-      const uint64_t lL = dbits((double)L);
+    if (Lb > 1) {  // t* >= Lb (every count below is taken at t >= Lb, where it is exact)
+      const uint64_t lL = dbits((double)Lb);
       if (lL > lb) lb = lL;
       if (hb <= lb) hb = lb + 1;
     }
@@ -750,7 +819,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     if (clo < 0) clo = cnt1(bitsd(lo));
   }
   KP_STAMPD(sc.dbg, 10);
-  while (hi - lo > 1 && clo - chi > (int64_t)sc.cap) {
+  while (hi - lo > 1 && clo - chi > (int64_t)ecap) {
     uint64_t mid = lo + (hi - lo) / 2;
     int64_t c = cnt1(bitsd(mid));
     if (c >= N) {
@@ -766,7 +835,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   if (hi - lo <= 1) {
     tstar = bitsd(lo);
   } else {
-    // enumerate every priority in [lo, hi) and select the (N - chi)-th largest
+    // enumerate the <= 64 priorities in [lo, hi); t* is the (N - chi)-th largest
     const double tl = bitsd(lo), th = bitsd(hi);
     int32_t mine = 0;
     parties([&](uint32_t, int64_t v) {
@@ -779,10 +848,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
       for (int64_t k = k0; k < k1; k++) sc.buf[pos++] = dbits(w_prio(v, k));
     });
     B.sync();
-    const int64_t kth_small = (int64_t)E - ((int64_t)N - chi) + 1;
-    auto all = [&](int) { return true; };
-    auto key = [&](int i) { return (uint64_t)sc.buf[i]; };
-    tstar = bitsd(radix_select(B, sc.hist, E, all, key, kth_small));
+    tstar = bitsd(rank_select(B, sc.buf, E, (int64_t)N - chi, true, (uint64_t*)sc.whist));
   }
   r.t = tstar;
   KP_STAMPD(sc.dbg, 12);
@@ -798,7 +864,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   KP_STAMPD(sc.dbg, 13);
   if (M >= T) {
     r.tie = ~0ull;
-  } else if (T <= (int64_t)sc.cap) {
+  } else if (T <= (int64_t)ecap) {
     int32_t mine = 0;
     parties([&](uint32_t, int64_t v) {
       int64_t base = w_count(v, tstar, (int64_t)N + 1, false);
@@ -811,9 +877,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
       if (w_prio(v, base) == tstar) sc.buf[pos++] = tie_key(base, rk, desc);
     });
     B.sync();
-    auto all = [&](int) { return true; };
-    auto key = [&](int i) { return (uint64_t)sc.buf[i]; };
-    r.tie = radix_select(B, sc.hist, n, all, key, M);
+    r.tie = rank_select(B, sc.buf, n, M, false, (uint64_t*)sc.whist);
   } else {
     uint64_t tlo = 0, thi = (uint64_t)1 << 62;  // smallest x with count(tk <= x) >= M
     while (tlo < thi) {
@@ -830,6 +894,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     r.tie = tlo;
   }
   KP_STAMPD(sc.dbg, 14);
+  B.sync();  // pl / buf / whist are free again for the caller
   return r;
 }
 

@@ -45,7 +45,7 @@ def sim_webster(votes, N, desc, ecap):
 
 def vote_sets(rng):
     for _ in range(60):
-        n = rng.choice([1, 2, 3, 7, 12, 13, 50, 200, 700])
+        n = rng.choice([1, 2, 3, 7, 12, 13, 50, 200, 700, 3000])
         kind = rng.choice(["uniform", "ties", "zeros", "huge", "powers", "one-big"])
         if kind == "uniform":
             v = [rng.randint(0, 1000) for _ in range(n)]
@@ -72,7 +72,9 @@ def test_webster_par_matches_reference_heap(seed):
         N = rng.choice([1, 2, 5, 17, 100, 999, 4000, 65536])
         desc = rng.random() < 0.5
         want = oracle_webster(votes, N, desc)
-        for ecap in (0, 4, 64, 4096):
+        # 0: bisection only; 4: no party compaction; 256: compaction that
+        # overflows on crowded votes (exact N-th largest, retry); 4096: compaction
+        for ecap in (0, 4, 64, 256, 4096):
             got = sim_webster(votes, N, desc, ecap)
             assert got == want, (votes[:20], N, desc, ecap)
 
