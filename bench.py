@@ -20,7 +20,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
-L2_PEAK_GBS = 34500.0  # aggregate of the 8 per-XCD L2s, measured (MI355X_MICROARCH.md, L2)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 instruction per 2 cycles per SIMD
+# at 2.4 GHz (MI355X_MICROARCH.md, "issues each VALU instruction over 2 cycles")
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # 1228.8 G wave-instructions/s
 # SURVEY.md §8(d) streamed-row model, config 3: B_row = 140 filter + 52 summary + 192 grades
 B_ROW = {2: 184, 3: 384, 4: 192, 5: 384, 6: 384, 1: 184}
 B_BIND = 256
@@ -66,14 +68,15 @@ def cpu_baseline(u, opts, budget_s):
 
 
 def load_traffic(config):
-    """Per-launch HBM bytes of the pair kernel from the committed PMC profile, if any."""
+    """Per-launch PMC figures of the pair kernel from the committed profile, if any:
+    (HBM bytes = FETCH_SIZE + WRITE_SIZE, VALU wave-instructions)."""
     p = os.path.join(ROOT, "profiles", f"traffic_config{config}.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get("k_pair_bytes_per_launch")
+        return d.get("k_pair_bytes_per_launch"), d.get("k_pair_valu_per_launch")
     except (OSError, ValueError):
-        return None
+        return None, None
 
 
 def main():
@@ -116,7 +119,12 @@ def main():
     opts = api.options()
     eng = Engine(local, lib_path=os.path.join(ROOT, args.lib)) if args.lib else Engine(local)
     t0 = time.perf_counter()
-    snap = Snapshot.from_structs(eng, u.clusters, u.n_clusters, u.names, opts)
+    if dist is None:
+        snap = Snapshot.from_structs(eng, u.clusters, u.n_clusters, u.names, opts)
+    else:  # rank 0 packs once; the packed bytes go to every rank over RCCL (dist.py)
+        from karmada_amd.dist import broadcast_snapshot
+        snap = Snapshot.from_structs(eng, u.clusters, u.n_clusters, u.names, opts) if rank == 0 else None
+        snap = broadcast_snapshot(eng, snap, u.names)
     snap_s = time.perf_counter() - t0
     t0 = time.perf_counter()
     batch = Batch(snap, structs=u.binding_slice(0, u.n_bindings))
@@ -144,18 +152,25 @@ def main():
     barrier_sync()
     elapsed = time.perf_counter() - t0
     n_ok = sum(1 for i in range(r.n_bindings) if r.status[i] == 0)
+    n_targets = int(r.n_targets)
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # per-rank result counts, all-gathered (after the timed region)
+        c = torch.tensor([n_ok, n_targets], dtype=torch.int64, device=f"cuda:{local}")
+        parts = [torch.zeros_like(c) for _ in range(world)]
+        dist.all_gather(parts, c)
+        n_ok = int(sum(p[0].item() for p in parts))
+        n_targets = int(sum(p[1].item() for p in parts))
 
     ms_per_step = 1e3 * elapsed / args.steps
     value = (B * world) / (elapsed / args.steps)
     avg_pair_ms = sum(pair_ms) / len(pair_ms)  # all pair launches of one step
     achieved = pair_bytes_per_binding(cfg, C_) * B / (avg_pair_ms * 1e-3) / 1e9
     launch_ms = avg_pair_ms / launches
-    traffic = load_traffic(cfg)
+    traffic, valu = load_traffic(cfg)
     line = {
         "metric": "ResourceBindings scheduled/sec at 100k bindings x 5k clusters",
         "value": round(value, 1),
@@ -176,16 +191,19 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "k_pair_fast", "kernel_ms": round(launch_ms, 4), "launches_per_step": launches,
-                     # The packed snapshot (~2 MB at config 3) stays resident in every XCD's
-                     # 4 MiB L2, so the streamed-row bytes are served by L2, not HBM: the
-                     # HBM fraction above exceeds 1 and the L2 fraction is the binding one.
-                     "l2": {"achieved": round(achieved, 1), "peak": L2_PEAK_GBS, "unit": "GB/s",
-                            "frac": round(achieved / L2_PEAK_GBS, 4)}},
+                     # SURVEY §8(d) streamed-row model: every binding re-reads every cluster
+                     # row. The packed snapshot (~2 MB) stays in each XCD's L2, so that
+                     # exceeds HBM peak; what bounds the kernel is instruction issue:
+                     "dram_gbs": round(traffic / (launch_ms * 1e-3) / 1e9, 1) if traffic else None,
+                     "valu": ({"achieved": round(valu / (launch_ms * 1e-3) / 1e9, 1), "peak": VALU_PEAK_GINST,
+                               "unit": "G wave-inst/s", "frac": round(valu / (launch_ms * 1e-3) / 1e9 / VALU_PEAK_GINST, 4)}
+                              if valu else None)},
         "stages_ms": {"pair_kernel": round(avg_pair_ms, 3), "select_kernels": round(sum(sel_ms) / len(sel_ms), 3),
                       "host_region": round(sum(host_ms) / len(host_ms), 3)},
         "setup_s": {"generate": round(gen_s, 2), "snapshot_pack_upload": round(snap_s, 3),
                     "binding_pack_upload": round(pack_s, 3)},
         "scheduled_ok": n_ok,
+        "result_targets": n_targets,
         "slow_path_bindings": n_slow,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -131,6 +131,45 @@ struct GpuBlk {
       y = opb(y, a[16 + w]);
     }
   }
+  // Four reductions for one barrier.
+  template <class OpA, class OpB, class OpC, class OpD>
+  KP_INLINE void reduce4(int64_t& x, OpA opa, int64_t ida, int64_t& y, OpB opb, int64_t idb, int64_t& z, OpC opc,
+                         int64_t idc, int64_t& u, OpD opd, int64_t idd) const {
+    x = wave_reduce(x, opa, ida);
+    y = wave_reduce(y, opb, idb);
+    z = wave_reduce(z, opc, idc);
+    u = wave_reduce(u, opd, idd);
+    int64_t* a = area();
+    if (lane() == 0) {
+      a[wid()] = x;
+      a[16 + wid()] = y;
+      a[32 + wid()] = z;
+      a[48 + wid()] = u;
+    }
+    sync();
+    x = a[0];
+    y = a[16];
+    z = a[32];
+    u = a[48];
+    for (int w = 1; w < nwaves(); w++) {
+      x = opa(x, a[w]);
+      y = opb(y, a[16 + w]);
+      z = opc(z, a[32 + w]);
+      u = opd(u, a[48 + w]);
+    }
+  }
+  // This thread's slot base for `mine` entries in a list filled by every wave
+  // independently: the wave reserves its total with one LDS atomic on *ctr
+  // (zeroed beforehand, behind a barrier). No barrier; slot order across
+  // waves is not deterministic, within a wave it follows the lanes.
+  KP_INLINE int32_t wave_reserve(int32_t mine, uint32_t* ctr) const {
+    const int32_t incl = wave_incl_scan(mine);
+    const int32_t tot = kp_readlane(incl, 63);
+    int32_t base = 0;
+    if (lane() == 63 && tot > 0) base = (int32_t)atomicAdd(ctr, (uint32_t)tot);
+    base = kp_readlane(base, 63);
+    return base + incl - mine;
+  }
   KP_INLINE int64_t sum64(int64_t v) const { return reduce(v, [](int64_t a, int64_t b) { return a + b; }, (int64_t)0); }
   KP_INLINE uint64_t minu64(uint64_t v) const {
     return reduce(v, [](uint64_t a, uint64_t b) { return a < b ? a : b; }, (uint64_t)~0ull);
@@ -257,6 +296,13 @@ struct CpuBlk {
   int64_t sum64(int64_t v) const { return v; }
   template <class OpA, class OpB>
   void reduce2(int64_t&, OpA, int64_t, int64_t&, OpB, int64_t) const {}
+  template <class OpA, class OpB, class OpC, class OpD>
+  void reduce4(int64_t&, OpA, int64_t, int64_t&, OpB, int64_t, int64_t&, OpC, int64_t, int64_t&, OpD, int64_t) const {}
+  int32_t wave_reserve(int32_t mine, uint32_t* ctr) const {
+    const int32_t b = (int32_t)*ctr;
+    *ctr += (uint32_t)mine;
+    return b;
+  }
   void sum2(int64_t&, int64_t&) const {}
   void maxsum(int64_t&, int64_t&) const {}
   void andor(uint64_t&, uint64_t&) const {}

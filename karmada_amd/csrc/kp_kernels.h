@@ -198,11 +198,10 @@ KP_FI void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
   SelScratch ss = carve_sel_scratch((unsigned char*)(cd.v + a.s.Cp), a.s.Cp);
   ss.dbg = a.dbg;
   const BindHdr* h = &a.bv.hdr[b];
-  build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
   SelCtx x = make_ctx(a, b, tgt);
   KP_STAMP(x, 0);
   const bool weights = h->strategy == ST_STATIC && h->sel == SEL_ALL;
-  cd.F = gather(B, x, cd, weights);
+  cd.F = gather(B, x, cd, weights, [&] { build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2); });
   KP_STAMP(x, 1);
   LdsCands cs{&cd, B.tid(), B.nth()};
   select_all_common(B, a, x, cs, cd.F, ss);

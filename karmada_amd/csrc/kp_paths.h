@@ -205,6 +205,14 @@ KP_HD inline bool scale_down_targets(const SelCtx& x, unsigned char* mem, size_t
   return true;
 }
 
+// divide_par's reductions over the candidate votes, when the caller already took
+// them in its own pass: |votes|, min, total, count, and over the targets with
+// scheduled replicas > 0 (the prior clusters, if merging) their sum and count.
+struct DivSums {
+  int64_t sabs = 0, vmin = 0, vtot = 0, nparty = 0, sp = 0, np = 0;
+  bool valid = false;
+};
+
 // ----------------------------------------------------------------------------
 // SEL_ALL: every feasible cluster is selected (select_clusters.go:29-32) and
 // AssignReplicas runs block-parallel over the candidate set `cs` (F members).
@@ -257,17 +265,44 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
   }
   // Dynamic / Aggregated (assignment.go:213-244)
   // GetSumOfReplicas(scheduledClusters) wraps in int32; the int64 sum taken
-  // mod 2^32 is the same value.
+  // mod 2^32 is the same value. One pass also takes divide_par's vote sums
+  // for the fresh / scale-up modes (the vote formula depends only on
+  // BF_FRESH; the prior-cluster sum is 0 unless some prior has replicas).
+  const bool fresh = (h.flags & BF_FRESH) != 0;
+  auto tgt = [&](uint32_t rk) { return h.tgt_cnt > 0 && bit_test(x.tgt_bits, (int)rk); };
   int64_t asum = 0, apos = 0;
   TgtCands{&x, B.tid(), B.nth()}.each([&](uint32_t, int32_t v) {
     asum += v;
     apos |= v > 0 ? 1 : 0;
   });
-  B.reduce2(asum, [](int64_t p, int64_t q) { return p + q; }, (int64_t)0, apos,
-            [](int64_t p, int64_t q) { return p | q; }, (int64_t)0);
+  DivSums ds;
+  cs.each([&](uint32_t rk, int32_t v0) {
+    int32_t v32 = v0;
+    bool pr = false;
+    if (tgt(rk)) {
+      const int32_t sr = sched_rep_of(x, rk);
+      if (fresh) v32 = add32(v32, sr);
+      pr = sr > 0;
+    }
+    const int64_t v = v32;
+    ds.sabs += v < 0 ? -v : v;
+    if (v < ds.vmin) ds.vmin = v;
+    ds.vtot += v;
+    ds.nparty++;
+    if (pr) {
+      ds.sp += v;
+      ds.np++;
+    }
+  });
+  {
+    auto add = [](int64_t p, int64_t q) { return p + q; };
+    B.reduce4(asum, add, 0, apos, [](int64_t p, int64_t q) { return p | q; }, 0, ds.sabs, add, 0, ds.vtot, add, 0);
+    B.reduce4(ds.vmin, [](int64_t p, int64_t q) { return p < q ? p : q; }, 0, ds.nparty, add, 0, ds.sp, add, 0, ds.np,
+              add, 0);
+  }
+  ds.valid = true;
   const int32_t assigned = wrap32(asum);
   const bool anyPriorPos = apos != 0;
-  const bool fresh = (h.flags & BF_FRESH) != 0;
   int mode;  // 0 fresh, 1 scale up, 2 unchanged, 3 scale down
   if (fresh) mode = 0;
   else if (assigned > h.replicas) mode = 3;
@@ -278,15 +313,13 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
     TgtCands tc{&x, B.tid(), B.nth()};
     return divide_par(B, x, tc, h.replicas, false, false, false, KP_ERR_SCALE_DOWN_NOT_ENOUGH, ss);
   }
-  // spec.Clusters membership of a candidate (candidates are feasible)
-  auto tgt = [&](uint32_t rk) { return h.tgt_cnt > 0 && bit_test(x.tgt_bits, (int)rk); };
   if (mode == 2) {  // unchanged: scheduledClusters, removeZero
     emit_each(B, x, cs, [&](uint32_t rk, int32_t) { return tgt(rk) ? sched_rep_of(x, rk) : (int32_t)0; }, prop);
     return SLOW_NONE;
   }
   const int32_t target = mode == 0 ? h.replicas : sub32(h.replicas, assigned);
   return divide_par(B, x, cs, target, mode == 0, mode == 1, anyPriorPos,
-                    mode == 0 ? KP_ERR_FRESH_NOT_ENOUGH : KP_ERR_SCALE_UP_NOT_ENOUGH, ss);
+                    mode == 0 ? KP_ERR_FRESH_NOT_ENOUGH : KP_ERR_SCALE_UP_NOT_ENOUGH, ss, &ds);
 }
 
 // dynamicDivideReplicas (division_algorithm.go:75-101) for DynamicWeight and
@@ -295,7 +328,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
 // (SpreadReplicasByTargetClusters) and MergeTargetClusters (scale-up).
 template <class BLK, class CS>
 KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target, bool fresh, bool merge,
-                     bool anyPriorPos, int not_enough, const SelScratch& ss) {
+                     bool anyPriorPos, int not_enough, const SelScratch& ss, const DivSums* pre = nullptr) {
   KP_STAMP_INIT
   const BindHdr& h = *x.h;
   const int st = h.strategy;
@@ -307,16 +340,23 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
     return v;
   };
   int64_t sabs = 0, vmin = 0, vtot = 0, nparty = 0;
-  cs.each([&](uint32_t rk, int32_t v0) {
-    int64_t v = vote32(rk, v0);
-    sabs += v < 0 ? -v : v;
-    if (v < vmin) vmin = v;
-    vtot += v;
-    nparty++;
-  });
-  B.sum2(sabs, vtot);
-  B.reduce2(vmin, [](int64_t p, int64_t q) { return p < q ? p : q; }, (int64_t)0, nparty,
-            [](int64_t p, int64_t q) { return p + q; }, (int64_t)0);
+  if (pre) {
+    sabs = pre->sabs;
+    vmin = pre->vmin;
+    vtot = pre->vtot;
+    nparty = pre->nparty;
+  } else {
+    cs.each([&](uint32_t rk, int32_t v0) {
+      int64_t v = vote32(rk, v0);
+      sabs += v < 0 ? -v : v;
+      if (v < vmin) vmin = v;
+      vtot += v;
+      nparty++;
+    });
+    B.sum2(sabs, vtot);
+    B.reduce2(vmin, [](int64_t p, int64_t q) { return p < q ? p : q; }, (int64_t)0, nparty,
+              [](int64_t p, int64_t q) { return p + q; }, (int64_t)0);
+  }
   if (vmin < 0 || sabs >= (int64_t)kInt32Max) return SLOW_WRAP;  // int32 wrap hazard
   KP_STAMP(x, 2);
   if ((int32_t)vtot < target) {
@@ -332,13 +372,18 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
   uint64_t tieCut = 0;  // straddle: tie-group members with okey <= tieCut are taken
   if (st == ST_AGGREGATED) {
     int64_t SP = 0, nP = 0;
-    cs.each([&](uint32_t rk, int32_t v0) {
-      if (prior(rk)) {
-        SP += vote32(rk, v0);
-        nP++;
-      }
-    });
-    B.sum2(SP, nP);
+    if (pre) {  // prior = merge && anyPriorPos && (target with replicas > 0)
+      SP = merge && anyPriorPos ? pre->sp : 0;
+      nP = merge && anyPriorPos ? pre->np : 0;
+    } else {
+      cs.each([&](uint32_t rk, int32_t v0) {
+        if (prior(rk)) {
+          SP += vote32(rk, v0);
+          nP++;
+        }
+      });
+      B.sum2(SP, nP);
+    }
     xIsPrior = nP > 0 && SP >= target;
     const int64_t tX = xIsPrior ? (int64_t)target : (int64_t)target - SP;
     auto xvals = [&](auto fn) {

@@ -538,8 +538,11 @@ KP_HD inline int32_t static_vote(const SelCtx& x, int c) {
 struct alignas(16) I32x4 {
   int32_t v[4];
 };
-template <class BLK>
-KP_FI int gather(const BLK& B, const SelCtx& x, Cands cd, bool weights) {
+// `between()` runs after the vector form has issued its row loads and before it
+// uses them (block-uniform; it may contain barriers), so independent setup
+// work overlaps the row's memory latency.
+template <class BLK, class Between>
+KP_FI int gather(const BLK& B, const SelCtx& x, Cands cd, bool weights, Between between) {
   // Vector form (no overflow tiers, AllocatableReplicas votes): thread t owns
   // the 4-cluster units t + nth*j and issues every 16-B row load before the
   // first use, so a binding's row costs one memory latency, not one per unit.
@@ -558,6 +561,7 @@ KP_UNROLL
       if (fm[j]) ev[j] = e4[u];
       mine += popc64(fm[j]);
     }
+    between();
     int32_t F;
     int32_t pos = B.excl_scan(mine, &F);
 KP_UNROLL
@@ -575,6 +579,7 @@ KP_UNROLL
   // is a broadcast load per wave), one scan places them, and the second pass
   // reads erow fully coalesced with no barrier between iterations. Candidate
   // order is thread-major; nothing downstream depends on it (keys carry ranks).
+  between();
   const SnapView& s = *x.s;
   const BindHdr& h = *x.h;
   const int tid = B.tid(), nth = B.nth();
@@ -590,6 +595,11 @@ KP_UNROLL
     }
   B.sync();
   return F;
+}
+
+template <class BLK>
+KP_FI int gather(const BLK& B, const SelCtx& x, Cands cd, bool weights) {
+  return gather(B, x, cd, weights, [] {});
 }
 
 // ----------------------------------------------------------------------------
@@ -660,27 +670,14 @@ KP_FI int64_t kth_largest_vote(const BLK& B, uint32_t* hist, Parties parties, in
   return (int64_t)prefix;
 }
 
-// Lower bound of the k-th largest vote (votes in [1, 2^31), k <= #votes > 0):
-// one 256-bin histogram over (octave, next 3 bits) and the lower edge of the
-// bin holding the k-th largest. Every vote >= the bound lies in that bin or
-// above it, so the bound also caps how many parties pass it.
+// Octave bins of a vote in [1, 2^31): (floor(log2 v), next 3 bits), monotone
+// in v; vote_bin_floor(b) is the smallest vote in bin b.
 KP_HD inline int vote_bin(uint32_t v) {
   const int e = 31 - __builtin_clz(v);
   const uint32_t m = e >= 3 ? (v >> (e - 3)) & 7u : (v << (3 - e)) & 7u;
   return e * 8 + (int)m;
 }
 KP_HD inline int64_t vote_bin_floor(int b) { return ((int64_t)(8 + (b & 7)) << (b >> 3)) >> 3; }
-template <class BLK, class Parties>
-KP_FI int64_t kth_vote_floor(const BLK& B, uint32_t* hist, Parties parties, int64_t k) {
-  for (int i = B.tid(); i < 256; i += B.nth()) hist[i] = 0;
-  B.sync();
-  parties([&](uint32_t, int64_t v) {
-    if (v > 0) kp_atomic_add(&hist[vote_bin((uint32_t)v)], 1u);
-  });
-  int64_t before;
-  const int bin = B.find_bin(hist, k, &before, true);
-  return vote_bin_floor(bin);
-}
 
 // k-th largest (1-based) of E <= 64 * (waves) u64 keys in LDS by rank counting:
 // the key x with #(> x) < k <= #(>= x). desc = false selects the k-th smallest.
@@ -722,14 +719,24 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   r.desc = desc;
   r.t = 0;
   r.tie = 0;
-  int64_t V = 0, vmax = 0, P = 0;
+  // One pass: totals and the octave histogram of the votes (kth_vote_floor).
+  uint32_t* ctr = (uint32_t*)sc.whist + 511;  // party list fill counter
+  for (int i = B.tid(); i < 256; i += B.nth()) sc.hist[i] = 0;
+  if (B.tid() == 0) *ctr = 0;
+  B.sync();
+  int64_t V = 0, vmax = 0, P = 0, none = 0;
   all_parties([&](uint32_t, int64_t v) {
     V += v;
     if (v > vmax) vmax = v;
-    if (v > 0) P++;
+    if (v > 0) {
+      P++;
+      kp_atomic_add(&sc.hist[vote_bin((uint32_t)v)], 1u);
+    }
   });
-  B.sum2(V, P);
-  vmax = B.max64(vmax);
+  {
+    auto add = [](int64_t p, int64_t q) { return p + q; };
+    B.reduce4(V, add, 0, P, add, 0, vmax, [](int64_t p, int64_t q) { return p > q ? p : q; }, INT64_MIN, none, add, 0);
+  }
   if (V == 0) {
     r.mode = 0;
     return r;
@@ -743,25 +750,38 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   const int ecap = sc.cap < 64 ? sc.cap : 64;
   const int pcap = sc.cap > 64 ? sc.cap - 64 : 0;
   uint64_t* pl = sc.buf + 64;
-  int64_t Lb = P > (int64_t)N ? kth_vote_floor(B, sc.hist, all_parties, (int64_t)N) : 1;
+  int64_t Lb = 1;
+  if (P > (int64_t)N) {  // lower edge of the octave bin holding the N-th largest vote
+    int64_t before;
+    Lb = vote_bin_floor(B.find_bin(sc.hist, (int64_t)N, &before, true));
+  }
   int32_t np = 0;
   bool compact = false;
   for (int attempt = 0; attempt < 2 && pcap > 0; attempt++) {
+    // parties with v >= Lb into pl: per-wave slot reservation, one barrier
     int32_t mine = 0;
     all_parties([&](uint32_t, int64_t v) { mine += v >= Lb ? 1 : 0; });
-    const int32_t pos0 = B.excl_scan(mine, &np);
+    int32_t pos = B.wave_reserve(mine, ctr);
+    all_parties([&](uint32_t rk, int64_t v) {
+      if (v >= Lb) {
+        if (pos < pcap) pl[pos] = ((uint64_t)rk << 32) | (uint64_t)(uint32_t)v;
+        pos++;
+      }
+    });
+    B.sync();
+    np = (int32_t)*ctr;
     if (np <= pcap) {
-      int32_t pos = pos0;
-      all_parties([&](uint32_t rk, int64_t v) {
-        if (v >= Lb) pl[pos++] = ((uint64_t)rk << 32) | (uint64_t)(uint32_t)v;
-      });
-      B.sync();
       compact = true;
       break;
     }
     // the octave bin was crowded: the exact N-th largest vote, then retry once
-    if (attempt == 0 && P > (int64_t)N) Lb = kth_largest_vote(B, sc.hist, all_parties, (int64_t)N);
-    else break;
+    if (attempt == 0 && P > (int64_t)N) {
+      Lb = kth_largest_vote(B, sc.hist, all_parties, (int64_t)N);  // (barriers: every thread read ctr)
+      if (B.tid() == 0) *ctr = 0;
+      B.sync();
+    } else {
+      break;
+    }
   }
   auto parties = [&](auto fn) {
     if (compact) {

@@ -48,11 +48,15 @@ def main():
         res[k] = e
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1, sort_keys=True)
-    if traffic_path and "k_pair" in res and "hbm_bytes_per_launch" in res["k_pair"]:
+    kp = "k_pair_fast" if "k_pair_fast" in res else "k_pair"
+    if traffic_path and kp in res and "hbm_bytes_per_launch" in res[kp]:
         with open(traffic_path, "w") as fh:
-            json.dump({"k_pair_bytes_per_launch": res["k_pair"]["hbm_bytes_per_launch"],
+            json.dump({"k_pair_bytes_per_launch": res[kp]["hbm_bytes_per_launch"],
+                       "k_pair_valu_per_launch": res[kp].get("SQ_INSTS_VALU"),
+                       "kernel": kp,
                        "source": os.path.basename(out),
-                       "note": "FETCH_SIZE+WRITE_SIZE per k_pair launch, rocprofv3 separate --pmc passes"}, fh, indent=1)
+                       "note": "FETCH_SIZE+WRITE_SIZE and SQ_INSTS_VALU per pair-kernel launch, "
+                               "rocprofv3 separate --pmc passes"}, fh, indent=1)
     print(json.dumps({k: {kk: v for kk, v in e.items() if not kk.startswith("SQ_")} for k, e in res.items()}, indent=1))
 
 
