@@ -133,6 +133,16 @@ int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const Sele
   return 0;
 }
 
+int region_groups(stream_t, const RegionOut* rout, const int32_t* rstat, const BindHdr* hdr, const int32_t* list,
+                  int n, int R, int32_t* rsel, int32_t* rnsel, uint32_t* nhost) {
+  for (int j = 0; j < n; j++) {
+    const int32_t k = region_groups_one(rout + (size_t)j * R, rstat[j], hdr[list[j]], R, rsel + (size_t)j * R);
+    if (k == kGroupsHost) ++*nhost;
+    rnsel[j] = k;
+  }
+  return 0;
+}
+
 int compact(stream_t, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
             const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n) {
   int64_t red[8];
@@ -183,6 +193,16 @@ int64_t kpsim_wsel_max(const int32_t* vals, int n, int64_t target) {
     for (int i = 0; i < n; i++) fn((int64_t)vals[i]);
   };
   return wsel_max(B, wh.data(), vs, target);
+}
+
+// select_groups_dev over n regions (ids 0..n-1 in name order; value = #clusters,
+// 0 = region absent; weight = group score). Returns the count or -KP_ERR_*.
+int kpsim_select_groups(const int32_t* values, const int64_t* weights, int n, int64_t min_c, int64_t max_c,
+                        int64_t target, int32_t* out) {
+  using namespace kp;
+  std::vector<RegionOut> ro(n);
+  for (int r = 0; r < n; r++) ro[r] = RegionOut{values[r], 0, weights[r]};
+  return select_groups_dev(ro.data(), n, min_c, max_c, target, out);
 }
 
 // Go sort.Sort over (name, rep)[0, n): mode 0 = the serial emulation

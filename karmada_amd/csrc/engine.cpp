@@ -155,6 +155,7 @@ struct kp_batch {
   int32_t* crep_d = nullptr;
   RegionOut* rout = nullptr;
   int32_t *rstat = nullptr, *rsel = nullptr, *rnsel = nullptr;
+  uint32_t* nhost = nullptr;  // region bindings the device group search left to the host
   unsigned char* slow_scratch = nullptr;
   size_t slow_slot = 0;
   int slow_grid = 0, slow_cap = 0, slow_lds = 0, slow_sort = 0;
@@ -1407,6 +1408,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->rstat, std::max(1, nr));
   a.add(&bt->rsel, (size_t)std::max(1, nr) * R);
   a.add(&bt->rnsel, std::max(1, nr));
+  a.add(&bt->nhost, 1);
   a.add(&bt->slow_scratch, bt->slow_slot * bt->slow_grid);
   HIPCHK(a.alloc());
   auto up = [&](void* d, const void* h, size_t bytes) {
@@ -1539,41 +1541,61 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     k.list = bt->d_region;
     k.n = nr;
     HIPCHK(dev::select(st, SEL_LAUNCH_REGION_A, k, smem_region_a(s), cap, sx));
-    bt->h_rout.resize((size_t)nr * std::max(R, 1));
-    bt->h_rstat.resize(nr);
-    HIPCHK(dev::d2h(bt->h_rout.data(), bt->rout, sizeof(RegionOut) * bt->h_rout.size(), st));
-    HIPCHK(dev::d2h(bt->h_rstat.data(), bt->rstat, 4 * nr, st));
-    HIPCHK(dev::sync(st));
-    th0 = now_ms();
-    bt->h_rsel.assign((size_t)nr * std::max(R, 1), -1);
-    bt->h_rnsel.assign(nr, 0);
-    parallel_for(nr, e->n_threads, [&](int j) {
-      if (bt->h_rstat[j] != 0) {
-        bt->h_rnsel[j] = -1000;
-        return;
+    // selectGroups: on the device (one thread per binding) unless the snapshot
+    // has more regions than its arrays hold; bindings whose DFS exceeds the node
+    // budget, and every binding on the other route, take the host DFS.
+    const bool dev_groups = R <= kGroupMax && !getenv("KP_REGION_HOST");
+    uint32_t nh = 0;
+    if (dev_groups) {
+      HIPCHK(dev::fill(bt->nhost, 0, 4, st));
+      HIPCHK(dev::region_groups(st, bt->rout, bt->rstat, bt->view.hdr, bt->d_region, nr, R, bt->rsel, bt->rnsel,
+                                bt->nhost));
+      HIPCHK(dev::d2h(&nh, bt->nhost, 4, st));
+      HIPCHK(dev::sync(st));
+    }
+    if (!dev_groups || nh > 0) {
+      bt->h_rout.resize((size_t)nr * std::max(R, 1));
+      bt->h_rstat.resize(nr);
+      HIPCHK(dev::d2h(bt->h_rout.data(), bt->rout, sizeof(RegionOut) * bt->h_rout.size(), st));
+      HIPCHK(dev::d2h(bt->h_rstat.data(), bt->rstat, 4 * nr, st));
+      bt->h_rsel.assign((size_t)nr * std::max(R, 1), -1);
+      bt->h_rnsel.assign(nr, 0);
+      if (dev_groups) {
+        HIPCHK(dev::d2h(bt->h_rsel.data(), bt->rsel, 4 * bt->h_rsel.size(), st));
+        HIPCHK(dev::d2h(bt->h_rnsel.data(), bt->rnsel, 4 * nr, st));
       }
-      const BindHdr& h = bt->hdr[bt->l_region[j]];
-      std::vector<G> groups;
-      for (int r = 0; r < R; r++) {
-        const RegionOut& ro = bt->h_rout[(size_t)j * R + r];
-        if (ro.count > 0) groups.push_back({r, ro.count, ro.score});
-      }
-      // selectBestClustersByRegion (select_clusters_by_region.go:25-40)
-      if ((int64_t)groups.size() < h.region_min) {
-        bt->h_rnsel[j] = -KP_ERR_REGION_MIN_GROUPS;
-        return;
-      }
-      auto sel = select_groups(groups, h.region_min, h.region_max, h.cluster_min);
-      if (sel.empty()) {
-        bt->h_rnsel[j] = -KP_ERR_REGION_CLUSTER_MIN;
-        return;
-      }
-      for (size_t q = 0; q < sel.size(); q++) bt->h_rsel[(size_t)j * R + q] = sel[q];
-      bt->h_rnsel[j] = (int32_t)sel.size();
-    });
-    th1 = now_ms();
-    HIPCHK(dev::h2d(bt->rsel, bt->h_rsel.data(), 4 * bt->h_rsel.size(), st));
-    HIPCHK(dev::h2d(bt->rnsel, bt->h_rnsel.data(), 4 * nr, st));
+      HIPCHK(dev::sync(st));
+      th0 = now_ms();
+      parallel_for(nr, e->n_threads, [&](int j) {
+        if (dev_groups && bt->h_rnsel[j] != kGroupsHost) return;
+        if (bt->h_rstat[j] != 0) {
+          bt->h_rnsel[j] = -1000;
+          return;
+        }
+        const BindHdr& h = bt->hdr[bt->l_region[j]];
+        std::vector<G> groups;
+        for (int r = 0; r < R; r++) {
+          const RegionOut& ro = bt->h_rout[(size_t)j * R + r];
+          if (ro.count > 0) groups.push_back({r, ro.count, ro.score});
+        }
+        // selectBestClustersByRegion (select_clusters_by_region.go:25-40)
+        if ((int64_t)groups.size() < h.region_min) {
+          bt->h_rnsel[j] = -KP_ERR_REGION_MIN_GROUPS;
+          return;
+        }
+        auto sel = select_groups(groups, h.region_min, h.region_max, h.cluster_min);
+        if (sel.empty()) {
+          bt->h_rnsel[j] = -KP_ERR_REGION_CLUSTER_MIN;
+          return;
+        }
+        for (int r = 0; r < R; r++) bt->h_rsel[(size_t)j * R + r] = -1;
+        for (size_t q = 0; q < sel.size(); q++) bt->h_rsel[(size_t)j * R + q] = sel[q];
+        bt->h_rnsel[j] = (int32_t)sel.size();
+      });
+      th1 = now_ms();
+      HIPCHK(dev::h2d(bt->rsel, bt->h_rsel.data(), 4 * bt->h_rsel.size(), st));
+      HIPCHK(dev::h2d(bt->rnsel, bt->h_rnsel.data(), 4 * nr, st));
+    }
     HIPCHK(dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sx));
   }
   if (!bt->l_slow.empty()) {

@@ -47,6 +47,15 @@ extern "C" __global__ void __launch_bounds__(kBlock) k_region_b(KArgs a, const i
   KP_SMEM;
   body_region_b(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, rsel, rnsel, cap);
 }
+extern "C" __global__ void __launch_bounds__(256) k_region_groups(const RegionOut* rout, const int32_t* rstat,
+                                                                  const BindHdr* hdr, const int32_t* list, int n, int R,
+                                                                  int32_t* rsel, int32_t* rnsel, uint32_t* nhost) {
+  const int j = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (j >= n) return;
+  const int32_t k = region_groups_one(rout + (size_t)j * R, rstat[j], hdr[list[j]], R, rsel + (size_t)j * R);
+  if (k == kGroupsHost) atomicAdd(nhost, 1u);
+  rnsel[j] = k;
+}
 extern "C" __global__ void __launch_bounds__(kSlowBlock) k_slow(KArgs a, unsigned char* scratch, size_t slot_bytes,
                                                                 int cap, int lds_area, int lds_sort) {
   KP_SMEM;
@@ -171,6 +180,14 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
     default:
       return chk(hipErrorInvalidValue);
   }
+  return chk(hipGetLastError());
+}
+
+int region_groups(stream_t st, const RegionOut* rout, const int32_t* rstat, const BindHdr* hdr, const int32_t* list,
+                  int n, int R, int32_t* rsel, int32_t* rnsel, uint32_t* nhost) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_region_groups, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)st, rout, rstat, hdr, list, n,
+                     R, rsel, rnsel, nhost);
   return chk(hipGetLastError());
 }
 

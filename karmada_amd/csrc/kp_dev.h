@@ -41,6 +41,10 @@ int fill(void* dst, int value, size_t bytes, stream_t s);
 int pair(stream_t st, const SnapView& s, const BatchView& bv, int b0, int nb, uint64_t* fmask, int32_t* est,
          int64_t* score, int est_mode, int md_cap, size_t smem, int fast = 0);
 int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x);
+// selectGroups for n region bindings (one thread each): rsel/rnsel as the host
+// step writes them; *nhost counts the bindings left to the host (kGroupsHost).
+int region_groups(stream_t st, const RegionOut* rout, const int32_t* rstat, const BindHdr* hdr, const int32_t* list,
+                  int n, int R, int32_t* rsel, int32_t* rnsel, uint32_t* nhost);
 int compact(stream_t st, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
             const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n);
 

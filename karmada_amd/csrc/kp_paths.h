@@ -624,6 +624,29 @@ struct RegionOut {
   int32_t pad;
   int64_t score;
 };
+// ----------------------------------------------------------------------------
+// selectGroups (select_groups.go:102-224) on the device, one thread per binding.
+// Groups are the regions with clusters: value = #clusters, weight = group score.
+// Same answer as the host DFS (engine.cpp select_groups) without storing the
+// feasible paths:
+//  - pass 1 runs the DFS and keeps the best path by (weight desc, value desc),
+//    the first found winning ties (= the smallest id);
+//  - prioritizePaths then only ever moves to a proper subpath of the current
+//    path, i.e. to a prefix (in weight order) of the best path. A prefix Q of
+//    the current path F sorts after F exactly when Q.weight <= F.weight (group
+//    values are >= 1, so Q.value < F.value), and the first such Q in sorted
+//    order has the largest weight, then value. A prefix is a feasible path iff
+//    it is feasible and none of its proper prefixes in DFS (value) order is.
+// Returns the number of selected regions (ids in sel, best-path order),
+// -KP_ERR_* for the reference's errors, or kGroupsHost when the DFS exceeds
+// kGroupNodes nodes (the host DFS answers those).
+// ----------------------------------------------------------------------------
+constexpr int kGroupMax = 64;         // regions per snapshot on the device path
+constexpr int64_t kGroupNodes = 1 << 20;
+constexpr int32_t kGroupsHost = -2000;
+KP_HD inline int32_t select_groups_dev(const struct RegionOut* ro, int R, int64_t minC, int64_t maxC, int64_t target,
+                                       int32_t* sel);
+
 struct RegionLds {
   int32_t* cnt;
   int32_t* dvalid;
@@ -638,6 +661,139 @@ struct RegionLds {
   unsigned long long* minkey;
   unsigned long long* last;
 };
+
+KP_HD inline int32_t select_groups_dev(const RegionOut* ro, int R, int64_t minC, int64_t maxC, int64_t target,
+                                       int32_t* sel) {
+  int32_t sid[kGroupMax], sv[kGroupMax];
+  int64_t sw[kGroupMax];
+  int n = 0;
+  for (int r = 0; r < R; r++)
+    if (ro[r].count > 0) {
+      int j = n++;  // insertion by (value asc, weight desc, id asc) (select_groups.go:140-151)
+      while (j > 0 && (sv[j - 1] > ro[r].count || (sv[j - 1] == ro[r].count && sw[j - 1] < ro[r].score))) {
+        sid[j] = sid[j - 1];
+        sv[j] = sv[j - 1];
+        sw[j] = sw[j - 1];
+        j--;
+      }
+      sid[j] = r;
+      sv[j] = ro[r].count;
+      sw[j] = ro[r].score;
+    }
+  if ((int64_t)n < minC) return -KP_ERR_REGION_MIN_GROUPS;  // select_clusters_by_region.go:30-32
+  if (n == 0) return -KP_ERR_REGION_CLUSTER_MIN;
+  // ---- pass 1: DFS (findFeasiblePaths), best path by (weight desc, value desc, id asc)
+  int32_t st[kGroupMax], nx[kGroupMax], best[kGroupMax];
+  int depth = 0, bl = -1;
+  int64_t sum = 0, wsum = 0, bw = 0, bv = 0, nodes = 0;
+  const bool nobt = (int64_t)n == minC;  // select_groups.go:179-182: no backtracking
+  for (;;) {
+    // node entry
+    bool down = false;
+    if (++nodes > kGroupNodes) return kGroupsHost;
+    if (sum >= target && depth >= minC && depth <= maxC) {
+      if (bl < 0 || wsum > bw || (wsum == bw && sum > bv)) {
+        bl = depth;
+        bw = wsum;
+        bv = sum;
+        for (int k = 0; k < depth; k++) best[k] = st[k];
+      }
+    } else if (depth < maxC) {
+      nx[depth] = depth == 0 ? 0 : st[depth - 1] + 1;
+      down = nx[depth] < n;
+    }
+    if (down) {
+      const int i = nx[depth];
+      st[depth] = i;
+      sum += sv[i];
+      wsum += sw[i];
+      depth++;
+      continue;
+    }
+    // return to the parent; try its next child
+    bool more = false;
+    while (depth > 0) {
+      depth--;
+      if (nobt) break;
+      const int i = st[depth];
+      sum -= sv[i];
+      wsum -= sw[i];
+      nx[depth] = i + 1;
+      if (nx[depth] < n) {
+        st[depth] = nx[depth];
+        sum += sv[st[depth]];
+        wsum += sw[st[depth]];
+        depth++;
+        more = true;
+        break;
+      }
+    }
+    if (!more) break;
+  }
+  if (bl < 0) return -KP_ERR_REGION_CLUSTER_MIN;  // no feasible path (select_clusters_by_region.go:37-39)
+  // ---- best path in weight order (sortGroups: weight desc, name asc; ids are name ranks)
+  int32_t w[kGroupMax];
+  for (int k = 0; k < bl; k++) {
+    int j = k;
+    const int32_t g = best[k];
+    while (j > 0 && (sw[w[j - 1]] < sw[g] || (sw[w[j - 1]] == sw[g] && sid[w[j - 1]] > sid[g]))) {
+      w[j] = w[j - 1];
+      j--;
+    }
+    w[j] = g;
+  }
+  // ---- prioritizePaths: walk to the first later subpath while one exists
+  int fl = bl;
+  int64_t fw = bw;
+  for (;;) {
+    int pick = -1;
+    int64_t pw = 0, pv = 0;
+    int64_t qw = 0, qv = 0;
+    for (int j = 1; j < fl; j++) {
+      qw += sw[w[j - 1]];
+      qv += sv[w[j - 1]];
+      if (qw > fw || !(qv >= target && j >= minC && j <= maxC)) continue;
+      // visited by the DFS: no proper prefix in index order is feasible (nor the
+      // root); without backtracking only the chain 0,1,2,.. is visited
+      int32_t idx[kGroupMax];
+      for (int k = 0; k < j; k++) {
+        int m = k;
+        while (m > 0 && idx[m - 1] > w[k]) {
+          idx[m] = idx[m - 1];
+          m--;
+        }
+        idx[m] = w[k];
+      }
+      bool visited = !(0 >= target && 0 >= minC && 0 <= maxC);  // the root returns when feasible
+      int64_t ps = 0;
+      for (int k = 0; k < j && visited; k++) {
+        if (nobt && idx[k] != k) visited = false;
+        if (k > 0 && ps >= target && k >= minC && k <= maxC) visited = false;
+        ps += sv[idx[k]];
+      }
+      if (!visited) continue;
+      if (pick < 0 || qw > pw || (qw == pw && qv > pv)) {
+        pick = j;
+        pw = qw;
+        pv = qv;
+      }
+    }
+    if (pick < 0) break;
+    fl = pick;
+    fw = pw;
+  }
+  if (fl == 0) return -KP_ERR_REGION_CLUSTER_MIN;  // the empty root path
+  for (int k = 0; k < fl; k++) sel[k] = sid[w[k]];
+  return fl;
+}
+
+// The group-combination step of one region binding (the host step it replaces:
+// engine.cpp kp_schedule_batch). rstat != 0: stage A already finalized it.
+KP_HD inline int32_t region_groups_one(const RegionOut* ro, int32_t rstat, const BindHdr& h, int R, int32_t* sel) {
+  if (rstat != 0) return -1000;
+  for (int r = 0; r < R; r++) sel[r] = -1;
+  return select_groups_dev(ro, R, h.region_min, h.region_max, h.cluster_min, sel);
+}
 KP_HD inline int64_t go_ceil_div_i64(int32_t a, int64_t b) {
   double q = kp_ceil((double)a / (double)b);
   if (q != q || q >= 9223372036854775808.0 || q < -9223372036854775808.0) return INT64_MIN;  // amd64 CVTTSD2SQ

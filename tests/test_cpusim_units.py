@@ -124,3 +124,44 @@ def test_sort_tcl_wave_form_matches_serial_and_oracle(seed):
         assert ok == 1, (n, kind)
         assert wave == want, (n, kind)
         assert wrep == [reps[i] for i in want]
+
+
+SIM.kpsim_select_groups.restype = C.c_int
+SIM.kpsim_select_groups.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.c_int, C.c_int64, C.c_int64,
+                                    C.c_int64, C.POINTER(C.c_int32)]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_select_groups_device_form_matches_oracle(seed):
+    """selectGroups (select_groups.go:102-224): the device form (one thread,
+    two passes, no path list) picks the oracle's DFS + prioritizePaths answer,
+    including the subpath walk, the no-backtracking case (#groups == min) and
+    the reference's errors."""
+    L = O.lib()
+    rng = random.Random(100 + seed)
+    w = api.World()
+    for _ in range(400):
+        R = rng.choice([1, 2, 3, 4, 6, 8, 12, 16])
+        vals = [rng.choice([0, 1, 1, 2, 3, 5, 8]) for _ in range(R)]
+        wts = [rng.choice([0, 1000, 2000, 2500, rng.randint(0, 10**6), 10**9]) for _ in range(R)]
+        present = [r for r in range(R) if vals[r] > 0]
+        min_c = rng.choice([0, 1, 2, 3, len(present)])
+        max_c = rng.choice([min_c, min_c + 1, 3, 5, 16])
+        target = rng.choice([0, 1, 2, 4, 7, 12, 30])
+        out = (C.c_int32 * max(1, R))()
+        got = SIM.kpsim_select_groups((C.c_int32 * R)(*vals), (C.c_int64 * R)(*wts), R, min_c, max_c, target, out)
+        # oracle: regions with clusters only (host step, select_clusters_by_region.go:25-40)
+        n = len(present)
+        if n < min_c:
+            want = -2
+        else:
+            names, _ = w.arr(api.kp_str, [w.s(f"r{r:03d}") for r in present])
+            o = (C.c_uint32 * max(1, n))()
+            k = L.kpo_select_groups(names, (C.c_int64 * max(1, n))(*[vals[r] for r in present]),
+                                    (C.c_int64 * max(1, n))(*[wts[r] for r in present]), n, min_c, max_c, target, o)
+            want = [present[o[i]] for i in range(k)] if k > 0 else -3
+        if isinstance(want, list):
+            assert got == len(want), (vals, wts, min_c, max_c, target, got, want)
+            assert [out[i] for i in range(got)] == want, (vals, wts, min_c, max_c, target)
+        else:
+            assert got == want, (vals, wts, min_c, max_c, target, got)
