@@ -919,16 +919,30 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
     rsel[r] = -1;
   }
   B.sync();
+  uint32_t* ctr = hist + 255;
+  if (B.tid() == 0) *ctr = 0;
   for (int j = B.tid(); j < nsel; j += B.nth()) rsel[sel[j]] = j;
   B.sync();
-  int64_t total = 0;
+  // One pass: each candidate of a selected region gets its sortClusters key
+  // once; the region heads take the minimum and the keys are compacted into
+  // `keys` (2*kSmallMax entries) when they fit.
+  const int kc = 2 * kSmallMax;
+  auto in_sel = [&](int i) {
+    const int r = x.s->region_idx[c_rank(cd, i)];
+    return r >= 0 && rsel[r] >= 0;
+  };
+  int32_t mine = 0;
+  for (int i = B.tid(); i < cd.F; i += B.nth()) mine += in_sel(i) ? 1 : 0;
+  int32_t pos = B.wave_reserve(mine, ctr);
   for (int i = B.tid(); i < cd.F; i += B.nth()) {
-    int r = x.s->region_idx[c_rank(cd, i)];
-    if (r < 0 || rsel[r] < 0) continue;
-    total++;
-    kp_atomic_min_u64(&heads[r], cand_key(x, cd, i, cd.v[i]));
+    if (!in_sel(i)) continue;
+    const uint64_t k = cand_key(x, cd, i, cd.v[i]);
+    kp_atomic_min_u64(&heads[x.s->region_idx[c_rank(cd, i)]], k);
+    if (pos < kc) keys[pos] = k;
+    pos++;
   }
-  total = B.sum64(total);
+  B.sync();
+  const int64_t total = *ctr;
   int64_t needCnt = total < h.cluster_max ? total : h.cluster_max;
   int64_t restCnt = needCnt - nsel;
   if (restCnt > kSmallMax - nsel) {  // engine limit: selected list capacity
@@ -940,7 +954,21 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
     for (int j = 0; j < nsel; j++) items[n++] = item_from_key(x, heads[sel[j]]);
   n = nsel;
   B.sync();
-  if (restCnt > 0) {
+  if (restCnt > 0 && total <= kc && restCnt <= 64) {
+    // the restCnt smallest non-head keys, ascending: one block minimum per pick
+    uint64_t prev = 0;
+    for (int64_t q = 0; q < restCnt; q++) {
+      uint64_t m = ~0ull;
+      for (int i = B.tid(); i < (int)total; i += B.nth()) {
+        const uint64_t k = keys[i];
+        if ((q == 0 || k > prev) && k < m && k != heads[x.s->region_idx[key_rank(k)]]) m = k;
+      }
+      prev = B.minu64(m);
+      if (B.tid() == 0) items[nsel + q] = item_from_key(x, prev);
+    }
+    n = nsel + (int)restCnt;
+    B.sync();
+  } else if (restCnt > 0) {
     auto incand = [&](int i) {
       int r = x.s->region_idx[c_rank(cd, i)];
       return r >= 0 && rsel[r] >= 0 && cand_key(x, cd, i, cd.v[i]) != heads[r];
