@@ -26,6 +26,8 @@ VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # 1228.8 G wave-instructions/s
 # SURVEY.md §8(d) streamed-row model, config 3: B_row = 140 filter + 52 summary + 192 grades
 B_ROW = {2: 184, 3: 384, 4: 192, 5: 384, 6: 384, 1: 184}
 B_BIND = 256
+# pair kernel instance per kp_stage_times.pair_kind (kp_algo.h EST_*)
+PAIR_KERNELS = {0: "k_pair", 1: "k_pair_fast", 2: "k_pair_fast_summary", 8: "k_pair_fast_m8", 16: "k_pair_fast_m16"}
 
 
 def pair_bytes_per_binding(config, n_clusters):
@@ -149,6 +151,7 @@ def main():
         host_ms.append(st["host_ms"])
         n_slow = st["n_slow"]
         launches = max(1, st["pair_launches"])
+        kind = st["pair_kind"]
     barrier_sync()
     elapsed = time.perf_counter() - t0
     n_ok = sum(1 for i in range(r.n_bindings) if r.status[i] == 0)
@@ -190,7 +193,8 @@ def main():
                    "bindings_per_gpu": B, "clusters": C_, "parallelism": f"binding-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "k_pair_fast", "kernel_ms": round(launch_ms, 4), "launches_per_step": launches,
+                     "kernel": PAIR_KERNELS.get(kind, "k_pair"), "kernel_ms": round(launch_ms, 4),
+                     "launches_per_step": launches,
                      # SURVEY §8(d) streamed-row model: every binding re-reads every cluster
                      # row. The packed snapshot (~2 MB) stays in each XCD's L2, so that
                      # exceeds HBM peak; what bounds the kernel is instruction issue:

@@ -305,7 +305,7 @@ typedef struct kp_stage_times {
   float select_kernel_ms; /* select kernels after the last pair launch (HIP events) */
   uint64_t n_slow;        /* bindings that took the exact serial path */
   uint32_t pair_launches; /* pair kernel launches (chunks) in the batch */
-  uint32_t pad;
+  uint32_t pair_kind;     /* pair kernel instance: 0 generic, 1 mixed, 2 summary-only, 8/16 model-only */
 } kp_stage_times;
 
 /* ------------------------------------------------------------------------- */

@@ -93,8 +93,14 @@ int fill(void* dst, int value, size_t bytes, stream_t) {
 int pair(stream_t, const SnapView& s, const BatchView& bv, int b0, int nb, uint64_t* fmask, int32_t* est,
          int64_t* score, int est_mode, int md_cap, size_t smem, int fast) {
   grid(nb, smem, [&](int blk, unsigned char* sm) {
-    if (fast) body_pair<true>(CpuBlk{(int64_t*)sm}, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap);
-    else body_pair<false>(CpuBlk{(int64_t*)sm}, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap);
+    const CpuBlk B{(int64_t*)sm};
+    switch (fast) {
+      case EST_MIXED: body_pair<EST_MIXED>(B, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap); break;
+      case EST_SUMMARY: body_pair<EST_SUMMARY>(B, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap); break;
+      case EST_MODEL8: body_pair<EST_MODEL8>(B, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap); break;
+      case EST_MODEL16: body_pair<EST_MODEL16>(B, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap); break;
+      default: body_pair<EST_GENERIC>(B, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap);
+    }
   });
   return 0;
 }

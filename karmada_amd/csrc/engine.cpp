@@ -159,7 +159,7 @@ struct kp_batch {
   unsigned char* slow_scratch = nullptr;
   size_t slow_slot = 0;
   int slow_grid = 0, slow_cap = 0, slow_lds = 0, slow_sort = 0;
-  bool pair_fast = false;
+  int pair_fast = 0;  // EST_* instance of the pair kernel (pair_kind)
   // host results
   std::vector<int32_t> h_status, h_err, h_rstat, h_rsel, h_rnsel;
   std::vector<int64_t> h_arg;
@@ -452,7 +452,7 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
     bool dense = s->n_tmpl > 0 && s->n_tmpl <= kTmplDense;
     for (int64_t x : s->tmpl) dense = dense && x >= 0;
     if (dense) {
-      std::vector<int64_t> acc((size_t)s->n_tmpl * Cp, 0);
+      std::vector<int64_t> acc((size_t)kTmplDense * Cp, 0);  // rows past n_tmpl stay zero
       for (int k = 0; k < kmax; k++)
         for (int r = 0; r < C; r++) {
           const int32_t cnt = s->mg_cnt[(size_t)k * Cp + r];
@@ -1043,19 +1043,28 @@ size_t smem_region_b(const kp_snapshot* s, int cap) {
 }
 const int kMdCap = 4096;
 // MaxDivided table entries staged per workgroup: the snapshot's template count.
-int md_cap_of(const kp_snapshot* s) { return s->n_tmpl <= kMdCap ? std::max(4, s->n_tmpl) : 0; }
+int md_cap_of(const kp_snapshot* s) { return s->n_tmpl <= kMdCap ? std::max(kTmplDense, s->n_tmpl) : 0; }
 // Whether the specialised pair kernel (est_compute<true>) covers every binding of
 // the batch: MaxDivided and taint-set tables fit in LDS, the dense node-count
 // matrix exists (or no cluster has models), at most kReqUnroll resource requests
 // per binding, divisors <= 2^60.
-bool pair_fast_ok(const kp_snapshot* s, const kp_batch* bt) {
-  if (md_cap_of(s) == 0 || s->view.n_tsets > kTsetMax || (s->n_tmpl > 0 && !s->view.mt_cnt)) return false;
+int pair_kind(const kp_snapshot* s, const kp_batch* bt) {
+  if (md_cap_of(s) == 0 || s->view.n_tsets > kTsetMax || (s->n_tmpl > 0 && !s->view.mt_cnt)) return EST_GENERIC;
   for (const BindHdr& h : bt->hdr) {
-    if (h.sreq_cnt > kReqUnroll) return false;
+    if (h.sreq_cnt > kReqUnroll) return EST_GENERIC;
     for (int j = 0; j < h.sreq_cnt; j++)
-      if (bt->lpool[h.sreq_q_off + j] > ((int64_t)1 << 60)) return false;
+      if (bt->lpool[h.sreq_q_off + j] > ((int64_t)1 << 60)) return EST_GENERIC;
   }
-  return true;
+  // which estimator paths the snapshot's clusters can take
+  bool any_model = false, any_summary_only = false;
+  for (int r = 0; r < s->C; r++) {
+    const uint32_t f = s->flags[r];
+    if (f & CF_MODEL_OK) any_model = true;
+    else if (f & CF_HAS_SUMMARY) any_summary_only = true;
+  }
+  if (!any_model) return EST_SUMMARY;
+  if (!any_summary_only) return s->n_tmpl <= 8 ? EST_MODEL8 : EST_MODEL16;
+  return EST_MIXED;
 }
 
 }  // namespace
@@ -1368,7 +1377,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   bt->slow_slot = (bt->slow_slot + 255) & ~(size_t)255;
   // k_slow: one workgroup per CU pass over the flagged bindings (appended on device)
   bt->slow_grid = (int)std::max<size_t>(1, std::min<size_t>(256, bt->l_slow.size()));
-  bt->pair_fast = pair_fast_ok(s, bt);
+  bt->pair_fast = pair_kind(s, bt);
   Arena& a = bt->dev;
   BindHdr* d_hdr;
   int32_t* d_ipool;
@@ -1496,7 +1505,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   dev::stream_t sp = e->stream2;
   HIPCHK(dev::event_record(e->ev[0], st));
   HIPCHK(dev::stream_wait(sp, e->ev[0]));  // the fills above precede every kernel
-  const bool fast = bt->pair_fast && !getenv("KP_PAIR_GENERIC");
+  const int fast = getenv("KP_PAIR_GENERIC") ? EST_GENERIC : bt->pair_fast;
   SelectExtra sx;
   sx.rout = bt->rout;
   sx.rstat = bt->rstat;
@@ -1646,6 +1655,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   for (int i = 0; i < nch; i++) ms_pair += dev::event_ms(e->ev_chunk[2 * i], e->ev_chunk[2 * i + 1]);
   ms_sel = dev::event_ms(e->ev_chunk[2 * nch - 1], e->ev[2]);
   tm.pair_launches = nch;
+  tm.pair_kind = (uint32_t)fast;
   tm.pair_kernel_ms = ms_pair;
   tm.select_kernel_ms = ms_sel;
   tm.n_slow = bt->h_stats[0];

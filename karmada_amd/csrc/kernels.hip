@@ -23,13 +23,19 @@ using namespace kp;
 extern "C" __global__ void __launch_bounds__(kBlock) k_pair(SnapView s, BatchView bv, int b0, uint64_t* fmask,
                                                             int32_t* est, int64_t* score, int est_mode, int md_cap) {
   KP_SMEM;
-  body_pair<false>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, b0, fmask, est, score, est_mode, md_cap);
+  body_pair<EST_GENERIC>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, b0, fmask, est, score, est_mode,
+                         md_cap);
 }
-extern "C" __global__ void __launch_bounds__(kBlock) k_pair_fast(SnapView s, BatchView bv, int b0, uint64_t* fmask,
-                                                                 int32_t* est, int md_cap) {
-  KP_SMEM;
-  body_pair<true>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, b0, fmask, est, nullptr, 0, md_cap);
-}
+#define KP_PAIR_FAST(NAME, KIND)                                                                                \
+  extern "C" __global__ void __launch_bounds__(kBlock) NAME(SnapView s, BatchView bv, int b0, uint64_t* fmask, \
+                                                            int32_t* est, int md_cap) {                       \
+    KP_SMEM;                                                                                                  \
+    body_pair<KIND>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, b0, fmask, est, nullptr, 0, md_cap); \
+  }
+KP_PAIR_FAST(k_pair_fast, EST_MIXED)
+KP_PAIR_FAST(k_pair_fast_summary, EST_SUMMARY)
+KP_PAIR_FAST(k_pair_fast_m8, EST_MODEL8)
+KP_PAIR_FAST(k_pair_fast_m16, EST_MODEL16)
 extern "C" __global__ void __launch_bounds__(1024) k_select_all(KArgs a) {
   KP_SMEM;
   body_select_all(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a);
@@ -146,8 +152,14 @@ int fill(void* dst, int value, size_t bytes, stream_t s) {
 int pair(stream_t st, const SnapView& s, const BatchView& bv, int b0, int nb, uint64_t* fmask, int32_t* est,
          int64_t* score, int est_mode, int md_cap, size_t smem, int fast) {
   if (nb <= 0) return 0;
-  if (fast)
-    hipLaunchKernelGGL(k_pair_fast, dim3(nb), dim3(kBlock), smem, (hipStream_t)st, s, bv, b0, fmask, est, md_cap);
+  auto* kf = fast == EST_MIXED     ? k_pair_fast
+             : fast == EST_SUMMARY ? k_pair_fast_summary
+             : fast == EST_MODEL8  ? k_pair_fast_m8
+             : fast == EST_MODEL16 ? k_pair_fast_m16
+                                   : nullptr;
+  if (fast != EST_GENERIC && !kf) return chk(hipErrorInvalidValue);
+  if (kf)
+    hipLaunchKernelGGL(kf, dim3(nb), dim3(kBlock), smem, (hipStream_t)st, s, bv, b0, fmask, est, md_cap);
   else
     hipLaunchKernelGGL(k_pair, dim3(nb), dim3(kBlock), smem, (hipStream_t)st, s, bv, b0, fmask, est, score, est_mode,
                        md_cap);

@@ -237,13 +237,22 @@ KP_HD inline int32_t template_md(const SnapView& s, const BatchView& bv, const B
   return (int32_t)res;
 }
 
+// Estimator instances of the pair kernel (the template argument `Fast`):
+//   EST_GENERIC  every fallback compiled in;
+//   EST_MIXED    pair_fast_ok: dense node counts, <= kReqUnroll requests, no cold paths;
+//   EST_SUMMARY  as MIXED, and no cluster of the snapshot has resource models;
+//   EST_MODEL8 / EST_MODEL16  as MIXED, and every cluster with a summary has
+//                models: only the <= 8 / 16 zero-padded template rows are loaded
+//                (summary-path bindings, BF_MODEL_ERR, read their columns late).
+enum : int { EST_GENERIC = 0, EST_MIXED = 1, EST_SUMMARY = 2, EST_MODEL8 = 8, EST_MODEL16 = 16 };
+
 // min(a / q, lim) for a >= 0, q >= 1, lim >= 0 without a 64-bit integer divide:
 // a double estimate decides "quotient >= lim" when it is far from the limit,
 // otherwise the quotient (< lim + 2 <= 2^31 + 2) is corrected exactly.
-template <bool Fast = false>
+template <int Fast = EST_GENERIC>
 KP_HD inline int64_t floor_div_below(int64_t a, int64_t q, int64_t lim) {
   if (a < q) return 0;
-  if (!Fast && q > ((int64_t)1 << 60)) {  // enormous request: the quotient is tiny, divide exactly
+  if (Fast == EST_GENERIC && q > ((int64_t)1 << 60)) {  // enormous request: the quotient is tiny, divide exactly
     const int64_t d = a / q;
     return d < lim ? d : lim;
   }
@@ -263,6 +272,7 @@ KP_HD inline int64_t floor_div_below(int64_t a, int64_t q, int64_t lim) {
 constexpr int kEstUnroll = 8;   // model node groups per cluster (generic path)
 constexpr int kReqUnroll = 4;   // summary-path resource requests per binding
 constexpr int kTmplDense = 16;  // templates of the dense node-count matrix (fast path)
+
 struct EstOps {
   uint32_t f;
   int64_t allowed;
@@ -270,15 +280,22 @@ struct EstOps {
   int32_t mt[kTmplDense];                  // fast: nodes of template t (SnapView::mt_cnt)
   int64_t av[kReqUnroll];                  // summary available of request j < kReqUnroll
 };
-template <bool Fast = false>
+template <int Fast = EST_GENERIC>
 KP_HD inline EstOps est_load(const SnapView& s, const BatchView& bv, const BindHdr& h, int c, uint32_t f) {
   EstOps o;
   o.f = f;
   o.allowed = s.allowed[c];
   const bool rr = (h.flags & BF_HAS_RR) != 0;
   const bool model = rr && !(h.flags & BF_MODEL_ERR);
-  const int jh = rr ? (h.sreq_cnt < kReqUnroll ? h.sreq_cnt : kReqUnroll) : 0;
-  if (Fast) {
+  const int jh = rr && Fast < EST_MODEL8 ? (h.sreq_cnt < kReqUnroll ? h.sreq_cnt : kReqUnroll) : 0;
+  if (Fast >= EST_MODEL8) {  // zero-padded rows: no per-template guard
+KP_UNROLL
+    for (int t = 0; t < kTmplDense; t++) {
+      o.mt[t] = 0;
+      if (t < Fast && model) o.mt[t] = s.mt_cnt[(size_t)t * s.Cp + c];
+    }
+  } else if (Fast == EST_SUMMARY) {
+  } else if (Fast == EST_MIXED) {
     const int th = model ? s.n_tmpl : 0;
 KP_UNROLL
     for (int t = 0; t < kTmplDense; t++) {
@@ -310,11 +327,11 @@ KP_UNROLL
 
 // GeneralEstimator.maxAvailableReplicas (general.go:66-108), assumed workloads empty.
 // md: per-template MaxDivided table (LDS) or nullptr to compute per pair.
-// Fast: the launch guarantees md != nullptr, the dense node-count matrix
-// (n_tmpl <= kTmplDense, every template value >= 0 so every MaxDivided is >= 0),
-// every sreq_cnt <= kReqUnroll and every divisor <= 2^60 (pair_fast_ok,
-// engine.cpp), so the cold fallbacks are compiled out of the pair kernel.
-template <bool Fast = false>
+// Fast != EST_GENERIC: the launch guarantees md != nullptr (zero past n_tmpl),
+// the dense node-count matrix (n_tmpl <= kTmplDense, every template value >= 0
+// so every MaxDivided is >= 0), every sreq_cnt <= kReqUnroll and every divisor
+// <= 2^60 (pair_fast_ok, engine.cpp), so the cold fallbacks are compiled out.
+template <int Fast = EST_GENERIC>
 KP_HD inline int32_t est_compute(const SnapView& s, const BatchView& bv, const BindHdr& h, int c, const int32_t* md,
                                  const EstOps& o) {
   const uint32_t f = o.f;
@@ -328,20 +345,20 @@ KP_HD inline int32_t est_compute(const SnapView& s, const BatchView& bv, const B
     // d <= 110 (MaxPodsPerNode) and cnt <= MaxInt32: d*cnt < 2^38, and the
     // sum stops growing at MaxInt32 (Go's break), so int64 cannot overflow.
     int64_t total = 0;
-    if (Fast) {
+    if (Fast != EST_GENERIC) {
       // Groups of one template merged: sum_t MaxDivided_t * nodes_t, each term
       // >= 0, so Go's stop at MaxInt32 is the clamp below; a node count
       // clamped at MaxInt32 only matters when its MaxDivided >= 1, where the
       // sum saturates either way.
 KP_UNROLL
       for (int t = 0; t < kTmplDense; t++)
-        if (t < s.n_tmpl) total += (int64_t)md[t] * (int64_t)o.mt[t];
+        if (Fast >= EST_MODEL8 ? t < Fast : t < s.n_tmpl) total += (int64_t)md[t] * (int64_t)o.mt[t];
     }
 KP_UNROLL
-    for (int k = 0; !Fast && k < kEstUnroll; k++)
+    for (int k = 0; Fast == EST_GENERIC && k < kEstUnroll; k++)
       if (k < s.kmax && o.gc[k] != 0 && total < kInt32Max)
         total += (int64_t)(md ? md[o.gt[k]] : template_md(s, bv, h, o.gt[k])) * o.gc[k];
-    for (int k = kEstUnroll; !Fast && k < s.kmax && total < kInt32Max; k++) {
+    for (int k = kEstUnroll; Fast == EST_GENERIC && k < s.kmax && total < kInt32Max; k++) {
       const int64_t cnt = s.mg_cnt[(size_t)k * s.Cp + c];
       if (cnt == 0) continue;
       const int32_t tid = s.mg_tid[(size_t)k * s.Cp + c];
@@ -354,6 +371,19 @@ KP_UNROLL
   // getMaximumReplicasBasedOnClusterSummary (general.go:465-505)
   int64_t num = INT64_MAX;
   bool zero = false;
+  if (Fast >= EST_MODEL8) {  // columns not preloaded (BF_MODEL_ERR bindings only)
+    for (int j = 0; j < h.sreq_cnt; j++) {
+      const int32_t rid = bv.ipool[h.sreq_off + j];
+      if (rid < 0) return 0;
+      const int64_t a = s.avail[(size_t)rid * s.Cp + c];
+      if (a <= 0) return 0;
+      const int64_t lim = num < m ? num : m;
+      const int64_t d = floor_div_below<Fast>(a, bv.lpool[h.sreq_q_off + j], lim);
+      if (d < num) num = d;
+    }
+    if (num < m) m = num;
+    return (int32_t)m;
+  }
 KP_UNROLL
   for (int j = 0; j < kReqUnroll; j++) {
     if (j < h.sreq_cnt && !zero) {
@@ -367,7 +397,7 @@ KP_UNROLL
     }
   }
   if (zero) return 0;
-  for (int j = kReqUnroll; !Fast && j < h.sreq_cnt; j++) {
+  for (int j = kReqUnroll; Fast == EST_GENERIC && j < h.sreq_cnt; j++) {
     int32_t rid = bv.ipool[h.sreq_off + j];
     if (rid < 0) return 0;
     int64_t a = s.avail[(size_t)rid * s.Cp + c];
@@ -406,7 +436,7 @@ KP_HD inline int32_t cal_available(const SnapView& s, const BatchView& bv, const
 // filter's and the estimator's memory latencies overlap. tol_bits: per taint
 // set "tolerated" bits of this binding (LDS), or nullptr for the per-taint
 // loop. Returns the estimate (0 when infeasible); *fit = feasibility.
-template <bool Fast = false>
+template <int Fast = EST_GENERIC>
 KP_HD inline int32_t pair_eval(const SnapView& s, const BatchView& bv, const BindHdr& h, int c,
                                const uint32_t* tgt_bits, const uint32_t* evict_bits, const uint32_t* tol_bits,
                                const int32_t* md, bool* fit) {
@@ -415,7 +445,7 @@ KP_HD inline int32_t pair_eval(const SnapView& s, const BatchView& bv, const Bin
   const bool api_on = (en & 1) && h.gvk >= 0;
   uint64_t aw = 0;
   if (api_on) aw = s.api_bits[(size_t)(h.gvk >> 6) * s.Cp + c];
-  const bool tset_on = (en & 2) && (Fast || tol_bits != nullptr);
+  const bool tset_on = (en & 2) && (Fast != EST_GENERIC || tol_bits != nullptr);
   int32_t ts = 0;
   if (tset_on) ts = s.taint_set[c];
   const bool est_on = !(h.flags & BF_NONWORKLOAD_EST);
@@ -432,7 +462,8 @@ KP_HD inline int32_t pair_eval(const SnapView& s, const BatchView& bv, const Bin
   bool ok = c < s.C && !(f & CF_DELETING) && aff;
   const bool in_t = h.tgt_cnt > 0 && bit_test(tgt_bits, c);
   if ((en & 1) && !in_t) ok = ok && api_on && ((aw >> (h.gvk & 63)) & 1ull);
-  if ((en & 2) && !in_t) ok = ok && ((Fast || tset_on) ? bit_test(tol_bits, ts) : taints_tolerated(s, bv, h, c));
+  if ((en & 2) && !in_t)
+    ok = ok && ((Fast != EST_GENERIC || tset_on) ? bit_test(tol_bits, ts) : taints_tolerated(s, bv, h, c));
   if (en & 8) {
     if ((h.flags & BF_NEED_PROVIDER) && !(f & CF_HAS_PROVIDER)) ok = false;
     if ((h.flags & BF_NEED_REGION) && !(f & CF_HAS_REGION)) ok = false;

@@ -37,7 +37,8 @@ int h2d(void* dst, const void* src, size_t bytes, stream_t s);  // stream-ordere
 int d2h(void* dst, const void* src, size_t bytes, stream_t s);
 int fill(void* dst, int value, size_t bytes, stream_t s);
 
-// fast: launch the specialised pair kernel (the batch meets pair_fast_ok).
+// fast: the estimator instance (EST_*); other than EST_GENERIC only for batches
+// that meet pair_fast_ok.
 int pair(stream_t st, const SnapView& s, const BatchView& bv, int b0, int nb, uint64_t* fmask, int32_t* est,
          int64_t* score, int est_mode, int md_cap, size_t smem, int fast = 0);
 int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x);

@@ -74,9 +74,10 @@ KP_FI bool pre_checks(const BLK& B, const SelCtx& x, int F) {
 // columns), stores their feasibility as one u64 word and calAvailableReplicas
 // per cluster. est_mode 1: raw GeneralEstimator answers for every cluster.
 // ---------------------------------------------------------------------------
-// Fast: the specialised instance for batches that meet pair_fast_ok (engine.cpp):
-// est_mode 0, the MaxDivided and taint-set tables in LDS, no cold fallbacks.
-template <bool Fast, class BLK>
+// Fast: the estimator instance (EST_*, kp_algo.h); every instance but
+// EST_GENERIC needs pair_fast_ok (engine.cpp): est_mode 0, the MaxDivided and
+// taint-set tables in LDS, no cold fallbacks.
+template <int Fast, class BLK>
 KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView& s, const BatchView& bv, int b0,
                      uint64_t* fmask, int32_t* est, int64_t* score, int est_mode, int md_cap) {
   const int b = b0 + blk;
@@ -90,6 +91,7 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
   const bool use_md = s.n_tmpl <= md_cap && (h.flags & BF_HAS_RR);
   if (use_md) {
     for (int t = B.tid(); t < s.n_tmpl; t += B.nth()) md[t] = template_md(s, bv, h, t);
+    for (int t = s.n_tmpl + B.tid(); t < kTmplDense; t += B.nth()) md[t] = 0;  // padded template rows
     B.sync();
   }
   // Stage this binding's predicate data (programs, value lists, tolerations) in
@@ -132,8 +134,8 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
     const int c = base + B.tid();
     bool fit = false;
     int32_t e = 0;
-    if (Fast) {
-      e = pair_eval<true>(s, lv, h, c, tgt, evict, tolb, md, &fit);
+    if (Fast != EST_GENERIC) {
+      e = pair_eval<Fast>(s, lv, h, c, tgt, evict, tolb, md, &fit);
     } else if (est_mode == 0) {
       e = pair_eval(s, lv, h, c, tgt, evict, use_ts ? tolb : nullptr, use_md ? md : nullptr, &fit);
     } else if (c < s.C) {
