@@ -69,13 +69,15 @@ def cpu_baseline(u, opts, budget_s):
     }
 
 
-def load_traffic(config):
-    """Per-launch PMC figures of the pair kernel from the committed profile, if any:
-    (HBM bytes = FETCH_SIZE + WRITE_SIZE, VALU wave-instructions)."""
+def load_traffic(config, kernel):
+    """Per-launch PMC figures of the pair kernel instance from the committed profile,
+    if any: (HBM bytes = FETCH_SIZE + WRITE_SIZE, VALU wave-instructions)."""
     p = os.path.join(ROOT, "profiles", f"traffic_config{config}.json")
     try:
         with open(p) as f:
             d = json.load(f)
+        if d.get("kernel", "k_pair") != kernel:
+            return None, None  # profiled another instance
         return d.get("k_pair_bytes_per_launch"), d.get("k_pair_valu_per_launch")
     except (OSError, ValueError):
         return None, None
@@ -173,7 +175,7 @@ def main():
     avg_pair_ms = sum(pair_ms) / len(pair_ms)  # all pair launches of one step
     achieved = pair_bytes_per_binding(cfg, C_) * B / (avg_pair_ms * 1e-3) / 1e9
     launch_ms = avg_pair_ms / launches
-    traffic, valu = load_traffic(cfg)
+    traffic, valu = load_traffic(cfg, PAIR_KERNELS.get(kind, "k_pair"))
     line = {
         "metric": "ResourceBindings scheduled/sec at 100k bindings x 5k clusters",
         "value": round(value, 1),

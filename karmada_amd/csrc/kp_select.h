@@ -558,7 +558,7 @@ KP_UNROLL
     for (int j = 0; j < kJ; j++) {
       const int u = tid + nth * j;
       fm[j] = u < nu ? (uint32_t)(x.frow[u >> 4] >> ((u & 15) * 4)) & 0xFu : 0u;
-      if (fm[j]) ev[j] = e4[u];
+      if (u < nu) ev[j] = e4[u];  // not behind the mask: one memory latency for both
       mine += popc64(fm[j]);
     }
     between();

@@ -48,7 +48,8 @@ def main():
         res[k] = e
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1, sort_keys=True)
-    kp = "k_pair_fast" if "k_pair_fast" in res else "k_pair"
+    pair = [k for k in res if k.startswith("k_pair") and "hbm_bytes_per_launch" in res[k]]
+    kp = max(pair, key=lambda k: res[k].get("SQ_WAVES", 0)) if pair else "k_pair"  # the instance the bench ran
     if traffic_path and kp in res and "hbm_bytes_per_launch" in res[kp]:
         with open(traffic_path, "w") as fh:
             json.dump({"k_pair_bytes_per_launch": res[kp]["hbm_bytes_per_launch"],
