@@ -107,8 +107,17 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        # one rank per GPU over RCCL ("nccl"); KP_DIST_BACKEND=gloo rehearses the
+        # same path with host tensors (ranks may then share a GPU)
+        backend = os.environ.get("KP_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend=backend)
+        tdev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
 
     cfg = args.config
     C_def, B_def = synth.CONFIGS[cfg]
@@ -160,11 +169,11 @@ def main():
     n_targets = int(r.n_targets)
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         # per-rank result counts, all-gathered (after the timed region)
-        c = torch.tensor([n_ok, n_targets], dtype=torch.int64, device=f"cuda:{local}")
+        c = torch.tensor([n_ok, n_targets], dtype=torch.int64, device=tdev)
         parts = [torch.zeros_like(c) for _ in range(world)]
         dist.all_gather(parts, c)
         n_ok = int(sum(p[0].item() for p in parts))
