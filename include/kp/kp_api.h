@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 2
+#define KP_ABI_VERSION 3
 
 /* ------------------------------------------------------------------------- */
 /* Object model                                                              */
@@ -337,6 +337,16 @@ const char* kp_last_error(const kp_engine* e);
 int kp_snapshot_create(kp_engine* e, const kp_cluster* clusters, uint64_t n_clusters,
                        const kp_options* opts, kp_snapshot** out);
 void kp_snapshot_destroy(kp_snapshot* s);
+/* Applies cluster events to a snapshot in place: `clusters` are new versions of
+ * clusters already in it (matched by name). Only those rows are re-packed; the
+ * device copy is refreshed. This replaces re-snapshotting all clusters on every
+ * informer event (cache.go:124-139, event_handler.go:314-378). *dict_grew = 1
+ * when the update added names, keys, GVKs or resources to the snapshot's
+ * dictionaries: batches packed before the call must then be re-created (their
+ * compiled selectors resolve strings against the old dictionaries); otherwise
+ * they stay valid. Adding or removing clusters needs kp_snapshot_create. */
+int kp_snapshot_update(kp_engine* e, kp_snapshot* s, const kp_cluster* clusters, uint64_t n_clusters,
+                       int* dict_grew);
 /* Packed snapshot as one relocatable byte image (for RCCL broadcast) and back. */
 int kp_snapshot_export(const kp_snapshot* s, const void** bytes, uint64_t* n_bytes);
 int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_snapshot** out);

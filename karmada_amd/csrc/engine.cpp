@@ -4,6 +4,7 @@
 #include "kp_dev.h"
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -71,6 +72,12 @@ struct Arena {
     }
     return 0;
   }
+  void reset() {
+    if (base) dev::release(base);
+    base = nullptr;
+    req.clear();
+    total = 0;
+  }
   ~Arena() {
     if (base) dev::release(base);
   }
@@ -111,6 +118,7 @@ struct kp_snapshot {
   std::vector<int32_t> inv;                          // caller index -> rank
   int32_t rid_cpu = -1, rid_mem = -1, rid_eph = -1;
   int n_tmpl = 0, kmax = 0;
+  int est_kind = 0;  // EST_* pair-kernel instance the clusters allow (snapshot_est_kind)
   std::vector<std::string> names;  // cluster names in rank order
   std::vector<unsigned char> blob;  // kp_snapshot_export buffer
   // host copies
@@ -159,7 +167,7 @@ struct kp_batch {
   unsigned char* slow_scratch = nullptr;
   size_t slow_slot = 0;
   int slow_grid = 0, slow_cap = 0, slow_lds = 0, slow_sort = 0;
-  int pair_fast = 0;  // EST_* instance of the pair kernel (pair_kind)
+  bool fast_ok = false;  // the batch half of the fast pair-kernel condition (batch_fast_ok)
   // host results
   std::vector<int32_t> h_status, h_err, h_rstat, h_rsel, h_rnsel;
   std::vector<int64_t> h_arg;
@@ -186,6 +194,226 @@ bool qmap(const kp_resource* r, uint32_t n, QtyMap* m) {
 }
 
 int upload_snapshot(kp_engine* e, kp_snapshot* s);
+int snapshot_est_kind(const kp_snapshot* s);
+
+// One cluster's packed row before it is laid out in the snapshot columns
+// (shared by kp_snapshot_create and kp_snapshot_update). Dictionary ids are
+// taken with Dict::add: create has filled the dictionaries already (pass 1),
+// an update may append to them.
+struct ClusterRow {
+  uint32_t flags = 0;
+  int32_t provider = -1, region = -1;
+  int64_t provider_int = 0, region_int = 0;
+  std::vector<int32_t> zones;
+  std::vector<std::pair<int32_t, int32_t>> labels;  // (key id, value id), later entries win
+  std::vector<std::array<int32_t, 3>> taints;       // (key, value, effect), NoSchedule/NoExecute only
+  std::vector<int32_t> gvks;
+  int64_t allowed = 0;
+  std::vector<std::pair<int32_t, int64_t>> avail;   // (resource id, available)
+  std::vector<std::pair<int32_t, int64_t>> groups;  // (template id, node count), grades ascending
+};
+
+int pack_row(kp_engine* e, kp_snapshot* s, const kp_cluster& c, std::map<std::vector<int64_t>, int32_t>& tmpl_ids,
+             ClusterRow* out) {
+  ClusterRow& w = *out;
+  w = ClusterRow();
+  uint32_t f = 0;
+  if (c.deleting) f |= CF_DELETING;
+  std::string prov = S(c.provider), reg = S(c.region);
+  if (!prov.empty()) {
+    f |= CF_HAS_PROVIDER;
+    w.provider = s->str.add(prov);
+    int64_t v;
+    if (k8s::parse_int64(prov, &v)) {
+      f |= CF_PROVIDER_INT;
+      w.provider_int = v;
+    }
+  }
+  if (!reg.empty()) {
+    f |= CF_HAS_REGION;
+    w.region = s->str.add(reg);
+    int64_t v;
+    if (k8s::parse_int64(reg, &v)) {
+      f |= CF_REGION_INT;
+      w.region_int = v;
+    }
+  }
+  if (c.n_zones) f |= CF_HAS_ZONES;
+  for (uint32_t i = 0; i < c.n_zones; i++) w.zones.push_back(s->str.add(S(c.zones[i])));
+  for (uint32_t i = 0; i < c.n_labels; i++)
+    w.labels.push_back({s->keys.add(S(c.labels[i].key)), s->str.add(S(c.labels[i].value))});
+  for (uint32_t i = 0; i < c.n_taints; i++) {
+    std::string eff = S(c.taints[i].effect);
+    int32_t ef = eff == "NoSchedule" ? EFF_NOSCHEDULE : (eff == "NoExecute" ? EFF_NOEXECUTE : 0);
+    if (!ef) continue;  // only NoSchedule/NoExecute are filtered (taint_toleration.go:65-67)
+    w.taints.push_back({s->str.add(S(c.taints[i].key)), s->str.add(S(c.taints[i].value)), ef});
+  }
+  for (uint32_t i = 0; i < c.n_api_enablements; i++)
+    w.gvks.push_back(s->gvk.add(S(c.api_enablements[i].group_version) + '\0' + S(c.api_enablements[i].kind)));
+  if (c.has_resource_summary) {
+    f |= CF_HAS_SUMMARY;
+    QtyMap al, ad, ag;
+    bool ok = qmap(c.allocatable, c.n_allocatable, &al) & qmap(c.allocated, c.n_allocated, &ad) &
+              qmap(c.allocating, c.n_allocating, &ag);
+    if (!ok) {
+      e->err = "unparsable quantity in cluster " + S(c.name);
+      return KP_EINVAL;
+    }
+    auto pods = [](const QtyMap& m) {
+      auto it = m.find("pods");
+      return it == m.end() ? 0 : k8s::value(it->second);
+    };
+    int64_t allowed = pods(al) - pods(ad) - pods(ag);  // getAllowedPodNumber (general.go:445-463)
+    w.allowed = allowed > 0 ? allowed : 0;
+    for (auto& kv : al) {  // getMaximumReplicasBasedOnClusterSummary operands (general.go:465-505)
+      k8s::Qty q = kv.second;
+      auto x = ad.find(kv.first);
+      if (x != ad.end()) q.nano -= x->second.nano;
+      x = ag.find(kv.first);
+      if (x != ag.end()) q.nano -= x->second.nano;
+      int64_t v = k8s::value(q);
+      int64_t d = v <= 0 ? 0 : (kv.first == "cpu" ? k8s::milli(q) : v);
+      w.avail.push_back({s->res.add(kv.first), d});
+    }
+    // buildModelNodes (general.go:296-361)
+    if (s->opts.customized_cluster_resource_modeling && c.n_allocatable_modelings > 0 && c.n_resource_models > 0) {
+      bool neg = false;
+      std::map<uint32_t, int64_t> cnt;
+      for (uint32_t i = 0; i < c.n_allocatable_modelings; i++) {
+        if (c.allocatable_modelings[i].count < 0) neg = true;
+        cnt[c.allocatable_modelings[i].grade] += c.allocatable_modelings[i].count;
+      }
+      if (!neg) {
+        std::map<uint32_t, std::map<int32_t, int64_t>> caps;  // grade -> (resource id -> min)
+        for (uint32_t m = 0; m < c.n_resource_models; m++) {
+          QtyMap rl;
+          for (uint32_t j = 0; j < c.resource_models[m].n_ranges; j++) {
+            k8s::Qty q;
+            if (!k8s::parse_quantity(S(c.resource_models[m].ranges[j].min), &q)) {
+              e->err = "unparsable resource model quantity";
+              return KP_EINVAL;
+            }
+            rl[S(c.resource_models[m].ranges[j].name)] = q;
+          }
+          std::map<int32_t, int64_t> t;
+          for (auto& kv : rl) {  // util.NewResource (resource.go:46-75); pods forced to 110
+            const std::string& nm = kv.first;
+            int32_t rid = s->res.add(nm);
+            if (nm == "cpu") t[rid] += k8s::milli(kv.second);
+            else if (nm == "memory" || nm == "ephemeral-storage") t[rid] += k8s::value(kv.second);
+            else if (nm == "pods") continue;
+            else if (k8s::scalar_resource(nm)) t[rid] += k8s::value(kv.second);
+          }
+          caps[c.resource_models[m].grade] = t;
+        }
+        const int R = (int)s->res.names.size();
+        for (auto& kv : caps) {  // grades ascending
+          auto it = cnt.find(kv.first);
+          int64_t k = it == cnt.end() ? 0 : it->second;
+          if (k == 0) continue;
+          std::vector<int64_t> t(R, 0);
+          for (auto& rv : kv.second) t[rv.first] = rv.second;
+          while (!t.empty() && t.back() == 0) t.pop_back();  // key independent of the resource count
+          auto ti = tmpl_ids.find(t);
+          int32_t tid;
+          if (ti == tmpl_ids.end()) {
+            tid = (int32_t)tmpl_ids.size();
+            tmpl_ids.emplace(t, tid);
+          } else {
+            tid = ti->second;
+          }
+          w.groups.push_back({tid, k});
+        }
+        f |= CF_MODEL_OK;
+      }
+    }
+  }
+  w.flags = f;
+  return KP_OK;
+}
+
+// Lays rows[0..C) (rank order) out in the snapshot's columns and derived arrays.
+void apply_rows(kp_snapshot* s, const std::vector<ClusterRow>& rows,
+                const std::map<std::vector<int64_t>, int32_t>& tmpl_ids) {
+  const int C = s->C, Cp = s->Cp;
+  const int K = (int)s->keys.names.size(), AW = ((int)s->gvk.names.size() + 63) / 64, R = (int)s->res.names.size();
+  // regions in name order (region_idx); an update may have added names
+  std::vector<std::string> regs;
+  for (int r = 0; r < C; r++)
+    if (rows[r].region >= 0) regs.push_back(s->str.names[rows[r].region]);
+  std::sort(regs.begin(), regs.end());
+  regs.erase(std::unique(regs.begin(), regs.end()), regs.end());
+  s->regions = Dict();
+  for (auto& r : regs) s->regions.add(r);
+  s->flags.assign(Cp, 0);
+  s->provider.assign(Cp, -1);
+  s->region.assign(Cp, -1);
+  s->region_idx.assign(Cp, -1);
+  s->provider_int.assign(Cp, 0);
+  s->region_int.assign(Cp, 0);
+  s->label_val.assign((size_t)std::max(K, 1) * Cp, -1);
+  s->api_bits.assign((size_t)std::max(AW, 1) * Cp, 0);
+  s->allowed.assign(Cp, 0);
+  s->avail.assign((size_t)std::max(R, 1) * Cp, 0);
+  s->zone_off.assign(C + 1, 0);
+  s->taint_off.assign(C + 1, 0);
+  s->mgrp_off.assign(C + 1, 0);
+  s->zone_ids.clear();
+  s->taint_key.clear();
+  s->taint_val.clear();
+  s->taint_eff.clear();
+  s->mgrp_tid.clear();
+  s->mgrp_cnt.clear();
+  for (int r = 0; r < C; r++) {
+    const ClusterRow& w = rows[r];
+    s->flags[r] = w.flags;
+    s->provider[r] = w.provider;
+    s->provider_int[r] = w.provider_int;
+    s->region[r] = w.region;
+    s->region_int[r] = w.region_int;
+    if (w.region >= 0) s->region_idx[r] = s->regions.get(s->str.names[w.region]);
+    for (int32_t z : w.zones) s->zone_ids.push_back(z);
+    s->zone_off[r + 1] = (int32_t)s->zone_ids.size();
+    for (auto& kv : w.labels) s->label_val[(size_t)kv.first * Cp + r] = kv.second;  // map semantics: later wins
+    for (auto& t : w.taints) {
+      s->taint_key.push_back(t[0]);
+      s->taint_val.push_back(t[1]);
+      s->taint_eff.push_back(t[2]);
+    }
+    s->taint_off[r + 1] = (int32_t)s->taint_key.size();
+    for (int32_t g : w.gvks) s->api_bits[(size_t)(g >> 6) * Cp + r] |= 1ull << (g & 63);
+    s->allowed[r] = w.allowed;
+    for (auto& kv : w.avail) s->avail[(size_t)kv.first * Cp + r] = kv.second;
+    for (auto& g : w.groups) {
+      s->mgrp_tid.push_back(g.first);
+      s->mgrp_cnt.push_back(g.second);
+    }
+    s->mgrp_off[r + 1] = (int32_t)s->mgrp_tid.size();
+  }
+  s->n_tmpl = (int)tmpl_ids.size();
+  s->tmpl.assign((size_t)std::max(s->n_tmpl, 1) * std::max(R, 1), 0);
+  for (auto& kv : tmpl_ids)  // (vectors of an earlier, shorter resource list read as zero-padded)
+    for (int j = 0; j < R && j < (int)kv.first.size(); j++) s->tmpl[(size_t)kv.second * R + j] = kv.first[j];
+  auto pad1 = [](auto& v) {
+    if (v.empty()) v.resize(1);
+  };
+  pad1(s->zone_ids);
+  pad1(s->taint_key);
+  pad1(s->taint_val);
+  pad1(s->taint_eff);
+  // model groups transposed to [kmax][Cp] so a wave reads 64 clusters' k-th group coalesced
+  int& kmax = s->kmax;
+  kmax = 0;
+  for (int r = 0; r < C; r++) kmax = std::max(kmax, s->mgrp_off[r + 1] - s->mgrp_off[r]);
+  s->mg_tid.assign((size_t)std::max(kmax, 1) * Cp, 0);
+  s->mg_cnt.assign((size_t)std::max(kmax, 1) * Cp, 0);
+  for (int r = 0; r < C; r++)
+    for (int g = s->mgrp_off[r]; g < s->mgrp_off[r + 1]; g++) {
+      size_t k = (size_t)(g - s->mgrp_off[r]);
+      s->mg_tid[k * Cp + r] = s->mgrp_tid[g];
+      s->mg_cnt[k * Cp + r] = (int32_t)std::min<int64_t>(s->mgrp_cnt[g], kInt32Max);
+    }
+}
 
 int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_options* o, kp_snapshot* s) {
   s->opts = o ? *o : kp_options{0, 1, KP_PLUGIN_ALL};
@@ -216,7 +444,6 @@ int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_opti
     }
   }
   // pass 1: dictionaries
-  std::vector<std::string> regs;
   for (int r = 0; r < C; r++) {
     const kp_cluster& c = cl[order[r]];
     for (uint32_t i = 0; i < c.n_labels; i++) {
@@ -235,171 +462,17 @@ int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_opti
     for (uint32_t i = 0; i < c.n_allocatable; i++) s->res.add(S(c.allocatable[i].name));
     for (uint32_t m = 0; m < c.n_resource_models; m++)
       for (uint32_t j = 0; j < c.resource_models[m].n_ranges; j++) s->res.add(S(c.resource_models[m].ranges[j].name));
-    if (c.region.len) regs.push_back(S(c.region));
   }
   s->rid_cpu = s->res.add("cpu");
   s->rid_mem = s->res.add("memory");
   s->rid_eph = s->res.add("ephemeral-storage");
-  std::sort(regs.begin(), regs.end());
-  regs.erase(std::unique(regs.begin(), regs.end()), regs.end());
-  for (auto& r : regs) s->regions.add(r);
-  const int K = (int)s->keys.names.size(), AW = ((int)s->gvk.names.size() + 63) / 64, R = (int)s->res.names.size();
-  s->flags.assign(Cp, 0);
-  s->provider.assign(Cp, -1);
-  s->region.assign(Cp, -1);
-  s->region_idx.assign(Cp, -1);
-  s->provider_int.assign(Cp, 0);
-  s->region_int.assign(Cp, 0);
-  s->label_val.assign((size_t)std::max(K, 1) * Cp, -1);
-  s->api_bits.assign((size_t)std::max(AW, 1) * Cp, 0);
-  s->allowed.assign(Cp, 0);
-  s->avail.assign((size_t)std::max(R, 1) * Cp, 0);
-  s->zone_off.assign(C + 1, 0);
-  s->taint_off.assign(C + 1, 0);
-  s->mgrp_off.assign(C + 1, 0);
   std::map<std::vector<int64_t>, int32_t> tmpl_ids;
+  std::vector<ClusterRow> rows(C);
   for (int r = 0; r < C; r++) {
-    const kp_cluster& c = cl[order[r]];
-    uint32_t f = 0;
-    if (c.deleting) f |= CF_DELETING;
-    std::string prov = S(c.provider), reg = S(c.region);
-    if (!prov.empty()) {
-      f |= CF_HAS_PROVIDER;
-      s->provider[r] = s->str.get(prov);
-      int64_t v;
-      if (k8s::parse_int64(prov, &v)) {
-        f |= CF_PROVIDER_INT;
-        s->provider_int[r] = v;
-      }
-    }
-    if (!reg.empty()) {
-      f |= CF_HAS_REGION;
-      s->region[r] = s->str.get(reg);
-      s->region_idx[r] = s->regions.get(reg);
-      int64_t v;
-      if (k8s::parse_int64(reg, &v)) {
-        f |= CF_REGION_INT;
-        s->region_int[r] = v;
-      }
-    }
-    if (c.n_zones) f |= CF_HAS_ZONES;
-    for (uint32_t i = 0; i < c.n_zones; i++) s->zone_ids.push_back(s->str.get(S(c.zones[i])));
-    s->zone_off[r + 1] = (int32_t)s->zone_ids.size();
-    for (uint32_t i = 0; i < c.n_labels; i++)  // map semantics: later entries win
-      s->label_val[(size_t)s->keys.get(S(c.labels[i].key)) * Cp + r] = s->str.get(S(c.labels[i].value));
-    for (uint32_t i = 0; i < c.n_taints; i++) {
-      std::string eff = S(c.taints[i].effect);
-      int32_t ef = eff == "NoSchedule" ? EFF_NOSCHEDULE : (eff == "NoExecute" ? EFF_NOEXECUTE : 0);
-      if (!ef) continue;  // only NoSchedule/NoExecute are filtered (taint_toleration.go:65-67)
-      s->taint_key.push_back(s->str.get(S(c.taints[i].key)));
-      s->taint_val.push_back(s->str.get(S(c.taints[i].value)));
-      s->taint_eff.push_back(ef);
-    }
-    s->taint_off[r + 1] = (int32_t)s->taint_key.size();
-    for (uint32_t i = 0; i < c.n_api_enablements; i++) {
-      int32_t g = s->gvk.get(S(c.api_enablements[i].group_version) + '\0' + S(c.api_enablements[i].kind));
-      s->api_bits[(size_t)(g >> 6) * Cp + r] |= 1ull << (g & 63);
-    }
-    if (c.has_resource_summary) {
-      f |= CF_HAS_SUMMARY;
-      QtyMap al, ad, ag;
-      bool ok = qmap(c.allocatable, c.n_allocatable, &al) & qmap(c.allocated, c.n_allocated, &ad) &
-                qmap(c.allocating, c.n_allocating, &ag);
-      if (!ok) {
-        e->err = "unparsable quantity in cluster " + names[order[r]];
-        return KP_EINVAL;
-      }
-      auto pods = [](const QtyMap& m) {
-        auto it = m.find("pods");
-        return it == m.end() ? 0 : k8s::value(it->second);
-      };
-      int64_t allowed = pods(al) - pods(ad) - pods(ag);  // getAllowedPodNumber (general.go:445-463)
-      s->allowed[r] = allowed > 0 ? allowed : 0;
-      for (auto& kv : al) {  // getMaximumReplicasBasedOnClusterSummary operands (general.go:465-505)
-        k8s::Qty q = kv.second;
-        auto x = ad.find(kv.first);
-        if (x != ad.end()) q.nano -= x->second.nano;
-        x = ag.find(kv.first);
-        if (x != ag.end()) q.nano -= x->second.nano;
-        int64_t v = k8s::value(q);
-        int64_t d = v <= 0 ? 0 : (kv.first == "cpu" ? k8s::milli(q) : v);
-        s->avail[(size_t)s->res.get(kv.first) * Cp + r] = d;
-      }
-      // buildModelNodes (general.go:296-361)
-      if (s->opts.customized_cluster_resource_modeling && c.n_allocatable_modelings > 0 && c.n_resource_models > 0) {
-        bool neg = false;
-        std::map<uint32_t, int64_t> cnt;
-        for (uint32_t i = 0; i < c.n_allocatable_modelings; i++) {
-          if (c.allocatable_modelings[i].count < 0) neg = true;
-          cnt[c.allocatable_modelings[i].grade] += c.allocatable_modelings[i].count;
-        }
-        if (!neg) {
-          std::map<uint32_t, std::vector<int64_t>> caps;
-          for (uint32_t m = 0; m < c.n_resource_models; m++) {
-            std::vector<int64_t> t(R, 0);
-            QtyMap rl;
-            for (uint32_t j = 0; j < c.resource_models[m].n_ranges; j++) {
-              k8s::Qty q;
-              if (!k8s::parse_quantity(S(c.resource_models[m].ranges[j].min), &q)) {
-                e->err = "unparsable resource model quantity";
-                return KP_EINVAL;
-              }
-              rl[S(c.resource_models[m].ranges[j].name)] = q;
-            }
-            for (auto& kv : rl) {  // util.NewResource (resource.go:46-75); pods forced to 110
-              const std::string& nm = kv.first;
-              int32_t rid = s->res.get(nm);
-              if (nm == "cpu") t[rid] += k8s::milli(kv.second);
-              else if (nm == "memory" || nm == "ephemeral-storage") t[rid] += k8s::value(kv.second);
-              else if (nm == "pods") continue;
-              else if (k8s::scalar_resource(nm)) t[rid] += k8s::value(kv.second);
-            }
-            caps[c.resource_models[m].grade] = t;
-          }
-          for (auto& kv : caps) {  // grades ascending
-            auto it = cnt.find(kv.first);
-            int64_t k = it == cnt.end() ? 0 : it->second;
-            if (k == 0) continue;
-            auto ti = tmpl_ids.find(kv.second);
-            int32_t tid;
-            if (ti == tmpl_ids.end()) {
-              tid = (int32_t)tmpl_ids.size();
-              tmpl_ids.emplace(kv.second, tid);
-            } else {
-              tid = ti->second;
-            }
-            s->mgrp_tid.push_back(tid);
-            s->mgrp_cnt.push_back(k);
-          }
-          f |= CF_MODEL_OK;
-        }
-      }
-    }
-    s->mgrp_off[r + 1] = (int32_t)s->mgrp_tid.size();
-    s->flags[r] = f;
+    int rc = pack_row(e, s, cl[order[r]], tmpl_ids, &rows[r]);
+    if (rc) return rc;
   }
-  s->n_tmpl = (int)tmpl_ids.size();
-  s->tmpl.assign((size_t)std::max(s->n_tmpl, 1) * std::max(R, 1), 0);
-  for (auto& kv : tmpl_ids)
-    for (int j = 0; j < R; j++) s->tmpl[(size_t)kv.second * R + j] = kv.first[j];
-  auto pad1 = [](auto& v) {
-    if (v.empty()) v.resize(1);
-  };
-  pad1(s->zone_ids);
-  pad1(s->taint_key);
-  pad1(s->taint_val);
-  pad1(s->taint_eff);
-  // model groups transposed to [kmax][Cp] so a wave reads 64 clusters' k-th group coalesced
-  int& kmax = s->kmax;
-  for (int r = 0; r < C; r++) kmax = std::max(kmax, s->mgrp_off[r + 1] - s->mgrp_off[r]);
-  s->mg_tid.assign((size_t)std::max(kmax, 1) * Cp, 0);
-  s->mg_cnt.assign((size_t)std::max(kmax, 1) * Cp, 0);
-  for (int r = 0; r < C; r++)
-    for (int g = s->mgrp_off[r]; g < s->mgrp_off[r + 1]; g++) {
-      size_t k = (size_t)(g - s->mgrp_off[r]);
-      s->mg_tid[k * Cp + r] = s->mgrp_tid[g];
-      s->mg_cnt[k * Cp + r] = (int32_t)std::min<int64_t>(s->mgrp_cnt[g], kInt32Max);
-    }
+  apply_rows(s, rows, tmpl_ids);
   s->names.resize(C);
   for (int r = 0; r < C; r++) s->names[r] = names[order[r]];
   return upload_snapshot(e, s);
@@ -538,6 +611,7 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
   v.mg_cnt = d_mcnt;
   v.tmpl = d_tmpl;
   v.mt_cnt = d_mt;
+  s->est_kind = snapshot_est_kind(s);
   return KP_OK;
 }
 
@@ -1048,13 +1122,20 @@ int md_cap_of(const kp_snapshot* s) { return s->n_tmpl <= kMdCap ? std::max(kTmp
 // the batch: MaxDivided and taint-set tables fit in LDS, the dense node-count
 // matrix exists (or no cluster has models), at most kReqUnroll resource requests
 // per binding, divisors <= 2^60.
-int pair_kind(const kp_snapshot* s, const kp_batch* bt) {
-  if (md_cap_of(s) == 0 || s->view.n_tsets > kTsetMax || (s->n_tmpl > 0 && !s->view.mt_cnt)) return EST_GENERIC;
+// The snapshot half (its clusters' estimator paths and table sizes), kept in
+// kp_snapshot::est_kind and refreshed by every upload; the batch half
+// (request counts and divisors) in kp_batch::fast_ok. The launch takes
+// est_kind when fast_ok, else EST_GENERIC.
+bool batch_fast_ok(const kp_batch* bt) {
   for (const BindHdr& h : bt->hdr) {
-    if (h.sreq_cnt > kReqUnroll) return EST_GENERIC;
+    if (h.sreq_cnt > kReqUnroll) return false;
     for (int j = 0; j < h.sreq_cnt; j++)
-      if (bt->lpool[h.sreq_q_off + j] > ((int64_t)1 << 60)) return EST_GENERIC;
+      if (bt->lpool[h.sreq_q_off + j] > ((int64_t)1 << 60)) return false;
   }
+  return true;
+}
+int snapshot_est_kind(const kp_snapshot* s) {
+  if (md_cap_of(s) == 0 || s->view.n_tsets > kTsetMax || (s->n_tmpl > 0 && !s->view.mt_cnt)) return EST_GENERIC;
   // which estimator paths the snapshot's clusters can take
   bool any_model = false, any_summary_only = false;
   for (int r = 0; r < s->C; r++) {
@@ -1195,6 +1276,105 @@ int kp_snapshot_create(kp_engine* e, const kp_cluster* clusters, uint64_t n, con
 }
 
 void kp_snapshot_destroy(kp_snapshot* s) { delete s; }
+
+namespace {
+// Rank r's packed row read back from the snapshot's host columns (the inverse
+// of apply_rows), for the clusters an update leaves as they are.
+ClusterRow row_of(const kp_snapshot* s, int r) {
+  ClusterRow w;
+  const int Cp = s->Cp;
+  const int K = (int)s->keys.names.size(), AW = ((int)s->gvk.names.size() + 63) / 64, R = (int)s->res.names.size();
+  w.flags = s->flags[r];
+  w.provider = s->provider[r];
+  w.provider_int = s->provider_int[r];
+  w.region = s->region[r];
+  w.region_int = s->region_int[r];
+  for (int z = s->zone_off[r]; z < s->zone_off[r + 1]; z++) w.zones.push_back(s->zone_ids[z]);
+  for (int k = 0; k < K; k++) {
+    const int32_t v = s->label_val[(size_t)k * Cp + r];
+    if (v >= 0) w.labels.push_back({k, v});
+  }
+  for (int t = s->taint_off[r]; t < s->taint_off[r + 1]; t++)
+    w.taints.push_back({s->taint_key[t], s->taint_val[t], s->taint_eff[t]});
+  for (int wd = 0; wd < AW; wd++) {
+    uint64_t bits = s->api_bits[(size_t)wd * Cp + r];
+    while (bits) {
+      const int b = __builtin_ctzll(bits);
+      w.gvks.push_back(wd * 64 + b);
+      bits &= bits - 1;
+    }
+  }
+  w.allowed = s->allowed[r];
+  for (int j = 0; j < R; j++) {
+    const int64_t a = s->avail[(size_t)j * Cp + r];
+    if (a != 0) w.avail.push_back({j, a});
+  }
+  for (int g = s->mgrp_off[r]; g < s->mgrp_off[r + 1]; g++) w.groups.push_back({s->mgrp_tid[g], s->mgrp_cnt[g]});
+  return w;
+}
+}  // namespace
+
+int kp_snapshot_update(kp_engine* e, kp_snapshot* s, const kp_cluster* clusters, uint64_t n, int* dict_grew) {
+  if (!e || !s || (n && !clusters)) return KP_EINVAL;
+  (void)dev::set_device(e->device);
+  const int C = s->C;
+  std::vector<int64_t> upd(C, -1);
+  for (uint64_t i = 0; i < n; i++) {
+    const std::string name = S(clusters[i].name);
+    auto it = s->rank_of.find(name);
+    if (it == s->rank_of.end()) {
+      e->err = "kp_snapshot_update: no cluster named " + name + " in the snapshot (re-create it to add clusters)";
+      return KP_EINVAL;
+    }
+    if (upd[it->second] >= 0) {
+      e->err = "kp_snapshot_update: cluster " + name + " listed twice";
+      return KP_EINVAL;
+    }
+    upd[it->second] = (int64_t)i;
+  }
+  const size_t n_str = s->str.names.size(), n_keys = s->keys.names.size(), n_gvk = s->gvk.names.size(),
+               n_res = s->res.names.size();
+  std::vector<ClusterRow> rows(C);
+  for (int r = 0; r < C; r++)
+    if (upd[r] < 0) rows[r] = row_of(s, r);
+  // the snapshot's templates by value (trailing zeros dropped, as pack_row keys them)
+  std::map<std::vector<int64_t>, int32_t> tmpl_ids;
+  std::vector<std::vector<int64_t>> tv(s->n_tmpl);
+  {
+    const int R0 = (int)n_res;
+    for (int t = 0; t < s->n_tmpl; t++) {
+      std::vector<int64_t> v(s->tmpl.begin() + (size_t)t * R0, s->tmpl.begin() + (size_t)(t + 1) * R0);
+      while (!v.empty() && v.back() == 0) v.pop_back();
+      tmpl_ids.emplace(v, t);
+      tv[t] = v;
+    }
+  }
+  for (int r = 0; r < C; r++)
+    if (upd[r] >= 0) {
+      const int rc = pack_row(e, s, clusters[upd[r]], tmpl_ids, &rows[r]);
+      if (rc) return rc;  // columns untouched (the dictionaries may hold unused entries)
+    }
+  // templates still in use, renumbered in first-use order
+  tv.resize(tmpl_ids.size());
+  for (auto& kv : tmpl_ids) tv[kv.second] = kv.first;
+  std::vector<int32_t> remap(tv.size(), -1);
+  std::map<std::vector<int64_t>, int32_t> used;
+  for (auto& w : rows)
+    for (auto& g : w.groups) {
+      if (remap[g.first] < 0) {
+        remap[g.first] = (int32_t)used.size();
+        used.emplace(tv[g.first], remap[g.first]);
+      }
+      g.first = remap[g.first];
+    }
+  apply_rows(s, rows, used);
+  s->blob.clear();
+  if (dict_grew)
+    *dict_grew = s->str.names.size() != n_str || s->keys.names.size() != n_keys || s->gvk.names.size() != n_gvk ||
+                 s->res.names.size() != n_res;
+  s->dev.reset();
+  return upload_snapshot(e, s);
+}
 
 int kp_snapshot_export(const kp_snapshot* cs, const void** bytes, uint64_t* n_bytes) {
   if (!cs || !bytes || !n_bytes) return KP_EINVAL;
@@ -1377,7 +1557,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   bt->slow_slot = (bt->slow_slot + 255) & ~(size_t)255;
   // k_slow: one workgroup per CU pass over the flagged bindings (appended on device)
   bt->slow_grid = (int)std::max<size_t>(1, std::min<size_t>(256, bt->l_slow.size()));
-  bt->pair_fast = pair_kind(s, bt);
+  bt->fast_ok = batch_fast_ok(bt);
   Arena& a = bt->dev;
   BindHdr* d_hdr;
   int32_t* d_ipool;
@@ -1505,7 +1685,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   dev::stream_t sp = e->stream2;
   HIPCHK(dev::event_record(e->ev[0], st));
   HIPCHK(dev::stream_wait(sp, e->ev[0]));  // the fills above precede every kernel
-  const int fast = getenv("KP_PAIR_GENERIC") ? EST_GENERIC : bt->pair_fast;
+  const int fast = getenv("KP_PAIR_GENERIC") || !bt->fast_ok ? EST_GENERIC : s->est_kind;
   SelectExtra sx;
   sx.rout = bt->rout;
   sx.rstat = bt->rstat;

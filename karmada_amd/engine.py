@@ -25,14 +25,15 @@ from karmada_amd import api
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libkp.so")
-KP_ABI_VERSION = 2
+KP_ABI_VERSION = 3
 
 _LIBS = {}
 
 # C-ABI entry points declared in include/kp/kp_api.h
 EXPORTS = (
     "kp_abi_version", "kp_engine_create", "kp_engine_destroy", "kp_last_error", "kp_snapshot_create",
-    "kp_snapshot_destroy", "kp_snapshot_export", "kp_snapshot_import", "kp_batch_create", "kp_batch_destroy",
+    "kp_snapshot_destroy", "kp_snapshot_export", "kp_snapshot_import", "kp_snapshot_update", "kp_batch_create",
+    "kp_batch_destroy",
     "kp_schedule_batch", "kp_filter_batch", "kp_score_batch", "kp_max_available_replicas", "kp_last_stage_times",
 )
 
@@ -70,6 +71,7 @@ def load_library(path: str = LIB_PATH):
     L.kp_last_stage_times.argtypes = [vp, C.POINTER(api.kp_stage_times)]
     L.kp_snapshot_export.argtypes = [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
     L.kp_snapshot_import.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(vp)]
+    L.kp_snapshot_update.argtypes = [vp, vp, C.POINTER(api.kp_cluster), C.c_uint64, C.POINTER(C.c_int)]
     if L.kp_abi_version() != KP_ABI_VERSION:
         raise EngineError("libkp.so ABI version mismatch")
     _LIBS[path] = L
@@ -168,6 +170,20 @@ class Snapshot:
         engine._check(engine.L.kp_snapshot_import(engine.h, data, len(data), C.byref(h)), "kp_snapshot_import")
         self.h = h
         return self
+
+    def update_structs(self, ca, n: int) -> bool:
+        """kp_snapshot_update: re-pack the n clusters of `ca` (existing names) in place.
+        Returns True when the dictionaries grew (batches packed before must be re-created)."""
+        grew = C.c_int(0)
+        self.engine._check(self.engine.L.kp_snapshot_update(self.engine.h, self.h, ca, n, C.byref(grew)),
+                           "kp_snapshot_update")
+        return bool(grew.value)
+
+    def update(self, clusters: Sequence[dict]) -> bool:
+        """Cluster events (informer updates) applied to the packed snapshot; see update_structs."""
+        w = api.World()
+        ca, n = w.clusters(clusters)
+        return self.update_structs(ca, n)
 
     def close(self):
         if getattr(self, "h", None):

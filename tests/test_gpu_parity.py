@@ -157,3 +157,21 @@ def test_empty_batch(engine):
     snap = Snapshot.from_structs(engine, u.clusters, u.n_clusters, u.names, api.options())
     b = Batch(snap, structs=(u.bindings, 0))
     assert b.schedule() == []
+
+
+def test_snapshot_update_matches_fresh(engine):
+    """kp_snapshot_update on the device: re-packed rows and the refreshed HBM copy
+    schedule like a snapshot created from the updated cluster list."""
+    from karmada_amd.engine import Batch, Snapshot
+    ua = synth.Universe(6, 61, 300, 0, 1500)
+    ub = synth.Universe(6, 62, 300, 0, 0)
+    opts = api.options()
+    idx = sorted(range(0, 300, 7))
+    sub_arr = (api.kp_cluster * len(idx))(*[ub.clusters[i] for i in idx])
+    mix = (api.kp_cluster * 300)(*[ub.clusters[i] if i in idx else ua.clusters[i] for i in range(300)])
+    snap = Snapshot.from_structs(engine, ua.clusters, ua.n_clusters, ua.names, opts)
+    snap.update_structs(sub_arr, len(idx))
+    got = Batch(snap, structs=ua.binding_slice(0, ua.n_bindings)).schedule()
+    ba, n = ua.binding_slice(0, ua.n_bindings)
+    compare(got, O.schedule_c(mix, 300, ba, n, opts, O.FAST, 8), "snapshot update")
+    snap.close()
