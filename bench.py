@@ -83,6 +83,23 @@ def load_traffic(config, kernel):
         return None, None
 
 
+def select_bytes(n_bindings, n_clusters, n_targets):
+    """Algorithmic bytes of the select stage per batch: each binding reads its feasibility
+    bitmask (C/8) and its calAvailableReplicas row (4*C) plus its packed header, and the
+    results are written as (cluster_idx u32, replicas i32) pairs."""
+    Cp = (n_clusters + 63) // 64 * 64
+    return n_bindings * (Cp / 8.0 + 4.0 * Cp + 144) + 8.0 * n_targets
+
+
+def load_select_pmc(config):
+    """k_select_all's per-launch HBM bytes (FETCH_SIZE + WRITE_SIZE) from the committed PMC summary."""
+    try:
+        with open(os.path.join(ROOT, "profiles", f"r01_pmc_config{config}.json")) as f:
+            return json.load(f).get("k_select_all", {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -166,7 +183,7 @@ def main():
     barrier_sync()
     elapsed = time.perf_counter() - t0
     n_ok = sum(1 for i in range(r.n_bindings) if r.status[i] == 0)
-    n_targets = int(r.n_targets)
+    n_targets = n_targets_rank = int(r.n_targets)
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
@@ -184,7 +201,11 @@ def main():
     avg_pair_ms = sum(pair_ms) / len(pair_ms)  # all pair launches of one step
     achieved = pair_bytes_per_binding(cfg, C_) * B / (avg_pair_ms * 1e-3) / 1e9
     launch_ms = avg_pair_ms / launches
-    traffic, valu = load_traffic(cfg, PAIR_KERNELS.get(kind, "k_pair"))
+    avg_sel_ms = sum(sel_ms) / len(sel_ms)
+    sel_gbs = select_bytes(B, C_, n_targets_rank) / (avg_sel_ms * 1e-3) / 1e9
+    # the committed PMC figures are per launch at the config's default sizes only
+    profiled = (C_, B) == tuple(synth.CONFIGS[cfg])
+    traffic, valu = load_traffic(cfg, PAIR_KERNELS.get(kind, "k_pair")) if profiled else (None, None)
     line = {
         "metric": "ResourceBindings scheduled/sec at 100k bindings x 5k clusters",
         "value": round(value, 1),
@@ -213,6 +234,11 @@ def main():
                      "valu": ({"achieved": round(valu / (launch_ms * 1e-3) / 1e9, 1), "peak": VALU_PEAK_GINST,
                                "unit": "G wave-inst/s", "frac": round(valu / (launch_ms * 1e-3) / 1e9 / VALU_PEAK_GINST, 4)}
                               if valu else None)},
+        # the select stage (k_select_all + k_slow + k_compact, HIP events after the last pair
+        # launch) is the larger share of the step; its byte roofline beside the pair kernel's
+        "select_roofline": {"bound": "hbm", "achieved": round(sel_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(sel_gbs / HBM_PEAK_GBS, 4), "traffic": load_select_pmc(cfg) if profiled else None,
+                            "kernel": "k_select_all", "stage_ms": round(avg_sel_ms, 4)},
         "stages_ms": {"pair_kernel": round(avg_pair_ms, 3), "select_kernels": round(sum(sel_ms) / len(sel_ms), 3),
                       "host_region": round(sum(host_ms) / len(host_ms), 3)},
         "setup_s": {"generate": round(gen_s, 2), "snapshot_pack_upload": round(snap_s, 3),

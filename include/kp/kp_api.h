@@ -31,6 +31,8 @@
  *                                      (pkg/estimator/client/interface.go:39-71,
  *                                       pkg/estimator/client/general.go:57-108)
  *        kp_snapshot_create         <- cache.Cache.Snapshot (pkg/scheduler/cache/cache.go:124-139)
+ *        kp_schedule_affinities     <- Scheduler.scheduleResourceBindingWithClusterAffinities
+ *                                      (pkg/scheduler/scheduler.go:584-585,618-684)
  *
  * Return convention: 0 = OK, <0 = KP_E* ; kp_last_error() gives the text.
  * No exceptions cross the ABI. An engine handle is not re-entrant.
@@ -45,7 +47,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 3
+#define KP_ABI_VERSION 4
 
 /* ------------------------------------------------------------------------- */
 /* Object model                                                              */
@@ -293,6 +295,21 @@ typedef struct kp_results {
   uint64_t n_targets;
 } kp_results;
 
+/* Results of kp_schedule_affinities, engine-owned like kp_results. `results` holds
+ * each binding's final Schedule outcome: the first successful term's targets, or,
+ * when every term failed, the FIRST term's error class/code/arg with no targets
+ * (scheduler.go:657-673). affinity_index[b] = the ClusterAffinities index that
+ * succeeded (its AffinityName becomes Status.SchedulerObservedAffinityName,
+ * scheduler.go:676-678), or -1 when the observed name stays as it was (all terms
+ * failed, or the binding has no ClusterAffinities). attempts[b] = Schedule calls
+ * made for binding b. rounds = batched passes run (1 + the largest retry depth). */
+typedef struct kp_affinity_results {
+  kp_results results;
+  const int32_t* affinity_index;
+  const int32_t* attempts;
+  uint32_t rounds;
+} kp_affinity_results;
+
 /* Per-stage timing of the last kp_schedule_batch call (milliseconds, host clock
  * around device work; kernel-only numbers come from rocprof). */
 typedef struct kp_stage_times {
@@ -358,6 +375,15 @@ void kp_batch_destroy(kp_batch* b);
 
 /* genericScheduler.Schedule for every binding of the batch. */
 int kp_schedule_batch(kp_engine* e, kp_batch* b, kp_results* out);
+
+/* Scheduler.scheduleResourceBindingWithClusterAffinities (scheduler.go:618-684),
+ * batched: bindings with n_cluster_affinities > 0 start at getAffinityIndex of their
+ * observed name (helper.go:99-110; index 0 when util.RescheduleRequired), and every
+ * binding whose term failed is re-packed with the next term's name and scheduled
+ * again in the next round, all failing bindings of a round in one batch. Bindings
+ * without ClusterAffinities run once (scheduleResourceBinding, scheduler.go:584-600). */
+int kp_schedule_affinities(kp_engine* e, const kp_snapshot* s, const kp_binding* bindings, uint64_t n_bindings,
+                           kp_affinity_results* out);
 
 /* FilterPlugin boundary: feasibility of every (binding, cluster) pair after
  * RunFilterPlugins (+ the skip-deleting rule of findClustersThatFit).

@@ -137,6 +137,11 @@ class kp_results(C.Structure):
                 ("cluster_idx", C.POINTER(u32)), ("replicas", C.POINTER(i32)), ("n_targets", u64)]
 
 
+class kp_affinity_results(C.Structure):
+    _fields_ = [("results", kp_results), ("affinity_index", C.POINTER(i32)), ("attempts", C.POINTER(i32)),
+                ("rounds", C.c_uint32)]
+
+
 class kp_stage_times(C.Structure):
     _fields_ = [("pair_ms", C.c_double), ("select_ms", C.c_double), ("host_ms", C.c_double),
                 ("copy_ms", C.c_double), ("total_ms", C.c_double),

@@ -104,6 +104,13 @@ struct kp_engine {
   std::vector<dev::event_t> ev_chunk;  // per chunk: [2i] before, [2i+1] after its pair launch
   std::string err;
   kp_stage_times times{};
+  struct {  // kp_schedule_affinities results
+    std::vector<int32_t> status, err, idx, attempts;
+    std::vector<int64_t> arg;
+    std::vector<uint64_t> offsets;
+    std::vector<uint32_t> cidx;
+    std::vector<int32_t> rep;
+  } aff;
   int n_threads = 8;
   size_t max_lds = 65536;
 };
@@ -1944,3 +1951,114 @@ int kp_last_stage_times(const kp_engine* e, kp_stage_times* out) {
 }
 
 }  // extern "C"
+
+// getAffinityIndex (pkg/scheduler/helper.go:99-110).
+static uint32_t affinity_index_of(const kp_binding& b) {
+  if (!b.observed_affinity_name.ptr || b.observed_affinity_name.len == 0) return 0;
+  const std::string obs(b.observed_affinity_name.ptr, b.observed_affinity_name.len);
+  for (uint32_t i = 0; i < b.n_cluster_affinities; i++) {
+    const kp_str& nm = b.cluster_affinities[i].affinity_name;
+    if (nm.len == obs.size() && (nm.len == 0 || memcmp(nm.ptr, obs.data(), nm.len) == 0)) return i;
+  }
+  return 0;
+}
+
+int kp_schedule_affinities(kp_engine* e, const kp_snapshot* s, const kp_binding* bs, uint64_t n,
+                           kp_affinity_results* out) {
+  if (!e || !s || !out || (n && !bs)) return KP_EINVAL;
+  auto& A = e->aff;
+  A.status.assign(n, KP_STATUS_OK);
+  A.err.assign(n, KP_ERR_NONE);
+  A.arg.assign(n, 0);
+  A.idx.assign(n, -1);
+  A.attempts.assign(n, 0);
+  // per binding: current term, first error seen, and its final (offset, count) in `pool`
+  std::vector<uint32_t> cur(n, 0);
+  std::vector<uint8_t> have_first(n, 0);
+  std::vector<uint64_t> f_off(n, 0), f_cnt(n, 0);
+  std::vector<uint32_t> pool_idx;
+  std::vector<int32_t> pool_rep;
+  std::vector<uint64_t> pending(n);
+  for (uint64_t i = 0; i < n; i++) {
+    pending[i] = i;
+    const kp_binding& b = bs[i];
+    if (b.n_cluster_affinities == 0) continue;
+    cur[i] = affinity_index_of(b);
+    if (b.has_reschedule_triggered_at && b.has_last_scheduled_time &&
+        b.reschedule_triggered_at_ns > b.last_scheduled_time_ns)  // util.RescheduleRequired (binding.go:118-127)
+      cur[i] = 0;
+  }
+  uint32_t rounds = 0;
+  std::vector<kp_binding> sub;
+  while (!pending.empty()) {
+    rounds++;
+    sub.resize(pending.size());
+    for (size_t j = 0; j < pending.size(); j++) {
+      sub[j] = bs[pending[j]];
+      if (sub[j].n_cluster_affinities)  // updatedStatus.SchedulerObservedAffinityName (scheduler.go:640)
+        sub[j].observed_affinity_name = sub[j].cluster_affinities[cur[pending[j]]].affinity_name;
+    }
+    kp_batch* bt = nullptr;
+    int rc = kp_batch_create(e, s, sub.data(), sub.size(), &bt);
+    if (rc) return rc;
+    kp_results r{};
+    rc = kp_schedule_batch(e, bt, &r);
+    if (rc) {
+      kp_batch_destroy(bt);
+      return rc;
+    }
+    std::vector<uint64_t> next;
+    for (size_t j = 0; j < pending.size(); j++) {
+      const uint64_t i = pending[j];
+      const kp_binding& b = bs[i];
+      A.attempts[i]++;
+      const bool ok = r.status[j] == KP_STATUS_OK;
+      if (ok || b.n_cluster_affinities == 0) {
+        A.status[i] = r.status[j];
+        A.err[i] = r.err_code[j];
+        A.arg[i] = r.err_arg[j];
+        if (b.n_cluster_affinities && ok) A.idx[i] = (int32_t)cur[i];
+        f_off[i] = pool_idx.size();
+        f_cnt[i] = r.offsets[j + 1] - r.offsets[j];
+        pool_idx.insert(pool_idx.end(), r.cluster_idx + r.offsets[j], r.cluster_idx + r.offsets[j + 1]);
+        pool_rep.insert(pool_rep.end(), r.replicas + r.offsets[j], r.replicas + r.offsets[j + 1]);
+        continue;
+      }
+      if (!have_first[i]) {  // firstErr (scheduler.go:646-649)
+        have_first[i] = 1;
+        A.status[i] = r.status[j];
+        A.err[i] = r.err_code[j];
+        A.arg[i] = r.err_arg[j];
+      }
+      if (++cur[i] < b.n_cluster_affinities) next.push_back(i);
+    }
+    kp_batch_destroy(bt);
+    pending.swap(next);
+  }
+  A.offsets.assign(n + 1, 0);
+  uint64_t tot = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    A.offsets[i] = tot;
+    tot += f_cnt[i];
+  }
+  A.offsets[n] = tot;
+  A.cidx.resize(std::max<uint64_t>(1, tot));
+  A.rep.resize(std::max<uint64_t>(1, tot));
+  for (uint64_t i = 0; i < n; i++)
+    for (uint64_t k = 0; k < f_cnt[i]; k++) {
+      A.cidx[A.offsets[i] + k] = pool_idx[f_off[i] + k];
+      A.rep[A.offsets[i] + k] = pool_rep[f_off[i] + k];
+    }
+  out->results.n_bindings = n;
+  out->results.status = A.status.data();
+  out->results.err_code = A.err.data();
+  out->results.err_arg = A.arg.data();
+  out->results.offsets = A.offsets.data();
+  out->results.cluster_idx = A.cidx.data();
+  out->results.replicas = A.rep.data();
+  out->results.n_targets = tot;
+  out->affinity_index = A.idx.data();
+  out->attempts = A.attempts.data();
+  out->rounds = rounds;
+  return KP_OK;
+}

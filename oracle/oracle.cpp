@@ -2054,23 +2054,77 @@ kpo_world* kpo_world_create(const kp_cluster* clusters, uint64_t n, const kp_opt
 
 void kpo_world_destroy(kpo_world* w) { delete w; }
 
-int kpo_schedule(kpo_world* k, const kp_binding* b, uint64_t n, int mode, int n_threads, kpo_results** outp) {
-  vector<ScheduleOut> res(n);
+}  // extern "C"
+
+namespace {
+// Runs fn(i) for i in [0, n) on n_threads host threads.
+template <class F>
+void ParallelFor(uint64_t n, int n_threads, F fn) {
   if (n_threads <= 1) {
-    for (uint64_t i = 0; i < n; i++) res[i] = Schedule(k->w, convBinding(b[i]), mode);
-  } else {
-    std::atomic<uint64_t> next(0);
-    vector<std::thread> th;
-    for (int t = 0; t < n_threads; t++)
-      th.emplace_back([&]() {
-        for (;;) {
-          uint64_t i = next.fetch_add(1);
-          if (i >= n) break;
-          res[i] = Schedule(k->w, convBinding(b[i]), mode);
-        }
-      });
-    for (auto& t : th) t.join();
+    for (uint64_t i = 0; i < n; i++) fn(i);
+    return;
   }
+  std::atomic<uint64_t> next(0);
+  vector<std::thread> th;
+  for (int t = 0; t < n_threads; t++)
+    th.emplace_back([&]() {
+      for (;;) {
+        uint64_t i = next.fetch_add(1);
+        if (i >= n) break;
+        fn(i);
+      }
+    });
+  for (auto& t : th) t.join();
+}
+
+// getAffinityIndex (pkg/scheduler/helper.go:99-110).
+uint32_t GetAffinityIndex(const kp_binding& b) {
+  string obs = S(b.observed_affinity_name);
+  if (obs.empty()) return 0;
+  for (uint32_t i = 0; i < b.n_cluster_affinities; i++)
+    if (S(b.cluster_affinities[i].affinity_name) == obs) return i;
+  return 0;
+}
+
+// Scheduler.scheduleResourceBindingWithClusterAffinities (pkg/scheduler/scheduler.go:618-684):
+// try the terms from the observed one on; the first success wins; when every term
+// fails the FIRST error is the binding's result (FitError -> empty result patched,
+// other errors returned as is; both are "no targets" here). *aff = the term index
+// that succeeded, or -1 (SchedulerObservedAffinityName left unchanged).
+// Bindings with no ClusterAffinities take scheduleResourceBinding (scheduler.go:584-585).
+// The StaticWeight WeightPreference mutation (assignment.go:202-204) happens
+// only on an attempt that then succeeds, so it is never seen by a later term here.
+ScheduleOut ScheduleWithAffinities(const World& w, const kp_binding& b0, int mode, int32_t* aff, int32_t* attempts) {
+  *aff = -1;
+  *attempts = 1;
+  if (b0.n_cluster_affinities == 0) return Schedule(w, convBinding(b0), mode);
+  uint32_t idx = GetAffinityIndex(b0);
+  if (b0.has_reschedule_triggered_at && b0.has_last_scheduled_time &&
+      b0.reschedule_triggered_at_ns > b0.last_scheduled_time_ns)  // util.RescheduleRequired (binding.go:118-127)
+    idx = 0;
+  ScheduleOut first;
+  bool have_first = false;
+  *attempts = 0;
+  for (; idx < b0.n_cluster_affinities; idx++) {
+    kp_binding b = b0;
+    b.observed_affinity_name = b0.cluster_affinities[idx].affinity_name;
+    ScheduleOut o = Schedule(w, convBinding(b), mode);
+    (*attempts)++;
+    if (o.status == KP_STATUS_OK) {
+      *aff = (int32_t)idx;
+      return o;
+    }
+    if (!have_first) {
+      first = o;
+      have_first = true;
+    }
+  }
+  first.targets.clear();
+  return first;
+}
+
+kpo_results* PackResults(const vector<ScheduleOut>& res) {
+  const uint64_t n = res.size();
   auto* r = (kpo_results*)calloc(1, sizeof(kpo_results));
   r->n = n;
   r->status = (int32_t*)malloc(sizeof(int32_t) * (n + 1));
@@ -2095,7 +2149,26 @@ int kpo_schedule(kpo_world* k, const kp_binding* b, uint64_t n, int mode, int n_
   }
   r->offsets[n] = o;
   r->n_targets = o;
-  *outp = r;
+  return r;
+}
+}  // namespace
+
+extern "C" {
+
+int kpo_schedule(kpo_world* k, const kp_binding* b, uint64_t n, int mode, int n_threads, kpo_results** outp) {
+  vector<ScheduleOut> res(n);
+  ParallelFor(n, n_threads, [&](uint64_t i) { res[i] = Schedule(k->w, convBinding(b[i]), mode); });
+  *outp = PackResults(res);
+  return 0;
+}
+
+int kpo_schedule_affinities(kpo_world* k, const kp_binding* b, uint64_t n, int mode, int n_threads,
+                            kpo_results** outp, int32_t* affinity_index, int32_t* attempts) {
+  vector<ScheduleOut> res(n);
+  ParallelFor(n, n_threads, [&](uint64_t i) {
+    res[i] = ScheduleWithAffinities(k->w, b[i], mode, &affinity_index[i], &attempts[i]);
+  });
+  *outp = PackResults(res);
   return 0;
 }
 

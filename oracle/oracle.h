@@ -66,6 +66,10 @@ void kpo_world_destroy(kpo_world* w);
 /* Schedule bindings with `n_threads` host threads (<=0: 1). */
 int kpo_schedule(kpo_world* w, const kp_binding* b, uint64_t n, int mode, int n_threads,
                  kpo_results** out);
+/* Scheduler.scheduleResourceBindingWithClusterAffinities (scheduler.go:618-684) per binding:
+ * affinity_index[i] = term that succeeded or -1, attempts[i] = Schedule calls made. */
+int kpo_schedule_affinities(kpo_world* w, const kp_binding* b, uint64_t n, int mode, int n_threads,
+                            kpo_results** out, int32_t* affinity_index, int32_t* attempts);
 void kpo_results_free(kpo_results* r);
 
 /* ---- unit hooks used by the golden-vector tests ---- */

@@ -36,6 +36,9 @@ def lib():
     L.kpo_world_destroy.argtypes = [C.c_void_p]
     L.kpo_schedule.argtypes = [C.c_void_p, C.POINTER(api.kp_binding), C.c_uint64, C.c_int, C.c_int,
                                C.POINTER(C.POINTER(kpo_results))]
+    L.kpo_schedule_affinities.argtypes = [C.c_void_p, C.POINTER(api.kp_binding), C.c_uint64, C.c_int, C.c_int,
+                                          C.POINTER(C.POINTER(kpo_results)), C.POINTER(C.c_int32),
+                                          C.POINTER(C.c_int32)]
     L.kpo_results_free.argtypes = [C.POINTER(kpo_results)]
     L.kpo_quantity.argtypes = [C.c_char_p, C.c_uint32, C.c_int, C.POINTER(C.c_int64)]
     L.kpo_cluster_matches.argtypes = [C.POINTER(api.kp_cluster), C.POINTER(api.kp_cluster_affinity)]
@@ -91,5 +94,22 @@ def schedule_c(ca, nc, ba, nb, opts, mode=FAITHFUL, threads=1):
         out = api.results_to_python(r.status, r.err_code, r.err_arg, r.offsets, r.cluster_idx, r.replicas, r.n)
         L.kpo_results_free(rp)
         return out
+    finally:
+        L.kpo_world_destroy(world)
+
+
+def schedule_affinities_c(ca, nc, ba, nb, opts, mode=FAITHFUL, threads=1):
+    """scheduleResourceBindingWithClusterAffinities per binding: (results, affinity_index, attempts)."""
+    L = lib()
+    world = L.kpo_world_create(ca, nc, C.byref(opts))
+    try:
+        rp = C.POINTER(kpo_results)()
+        aff = (C.c_int32 * max(1, nb))()
+        att = (C.c_int32 * max(1, nb))()
+        L.kpo_schedule_affinities(world, ba, nb, mode, threads, C.byref(rp), aff, att)
+        r = rp.contents
+        out = api.results_to_python(r.status, r.err_code, r.err_arg, r.offsets, r.cluster_idx, r.replicas, r.n)
+        L.kpo_results_free(rp)
+        return out, list(aff[:nb]), list(att[:nb])
     finally:
         L.kpo_world_destroy(world)
