@@ -1543,9 +1543,14 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   pad1(bt->instrs);
   const int B = bt->B ? bt->B : 1;
   const int nr = (int)bt->l_region.size(), R = std::max(1, s->view.n_regions);
-  int max_tgt = 0;
-  for (auto& h : bt->hdr) max_tgt = std::max(max_tgt, (int)h.tgt_cnt);
-  bt->slow_cap = s->Cp + max_tgt + 64;
+  int max_tgt = 0, max_tiers = 1;
+  for (auto& h : bt->hdr) {
+    max_tgt = std::max(max_tgt, (int)h.tgt_cnt);
+    max_tiers = std::max(max_tiers, (int)h.ovf_cnt + 2);  // primary, each overflow term, unmatched (1000)
+  }
+  // SerialAssign's result list: every candidate once, plus, per overflow tier, the
+  // spec.Clusters entries MergeTargetClusters appends (common.go:97-139; util/binding.go:91-115).
+  bt->slow_cap = s->Cp + max_tiers * max_tgt + 64;
   {  // LDS for the targets-only serial problems (scale-down), if small
     size_t b = sizeof(Item) * (size_t)max_tgt + serial_scratch_bytes(2 * max_tgt + 16) + 64;
     bt->slow_lds = b <= 32768 ? (int)((b + 15) & ~(size_t)15) : 0;

@@ -19,6 +19,16 @@
 using namespace kp;
 
 #define KP_SMEM extern __shared__ __align__(16) unsigned char smem[]
+// k_select_all: workgroup size bound and minimum waves per SIMD. Its LDS (~53 KB at
+// C = 5k with KP_ECAP_MAX = 1024) allows 3 workgroups of 512 threads per CU, i.e. 6
+// waves per SIMD; asking the compiler for 6 keeps the VGPRs at <= 80 so that those 3
+// workgroups are resident together (89 VGPRs allowed only 2: 5.5 -> 4.2 ms at config 3).
+#ifndef KP_SEL_MAX_THREADS
+#define KP_SEL_MAX_THREADS 512
+#endif
+#ifndef KP_SEL_MIN_WAVES
+#define KP_SEL_MIN_WAVES 6
+#endif
 
 extern "C" __global__ void __launch_bounds__(kBlock) k_pair(SnapView s, BatchView bv, int b0, uint64_t* fmask,
                                                             int32_t* est, int64_t* score, int est_mode, int md_cap) {
@@ -36,7 +46,7 @@ KP_PAIR_FAST(k_pair_fast, EST_MIXED)
 KP_PAIR_FAST(k_pair_fast_summary, EST_SUMMARY)
 KP_PAIR_FAST(k_pair_fast_m8, EST_MODEL8)
 KP_PAIR_FAST(k_pair_fast_m16, EST_MODEL16)
-extern "C" __global__ void __launch_bounds__(1024) k_select_all(KArgs a) {
+extern "C" __global__ void __launch_bounds__(KP_SEL_MAX_THREADS, KP_SEL_MIN_WAVES) k_select_all(KArgs a) {
   KP_SMEM;
   body_select_all(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a);
 }
@@ -89,7 +99,7 @@ int sel_threads() {
   static int n = [] {
     const char* e = getenv("KP_SEL_THREADS");
     int v = e ? atoi(e) : 512;
-    return (v == 256 || v == 512 || v == 1024) ? v : 512;
+    return (v == 256 || v == 512) && v <= KP_SEL_MAX_THREADS ? v : 512;
   }();
   return n;
 }

@@ -30,8 +30,13 @@ struct SerialScratch {
   int32_t* pos;                  // optional rank-indexed scratch (all -1 between uses)
   int presorted;                 // an/ar already hold the sorted TargetClustersList (body_slow)
 };
+// Bytes serial_scratch_carve takes: 2 i64 arrays, the tier list and 15 u32 arrays of
+// `cap` entries, each rounded up to 16 B. (This once counted 14 u32 arrays: the last
+// one, rr, ran 4*cap bytes past a k_slow slot into the next workgroup's.)
 KP_HD inline size_t serial_scratch_bytes(int cap) {
-  return (size_t)cap * (sizeof(Item) + 2 * sizeof(int64_t) + 14 * sizeof(uint32_t)) + 256;
+  const size_t c = (size_t)cap;
+  auto r16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  return 2 * r16(c * sizeof(int64_t)) + r16(c * sizeof(Item)) + 15 * r16(c * sizeof(uint32_t)) + 16;
 }
 KP_HD inline SerialScratch serial_scratch_carve(void* mem, int cap) {
   SerialScratch s;

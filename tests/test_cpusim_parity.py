@@ -65,3 +65,15 @@ def test_cpusim_options(engine, prop, plugins, gate):
     ba, n = u.binding_slice(0, u.n_bindings)
     want = O.schedule_c(u.clusters, u.n_clusters, ba, n, opts, O.FAST, 8)
     compare(run(engine, u, opts), want, f"options {prop} {plugins} {gate}")
+
+
+def test_cpusim_overflow_tiers_large_c(engine):
+    """Config 6 at C = 5000: overflow-tier bindings take k_slow's exact serial path with
+    candidate lists of ~5k, run by 8 concurrent host 'workgroups'. Guards the serial
+    scratch sizing (serial_scratch_bytes once undercounted its u32 arrays, so a slot's
+    result list ran into the next workgroup's slot)."""
+    u = synth.Universe(6, 13, 5000, 0, 4000)
+    opts = api.options()
+    ba, n = u.binding_slice(0, 4000)
+    want = O.schedule_c(u.clusters, u.n_clusters, ba, n, opts, O.FAST, 8)
+    compare(run(engine, u, opts, 0, 4000), want, "config 6 seed 13 C=5000")
