@@ -77,6 +77,8 @@ int alloc(void** p, size_t bytes) {
   return *p ? 0 : -1;
 }
 void release(void* p) { free(p); }
+int host_alloc(void** p, size_t bytes) { return alloc(p, bytes); }
+void host_release(void* p) { free(p); }
 int h2d(void* dst, const void* src, size_t bytes, stream_t) {
   if (bytes) memcpy(dst, src, bytes);
   return 0;

@@ -179,8 +179,15 @@ struct kp_batch {
   std::vector<int32_t> h_status, h_err, h_rstat, h_rsel, h_rnsel;
   std::vector<int64_t> h_arg;
   std::vector<uint64_t> h_start, h_offsets;
-  std::vector<uint32_t> h_count, h_cidx;
-  std::vector<int32_t> h_crep;
+  std::vector<uint32_t> h_count;
+  // result CSR in page-locked host memory (h_res_cap entries each)
+  uint32_t* h_cidx = nullptr;
+  int32_t* h_crep = nullptr;
+  uint64_t h_res_cap = 0;
+  ~kp_batch() {
+    dev::host_release(h_cidx);
+    dev::host_release(h_crep);
+  }
   std::vector<RegionOut> h_rout;
 };
 
@@ -1832,11 +1839,22 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   HIPCHK(dev::h2d(bt->offsets_d, bt->h_offsets.data(), 8 * (size_t)(B + 1), st));
   HIPCHK(dev::h2d(bt->count, bt->h_count.data(), 4 * (size_t)B, st));
   HIPCHK(dev::compact(st, bt->start, bt->count, bt->offsets_d, bt->out_idx, bt->out_rep, bt->cidx_d, bt->crep_d, B));
-  bt->h_cidx.resize(std::max<uint64_t>(1, tot));
-  bt->h_crep.resize(std::max<uint64_t>(1, tot));
+  if (tot > bt->h_res_cap || !bt->h_cidx) {
+    dev::host_release(bt->h_cidx);
+    dev::host_release(bt->h_crep);
+    bt->h_cidx = nullptr;
+    bt->h_crep = nullptr;
+    bt->h_res_cap = 0;
+    const uint64_t cap = std::max<uint64_t>(1, tot + tot / 4);  // headroom for repeated calls
+    if (dev::host_alloc((void**)&bt->h_cidx, 4 * cap) || dev::host_alloc((void**)&bt->h_crep, 4 * cap)) {
+      e->err = "kp_schedule_batch: page-locked result buffers";
+      return KP_ENOMEM;
+    }
+    bt->h_res_cap = cap;
+  }
   if (tot) {
-    HIPCHK(dev::d2h(bt->h_cidx.data(), bt->cidx_d, 4 * tot, st));
-    HIPCHK(dev::d2h(bt->h_crep.data(), bt->crep_d, 4 * tot, st));
+    HIPCHK(dev::d2h(bt->h_cidx, bt->cidx_d, 4 * tot, st));
+    HIPCHK(dev::d2h(bt->h_crep, bt->crep_d, 4 * tot, st));
   }
   HIPCHK(dev::sync(st));
   double t1 = now_ms();
@@ -1878,8 +1896,8 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   out->err_code = bt->h_err.data();
   out->err_arg = bt->h_arg.data();
   out->offsets = bt->h_offsets.data();
-  out->cluster_idx = bt->h_cidx.data();
-  out->replicas = bt->h_crep.data();
+  out->cluster_idx = bt->h_cidx;
+  out->replicas = bt->h_crep;
   out->n_targets = tot;
   return KP_OK;
 }

@@ -149,6 +149,10 @@ float event_ms(event_t a, event_t b) {
 
 int alloc(void** p, size_t bytes) { return chk(hipMalloc(p, bytes)); }
 void release(void* p) { (void)hipFree(p); }
+int host_alloc(void** p, size_t bytes) { return chk(hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault)); }
+void host_release(void* p) {
+  if (p) (void)hipHostFree(p);
+}
 int h2d(void* dst, const void* src, size_t bytes, stream_t s) {
   return bytes ? chk(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)s)) : 0;
 }

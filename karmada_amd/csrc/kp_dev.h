@@ -33,6 +33,9 @@ float event_ms(event_t a, event_t b);
 
 int alloc(void** p, size_t bytes);
 void release(void* p);
+// Page-locked host memory: the result copy-back DMAs straight into it.
+int host_alloc(void** p, size_t bytes);
+void host_release(void* p);
 int h2d(void* dst, const void* src, size_t bytes, stream_t s);  // stream-ordered
 int d2h(void* dst, const void* src, size_t bytes, stream_t s);
 int fill(void* dst, int value, size_t bytes, stream_t s);
