@@ -23,6 +23,9 @@ using namespace kp;
 // C = 5k with KP_ECAP_MAX = 1024) allows 3 workgroups of 512 threads per CU, i.e. 6
 // waves per SIMD; asking the compiler for 6 keeps the VGPRs at <= 80 so that those 3
 // workgroups are resident together (89 VGPRs allowed only 2: 5.5 -> 4.2 ms at config 3).
+#ifndef KP_PAIR_MIN_WAVES
+#define KP_PAIR_MIN_WAVES 1
+#endif
 #ifndef KP_SEL_MAX_THREADS
 #define KP_SEL_MAX_THREADS 512
 #endif
@@ -37,7 +40,8 @@ extern "C" __global__ void __launch_bounds__(kBlock) k_pair(SnapView s, BatchVie
                          md_cap);
 }
 #define KP_PAIR_FAST(NAME, KIND)                                                                                \
-  extern "C" __global__ void __launch_bounds__(kBlock) NAME(SnapView s, BatchView bv, int b0, uint64_t* fmask, \
+  extern "C" __global__ void __launch_bounds__(kBlock, KP_PAIR_MIN_WAVES) NAME(SnapView s, BatchView bv, int b0, \
+                                                                              uint64_t* fmask, \
                                                             int32_t* est, int md_cap) {                       \
     KP_SMEM;                                                                                                  \
     body_pair<KIND>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, b0, fmask, est, nullptr, 0, md_cap); \
