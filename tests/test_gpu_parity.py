@@ -69,6 +69,9 @@ CASES = [
     (7, 18, 13, 2000),
     (7, 19, 100, 2000),
     (7, 20, 5000, 1000),
+    # overflow tiers with ~5k-entry serial lists in many concurrent k_slow workgroups
+    # (the serial scratch sizing fix)
+    (6, 13, 5000, 4000),
 ]
 
 
