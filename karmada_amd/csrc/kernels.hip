@@ -23,6 +23,7 @@ using namespace kp;
 // C = 5k with KP_ECAP_MAX = 1024) allows 3 workgroups of 512 threads per CU, i.e. 6
 // waves per SIMD; asking the compiler for 6 keeps the VGPRs at <= 80 so that those 3
 // workgroups are resident together (89 VGPRs allowed only 2: 5.5 -> 4.2 ms at config 3).
+constexpr size_t kLdsPerCu = 160 * 1024;  // gfx950 LDS per CU
 #ifndef KP_PAIR_MIN_WAVES
 #define KP_PAIR_MIN_WAVES 1
 #endif
@@ -51,6 +52,12 @@ KP_PAIR_FAST(k_pair_fast_summary, EST_SUMMARY)
 KP_PAIR_FAST(k_pair_fast_m8, EST_MODEL8)
 KP_PAIR_FAST(k_pair_fast_m16, EST_MODEL16)
 extern "C" __global__ void __launch_bounds__(KP_SEL_MAX_THREADS, KP_SEL_MIN_WAVES) k_select_all(KArgs a) {
+  KP_SMEM;
+  body_select_all(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a);
+}
+// Large snapshots (C ~ 10k): the candidate arrays alone take 8 B per cluster, so a
+// single workgroup fits a CU; 1024 threads then keep 16 waves in flight instead of 8.
+extern "C" __global__ void __launch_bounds__(1024) k_select_all_wide(KArgs a) {
   KP_SMEM;
   body_select_all(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a);
 }
@@ -189,7 +196,10 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
   hipStream_t h = (hipStream_t)st;
   switch (which) {
     case SEL_LAUNCH_ALL:
-      hipLaunchKernelGGL(k_select_all, dim3(a.n), dim3(sel_threads()), smem, h, a);
+      if (smem > kLdsPerCu / 2 && !getenv("KP_SEL_THREADS"))  // one workgroup per CU: go wide
+        hipLaunchKernelGGL(k_select_all_wide, dim3(a.n), dim3(1024), smem, h, a);
+      else
+        hipLaunchKernelGGL(k_select_all, dim3(a.n), dim3(sel_threads()), smem, h, a);
       break;
     case SEL_LAUNCH_CLUSTER:
       hipLaunchKernelGGL(k_select_cluster, dim3(a.n), dim3(kBlock), smem, h, a, cap);

@@ -72,6 +72,9 @@ CASES = [
     # overflow tiers with ~5k-entry serial lists in many concurrent k_slow workgroups
     # (the serial scratch sizing fix)
     (6, 13, 5000, 4000),
+    # C > ~8.6k: k_select_all's LDS leaves one workgroup per CU -> k_select_all_wide
+    (6, 21, 9000, 1000),
+    (7, 22, 9000, 600),
 ]
 
 
