@@ -147,7 +147,10 @@ typedef struct kp_binding {
   kp_str name;
   int32_t replicas;
   uint8_t has_replica_requirements; /* spec.ReplicaRequirements != nil */
-  uint8_t has_node_claim;           /* ReplicaRequirements.NodeClaim != nil */
+  uint8_t has_node_claim;           /* ReplicaRequirements.NodeClaim != nil: no effect on the
+                                       general estimator (a NodeClaim converts without error and
+                                       every model node matches it, accurate.go:155-177,
+                                       scheduling_simulator_components.go:149-153) */
   const kp_resource* resource_request;
   uint32_t n_resource_request;
   uint32_t n_components; /* len(spec.Components) */
@@ -359,9 +362,12 @@ void kp_snapshot_destroy(kp_snapshot* s);
  * device copy is refreshed. This replaces re-snapshotting all clusters on every
  * informer event (cache.go:124-139, event_handler.go:314-378). *dict_grew = 1
  * when the update added names, keys, GVKs or resources to the snapshot's
- * dictionaries: batches packed before the call must then be re-created (their
- * compiled selectors resolve strings against the old dictionaries); otherwise
- * they stay valid. Adding or removing clusters needs kp_snapshot_create. */
+ * dictionaries or changed its set of regions: batches packed before the call
+ * must then be re-created (their compiled selectors resolve strings against the
+ * old dictionaries; their region buffers are sized by the region count), and
+ * kp_schedule_batch returns KP_ESTATE for a region-spread batch whose region
+ * count no longer matches; otherwise they stay valid. Adding or removing
+ * clusters needs kp_snapshot_create. */
 int kp_snapshot_update(kp_engine* e, kp_snapshot* s, const kp_cluster* clusters, uint64_t n_clusters,
                        int* dict_grew);
 /* Packed snapshot as one relocatable byte image (for RCCL broadcast) and back. */

@@ -175,6 +175,7 @@ struct kp_batch {
   size_t slow_slot = 0;
   int slow_grid = 0, slow_cap = 0, slow_lds = 0, slow_sort = 0;
   bool fast_ok = false;  // the batch half of the fast pair-kernel condition (batch_fast_ok)
+  int n_regions = 0;     // the snapshot's region count the region buffers were sized for
   // host results
   std::vector<int32_t> h_status, h_err, h_rstat, h_rsel, h_rnsel;
   std::vector<int64_t> h_arg;
@@ -440,7 +441,6 @@ int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_opti
   s->Cp = ((C + 63) / 64) * 64;
   if (s->Cp == 0) s->Cp = 64;
   s->W = s->Cp / 64;
-  const int Cp = s->Cp;
   std::vector<uint32_t> order(C);
   std::vector<std::string> names(C);
   for (int i = 0; i < C; i++) {
@@ -1148,6 +1148,23 @@ bool batch_fast_ok(const kp_batch* bt) {
   }
   return true;
 }
+// The largest dynamic LDS any kernel of the batch takes must fit one workgroup.
+// Checked at kp_batch_create and again at every kp_schedule_batch: an
+// intervening kp_snapshot_update can change the region and template counts the
+// sizes depend on.
+int batch_lds_check(kp_engine* e, const kp_snapshot* s, const kp_batch* bt) {
+  const int cap = kSmallMax + kTgtSmallMax + 16;
+  size_t need = smem_pair(s, md_cap_of(s));
+  if (!bt->l_all.empty()) need = std::max(need, smem_all(s));
+  if (!bt->l_cluster.empty()) need = std::max(need, smem_cluster(s, cap));
+  if (!bt->l_region.empty()) need = std::max({need, smem_region_a(s), smem_region_b(s, cap)});
+  if (need > e->max_lds) {
+    e->err = "snapshot too large for one workgroup's LDS (" + std::to_string(need) + " > " +
+             std::to_string(e->max_lds) + " bytes)";
+    return -1;
+  }
+  return 0;
+}
 int snapshot_est_kind(const kp_snapshot* s) {
   if (md_cap_of(s) == 0 || s->view.n_tsets > kTsetMax || (s->n_tmpl > 0 && !s->view.mt_cnt)) return EST_GENERIC;
   // which estimator paths the snapshot's clusters can take
@@ -1167,7 +1184,7 @@ int snapshot_est_kind(const kp_snapshot* s) {
 // Packed-snapshot bytes: pack once on one rank, broadcast the bytes, import on
 // the others. Host-endian; same engine build on every rank.
 namespace {
-const char kSnapMagic[8] = {'K', 'P', 'S', 'N', 'A', 'P', '0', '1'};
+const char kSnapMagic[8] = {'K', 'P', 'S', 'N', 'A', 'P', '0', '2'};
 struct Wr {
   std::vector<unsigned char>& b;
   void raw(const void* p, size_t n) { b.insert(b.end(), (const unsigned char*)p, (const unsigned char*)p + n); }
@@ -1232,6 +1249,66 @@ struct Rd {
 };
 void dict_from(Dict& d, const std::vector<std::string>& names) {
   for (auto& n : names) d.add(n);
+}
+
+// Every column of an imported snapshot against the sizes and id ranges the
+// kernels and kp_snapshot_update index with (a foreign or corrupt image must
+// fail here, not fault in a kernel).
+bool snapshot_consistent(const kp_snapshot* s) {
+  const int C = s->C;
+  if (C < 0 || C > kMaxClusters) return false;
+  const size_t Cp = (size_t)s->Cp, C1 = (size_t)C + 1;
+  const int K = (int)s->keys.names.size(), AW = ((int)s->gvk.names.size() + 63) / 64, R = (int)s->res.names.size();
+  const int NS = (int)s->str.names.size(), NR = (int)s->regions.names.size(), T = s->n_tmpl, km = s->kmax;
+  if ((int)s->names.size() != C || s->perm.size() != (size_t)C || T < 0 || km < 0) return false;
+  if (s->str.names.size() != s->str.m.size() || s->keys.names.size() != s->keys.m.size() ||
+      s->gvk.names.size() != s->gvk.m.size() || s->res.names.size() != s->res.m.size() ||
+      s->regions.names.size() != s->regions.m.size())
+    return false;  // duplicate dictionary entries
+  for (int r = 1; r < C; r++)
+    if (!(s->names[r - 1] < s->names[r])) return false;  // ranks are name order, names unique
+  std::vector<char> seen(C, 0);
+  for (uint32_t p : s->perm) {
+    if (p >= (uint32_t)C || seen[p]) return false;
+    seen[p] = 1;
+  }
+  for (size_t n : {s->flags.size(), s->provider.size(), s->region.size(), s->region_idx.size(),
+                   s->provider_int.size(), s->region_int.size(), s->allowed.size()})
+    if (n != Cp) return false;
+  if (s->label_val.size() != (size_t)std::max(K, 1) * Cp || s->api_bits.size() != (size_t)std::max(AW, 1) * Cp ||
+      s->avail.size() != (size_t)std::max(R, 1) * Cp || s->tmpl.size() != (size_t)std::max(T, 1) * std::max(R, 1) ||
+      s->mg_tid.size() != (size_t)std::max(km, 1) * Cp || s->mg_cnt.size() != s->mg_tid.size())
+    return false;
+  if (s->taint_val.size() != s->taint_key.size() || s->taint_eff.size() != s->taint_key.size() ||
+      s->mgrp_cnt.size() != s->mgrp_tid.size())
+    return false;
+  auto offsets_ok = [&](const std::vector<int32_t>& off, size_t pool) {
+    if (off.size() != C1 || off[0] != 0 || (size_t)off[C] > pool) return false;
+    for (int r = 0; r < C; r++)
+      if (off[r + 1] < off[r]) return false;
+    return true;
+  };
+  if (!offsets_ok(s->zone_off, s->zone_ids.size()) || !offsets_ok(s->taint_off, s->taint_key.size()) ||
+      !offsets_ok(s->mgrp_off, s->mgrp_tid.size()))
+    return false;
+  int kmax = 0;
+  for (int r = 0; r < C; r++) kmax = std::max(kmax, s->mgrp_off[r + 1] - s->mgrp_off[r]);
+  if (kmax != km) return false;
+  auto ids_ok = [](const std::vector<int32_t>& v, int lo, int hi) {
+    for (int32_t x : v)
+      if (x < lo || x >= hi) return false;
+    return true;
+  };
+  if (!ids_ok(s->provider, -1, NS) || !ids_ok(s->region, -1, NS) || !ids_ok(s->region_idx, -1, std::max(NR, 1)) ||
+      !ids_ok(s->label_val, -1, NS) || !ids_ok(s->zone_ids, 0, std::max(NS, 1)) ||
+      !ids_ok(s->taint_key, 0, std::max(NS, 1)) || !ids_ok(s->taint_val, 0, std::max(NS, 1)) ||
+      !ids_ok(s->taint_eff, 0, 4) || !ids_ok(s->mgrp_tid, 0, std::max(T, 1)) || !ids_ok(s->mg_tid, 0, std::max(T, 1)))
+    return false;
+  for (int32_t x : s->mg_cnt)
+    if (x < 0) return false;
+  for (int64_t x : s->mgrp_cnt)
+    if (x < 0) return false;
+  return s->rid_cpu >= 0 && s->rid_cpu < R && s->rid_mem >= 0 && s->rid_mem < R && s->rid_eph >= 0 && s->rid_eph < R;
 }
 }  // namespace
 
@@ -1348,6 +1425,7 @@ int kp_snapshot_update(kp_engine* e, kp_snapshot* s, const kp_cluster* clusters,
   }
   const size_t n_str = s->str.names.size(), n_keys = s->keys.names.size(), n_gvk = s->gvk.names.size(),
                n_res = s->res.names.size();
+  const std::vector<std::string> regions0 = s->regions.names;
   std::vector<ClusterRow> rows(C);
   for (int r = 0; r < C; r++)
     if (upd[r] < 0) rows[r] = row_of(s, r);
@@ -1383,9 +1461,9 @@ int kp_snapshot_update(kp_engine* e, kp_snapshot* s, const kp_cluster* clusters,
     }
   apply_rows(s, rows, used);
   s->blob.clear();
-  if (dict_grew)
+  if (dict_grew)  // region ids index the batches' region buffers: a changed region set counts too
     *dict_grew = s->str.names.size() != n_str || s->keys.names.size() != n_keys || s->gvk.names.size() != n_gvk ||
-                 s->res.names.size() != n_res;
+                 s->res.names.size() != n_res || s->regions.names != regions0;
   s->dev.reset();
   return upload_snapshot(e, s);
 }
@@ -1423,6 +1501,9 @@ int kp_snapshot_export(const kp_snapshot* cs, const void** bytes, uint64_t* n_by
   w.vec(s->taint_key);
   w.vec(s->taint_val);
   w.vec(s->taint_eff);
+  w.vec(s->mgrp_off);
+  w.vec(s->mgrp_tid);
+  w.vec(s->mgrp_cnt);
   w.vec(s->mg_tid);
   w.vec(s->mg_cnt);
   w.vec(s->provider_int);
@@ -1477,6 +1558,9 @@ int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_sna
   s->taint_key = r.vec<int32_t>();
   s->taint_val = r.vec<int32_t>();
   s->taint_eff = r.vec<int32_t>();
+  s->mgrp_off = r.vec<int32_t>();
+  s->mgrp_tid = r.vec<int32_t>();
+  s->mgrp_cnt = r.vec<int64_t>();
   s->mg_tid = r.vec<int32_t>();
   s->mg_cnt = r.vec<int32_t>();
   s->provider_int = r.vec<int64_t>();
@@ -1485,10 +1569,7 @@ int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_sna
   s->avail = r.vec<int64_t>();
   s->tmpl = r.vec<int64_t>();
   s->api_bits = r.vec<uint64_t>();
-  const size_t Cp = (size_t)s->Cp;
-  if (!r.ok || s->C > kMaxClusters || (int)s->names.size() != s->C || s->perm.size() != (size_t)s->C ||
-      s->flags.size() != Cp || s->allowed.size() != Cp || s->zone_off.size() != (size_t)s->C + 1 ||
-      s->taint_off.size() != (size_t)s->C + 1 || s->mg_tid.size() != s->mg_cnt.size()) {
+  if (!r.ok || r.p != r.end || !snapshot_consistent(s)) {
     e->err = "truncated or inconsistent snapshot bytes";
     return KP_EINVAL;
   }
@@ -1528,18 +1609,8 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
     e->err = "region spread over more than 256 regions is not supported";
     return KP_ENOTSUP;
   }
-  {
-    const int cap = kSmallMax + kTgtSmallMax + 16;
-    size_t need = smem_pair(s, md_cap_of(s));
-    if (!bt->l_all.empty()) need = std::max(need, smem_all(s));
-    if (!bt->l_cluster.empty()) need = std::max(need, smem_cluster(s, cap));
-    if (!bt->l_region.empty()) need = std::max({need, smem_region_a(s), smem_region_b(s, cap)});
-    if (need > e->max_lds) {
-      e->err = "snapshot too large for one workgroup's LDS (" + std::to_string(need) + " > " +
-               std::to_string(e->max_lds) + " bytes)";
-      return KP_ENOTSUP;
-    }
-  }
+  if (batch_lds_check(e, s, bt)) return KP_ENOTSUP;
+  bt->n_regions = s->view.n_regions;
   auto pad1 = [](auto& v) {
     if (v.empty()) v.resize(1);
   };
@@ -1661,6 +1732,11 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     out->offsets = bt->h_offsets.data();
     return KP_OK;
   }
+  if (!bt->l_region.empty() && s->view.n_regions != bt->n_regions) {
+    e->err = "kp_schedule_batch: the snapshot's region set changed since the batch was packed (re-create it)";
+    return KP_ESTATE;
+  }
+  if (batch_lds_check(e, s, bt)) return KP_ENOTSUP;
   HIPCHK(dev::fill(bt->counter, 0, sizeof(unsigned long long), st));
   HIPCHK(dev::fill(bt->stats, 0, 8 * sizeof(uint32_t), st));
   KArgs ka;

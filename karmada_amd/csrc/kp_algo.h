@@ -243,7 +243,8 @@ KP_HD inline int32_t template_md(const SnapView& s, const BatchView& bv, const B
 //   EST_SUMMARY  as MIXED, and no cluster of the snapshot has resource models;
 //   EST_MODEL8 / EST_MODEL16  as MIXED, and every cluster with a summary has
 //                models: only the <= 8 / 16 zero-padded template rows are loaded
-//                (summary-path bindings, BF_MODEL_ERR, read their columns late).
+//                (the summary columns are read late, on a path these snapshots
+//                never take).
 enum : int { EST_GENERIC = 0, EST_MIXED = 1, EST_SUMMARY = 2, EST_MODEL8 = 8, EST_MODEL16 = 16 };
 
 // min(a / q, lim) for a >= 0, q >= 1, lim >= 0 without a 64-bit integer divide:
@@ -286,7 +287,7 @@ KP_HD inline EstOps est_load(const SnapView& s, const BatchView& bv, const BindH
   o.f = f;
   o.allowed = s.allowed[c];
   const bool rr = (h.flags & BF_HAS_RR) != 0;
-  const bool model = rr && !(h.flags & BF_MODEL_ERR);
+  const bool model = rr;
   const int jh = rr && Fast < EST_MODEL8 ? (h.sreq_cnt < kReqUnroll ? h.sreq_cnt : kReqUnroll) : 0;
   if (Fast >= EST_MODEL8) {  // zero-padded rows: no per-template guard
 KP_UNROLL
@@ -339,7 +340,10 @@ KP_HD inline int32_t est_compute(const SnapView& s, const BatchView& bv, const B
   int64_t m = o.allowed;
   if (m <= 0) return 0;
   if (!(h.flags & BF_HAS_RR)) return (int32_t)m;
-  if ((f & CF_MODEL_OK) && !(h.flags & BF_MODEL_ERR)) {
+  // A NodeClaim never diverts a binding from the model path: it converts without
+  // error and every model node matches it (accurate.go:155-177,
+  // scheduling_simulator_components.go:149-153).
+  if (f & CF_MODEL_OK) {
     // getMaximumReplicasBasedOnResourceModels: each identical model node absorbs
     // exactly its initial MaxDivided, capped at MaxInt32.
     // d <= 110 (MaxPodsPerNode) and cnt <= MaxInt32: d*cnt < 2^38, and the
@@ -371,7 +375,7 @@ KP_UNROLL
   // getMaximumReplicasBasedOnClusterSummary (general.go:465-505)
   int64_t num = INT64_MAX;
   bool zero = false;
-  if (Fast >= EST_MODEL8) {  // columns not preloaded (BF_MODEL_ERR bindings only)
+  if (Fast >= EST_MODEL8) {  // not preloaded: these snapshots give every summary cluster models
     for (int j = 0; j < h.sreq_cnt; j++) {
       const int32_t rid = bv.ipool[h.sreq_off + j];
       if (rid < 0) return 0;

@@ -475,6 +475,9 @@ void gen_binding(kps_world& w, uint64_t i, kp_binding& b) {
     b.n_tolerations = 1;
   }
   if (r.p(0.05)) b.n_resource_request = 0;
+  // ReplicaRequirements.NodeClaim: the model path still answers (accurate.go:155-177,
+  // scheduling_simulator_components.go:149-153)
+  if (b.has_replica_requirements && r.p(0.15)) b.has_node_claim = 1;
 }
 
 }  // namespace

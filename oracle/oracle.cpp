@@ -1045,7 +1045,10 @@ i32 maxAvailableReplicas(const Cluster& c, const Binding& b, const Options& o, i
   i64 maximum = getAllowedPodNumber(c);
   if (maximum <= 0) return 0;
   if (!b.has_rr) return (i32)maximum;
-  if (o.models_gate && !c.modelings.empty() && !b.has_node_claim) {
+  // A NodeClaim does not divert the model path: toPBReplicaRequirements converts
+  // it without error (accurate.go:155-177) and MatchNode accepts every model node,
+  // which carries no Node object (scheduling_simulator_components.go:149-153).
+  if (o.models_gate && !c.modelings.empty()) {
     i64 num;
     if (getMaximumReplicasBasedOnResourceModels(c, b, mode, &num)) {
       if (num < maximum) maximum = num;

@@ -68,3 +68,68 @@ def test_update_rejects_unknown_and_duplicate_names(engine):
         snap.update_structs(two, 2)
     snap.update_structs(subset(ub, {3, 7}), 2)  # still usable after the rejected calls
     snap.close()
+
+
+@pytest.mark.parametrize("config,seed_a,seed_b,n_clusters", [(6, 71, 72, 120), (3, 73, 74, 200), (4, 75, 76, 150)])
+def test_import_update_matches_fresh(engine, config, seed_a, seed_b, n_clusters):
+    """The broadcast path: an imported snapshot (kp_snapshot_import, every non-source
+    rank) takes kp_snapshot_update like the snapshot it was exported from."""
+    ua = synth.Universe(config, seed_a, n_clusters, 0, 500)
+    ub = synth.Universe(config, seed_b, n_clusters, 0, 0)
+    opts = api.options()
+    idx = set(range(1, n_clusters, 5))
+    src = Snapshot.from_structs(engine, ua.clusters, ua.n_clusters, ua.names, opts)
+    imp = Snapshot.from_bytes(engine, src.to_bytes(), ua.names)
+    imp.update_structs(subset(ub, idx), len(idx))
+    got = Batch(imp, structs=ua.binding_slice(0, ua.n_bindings)).schedule()
+    mix = mixed(ua, ub, idx)
+    fresh = Snapshot.from_structs(engine, mix, ua.n_clusters, ua.names, opts)
+    assert got == Batch(fresh, structs=ua.binding_slice(0, ua.n_bindings)).schedule()
+    src.update_structs(subset(ub, idx), len(idx))
+    assert imp.to_bytes() == src.to_bytes()
+    for s in (src, imp, fresh):
+        s.close()
+
+
+def test_import_rejects_corrupt_images(engine):
+    """kp_snapshot_import validates every column and offset array: truncated or
+    tampered images fail with KP_EINVAL instead of reaching a kernel."""
+    import random
+    u = synth.Universe(6, 77, 70, 0, 0)
+    data = Snapshot.from_structs(engine, u.clusters, u.n_clusters, u.names, api.options()).to_bytes()
+    for cut in (8, 100, len(data) // 3, len(data) - 1):
+        with pytest.raises(Exception):
+            Snapshot.from_bytes(engine, data[:cut], u.names)
+    with pytest.raises(Exception):
+        Snapshot.from_bytes(engine, data + b"\0", u.names)
+    rng = random.Random(5)
+    rejected = 0
+    for _ in range(300):
+        b = bytearray(data)
+        i = rng.randrange(8, len(b))
+        b[i] ^= 1 << rng.randrange(8)
+        try:
+            s = Snapshot.from_bytes(engine, bytes(b), u.names)
+            s.close()  # a flip inside a value column can be a valid image
+        except Exception:
+            rejected += 1
+    assert rejected > 0
+
+
+def test_region_set_change_is_reported(engine):
+    """A region-spread batch packed before an update that changes the region set
+    is refused (KP_ESTATE) instead of writing past its region buffers."""
+    from karmada_amd.engine import EngineError
+    ua = synth.Universe(4, 78, 120, 0, 200)
+    snap = Snapshot.from_structs(engine, ua.clusters, ua.n_clusters, ua.names, api.options())
+    b = Batch(snap, structs=ua.binding_slice(0, ua.n_bindings))
+    w = api.World()
+    c = w.cluster({"name": ua.names[3], "region": "region-zz-new",
+                   "resourceSummary": {"allocatable": {"cpu": "10", "pods": "100"}}})
+    arr = (api.kp_cluster * 1)(c)
+    assert snap.update_structs(arr, 1) is True
+    with pytest.raises(EngineError):
+        b.schedule()
+    b2 = Batch(snap, structs=ua.binding_slice(0, ua.n_bindings))
+    assert len(b2.schedule()) == ua.n_bindings
+    snap.close()
