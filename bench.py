@@ -69,6 +69,26 @@ def cpu_baseline(u, opts, budget_s):
     }
 
 
+def parity_check(u, r, opts, n_check, seed):
+    """Oracle (FAST mode) on n_check bindings sampled from the timed batch, compared
+    with the engine's results of the last timed step (status, error, multiset of
+    targets). Test infrastructure, after the timed region."""
+    import ctypes as C
+    import random
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    from karmada_amd import api
+    n = min(n_check, u.n_bindings)
+    if n <= 0:
+        return 0, 0
+    idx = sorted(random.Random(seed).sample(range(u.n_bindings), n))
+    arr = (api.kp_binding * n)(*[u.bindings[i] for i in idx])
+    want = O.schedule_c(u.clusters, u.n_clusters, arr, n, opts, O.FAST, min(16, os.cpu_count() or 1))
+    got = api.results_to_python(r.status, r.err_code, r.err_arg, r.offsets, r.cluster_idx, r.replicas, r.n_bindings)
+    bad = sum(1 for k, i in enumerate(idx) if got[i] != want[k])
+    return n, bad
+
+
 def load_traffic(config, kernel):
     """Per-launch PMC figures of the pair kernel instance from the committed profile,
     if any: (HBM bytes = FETCH_SIZE + WRITE_SIZE, VALU wave-instructions)."""
@@ -103,14 +123,16 @@ def load_select_pmc(config):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--clusters", type=int, default=None)
     ap.add_argument("--bindings", type=int, default=None, help="bindings per GPU")
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--check", type=int, default=1000,
+                    help="bindings of the timed batch re-checked against the oracle after timing (0: off)")
     ap.add_argument("--lib", default=None, help="engine library (default karmada_amd/libkp.so)")
     args = ap.parse_args()
 
@@ -196,6 +218,11 @@ def main():
         n_ok = int(sum(p[0].item() for p in parts))
         n_targets = int(sum(p[1].item() for p in parts))
 
+    n_chk, n_bad = parity_check(u, r, opts, args.check, 1000 + rank) if args.check > 0 else (0, 0)
+    if dist is not None:
+        t = torch.tensor([n_chk, n_bad], dtype=torch.int64, device=tdev)
+        dist.all_reduce(t)
+        n_chk, n_bad = int(t[0].item()), int(t[1].item())
     ms_per_step = 1e3 * elapsed / args.steps
     value = (B * world) / (elapsed / args.steps)
     avg_pair_ms = sum(pair_ms) / len(pair_ms)  # all pair launches of one step
@@ -246,6 +273,9 @@ def main():
         "scheduled_ok": n_ok,
         "result_targets": n_targets,
         "slow_path_bindings": n_slow,
+        # bindings of the timed batch (sampled over all ranks) re-checked against the oracle
+        "parity_checked": n_chk,
+        "parity_bad": n_bad,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(u, opts, args.cpu_budget)

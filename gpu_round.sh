@@ -16,7 +16,7 @@ for s in "$@"; do
     smoke) step smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
     tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     bench_small) step bench_small 300 python bench.py --steps 3 --warmup 1 --bindings 5000 --no-cpu ;;
-    bench) step bench 600 python bench.py --steps 5 --warmup 1 ;;
+    bench) step bench 600 python bench.py ;;
     benchq) step benchq 300 python bench.py --steps 5 --warmup 1 --no-cpu ;;
     sweep) for t in 256 512; do KP_SEL_THREADS=$t step sweep_$t 300 python bench.py --steps 3 --warmup 1 --no-cpu; done ;;
     chunks) for c in 4096 8192 16384 32768 200000; do KP_CHUNK=$c step chunk_$c 300 python bench.py --steps 5 --warmup 1 --no-cpu; done ;;

@@ -75,6 +75,12 @@ CASES = [
     # C > ~8.6k: k_select_all's LDS leaves one workgroup per CU -> k_select_all_wide
     (6, 21, 9000, 1000),
     (7, 22, 9000, 600),
+    # BASELINE configs at the cluster counts they are quoted on (binding slices of
+    # the bench universes: same seeds as bench.py)
+    (3, 3, 5000, 2000),
+    (4, 4, 5000, 2000),
+    (5, 5, 10000, 1500),
+    (2, 2, 1000, 4000),
 ]
 
 
