@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 4
+#define KP_ABI_VERSION 5
 
 /* ------------------------------------------------------------------------- */
 /* Object model                                                              */
@@ -316,16 +316,18 @@ typedef struct kp_affinity_results {
 /* Per-stage timing of the last kp_schedule_batch call (milliseconds, host clock
  * around device work; kernel-only numbers come from rocprof). */
 typedef struct kp_stage_times {
-  double pair_ms;      /* filter + score + estimate kernel */
-  double select_ms;    /* candidate/group/select/divide kernels */
+  double pair_ms;      /* filter + score + estimate kernel (rows to HBM) */
+  double select_ms;    /* candidate/group/select/divide kernels after the pair and fused kernels */
   double host_ms;      /* host group-combination (region DFS) */
   double copy_ms;      /* device -> host result copies */
   double total_ms;
   float pair_kernel_ms;   /* sum of the pair kernel launches' HIP event times */
   float select_kernel_ms; /* select kernels after the last pair launch (HIP events) */
   uint64_t n_slow;        /* bindings that took the exact serial path */
-  uint32_t pair_launches; /* pair kernel launches (chunks) in the batch */
+  uint32_t pair_launches; /* pair kernel launches in the batch (0 or 1) */
   uint32_t pair_kind;     /* pair kernel instance: 0 generic, 1 mixed, 2 summary-only, 8/16 model-only */
+  float fused_kernel_ms;  /* fused pair + SEL_ALL select kernel (HIP events), 0 when not run */
+  uint32_t fused;         /* 1: the SEL_ALL bindings took the fused kernel (rows kept in LDS) */
 } kp_stage_times;
 
 /* ------------------------------------------------------------------------- */

@@ -146,7 +146,8 @@ class kp_stage_times(C.Structure):
     _fields_ = [("pair_ms", C.c_double), ("select_ms", C.c_double), ("host_ms", C.c_double),
                 ("copy_ms", C.c_double), ("total_ms", C.c_double),
                 ("pair_kernel_ms", C.c_float), ("select_kernel_ms", C.c_float), ("n_slow", u64),
-                ("pair_launches", C.c_uint32), ("pair_kind", C.c_uint32)]
+                ("pair_launches", C.c_uint32), ("pair_kind", C.c_uint32),
+                ("fused_kernel_ms", C.c_float), ("fused", C.c_uint32)]
 
 
 PLUGIN_API_ENABLEMENT = 1 << 0

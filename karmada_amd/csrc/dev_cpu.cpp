@@ -92,16 +92,16 @@ int fill(void* dst, int value, size_t bytes, stream_t) {
   return 0;
 }
 
-int pair(stream_t, const SnapView& s, const BatchView& bv, int b0, int nb, uint64_t* fmask, int32_t* est,
-         int64_t* score, int est_mode, int md_cap, size_t smem, int fast) {
+int pair(stream_t, const SnapView& s, const BatchView& bv, const int32_t* list, int b0, int nb, uint64_t* fmask,
+         int32_t* est, int64_t* score, int est_mode, int md_cap, size_t smem, int fast) {
   grid(nb, smem, [&](int blk, unsigned char* sm) {
     const CpuBlk B{(int64_t*)sm};
     switch (fast) {
-      case EST_MIXED: body_pair<EST_MIXED>(B, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap); break;
-      case EST_SUMMARY: body_pair<EST_SUMMARY>(B, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap); break;
-      case EST_MODEL8: body_pair<EST_MODEL8>(B, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap); break;
-      case EST_MODEL16: body_pair<EST_MODEL16>(B, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap); break;
-      default: body_pair<EST_GENERIC>(B, blk, sm, s, bv, b0, fmask, est, score, est_mode, md_cap);
+      case EST_MIXED: body_pair<EST_MIXED>(B, blk, sm, s, bv, list, b0, fmask, est, score, est_mode, md_cap); break;
+      case EST_SUMMARY: body_pair<EST_SUMMARY>(B, blk, sm, s, bv, list, b0, fmask, est, score, est_mode, md_cap); break;
+      case EST_MODEL8: body_pair<EST_MODEL8>(B, blk, sm, s, bv, list, b0, fmask, est, score, est_mode, md_cap); break;
+      case EST_MODEL16: body_pair<EST_MODEL16>(B, blk, sm, s, bv, list, b0, fmask, est, score, est_mode, md_cap); break;
+      default: body_pair<EST_GENERIC>(B, blk, sm, s, bv, list, b0, fmask, est, score, est_mode, md_cap);
     }
   });
   return 0;
@@ -138,6 +138,29 @@ int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const Sele
     default:
       return -1;
   }
+  return 0;
+}
+
+int fused_all(stream_t, const KArgs& a, size_t smem, int md_cap, int fast) {
+  grid(a.n, smem, [&](int blk, unsigned char* sm) {
+    const CpuBlk B{(int64_t*)sm};
+    switch (fast) {
+      case EST_MIXED: body_fused_all<EST_MIXED>(B, blk, sm, a, md_cap); break;
+      case EST_SUMMARY: body_fused_all<EST_SUMMARY>(B, blk, sm, a, md_cap); break;
+      case EST_MODEL8: body_fused_all<EST_MODEL8>(B, blk, sm, a, md_cap); break;
+      case EST_MODEL16: body_fused_all<EST_MODEL16>(B, blk, sm, a, md_cap); break;
+      default: break;
+    }
+  });
+  return fast == EST_MIXED || fast == EST_SUMMARY || fast == EST_MODEL8 || fast == EST_MODEL16 ? 0 : -1;
+}
+
+int pair_list(stream_t, const SnapView& s, const BatchView& bv, const int32_t* list, const uint32_t* count, int max_n,
+              uint64_t* fmask, int32_t* est, int md_cap, size_t smem) {
+  const int n = (int)*count < max_n ? (int)*count : max_n;
+  grid(n, smem, [&](int blk, unsigned char* sm) {
+    body_pair_list<EST_GENERIC>(CpuBlk{(int64_t*)sm}, blk, n, sm, s, bv, list, count, max_n, fmask, est, md_cap);
+  });
   return 0;
 }
 

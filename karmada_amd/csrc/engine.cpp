@@ -100,8 +100,7 @@ struct kp_engine {
   int device = 0;
   dev::stream_t stream = nullptr;   // select kernels, copies (the batch's result order)
   dev::stream_t stream2 = nullptr;  // pair kernels, one launch per chunk ahead of the selects
-  dev::event_t ev[6] = {};
-  std::vector<dev::event_t> ev_chunk;  // per chunk: [2i] before, [2i+1] after its pair launch
+  dev::event_t ev[8] = {};
   std::string err;
   kp_stage_times times{};
   struct {  // kp_schedule_affinities results
@@ -147,14 +146,14 @@ struct kp_batch {
   std::vector<Tol> tols;
   std::vector<Prog> progs;
   std::vector<Instr> instrs;
-  std::vector<int32_t> l_all, l_cluster, l_region, l_slow;
+  std::vector<int32_t> l_all, l_cluster, l_region, l_slow, l_cs;  // l_cs: cluster + region bindings
   uint64_t out_cap = 0;
   Arena dev;
   BatchView view{};
   // device work buffers
   uint64_t* fmask = nullptr;
   int32_t* est = nullptr;
-  int32_t *d_all = nullptr, *d_cluster = nullptr, *d_region = nullptr, *d_slowlist = nullptr;
+  int32_t *d_all = nullptr, *d_cluster = nullptr, *d_region = nullptr, *d_slowlist = nullptr, *d_cs = nullptr;
   int32_t *status = nullptr, *errc = nullptr, *slow = nullptr;
   int64_t* arg = nullptr;
   uint64_t* start = nullptr;
@@ -1342,8 +1341,6 @@ void kp_engine_destroy(kp_engine* e) {
   (void)dev::set_device(e->device);
   for (auto& ev : e->ev)
     if (ev) dev::event_destroy(ev);
-  for (auto& ev : e->ev_chunk)
-    if (ev) dev::event_destroy(ev);
   if (e->stream) dev::stream_destroy(e->stream);
   if (e->stream2) dev::stream_destroy(e->stream2);
   delete e;
@@ -1605,6 +1602,9 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   }
   bt->l_slow = bt->l_all;
   bt->l_slow.insert(bt->l_slow.end(), bt->l_cluster.begin(), bt->l_cluster.end());
+  bt->l_cs = bt->l_cluster;
+  bt->l_cs.insert(bt->l_cs.end(), bt->l_region.begin(), bt->l_region.end());
+  std::sort(bt->l_cs.begin(), bt->l_cs.end());
   if (s->view.n_regions > kRegionMax && !bt->l_region.empty()) {
     e->err = "region spread over more than 256 regions is not supported";
     return KP_ENOTSUP;
@@ -1667,6 +1667,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->d_cluster, std::max<size_t>(1, bt->l_cluster.size()));
   a.add(&bt->d_region, std::max<size_t>(1, bt->l_region.size()));
   a.add(&bt->d_slowlist, std::max<size_t>(1, bt->l_slow.size()));
+  a.add(&bt->d_cs, std::max<size_t>(1, bt->l_cs.size()));
   a.add(&bt->status, B);
   a.add(&bt->errc, B);
   a.add(&bt->slow, B);
@@ -1702,6 +1703,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   HIPCHK(up(bt->d_all, bt->l_all.data(), 4 * bt->l_all.size()));
   HIPCHK(up(bt->d_cluster, bt->l_cluster.data(), 4 * bt->l_cluster.size()));
   HIPCHK(up(bt->d_region, bt->l_region.data(), 4 * bt->l_region.size()));
+  HIPCHK(up(bt->d_cs, bt->l_cs.data(), 4 * bt->l_cs.size()));
   HIPCHK(dev::fill(bt->slow, 0, 4 * (size_t)B, e->stream));
   HIPCHK(dev::sync(e->stream));
   BatchView& v = bt->view;
@@ -1759,28 +1761,16 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
 #ifdef KP_STAMPS
   HIPCHK(dev::fill(bt->dbg, 0, 32 * 8, st));
 #endif
-  // Optional chunked pipeline (KP_CHUNK=n): the pair kernel of chunk i+1
-  // (stream2) runs beside the SEL_ALL select kernel of chunk i (stream). On
-  // MI355X at config 3 the two kernels contend rather than overlap (measured:
-  // 16k chunks 14.6 ms/step vs 13.7 whole-batch), so the default is one chunk.
-  static const int kChunk = [] {
-    const char* v = getenv("KP_CHUNK");
-    const int c = v ? atoi(v) : 0;
-    return c > 0 ? c : INT32_MAX;
-  }();
-  const int nch = (int)(((int64_t)B + kChunk - 1) / kChunk);
-  while ((int)e->ev_chunk.size() < 2 * nch) {
-    dev::event_t ev = nullptr;
-    if (dev::event_create(&ev)) {
-      e->err = "event create failed";
-      return KP_EDEVICE;
-    }
-    e->ev_chunk.push_back(ev);
-  }
   dev::stream_t sp = e->stream2;
   HIPCHK(dev::event_record(e->ev[0], st));
   HIPCHK(dev::stream_wait(sp, e->ev[0]));  // the fills above precede every kernel
   const int fast = getenv("KP_PAIR_GENERIC") || !bt->fast_ok ? EST_GENERIC : s->est_kind;
+  const int md_cap = md_cap_of(s);
+  // SEL_ALL bindings take the fused pair + select kernel when the batch runs a fast
+  // estimator instance and its LDS fits: their rows never leave LDS. The pair
+  // kernel then covers only the cluster/region-spread bindings, on stream2 beside it.
+  const bool fused = fast != EST_GENERIC && !bt->l_all.empty() && !getenv("KP_NO_FUSE") &&
+                     fused_lds_bytes(s->Cp, md_cap) <= e->max_lds;
   SelectExtra sx;
   sx.rout = bt->rout;
   sx.rstat = bt->rstat;
@@ -1792,26 +1782,28 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   sx.lds_area = bt->slow_lds;
   sx.lds_sort = bt->slow_sort;
   const int cap = kSmallMax + kTgtSmallMax + 16;
-  size_t a0 = 0;  // l_all is in binding order: chunk i's SEL_ALL bindings are a contiguous run
-  for (int i = 0; i < nch; i++) {
-    const int b0 = (int)((int64_t)i * kChunk), nb = (int)std::min<int64_t>(kChunk, B - b0);
-    HIPCHK(dev::event_record(e->ev_chunk[2 * i], sp));
-    HIPCHK(dev::pair(sp, s->view, bt->view, b0, nb, bt->fmask, bt->est, nullptr, 0, md_cap_of(s),
-                     smem_pair(s, md_cap_of(s)), fast));
-    HIPCHK(dev::event_record(e->ev_chunk[2 * i + 1], sp));
-    size_t a1 = a0;
-    while (a1 < bt->l_all.size() && bt->l_all[a1] < b0 + nb) a1++;
-    if (a1 > a0) {
-      HIPCHK(dev::stream_wait(st, e->ev_chunk[2 * i + 1]));
-      KArgs k = ka;
-      k.list = bt->d_all + a0;
-      k.n = (int)(a1 - a0);
-      HIPCHK(dev::select(st, SEL_LAUNCH_ALL, k, smem_all(s), cap, sx));
-    }
-    a0 = a1;
+  const int n_pair = fused ? (int)bt->l_cs.size() : B;
+  HIPCHK(dev::event_record(e->ev[3], sp));
+  if (n_pair > 0)
+    HIPCHK(dev::pair(sp, s->view, bt->view, fused ? bt->d_cs : nullptr, 0, n_pair, bt->fmask, bt->est, nullptr, 0,
+                     md_cap, smem_pair(s, md_cap), fast));
+  HIPCHK(dev::event_record(e->ev[4], sp));
+  if (fused) {
+    KArgs k = ka;
+    k.list = bt->d_all;
+    k.n = (int)bt->l_all.size();
+    HIPCHK(dev::event_record(e->ev[5], st));
+    HIPCHK(dev::fused_all(st, k, fused_lds_bytes(s->Cp, md_cap), md_cap, fast));
+    HIPCHK(dev::event_record(e->ev[6], st));
   }
-  HIPCHK(dev::stream_wait(st, e->ev_chunk[2 * nch - 1]));  // every pair row precedes the rest
+  HIPCHK(dev::stream_wait(st, e->ev[4]));  // every pair row precedes the rest
   HIPCHK(dev::event_record(e->ev[1], st));
+  if (!fused && !bt->l_all.empty()) {
+    KArgs k = ka;
+    k.list = bt->d_all;
+    k.n = (int)bt->l_all.size();
+    HIPCHK(dev::select(st, SEL_LAUNCH_ALL, k, smem_all(s), cap, sx));
+  }
   if (!bt->l_cluster.empty()) {
     KArgs k = ka;
     k.list = bt->d_cluster;
@@ -1882,6 +1874,9 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     }
     HIPCHK(dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sx));
   }
+  if (fused)  // HBM rows of the bindings the fused kernel flagged for k_slow
+    HIPCHK(dev::pair_list(st, s->view, bt->view, bt->d_slowlist, bt->stats, (int)bt->l_slow.size(), bt->fmask, bt->est,
+                          md_cap, smem_pair(s, md_cap)));
   if (!bt->l_slow.empty()) {
     KArgs k = ka;
     k.list = bt->d_slowlist;
@@ -1934,16 +1929,18 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   }
   HIPCHK(dev::sync(st));
   double t1 = now_ms();
-  // pair: the sum of the pair launches' own durations (each bracketed on stream2);
-  // select: from the end of the last pair launch to the end of the last select
-  // kernel (the part not overlapped by pair launches).
-  float ms_pair = 0, ms_sel = 0;
-  for (int i = 0; i < nch; i++) ms_pair += dev::event_ms(e->ev_chunk[2 * i], e->ev_chunk[2 * i + 1]);
-  ms_sel = dev::event_ms(e->ev_chunk[2 * nch - 1], e->ev[2]);
-  tm.pair_launches = nch;
+  // pair: the pair launch (stream2); fused: the fused SEL_ALL kernel (stream);
+  // select: from the point where both are complete to the end of the last
+  // select kernel.
+  const float ms_pair = dev::event_ms(e->ev[3], e->ev[4]);
+  const float ms_fused = fused ? dev::event_ms(e->ev[5], e->ev[6]) : 0.f;
+  const float ms_sel = dev::event_ms(e->ev[1], e->ev[2]);
+  tm.pair_launches = n_pair > 0 ? 1 : 0;
   tm.pair_kind = (uint32_t)fast;
   tm.pair_kernel_ms = ms_pair;
   tm.select_kernel_ms = ms_sel;
+  tm.fused_kernel_ms = ms_fused;
+  tm.fused = fused ? 1u : 0u;
   tm.n_slow = bt->h_stats[0];
 #ifdef KP_STAMPS
   {
@@ -1981,7 +1978,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
 // Runs the pair kernel and returns the rank-ordered device row pointers.
 static int run_pair(kp_engine* e, kp_batch* bt, int64_t* score, int est_mode, int b0, int nb) {
   kp_snapshot* s = bt->snap;
-  HIPCHK(dev::pair(e->stream, s->view, bt->view, b0, nb, bt->fmask, bt->est, score, est_mode, md_cap_of(s),
+  HIPCHK(dev::pair(e->stream, s->view, bt->view, nullptr, b0, nb, bt->fmask, bt->est, score, est_mode, md_cap_of(s),
                      smem_pair(s, md_cap_of(s))));
   HIPCHK(dev::sync(e->stream));
   return KP_OK;

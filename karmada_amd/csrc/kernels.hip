@@ -34,23 +34,48 @@ constexpr size_t kLdsPerCu = 160 * 1024;  // gfx950 LDS per CU
 #define KP_SEL_MIN_WAVES 6
 #endif
 
-extern "C" __global__ void __launch_bounds__(kBlock) k_pair(SnapView s, BatchView bv, int b0, uint64_t* fmask,
-                                                            int32_t* est, int64_t* score, int est_mode, int md_cap) {
+extern "C" __global__ void __launch_bounds__(kBlock) k_pair(SnapView s, BatchView bv, const int32_t* list, int b0,
+                                                            uint64_t* fmask, int32_t* est, int64_t* score,
+                                                            int est_mode, int md_cap) {
   KP_SMEM;
-  body_pair<EST_GENERIC>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, b0, fmask, est, score, est_mode,
+  body_pair<EST_GENERIC>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, list, b0, fmask, est, score, est_mode,
                          md_cap);
 }
-#define KP_PAIR_FAST(NAME, KIND)                                                                                \
-  extern "C" __global__ void __launch_bounds__(kBlock, KP_PAIR_MIN_WAVES) NAME(SnapView s, BatchView bv, int b0, \
-                                                                              uint64_t* fmask, \
-                                                            int32_t* est, int md_cap) {                       \
+#define KP_PAIR_FAST(NAME, KIND)                                                                              \
+  extern "C" __global__ void __launch_bounds__(kBlock, KP_PAIR_MIN_WAVES)                                     \
+      NAME(SnapView s, BatchView bv, const int32_t* list, int b0, uint64_t* fmask, int32_t* est, int md_cap) { \
     KP_SMEM;                                                                                                  \
-    body_pair<KIND>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, b0, fmask, est, nullptr, 0, md_cap); \
+    body_pair<KIND>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, list, b0, fmask, est, nullptr, 0,   \
+                    md_cap);                                                                                  \
   }
 KP_PAIR_FAST(k_pair_fast, EST_MIXED)
 KP_PAIR_FAST(k_pair_fast_summary, EST_SUMMARY)
 KP_PAIR_FAST(k_pair_fast_m8, EST_MODEL8)
 KP_PAIR_FAST(k_pair_fast_m16, EST_MODEL16)
+// Fused pair + SEL_ALL select, one instance per estimator kind (fast batches only).
+#ifndef KP_FUSED_THREADS
+#define KP_FUSED_THREADS 256
+#endif
+#ifndef KP_FUSED_MIN_WAVES
+#define KP_FUSED_MIN_WAVES 1
+#endif
+#define KP_FUSED(NAME, KIND)                                                                             \
+  extern "C" __global__ void __launch_bounds__(KP_FUSED_THREADS, KP_FUSED_MIN_WAVES) NAME(KArgs a, int md_cap) { \
+    KP_SMEM;                                                                                             \
+    body_fused_all<KIND>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, md_cap);                      \
+  }
+KP_FUSED(k_fused_all, EST_MIXED)
+KP_FUSED(k_fused_all_summary, EST_SUMMARY)
+KP_FUSED(k_fused_all_m8, EST_MODEL8)
+KP_FUSED(k_fused_all_m16, EST_MODEL16)
+// Pair rows of the bindings flagged for k_slow (persistent grid over the device list).
+extern "C" __global__ void __launch_bounds__(kBlock) k_pair_list(SnapView s, BatchView bv, const int32_t* list,
+                                                                 const uint32_t* count, int max_n, uint64_t* fmask,
+                                                                 int32_t* est, int md_cap) {
+  KP_SMEM;
+  body_pair_list<EST_GENERIC>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, (int)gridDim.x, smem, s, bv, list, count, max_n,
+                              fmask, est, md_cap);
+}
 extern "C" __global__ void __launch_bounds__(KP_SEL_MAX_THREADS, KP_SEL_MIN_WAVES) k_select_all(KArgs a) {
   KP_SMEM;
   body_select_all(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a);
@@ -174,8 +199,8 @@ int fill(void* dst, int value, size_t bytes, stream_t s) {
   return bytes ? chk(hipMemsetAsync(dst, value, bytes, (hipStream_t)s)) : 0;
 }
 
-int pair(stream_t st, const SnapView& s, const BatchView& bv, int b0, int nb, uint64_t* fmask, int32_t* est,
-         int64_t* score, int est_mode, int md_cap, size_t smem, int fast) {
+int pair(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* list, int b0, int nb, uint64_t* fmask,
+         int32_t* est, int64_t* score, int est_mode, int md_cap, size_t smem, int fast) {
   if (nb <= 0) return 0;
   auto* kf = fast == EST_MIXED     ? k_pair_fast
              : fast == EST_SUMMARY ? k_pair_fast_summary
@@ -184,10 +209,10 @@ int pair(stream_t st, const SnapView& s, const BatchView& bv, int b0, int nb, ui
                                    : nullptr;
   if (fast != EST_GENERIC && !kf) return chk(hipErrorInvalidValue);
   if (kf)
-    hipLaunchKernelGGL(kf, dim3(nb), dim3(kBlock), smem, (hipStream_t)st, s, bv, b0, fmask, est, md_cap);
+    hipLaunchKernelGGL(kf, dim3(nb), dim3(kBlock), smem, (hipStream_t)st, s, bv, list, b0, fmask, est, md_cap);
   else
-    hipLaunchKernelGGL(k_pair, dim3(nb), dim3(kBlock), smem, (hipStream_t)st, s, bv, b0, fmask, est, score, est_mode,
-                       md_cap);
+    hipLaunchKernelGGL(k_pair, dim3(nb), dim3(kBlock), smem, (hipStream_t)st, s, bv, list, b0, fmask, est, score,
+                       est_mode, md_cap);
   return chk(hipGetLastError());
 }
 
@@ -220,6 +245,29 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
     default:
       return chk(hipErrorInvalidValue);
   }
+  return chk(hipGetLastError());
+}
+
+int fused_all(stream_t st, const KArgs& a, size_t smem, int md_cap, int fast) {
+  if (a.n <= 0) return 0;
+  auto* kf = fast == EST_MIXED     ? k_fused_all
+             : fast == EST_SUMMARY ? k_fused_all_summary
+             : fast == EST_MODEL8  ? k_fused_all_m8
+             : fast == EST_MODEL16 ? k_fused_all_m16
+                                   : nullptr;
+  if (!kf) return chk(hipErrorInvalidValue);
+  if (smem > 65536 && chk(hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)))
+    return -1;
+  hipLaunchKernelGGL(kf, dim3(a.n), dim3(KP_FUSED_THREADS), smem, (hipStream_t)st, a, md_cap);
+  return chk(hipGetLastError());
+}
+
+int pair_list(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* list, const uint32_t* count,
+              int max_n, uint64_t* fmask, int32_t* est, int md_cap, size_t smem) {
+  if (max_n <= 0) return 0;
+  const int grid = max_n < 256 ? max_n : 256;
+  hipLaunchKernelGGL(k_pair_list, dim3(grid), dim3(kBlock), smem, (hipStream_t)st, s, bv, list, count, max_n, fmask,
+                     est, md_cap);
   return chk(hipGetLastError());
 }
 

@@ -74,35 +74,51 @@ KP_FI bool pre_checks(const BLK& B, const SelCtx& x, int F) {
 // columns), stores their feasibility as one u64 word and calAvailableReplicas
 // per cluster. est_mode 1: raw GeneralEstimator answers for every cluster.
 // ---------------------------------------------------------------------------
-// Fast: the estimator instance (EST_*, kp_algo.h); every instance but
-// EST_GENERIC needs pair_fast_ok (engine.cpp): est_mode 0, the MaxDivided and
-// taint-set tables in LDS, no cold fallbacks.
-template <int Fast, class BLK>
-KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView& s, const BatchView& bv, int b0,
-                     uint64_t* fmask, int32_t* est, int64_t* score, int est_mode, int md_cap) {
-  const int b = b0 + blk;
-  const BindHdr h = bv.hdr[b];
+// Per-binding LDS state of the pair stage: spec.Clusters and eviction bitsets,
+// the per-template MaxDivided table, the binding's predicate data (programs,
+// value lists, tolerations) and the per-taint-list TaintToleration answers.
+struct PairLds {
+  uint32_t* tgt;    // [words] TargetContains bits (also read by the select stage)
+  uint32_t* evict;  // [words]
+  int32_t* md;      // [md_cap]
+  unsigned char* stage;  // kPairStage bytes
+  uint32_t* tolb;   // kTsetMax bits
+};
+KP_HD inline PairLds pair_lds_carve(uint32_t* tgt, unsigned char* tail, int Cp, int md_cap) {
+  const int words = (Cp + 31) >> 5;
+  PairLds L;
+  L.tgt = tgt;
+  L.evict = (uint32_t*)tail;
+  L.md = (int32_t*)(L.evict + ((words + 3) & ~3));
+  L.stage = (unsigned char*)(L.md + ((md_cap + 3) & ~3));
+  L.tolb = (uint32_t*)(L.stage + kPairStage);
+  return L;
+}
+
+// Fills the pair stage's LDS state for binding h; returns the view of the batch
+// whose predicate pools point into LDS when they fit the stage (absolute pool
+// indices keep working). *use_md / *use_ts: whether the MaxDivided table and the
+// taint-list answers were built.
+template <class BLK>
+KP_FI BatchView pair_setup(const BLK& B, const SnapView& s, const BatchView& bv, const BindHdr& h, const PairLds& L,
+                           int est_mode, int md_cap, bool* use_md, bool* use_ts) {
   const int words = (s.Cp + 31) >> 5;
-  uint32_t* tgt = (uint32_t*)(smem + kRedBytes);
-  uint32_t* evict = tgt + words;
-  int32_t* md = (int32_t*)(evict + words);
-  build_bits(B, tgt, words, bv.ipool, h.tgt_off, h.tgt_cnt, 2);
-  build_bits(B, evict, words, bv.ipool, h.evict_off, h.evict_cnt, 1);
-  const bool use_md = s.n_tmpl <= md_cap && (h.flags & BF_HAS_RR);
-  if (use_md) {
-    for (int t = B.tid(); t < s.n_tmpl; t += B.nth()) md[t] = template_md(s, bv, h, t);
-    for (int t = s.n_tmpl + B.tid(); t < kTmplDense; t += B.nth()) md[t] = 0;  // padded template rows
+  build_bits(B, L.tgt, words, bv.ipool, h.tgt_off, h.tgt_cnt, 2);
+  build_bits(B, L.evict, words, bv.ipool, h.evict_off, h.evict_cnt, 1);
+  *use_md = s.n_tmpl <= md_cap && (h.flags & BF_HAS_RR);
+  if (*use_md) {
+    for (int t = B.tid(); t < s.n_tmpl; t += B.nth()) L.md[t] = template_md(s, bv, h, t);
+    for (int t = s.n_tmpl + B.tid(); t < kTmplDense; t += B.nth()) L.md[t] = 0;  // padded template rows
     B.sync();
   }
   // Stage this binding's predicate data (programs, value lists, tolerations) in
   // LDS: every lane reads it for every cluster, uniformly.
   BatchView lv = bv;
-  unsigned char* st = (unsigned char*)(md + ((md_cap + 3) & ~3));
   {
     const int nin = h.in_end - h.in_beg, npr = h.pr_end - h.pr_beg, nip = h.ip_end - h.ip_beg, nto = h.tol_cnt;
     const size_t need = sizeof(Instr) * nin + sizeof(Prog) * npr + sizeof(Tol) * nto + 4 * (size_t)nip;
     if (need <= (size_t)kPairStage) {
-      Instr* si = (Instr*)st;
+      Instr* si = (Instr*)L.stage;
       Prog* sp = (Prog*)(si + nin);
       Tol* so = (Tol*)(sp + npr);
       int32_t* sv = (int32_t*)(so + nto);
@@ -111,23 +127,37 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
       for (int i = B.tid(); i < nto; i += B.nth()) so[i] = bv.tols[h.tol_off + i];
       for (int i = B.tid(); i < nip; i += B.nth()) sv[i] = bv.ipool[h.ip_beg + i];
       B.sync();
-      lv.instrs = rebase(si, h.in_beg);  // absolute pool indices keep working
+      lv.instrs = rebase(si, h.in_beg);
       lv.progs = rebase(sp, h.pr_beg);
       lv.tols = rebase(so, h.tol_off);
       lv.ipool = rebase(sv, h.ip_beg);
     }
   }
   // TaintToleration once per distinct taint list of the snapshot, not per cluster
-  uint32_t* tolb = (uint32_t*)(st + kPairStage);
-  const bool use_ts = est_mode == 0 && (h.enabled & 2) && s.n_tsets <= kTsetMax;
-  if (use_ts) {
+  *use_ts = est_mode == 0 && (h.enabled & 2) && s.n_tsets <= kTsetMax;
+  if (*use_ts) {
     const int tw = (s.n_tsets + 31) >> 5;
-    for (int i = B.tid(); i < tw; i += B.nth()) tolb[i] = 0;
+    for (int i = B.tid(); i < tw; i += B.nth()) L.tolb[i] = 0;
     B.sync();
     for (int t = B.tid(); t < s.n_tsets; t += B.nth())
-      if (taints_tolerated(s, lv, h, s.tset_rep[t])) kp_atomic_or(&tolb[t >> 5], 1u << (t & 31));
+      if (taints_tolerated(s, lv, h, s.tset_rep[t])) kp_atomic_or(&L.tolb[t >> 5], 1u << (t & 31));
     B.sync();
   }
+  return lv;
+}
+
+// Fast: the estimator instance (EST_*, kp_algo.h); every instance but
+// EST_GENERIC needs pair_fast_ok (engine.cpp): est_mode 0, the MaxDivided and
+// taint-set tables in LDS, no cold fallbacks.
+template <int Fast, class BLK>
+KP_FI void pair_one(const BLK& B, int b, unsigned char* smem, const SnapView& s, const BatchView& bv, uint64_t* fmask,
+                    int32_t* est, int64_t* score, int est_mode, int md_cap) {
+  const BindHdr h = bv.hdr[b];
+  const int words = (s.Cp + 31) >> 5;
+  uint32_t* tgt = (uint32_t*)(smem + kRedBytes);
+  const PairLds L = pair_lds_carve(tgt, (unsigned char*)(tgt + ((words + 3) & ~3)), s.Cp, md_cap);
+  bool use_md, use_ts;
+  const BatchView lv = pair_setup(B, s, bv, h, L, est_mode, md_cap, &use_md, &use_ts);
   uint64_t* frow = fmask + (size_t)b * s.W;
   int32_t* erow = est + (size_t)b * s.Cp;
   for (int base = 0; base < s.Cp; base += B.nth()) {
@@ -135,11 +165,11 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
     bool fit = false;
     int32_t e = 0;
     if (Fast != EST_GENERIC) {
-      e = pair_eval<Fast>(s, lv, h, c, tgt, evict, tolb, md, &fit);
+      e = pair_eval<Fast>(s, lv, h, c, tgt, L.evict, L.tolb, L.md, &fit);
     } else if (est_mode == 0) {
-      e = pair_eval(s, lv, h, c, tgt, evict, use_ts ? tolb : nullptr, use_md ? md : nullptr, &fit);
+      e = pair_eval(s, lv, h, c, tgt, L.evict, use_ts ? L.tolb : nullptr, use_md ? L.md : nullptr, &fit);
     } else if (c < s.C) {
-      e = general_estimate(s, lv, h, c, use_md ? md : nullptr);
+      e = general_estimate(s, lv, h, c, use_md ? L.md : nullptr);
       fit = true;
     }
     B.mask_store(frow, c, fit, s.W);
@@ -149,6 +179,31 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
       if ((h.enabled & KP_PLUGIN_CLUSTER_LOCALITY) && h.n_targets_all > 0 && h.tgt_cnt > 0 && bit_test(tgt, c)) sc = 100;
       score[(size_t)b * s.C + c] = sc;
     }
+  }
+}
+
+// Pair stage for binding list[b0 + blk] (b0 + blk without a list): each wave evaluates 64 consecutive clusters
+// (coalesced SoA columns), stores their feasibility as one u64 word and
+// calAvailableReplicas per cluster. est_mode 1: raw GeneralEstimator answers for
+// every cluster.
+template <int Fast, class BLK>
+KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView& s, const BatchView& bv,
+                     const int32_t* list, int b0, uint64_t* fmask, int32_t* est, int64_t* score, int est_mode,
+                     int md_cap) {
+  pair_one<Fast>(B, list ? list[b0 + blk] : b0 + blk, smem, s, bv, fmask, est, score, est_mode, md_cap);
+}
+
+// Pair stage for the bindings flagged for k_slow (list entries [0, *count),
+// appended on the device by the select kernels), persistent over the grid:
+// the fused SEL_ALL kernel keeps its rows in LDS, and k_slow reads them from HBM.
+template <int Fast, class BLK>
+KP_FI void body_pair_list(const BLK& B, int blk, int grid, unsigned char* smem, const SnapView& s,
+                          const BatchView& bv, const int32_t* list, const uint32_t* count, int max_n, uint64_t* fmask,
+                          int32_t* est, int md_cap) {
+  const int n = (int)*(const volatile uint32_t*)count;
+  for (int i = blk; i < n && i < max_n; i += grid) {
+    B.sync();  // the previous binding's LDS readers are done
+    pair_one<Fast>(B, list[i], smem, s, bv, fmask, est, nullptr, 0, md_cap);
   }
 }
 
@@ -207,6 +262,54 @@ KP_FI void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
   KP_STAMP(x, 1);
   LdsCands cs{&cd, B.tid(), B.nth()};
   select_all_common(B, a, x, cs, cd.F, ss);
+}
+
+// ---------------------------------------------------------------------------
+// Fused pair + SEL_ALL select (k_fused_all): one workgroup per SEL_ALL binding.
+// The pair stage leaves the binding's feasibility bits and per-cluster votes
+// (calAvailableReplicas, or the StaticWeight vote) in LDS, and the assignment
+// reads them there: no per-pair row is written to HBM and read back. Bindings
+// the fast assignment refuses are flagged for k_slow; k_pair_list writes their
+// HBM rows (the same pair body) before k_slow reads them.
+// LDS: [red | tgt bits | fit u64[W] | row i32[Cp] | union{ pair: PairLds tail ; select: SelScratch }]
+// ---------------------------------------------------------------------------
+template <int Fast, class BLK>
+KP_FI void body_fused_all(const BLK& B, int blk, unsigned char* smem, const KArgs& a, int md_cap) {
+  if (blk >= a.n) return;
+  const int b = a.list[blk];
+  const SnapView& s = a.s;
+  const BindHdr h = a.bv.hdr[b];
+  const int words = (s.Cp + 31) >> 5;
+  uint32_t* tgt = (uint32_t*)(smem + kRedBytes);
+  uint64_t* fit = (uint64_t*)(tgt + ((words + 3) & ~3));
+  int32_t* row = (int32_t*)(fit + ((s.W + 1) & ~1));
+  unsigned char* un = (unsigned char*)(row + s.Cp);
+  const PairLds L = pair_lds_carve(tgt, un, s.Cp, md_cap);
+  bool use_md, use_ts;
+  const BatchView lv = pair_setup(B, s, a.bv, h, L, 0, md_cap, &use_md, &use_ts);
+  // StaticWeight SEL_ALL bindings vote with their static weights: the estimator is
+  // not evaluated for them (getStaticWeightInfoList, division_algorithm.go:38-72).
+  const bool weights = h.strategy == ST_STATIC && h.sel == SEL_ALL;
+  BindHdr hp = h;
+  if (weights) hp.flags |= BF_NONWORKLOAD_EST;
+  SelCtx xs = make_ctx(a, b, tgt);
+  xs.bv = &lv;
+  int32_t mine = 0;
+  for (int base = 0; base < s.Cp; base += B.nth()) {
+    const int c = base + B.tid();
+    bool ok = false;
+    int32_t v = pair_eval<Fast>(s, lv, hp, c, tgt, L.evict, L.tolb, L.md, &ok);
+    if (weights && ok) v = static_vote(xs, c);
+    B.mask_store(fit, c, ok, s.W);
+    row[c] = v;
+    mine += ok ? 1 : 0;
+  }
+  const int F = (int)B.sum64(mine);  // (its barrier also publishes fit and row)
+  SelCtx x = make_ctx(a, b, tgt);
+  x.frow = fit;
+  x.erow = row;
+  const SelScratch ss = carve_sel_scratch(un, s.Cp);  // the pair state is dead now
+  select_all_common(B, a, x, RowCands{fit, row, s.C, B.tid(), B.nth()}, F, ss);
 }
 
 // Candidates in registers: thread t owns clusters t + nth*j, j < J (C <= nth*J).

@@ -62,4 +62,18 @@ KP_HD inline int sel_all_slots(int C) {
   return 0;
 }
 
+// LDS bytes of the pair stage's per-binding tail (evict bits | md table | predicate
+// stage | taint-list bits; kp_kernels.h PairLds).
+KP_HD inline size_t pair_lds_tail_bytes(int Cp, int md_cap) {  // evict | md | stage | tolb
+  const int words = (Cp + 31) >> 5;
+  return 4 * (size_t)((words + 3) & ~3) + 4 * (size_t)((md_cap + 3) & ~3) + kPairStage + kTsetMax / 8;
+}
+// Dynamic LDS of k_fused_all (kp_kernels.h body_fused_all).
+KP_HD inline size_t fused_lds_bytes(int Cp, int md_cap) {
+  const int words = (Cp + 31) >> 5, W = Cp / 64;
+  const size_t pair_tail = pair_lds_tail_bytes(Cp, md_cap);
+  const size_t sel = 3072 + 8 * (size_t)sel_all_ecap(Cp);
+  return kRedBytes + 4 * (size_t)((words + 3) & ~3) + 8 * (size_t)((W + 1) & ~1) + 4 * (size_t)Cp +
+         (pair_tail > sel ? pair_tail : sel) + 64;
+}
 }  // namespace kp

@@ -85,6 +85,29 @@ KP_UNROLL
   static constexpr bool kSettable = false;
 };
 
+// The fused pair + select kernel's candidates: the clusters whose feasibility
+// bit is set in the LDS bitset `fit` (u64 words, the fmask row layout), with
+// v = row[c] (calAvailableReplicas, or the StaticWeight vote) in LDS. Thread t
+// owns clusters t + nth*j.
+struct RowCands {
+  const uint64_t* fit;
+  int32_t* row;
+  int C, tid, nth;
+  template <class Fn>
+  KP_FI void each(Fn fn) const {
+    for (int c = tid; c < C; c += nth)
+      if ((fit[c >> 6] >> (c & 63)) & 1ull) fn((uint32_t)c, row[c]);
+  }
+  template <class Fn>
+  KP_FI void each_set(Fn fn) const {
+    for (int c = tid; c < C; c += nth)
+      if ((fit[c >> 6] >> (c & 63)) & 1ull) row[c] = fn((uint32_t)c, row[c]);
+  }
+  static constexpr bool kSettable = true;
+  KP_FI uint64_t okey(const SelCtx& x, uint32_t rk, int32_t v0) const { return cand_order_key(x, rk, v0); }
+  static constexpr bool kExact = false;
+};
+
 // Gathered candidates (any memory) whose sort.Sort output order is known:
 // pos[rank] = position after the emulated sort (k_slow, kp_pdq.h).
 struct PosCands {

@@ -27,13 +27,26 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
-def test_abi_version_and_struct_sizes():
+STRUCTS = ("kp_str", "kp_label", "kp_requirement", "kp_cluster_affinity", "kp_affinity_term", "kp_toleration",
+           "kp_taint", "kp_spread_constraint", "kp_static_weight", "kp_resource", "kp_target_cluster", "kp_binding",
+           "kp_api_enablement", "kp_model_range", "kp_resource_model", "kp_allocatable_modeling", "kp_cluster",
+           "kp_options", "kp_results", "kp_affinity_results", "kp_stage_times")
+
+
+def test_abi_version_and_struct_sizes(tmp_path):
+    """The ctypes mirrors (karmada_amd/api.py) have the C layout of every struct the
+    header declares: sizes compiled from the header itself with the host compiler."""
+    import subprocess
     L = engine.load_library()
     assert L.kp_abi_version() == engine.KP_ABI_VERSION
-    # ctypes mirrors must match the C layout (x86-64 SysV)
-    assert C.sizeof(api.kp_str) == 16
-    assert C.sizeof(api.kp_results) == 64
-    assert C.sizeof(api.kp_stage_times) == 64
+    src = tmp_path / "sizes.c"
+    src.write_text('#include <stdio.h>\n#include "kp/kp_api.h"\nint main(void) {\n' +
+                   "".join(f'  printf("%zu\\n", sizeof({n}));\n' for n in STRUCTS) + "  return 0;\n}\n")
+    exe = tmp_path / "sizes"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)])
+    sizes = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    for n, sz in zip(STRUCTS, sizes):
+        assert C.sizeof(getattr(api, n)) == sz, n
 
 
 def test_engine_create_fails_loudly_without_gpu():
