@@ -162,6 +162,7 @@ KP_FI void pair_one(const BLK& B, int b, unsigned char* smem, const SnapView& s,
   int32_t* erow = est + (size_t)b * s.Cp;
   for (int base = 0; base < s.Cp; base += B.nth()) {
     const int c = base + B.tid();
+    if (c >= s.Cp) break;  // wave-uniform: Cp and the wave bases are multiples of 64
     bool fit = false;
     int32_t e = 0;
     if (Fast != EST_GENERIC) {
@@ -173,7 +174,7 @@ KP_FI void pair_one(const BLK& B, int b, unsigned char* smem, const SnapView& s,
       fit = true;
     }
     B.mask_store(frow, c, fit, s.W);
-    if (c < s.Cp) erow[c] = e;
+    erow[c] = e;
     if (score && c < s.C) {
       int64_t sc = 0;
       if ((h.enabled & KP_PLUGIN_CLUSTER_LOCALITY) && h.n_targets_all > 0 && h.tgt_cnt > 0 && bit_test(tgt, c)) sc = 100;
@@ -297,6 +298,7 @@ KP_FI void body_fused_all(const BLK& B, int blk, unsigned char* smem, const KArg
   int32_t mine = 0;
   for (int base = 0; base < s.Cp; base += B.nth()) {
     const int c = base + B.tid();
+    if (c >= s.Cp) break;  // wave-uniform: Cp and the wave bases are multiples of 64
     bool ok = false;
     int32_t v = pair_eval<Fast>(s, lv, hp, c, tgt, L.evict, L.tolb, L.md, &ok);
     if (weights && ok) v = static_vote(xs, c);
