@@ -23,7 +23,9 @@ for s in "$@"; do
     chunks) for c in 4096 8192 16384 32768 200000; do KP_CHUNK=$c step chunk_$c 300 python bench.py --steps 5 --warmup 1 --no-cpu; done ;;
     configs) for c in 2 4 6; do step bench_config$c 300 python bench.py --config $c --steps 3 --warmup 1 --no-cpu; done
              step bench_config5 300 python bench.py --config 5 --bindings 125000 --steps 3 --warmup 1 --no-cpu ;;
-    stamps) step stamps 300 python bench.py --lib karmada_amd/libkp_stamps.so --steps 2 --warmup 1 --no-cpu ;;
+    stamps) step stamps 300 python bench.py --lib karmada_amd/libkp_stamps.so --steps 2 --warmup 1 --no-cpu --check 0 ;;
+    lib_*) n=${s#lib_}; step bench_$n 300 python bench.py --lib karmada_amd/libkp_$n.so --steps 50 --warmup 2 --no-cpu --check 200 ;;
+    libst_*) n=${s#libst_}; step stamps_$n 300 python bench.py --lib karmada_amd/libkp_$n.so --steps 2 --warmup 1 --no-cpu --check 0 ;;
     prof_sq) step prof_sq 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $ROOT/gpurun_out/prof_sq -o sq -- python3 $ROOT/bench.py --steps 1 --warmup 0 --no-cpu" ;;
     prof_kt) step prof_kt 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/prof_kt -o kt -- python3 $ROOT/bench.py --steps 5 --warmup 1 --no-cpu" ;;
     prof_fetch) step prof_fetch 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --pmc FETCH_SIZE --output-format csv -d $ROOT/gpurun_out/prof_fetch -o f -- python3 $ROOT/bench.py --steps 2 --warmup 0 --no-cpu" ;;

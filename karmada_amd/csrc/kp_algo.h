@@ -174,6 +174,87 @@ KP_HD inline bool prog_match(const SnapView& s, const BatchView& bv, int32_t pro
   return true;
 }
 
+// The same program evaluated with block-uniform control flow, for the fast pair
+// kernels: the program text is read at uniform addresses (scalar loads from the
+// batch pools in HBM), every lane runs every instruction (no per-lane early
+// exit, so the loops stay uniform), and list membership is an OR over the
+// uniform list. Same answer as prog_match for c < C; lanes C <= c < Cp read
+// in-bounds padding and are masked out by the caller. Requires C >= 1.
+KP_HD inline bool prog_eval_u(const SnapView& s, const BatchView& bv, int32_t prog_id, int c) {
+  const Prog p = bv.progs[prog_id];
+  bool ok = true;
+  for (int i = 0; i < p.ins_cnt; i++) {
+    const Instr in = bv.instrs[p.ins_off + i];
+    const int32_t* lst = bv.ipool + (in.op == OP_EXCLUDE || in.op == OP_NAMES ? in.a : in.b);
+    const int nl = in.op == OP_EXCLUDE || in.op == OP_NAMES ? in.b : in.c;
+    switch (in.op) {
+      case OP_FALSE:
+        ok = false;
+        break;
+      case OP_TRUE:
+        break;
+      case OP_EXCLUDE:
+      case OP_NAMES: {
+        bool hit = false;
+        for (int k = 0; k < nl; k++) hit = hit | (lst[k] == c);
+        ok = ok & (in.op == OP_NAMES ? hit : !hit);
+        break;
+      }
+      case OP_LBL_IN:
+      case OP_LBL_NOTIN:
+      case OP_FLD_IN:
+      case OP_FLD_NOTIN: {
+        const bool lbl = in.op == OP_LBL_IN || in.op == OP_LBL_NOTIN;
+        const int32_t v = lbl ? s.label_val[(size_t)in.a * s.Cp + c] : (in.a == 0 ? s.provider[c] : s.region[c]);
+        bool hit = false;
+        for (int k = 0; k < nl; k++) hit = hit | (lst[k] == v);
+        const bool isin = in.op == OP_LBL_IN || in.op == OP_FLD_IN;
+        ok = ok & (isin ? ((v >= 0) & hit) : ((v < 0) | !hit));
+        break;
+      }
+      case OP_LBL_EXISTS:
+      case OP_LBL_DNE: {
+        const int32_t v = s.label_val[(size_t)in.a * s.Cp + c];
+        ok = ok & (in.op == OP_LBL_EXISTS ? v >= 0 : v < 0);
+        break;
+      }
+      case OP_FLD_EXISTS:
+      case OP_FLD_DNE: {
+        const int32_t v = in.a == 0 ? s.provider[c] : s.region[c];
+        ok = ok & (in.op == OP_FLD_EXISTS ? v >= 0 : v < 0);
+        break;
+      }
+      case OP_FLD_GT:
+      case OP_FLD_LT: {
+        const uint32_t f = s.flags[c];
+        const bool has = (in.a == 0 ? (f & CF_PROVIDER_INT) : (f & CF_REGION_INT)) != 0;
+        const int64_t x = in.a == 0 ? s.provider_int[c] : s.region_int[c];
+        ok = ok & has & (in.op == OP_FLD_GT ? x > in.v : x < in.v);
+        break;
+      }
+      case OP_ZONE_IN:
+      case OP_ZONE_NOTIN:
+      case OP_ZONE_EXISTS:
+      case OP_ZONE_DNE: {
+        const int cc = c < s.C ? c : s.C - 1;  // zone_off has C + 1 entries
+        const int z0 = s.zone_off[cc], z1 = s.zone_off[cc + 1];
+        if (in.op == OP_ZONE_EXISTS || in.op == OP_ZONE_DNE) {
+          ok = ok & (in.op == OP_ZONE_EXISTS ? z1 > z0 : z1 == z0);
+        } else {
+          bool hit = false;
+          for (int z = z0; z < z1; z++)
+            for (int k = 0; k < nl; k++) hit = hit | (lst[k] == s.zone_ids[z]);
+          ok = ok & (in.op == OP_ZONE_IN ? ((z1 > z0) & hit) : !hit);
+        }
+        break;
+      }
+      default:
+        ok = false;
+    }
+  }
+  return ok;
+}
+
 // ============================================================================
 // Pair stage
 // ============================================================================
@@ -458,7 +539,13 @@ KP_HD inline int32_t pair_eval(const SnapView& s, const BatchView& bv, const Bin
   // ClusterAffinity first: its selector loads then issue while the loads above
   // are still in flight (it reads none of them).
   bool aff = true;
-  if ((en & 4) && !(h.flags & BF_AFF_ALL) && c < s.C) {  // (zone lists are [C+1])
+  if (Fast != EST_GENERIC) {
+    // uniform loop over the affinity terms (scalar program loads), no early exit
+    if ((en & 4) && !(h.flags & BF_AFF_ALL) && s.C > 0) {
+      aff = false;
+      for (int j = 0; j < h.filt_cnt; j++) aff = aff | prog_eval_u(s, bv, bv.ipool[h.filt_off + j], c);
+    }
+  } else if ((en & 4) && !(h.flags & BF_AFF_ALL) && c < s.C) {  // (zone lists are [C+1])
     aff = false;
     for (int j = 0; j < h.filt_cnt && !aff; j++) aff = prog_match(s, bv, bv.ipool[h.filt_off + j], c);
   }

@@ -344,6 +344,16 @@ struct CpuBlk {
   }
 };
 
+// A block-uniform value moved to a scalar register (the first active lane's
+// copy): lets the compiler keep per-binding tables in SGPRs. Identity on the host.
+KP_HD inline int32_t kp_uniform(int32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_readfirstlane(v);
+#else
+  return v;
+#endif
+}
+
 // Atomics on LDS/global memory, usable from both builds.
 template <class T>
 KP_HD inline T kp_atomic_add(T* p, T v) {

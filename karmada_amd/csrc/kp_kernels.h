@@ -96,12 +96,13 @@ KP_HD inline PairLds pair_lds_carve(uint32_t* tgt, unsigned char* tail, int Cp, 
 }
 
 // Fills the pair stage's LDS state for binding h; returns the view of the batch
-// whose predicate pools point into LDS when they fit the stage (absolute pool
-// indices keep working). *use_md / *use_ts: whether the MaxDivided table and the
-// taint-list answers were built.
+// whose predicate pools point into LDS when they fit the stage and `stage` is
+// set (absolute pool indices keep working; the fast kernels read the programs
+// with scalar loads from HBM instead). *use_md / *use_ts: whether the
+// MaxDivided table and the taint-list answers were built.
 template <class BLK>
 KP_FI BatchView pair_setup(const BLK& B, const SnapView& s, const BatchView& bv, const BindHdr& h, const PairLds& L,
-                           int est_mode, int md_cap, bool* use_md, bool* use_ts) {
+                           int est_mode, int md_cap, bool* use_md, bool* use_ts, bool stage = true) {
   const int words = (s.Cp + 31) >> 5;
   build_bits(B, L.tgt, words, bv.ipool, h.tgt_off, h.tgt_cnt, 2);
   build_bits(B, L.evict, words, bv.ipool, h.evict_off, h.evict_cnt, 1);
@@ -117,7 +118,7 @@ KP_FI BatchView pair_setup(const BLK& B, const SnapView& s, const BatchView& bv,
   {
     const int nin = h.in_end - h.in_beg, npr = h.pr_end - h.pr_beg, nip = h.ip_end - h.ip_beg, nto = h.tol_cnt;
     const size_t need = sizeof(Instr) * nin + sizeof(Prog) * npr + sizeof(Tol) * nto + 4 * (size_t)nip;
-    if (need <= (size_t)kPairStage) {
+    if (stage && need <= (size_t)kPairStage) {
       Instr* si = (Instr*)L.stage;
       Prog* sp = (Prog*)(si + nin);
       Tol* so = (Tol*)(sp + npr);
@@ -146,6 +147,19 @@ KP_FI BatchView pair_setup(const BLK& B, const SnapView& s, const BatchView& bv,
   return lv;
 }
 
+// The per-template MaxDivided table of the fast kernels in scalar registers
+// (kTmplDense entries, zero past n_tmpl): built in LDS by pair_setup, one
+// template per thread, then read once per binding.
+struct MdTab {
+  int32_t v[kTmplDense];
+};
+KP_FI MdTab md_regs(const int32_t* md) {
+  MdTab t;
+KP_UNROLL
+  for (int i = 0; i < kTmplDense; i++) t.v[i] = kp_uniform(md[i]);
+  return t;
+}
+
 // Fast: the estimator instance (EST_*, kp_algo.h); every instance but
 // EST_GENERIC needs pair_fast_ok (engine.cpp): est_mode 0, the MaxDivided and
 // taint-set tables in LDS, no cold fallbacks.
@@ -157,7 +171,9 @@ KP_FI void pair_one(const BLK& B, int b, unsigned char* smem, const SnapView& s,
   uint32_t* tgt = (uint32_t*)(smem + kRedBytes);
   const PairLds L = pair_lds_carve(tgt, (unsigned char*)(tgt + ((words + 3) & ~3)), s.Cp, md_cap);
   bool use_md, use_ts;
-  const BatchView lv = pair_setup(B, s, bv, h, L, est_mode, md_cap, &use_md, &use_ts);
+  const BatchView lv = pair_setup(B, s, bv, h, L, est_mode, md_cap, &use_md, &use_ts, Fast == EST_GENERIC);
+  MdTab mdt;
+  if (Fast != EST_GENERIC) mdt = md_regs(L.md);
   uint64_t* frow = fmask + (size_t)b * s.W;
   int32_t* erow = est + (size_t)b * s.Cp;
   for (int base = 0; base < s.Cp; base += B.nth()) {
@@ -166,7 +182,7 @@ KP_FI void pair_one(const BLK& B, int b, unsigned char* smem, const SnapView& s,
     bool fit = false;
     int32_t e = 0;
     if (Fast != EST_GENERIC) {
-      e = pair_eval<Fast>(s, lv, h, c, tgt, L.evict, L.tolb, L.md, &fit);
+      e = pair_eval<Fast>(s, bv, h, c, tgt, L.evict, L.tolb, mdt.v, &fit);
     } else if (est_mode == 0) {
       e = pair_eval(s, lv, h, c, tgt, L.evict, use_ts ? L.tolb : nullptr, use_md ? L.md : nullptr, &fit);
     } else if (c < s.C) {
@@ -277,6 +293,7 @@ KP_FI void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
 template <int Fast, class BLK>
 KP_FI void body_fused_all(const BLK& B, int blk, unsigned char* smem, const KArgs& a, int md_cap) {
   if (blk >= a.n) return;
+  KP_STAMP_INIT
   const int b = a.list[blk];
   const SnapView& s = a.s;
   const BindHdr h = a.bv.hdr[b];
@@ -287,26 +304,27 @@ KP_FI void body_fused_all(const BLK& B, int blk, unsigned char* smem, const KArg
   unsigned char* un = (unsigned char*)(row + s.Cp);
   const PairLds L = pair_lds_carve(tgt, un, s.Cp, md_cap);
   bool use_md, use_ts;
-  const BatchView lv = pair_setup(B, s, a.bv, h, L, 0, md_cap, &use_md, &use_ts);
+  (void)pair_setup(B, s, a.bv, h, L, 0, md_cap, &use_md, &use_ts, false);
+  const MdTab mdt = md_regs(L.md);
   // StaticWeight SEL_ALL bindings vote with their static weights: the estimator is
   // not evaluated for them (getStaticWeightInfoList, division_algorithm.go:38-72).
   const bool weights = h.strategy == ST_STATIC && h.sel == SEL_ALL;
   BindHdr hp = h;
   if (weights) hp.flags |= BF_NONWORKLOAD_EST;
-  SelCtx xs = make_ctx(a, b, tgt);
-  xs.bv = &lv;
+  KP_STAMPD(a.dbg, 0);  // pair setup
   int32_t mine = 0;
   for (int base = 0; base < s.Cp; base += B.nth()) {
     const int c = base + B.tid();
     if (c >= s.Cp) break;  // wave-uniform: Cp and the wave bases are multiples of 64
     bool ok = false;
-    int32_t v = pair_eval<Fast>(s, lv, hp, c, tgt, L.evict, L.tolb, L.md, &ok);
-    if (weights && ok) v = static_vote(xs, c);
+    int32_t v = pair_eval<Fast>(s, a.bv, hp, c, tgt, L.evict, L.tolb, mdt.v, &ok);
+    if (weights && ok) v = static_vote_u(s, a.bv, h, c);
     B.mask_store(fit, c, ok, s.W);
     row[c] = v;
     mine += ok ? 1 : 0;
   }
   const int F = (int)B.sum64(mine);  // (its barrier also publishes fit and row)
+  KP_STAMPD(a.dbg, 15);  // pair loop
   SelCtx x = make_ctx(a, b, tgt);
   x.frow = fit;
   x.erow = row;

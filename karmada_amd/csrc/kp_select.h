@@ -85,11 +85,11 @@ struct SelCtx {
 // Diagnostic phase stamps (a separate -DKP_STAMPS build; never in libkp.so).
 #if defined(KP_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
 #define KP_STAMP_INIT unsigned long long kp_t0 = __builtin_amdgcn_s_memtime();
-#define KP_STAMP(x, i)                                                   \
+#define KP_STAMP(ctx_, i)                                                \
   do {                                                                   \
-    if (threadIdx.x == 0 && (x).dbg) {                                   \
+    if (threadIdx.x == 0 && (ctx_).dbg) {                                \
       unsigned long long t = __builtin_amdgcn_s_memtime();               \
-      atomicAdd(&(x).dbg[i], t - kp_t0);                                 \
+      atomicAdd(&(ctx_).dbg[i], t - kp_t0);                              \
       kp_t0 = t;                                                         \
     }                                                                    \
   } while (0)
@@ -533,6 +533,21 @@ KP_HD inline int32_t static_vote(const SelCtx& x, int c) {
         int64_t rw = x.bv->lpool[h.sw_w_off + j];
         if (rw > wt) wt = rw;
       }
+  }
+  return (int32_t)(wt > kInt32Max ? kInt32Max : wt);
+}
+
+// static_vote with the uniform program evaluation of the fast kernels (c < C).
+KP_HD inline int32_t static_vote_u(const SnapView& s, const BatchView& bv, const BindHdr& h, int c) {
+  int64_t wt = 0;
+  if (!(h.flags & BF_HAS_WP)) {
+    wt = 1;
+  } else {
+    for (int j = 0; j < h.sw_cnt; j++) {
+      const bool m = prog_eval_u(s, bv, bv.ipool[h.sw_off + j], c);
+      const int64_t rw = bv.lpool[h.sw_w_off + j];
+      if (m && rw > wt) wt = rw;
+    }
   }
   return (int32_t)(wt > kInt32Max ? kInt32Max : wt);
 }
