@@ -180,24 +180,38 @@ KP_HD inline bool prog_match(const SnapView& s, const BatchView& bv, int32_t pro
 // exit, so the loops stay uniform), and list membership is an OR over the
 // uniform list. Same answer as prog_match for c < C; lanes C <= c < Cp read
 // in-bounds padding and are masked out by the caller. Requires C >= 1.
-KP_HD inline bool prog_eval_u(const SnapView& s, const BatchView& bv, int32_t prog_id, int c) {
+// U clusters per lane (c[0..U)): every instruction issues its loads for all U
+// clusters before comparing, so a wave has U memory round trips in flight.
+template <int U>
+KP_HD inline void prog_eval_u(const SnapView& s, const BatchView& bv, int32_t prog_id, const int (&c)[U],
+                              bool (&res)[U]) {
   const Prog p = bv.progs[prog_id];
-  bool ok = true;
+  bool ok[U];
+KP_UNROLL
+  for (int u = 0; u < U; u++) ok[u] = true;
   for (int i = 0; i < p.ins_cnt; i++) {
     const Instr in = bv.instrs[p.ins_off + i];
     const int32_t* lst = bv.ipool + (in.op == OP_EXCLUDE || in.op == OP_NAMES ? in.a : in.b);
     const int nl = in.op == OP_EXCLUDE || in.op == OP_NAMES ? in.b : in.c;
     switch (in.op) {
       case OP_FALSE:
-        ok = false;
+KP_UNROLL
+        for (int u = 0; u < U; u++) ok[u] = false;
         break;
       case OP_TRUE:
         break;
       case OP_EXCLUDE:
       case OP_NAMES: {
-        bool hit = false;
-        for (int k = 0; k < nl; k++) hit = hit | (lst[k] == c);
-        ok = ok & (in.op == OP_NAMES ? hit : !hit);
+        bool hit[U];
+KP_UNROLL
+        for (int u = 0; u < U; u++) hit[u] = false;
+        for (int k = 0; k < nl; k++) {
+          const int32_t x = lst[k];
+KP_UNROLL
+          for (int u = 0; u < U; u++) hit[u] = hit[u] | (x == c[u]);
+        }
+KP_UNROLL
+        for (int u = 0; u < U; u++) ok[u] = ok[u] & (in.op == OP_NAMES ? hit[u] : !hit[u]);
         break;
       }
       case OP_LBL_IN:
@@ -205,54 +219,79 @@ KP_HD inline bool prog_eval_u(const SnapView& s, const BatchView& bv, int32_t pr
       case OP_FLD_IN:
       case OP_FLD_NOTIN: {
         const bool lbl = in.op == OP_LBL_IN || in.op == OP_LBL_NOTIN;
-        const int32_t v = lbl ? s.label_val[(size_t)in.a * s.Cp + c] : (in.a == 0 ? s.provider[c] : s.region[c]);
-        bool hit = false;
-        for (int k = 0; k < nl; k++) hit = hit | (lst[k] == v);
+        const int32_t* col = lbl ? s.label_val + (size_t)in.a * s.Cp : (in.a == 0 ? s.provider : s.region);
+        int32_t v[U];
+        bool hit[U];
+KP_UNROLL
+        for (int u = 0; u < U; u++) {
+          v[u] = col[c[u]];
+          hit[u] = false;
+        }
+        for (int k = 0; k < nl; k++) {
+          const int32_t x = lst[k];
+KP_UNROLL
+          for (int u = 0; u < U; u++) hit[u] = hit[u] | (x == v[u]);
+        }
         const bool isin = in.op == OP_LBL_IN || in.op == OP_FLD_IN;
-        ok = ok & (isin ? ((v >= 0) & hit) : ((v < 0) | !hit));
+KP_UNROLL
+        for (int u = 0; u < U; u++) ok[u] = ok[u] & (isin ? ((v[u] >= 0) & hit[u]) : ((v[u] < 0) | !hit[u]));
         break;
       }
       case OP_LBL_EXISTS:
-      case OP_LBL_DNE: {
-        const int32_t v = s.label_val[(size_t)in.a * s.Cp + c];
-        ok = ok & (in.op == OP_LBL_EXISTS ? v >= 0 : v < 0);
-        break;
-      }
+      case OP_LBL_DNE:
       case OP_FLD_EXISTS:
       case OP_FLD_DNE: {
-        const int32_t v = in.a == 0 ? s.provider[c] : s.region[c];
-        ok = ok & (in.op == OP_FLD_EXISTS ? v >= 0 : v < 0);
-        break;
-      }
-      case OP_FLD_GT:
-      case OP_FLD_LT: {
-        const uint32_t f = s.flags[c];
-        const bool has = (in.a == 0 ? (f & CF_PROVIDER_INT) : (f & CF_REGION_INT)) != 0;
-        const int64_t x = in.a == 0 ? s.provider_int[c] : s.region_int[c];
-        ok = ok & has & (in.op == OP_FLD_GT ? x > in.v : x < in.v);
-        break;
-      }
-      case OP_ZONE_IN:
-      case OP_ZONE_NOTIN:
-      case OP_ZONE_EXISTS:
-      case OP_ZONE_DNE: {
-        const int cc = c < s.C ? c : s.C - 1;  // zone_off has C + 1 entries
-        const int z0 = s.zone_off[cc], z1 = s.zone_off[cc + 1];
-        if (in.op == OP_ZONE_EXISTS || in.op == OP_ZONE_DNE) {
-          ok = ok & (in.op == OP_ZONE_EXISTS ? z1 > z0 : z1 == z0);
-        } else {
-          bool hit = false;
-          for (int z = z0; z < z1; z++)
-            for (int k = 0; k < nl; k++) hit = hit | (lst[k] == s.zone_ids[z]);
-          ok = ok & (in.op == OP_ZONE_IN ? ((z1 > z0) & hit) : !hit);
+        const bool lbl = in.op == OP_LBL_EXISTS || in.op == OP_LBL_DNE;
+        const int32_t* col = lbl ? s.label_val + (size_t)in.a * s.Cp : (in.a == 0 ? s.provider : s.region);
+        const bool ex = in.op == OP_LBL_EXISTS || in.op == OP_FLD_EXISTS;
+KP_UNROLL
+        for (int u = 0; u < U; u++) {
+          const int32_t v = col[c[u]];
+          ok[u] = ok[u] & (ex ? v >= 0 : v < 0);
         }
         break;
       }
+      case OP_FLD_GT:
+      case OP_FLD_LT:
+KP_UNROLL
+        for (int u = 0; u < U; u++) {
+          const uint32_t f = s.flags[c[u]];
+          const bool has = (in.a == 0 ? (f & CF_PROVIDER_INT) : (f & CF_REGION_INT)) != 0;
+          const int64_t x = in.a == 0 ? s.provider_int[c[u]] : s.region_int[c[u]];
+          ok[u] = ok[u] & has & (in.op == OP_FLD_GT ? x > in.v : x < in.v);
+        }
+        break;
+      case OP_ZONE_IN:
+      case OP_ZONE_NOTIN:
+      case OP_ZONE_EXISTS:
+      case OP_ZONE_DNE:
+KP_UNROLL
+        for (int u = 0; u < U; u++) {
+          const int cc = c[u] < s.C ? c[u] : s.C - 1;  // zone_off has C + 1 entries
+          const int z0 = s.zone_off[cc], z1 = s.zone_off[cc + 1];
+          if (in.op == OP_ZONE_EXISTS || in.op == OP_ZONE_DNE) {
+            ok[u] = ok[u] & (in.op == OP_ZONE_EXISTS ? z1 > z0 : z1 == z0);
+          } else {
+            bool hit = false;
+            for (int z = z0; z < z1; z++)
+              for (int k = 0; k < nl; k++) hit = hit | (lst[k] == s.zone_ids[z]);
+            ok[u] = ok[u] & (in.op == OP_ZONE_IN ? ((z1 > z0) & hit) : !hit);
+          }
+        }
+        break;
       default:
-        ok = false;
+KP_UNROLL
+        for (int u = 0; u < U; u++) ok[u] = false;
     }
   }
-  return ok;
+KP_UNROLL
+  for (int u = 0; u < U; u++) res[u] = ok[u];
+}
+KP_HD inline bool prog_eval_u(const SnapView& s, const BatchView& bv, int32_t prog_id, int c) {
+  const int cc[1] = {c};
+  bool r[1];
+  prog_eval_u<1>(s, bv, prog_id, cc, r);
+  return r[0];
 }
 
 // ============================================================================
@@ -499,6 +538,63 @@ KP_HD inline int32_t general_estimate(const SnapView& s, const BatchView& bv, co
   return est_compute(s, bv, h, c, md, est_load(s, bv, h, c, s.flags[c]));
 }
 
+// Branch-free forms of est_compute / cal_merge for the fast instances (the
+// same answers; per-lane conditions become selects, so a wave's lanes never
+// diverge inside the pair loop). floor_div_bf: min(a / q, lim) for a >= 1,
+// 1 <= q <= 2^60, 0 <= lim < 2^31 + 2: the double quotient is within 1 of the
+// true one below 2^33 (three roundings of relative 2^-53), so two selects fix it.
+KP_HD inline int64_t floor_div_bf(int64_t a, int64_t q, int64_t lim) {
+  const double est = kp_floor((double)a / (double)q);
+  const bool big = est >= (double)lim + 2.0;
+  uint64_t e = big ? 0ull : (uint64_t)est;
+  const uint64_t ua = (uint64_t)a, uq = (uint64_t)q;
+  e = (e > 0 && e * uq > ua) ? e - 1 : e;
+  e = ((e + 1) * uq <= ua) ? e + 1 : e;
+  const int64_t d = (int64_t)e < lim ? (int64_t)e : lim;
+  return big ? lim : (a < q ? 0 : d);
+}
+template <int Fast>
+KP_HD inline int32_t est_compute_bf(const SnapView& s, const BatchView& bv, const BindHdr& h, int c,
+                                    const int32_t* md, const EstOps& o) {
+  const uint32_t f = o.f;
+  const int64_t allowed = o.allowed;
+  int64_t m = allowed;
+  const bool rr = (h.flags & BF_HAS_RR) != 0;  // uniform
+  // model path: sum_t MaxDivided_t * nodes_t, clamped at MaxInt32
+  int64_t total = 0;
+KP_UNROLL
+  for (int t = 0; t < kTmplDense; t++)
+    if (Fast >= EST_MODEL8 ? t < Fast : (Fast == EST_MIXED && t < s.n_tmpl)) total += (int64_t)md[t] * (int64_t)o.mt[t];
+  total = total >= kInt32Max ? (int64_t)kInt32Max : total;
+  const int64_t mod = total < m ? total : m;
+  // summary path (general.go:465-505), requests j < kReqUnroll (pair_fast_ok)
+  int64_t sum = m;
+  if (Fast == EST_MIXED || Fast == EST_SUMMARY) {
+    int64_t num = INT64_MAX;
+    bool zero = false;
+KP_UNROLL
+    for (int j = 0; j < kReqUnroll; j++) {
+      if (j < h.sreq_cnt) {  // uniform
+        const bool z = bv.ipool[h.sreq_off + j] < 0 || o.av[j] <= 0;
+        const int64_t lim = num < m ? num : m;
+        const int64_t d = floor_div_bf(z ? 1 : o.av[j], bv.lpool[h.sreq_q_off + j], lim);
+        zero = zero | z;
+        num = d < num ? d : num;
+      }
+    }
+    sum = zero ? 0 : (num < m ? num : m);
+  } else if (rr) {  // (model-only snapshots: every summary cluster has models; exact fallback)
+    if (!(f & CF_MODEL_OK) && (f & CF_HAS_SUMMARY) && allowed > 0) sum = est_compute<Fast>(s, bv, h, c, md, o);
+  }
+  int64_t r = !rr ? m : ((f & CF_MODEL_OK) ? mod : sum);
+  r = ((f & CF_HAS_SUMMARY) && allowed > 0) ? r : 0;
+  return (int32_t)r;
+}
+KP_HD inline int32_t cal_merge_bf(int32_t replicas, int32_t r) {
+  const int32_t v = (r != -1 && r < kInt32Max) ? r : kInt32Max;
+  return v == kInt32Max ? replicas : v;
+}
+
 // calAvailableReplicas over an estimate: MaxInt32 init, min with the
 // GeneralEstimator answer (-1 = UnauthenticReplica is skipped, core/util.go:86-99),
 // leftover MaxInt32 -> spec.Replicas.
@@ -533,13 +629,21 @@ KP_HD inline int32_t pair_eval(const SnapView& s, const BatchView& bv, const Bin
   const bool tset_on = (en & 2) && (Fast != EST_GENERIC || tol_bits != nullptr);
   int32_t ts = 0;
   if (tset_on) ts = s.taint_set[c];
+#ifdef KP_EXP_NOEST  // timing experiments only (tuning variants, wrong answers)
+  const bool est_on = false;
+#else
   const bool est_on = !(h.flags & BF_NONWORKLOAD_EST);
+#endif
   EstOps o;
   if (est_on) o = est_load<Fast>(s, bv, h, c, f);
   // ClusterAffinity first: its selector loads then issue while the loads above
   // are still in flight (it reads none of them).
   bool aff = true;
+#ifdef KP_EXP_NOAFF  // timing experiments only (tuning variants, wrong answers)
+  if (false) {
+#else
   if (Fast != EST_GENERIC) {
+#endif
     // uniform loop over the affinity terms (scalar program loads), no early exit
     if ((en & 4) && !(h.flags & BF_AFF_ALL) && s.C > 0) {
       aff = false;
@@ -564,6 +668,70 @@ KP_HD inline int32_t pair_eval(const SnapView& s, const BatchView& bv, const Bin
   *fit = ok;
   if (!ok) return 0;
   return est_on ? cal_merge(h, est_compute<Fast>(s, bv, h, c, md, o)) : kInt32Max;
+}
+
+// pair_eval of the fast instances for U clusters per lane (c[u] < Cp): every
+// column load of all U clusters issues before the first use, so a wave keeps U
+// memory round trips in flight per loop step instead of one.
+template <int Fast, int U>
+KP_HD inline void pair_eval_fast(const SnapView& s, const BatchView& bv, const BindHdr& h, const int (&c)[U],
+                                 const uint32_t* tgt_bits, const uint32_t* evict_bits, const uint32_t* tol_bits,
+                                 const int32_t* md, bool (&fit)[U], int32_t (&out)[U]) {
+  static_assert(Fast != EST_GENERIC, "fast instances only");
+  const int en = h.enabled;
+  const bool api_on = (en & 1) && h.gvk >= 0;
+#ifdef KP_EXP_NOEST  // timing experiments only (tuning variants, wrong answers)
+  const bool est_on = false;
+#else
+  const bool est_on = !(h.flags & BF_NONWORKLOAD_EST);
+#endif
+  uint32_t f[U];
+  uint64_t aw[U];
+  int32_t ts[U];
+  EstOps o[U];
+KP_UNROLL
+  for (int u = 0; u < U; u++) {
+    f[u] = s.flags[c[u]];
+    aw[u] = 0;
+    if (api_on) aw[u] = s.api_bits[(size_t)(h.gvk >> 6) * s.Cp + c[u]];
+    ts[u] = 0;
+    if (en & 2) ts[u] = s.taint_set[c[u]];
+    if (est_on) o[u] = est_load<Fast>(s, bv, h, c[u], f[u]);
+  }
+  bool aff[U];
+KP_UNROLL
+  for (int u = 0; u < U; u++) aff[u] = true;
+#ifndef KP_EXP_NOAFF
+  if ((en & 4) && !(h.flags & BF_AFF_ALL) && s.C > 0) {  // uniform loop over the terms, no early exit
+KP_UNROLL
+    for (int u = 0; u < U; u++) aff[u] = false;
+    for (int j = 0; j < h.filt_cnt; j++) {
+      bool m[U];
+      prog_eval_u<U>(s, bv, bv.ipool[h.filt_off + j], c, m);
+KP_UNROLL
+      for (int u = 0; u < U; u++) aff[u] = aff[u] | m[u];
+    }
+  }
+#endif
+  // the filter plugins as one bitwise expression per lane (uniform parts fold
+  // into scalar masks): no divergent branch in the loop
+  const uint32_t need = (en & 8) ? (((h.flags & BF_NEED_PROVIDER) ? CF_HAS_PROVIDER : 0u) |
+                                    ((h.flags & BF_NEED_REGION) ? CF_HAS_REGION : 0u) |
+                                    ((h.flags & BF_NEED_ZONES) ? CF_HAS_ZONES : 0u))
+                                 : 0u;
+  const bool chk_api = (en & 1) != 0, chk_tol = (en & 2) != 0;
+  const bool chk_ev = (en & 32) && h.evict_cnt > 0, any_t = h.tgt_cnt > 0;
+KP_UNROLL
+  for (int u = 0; u < U; u++) {
+    const bool in_t = any_t & bit_test(tgt_bits, c[u]);
+    const bool api_ok = api_on & (((aw[u] >> (h.gvk & 63)) & 1ull) != 0);
+    const bool ok = (c[u] < s.C) & ((f[u] & CF_DELETING) == 0) & aff[u] & (!chk_api | in_t | api_ok) &
+                    (!chk_tol | in_t | bit_test(tol_bits, ts[u])) & ((f[u] & need) == need) &
+                    !(chk_ev & bit_test(evict_bits, c[u]));
+    fit[u] = ok;
+    const int32_t e = est_on ? cal_merge_bf(h.replicas, est_compute_bf<Fast>(s, bv, h, c[u], md, o[u])) : kInt32Max;
+    out[u] = ok ? e : 0;
+  }
 }
 
 // getClusterOverflowOrder (group_clusters.go:517-543)

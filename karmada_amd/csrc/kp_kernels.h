@@ -160,6 +160,32 @@ KP_UNROLL
   return t;
 }
 
+// The fast instances' loop over the binding's clusters: kPairUnroll clusters
+// per lane per step (c = base + u*nth + tid), fn(c, fit, value) for each c < Cp.
+// Validity of a slot is wave-uniform (Cp and wave bases are multiples of 64).
+#ifndef KP_PAIR_UNROLL
+#define KP_PAIR_UNROLL 2
+#endif
+constexpr int kPairUnroll = KP_PAIR_UNROLL;
+template <int Fast, class BLK, class Fn>
+KP_FI void pair_loop_fast(const BLK& B, const SnapView& s, const BatchView& bv, const BindHdr& h, const PairLds& L,
+                          const MdTab& mdt, Fn fn) {
+  for (int base = 0; base < s.Cp; base += kPairUnroll * B.nth()) {
+    int c[kPairUnroll];
+    bool ok[kPairUnroll];
+    int32_t v[kPairUnroll];
+KP_UNROLL
+    for (int u = 0; u < kPairUnroll; u++) {
+      const int cu = base + u * B.nth() + B.tid();
+      c[u] = cu < s.Cp ? cu : 0;  // (an out-of-range slot evaluates cluster 0 and is dropped)
+    }
+    pair_eval_fast<Fast, kPairUnroll>(s, bv, h, c, L.tgt, L.evict, L.tolb, mdt.v, ok, v);
+KP_UNROLL
+    for (int u = 0; u < kPairUnroll; u++)
+      if (base + u * B.nth() + B.tid() < s.Cp) fn(base + u * B.nth() + B.tid(), ok[u], v[u]);
+  }
+}
+
 // Fast: the estimator instance (EST_*, kp_algo.h); every instance but
 // EST_GENERIC needs pair_fast_ok (engine.cpp): est_mode 0, the MaxDivided and
 // taint-set tables in LDS, no cold fallbacks.
@@ -176,6 +202,13 @@ KP_FI void pair_one(const BLK& B, int b, unsigned char* smem, const SnapView& s,
   if (Fast != EST_GENERIC) mdt = md_regs(L.md);
   uint64_t* frow = fmask + (size_t)b * s.W;
   int32_t* erow = est + (size_t)b * s.Cp;
+  if constexpr (Fast != EST_GENERIC) {  // kPairUnroll clusters per lane per step
+    pair_loop_fast<Fast>(B, s, bv, h, L, mdt, [&](int c, bool ok, int32_t v) {
+      B.mask_store(frow, c, ok, s.W);
+      erow[c] = v;
+    });
+    return;
+  }
   for (int base = 0; base < s.Cp; base += B.nth()) {
     const int c = base + B.tid();
     if (c >= s.Cp) break;  // wave-uniform: Cp and the wave bases are multiples of 64
@@ -313,22 +346,22 @@ KP_FI void body_fused_all(const BLK& B, int blk, unsigned char* smem, const KArg
   if (weights) hp.flags |= BF_NONWORKLOAD_EST;
   KP_STAMPD(a.dbg, 0);  // pair setup
   int32_t mine = 0;
-  for (int base = 0; base < s.Cp; base += B.nth()) {
-    const int c = base + B.tid();
-    if (c >= s.Cp) break;  // wave-uniform: Cp and the wave bases are multiples of 64
-    bool ok = false;
-    int32_t v = pair_eval<Fast>(s, a.bv, hp, c, tgt, L.evict, L.tolb, mdt.v, &ok);
+  pair_loop_fast<Fast>(B, s, a.bv, hp, L, mdt, [&](int c, bool ok, int32_t v) {
     if (weights && ok) v = static_vote_u(s, a.bv, h, c);
     B.mask_store(fit, c, ok, s.W);
     row[c] = v;
     mine += ok ? 1 : 0;
-  }
+  });
   const int F = (int)B.sum64(mine);  // (its barrier also publishes fit and row)
   KP_STAMPD(a.dbg, 15);  // pair loop
   SelCtx x = make_ctx(a, b, tgt);
   x.frow = fit;
   x.erow = row;
   const SelScratch ss = carve_sel_scratch(un, s.Cp);  // the pair state is dead now
+#ifdef KP_EXP_NOSEL  // timing experiments only (tuning variants, wrong answers)
+  if (B.tid() == 0) sink_error(x, KP_STATUS_OK, 0, F);
+  return;
+#endif
   select_all_common(B, a, x, RowCands{fit, row, s.C, B.tid(), B.nth()}, F, ss);
 }
 

@@ -2358,6 +2358,104 @@ int kpo_select_clusters(const kp_cluster* clusters, const int64_t* scores, const
   return (int)r.clusters.size();
 }
 
+namespace {
+DetailInfo detail_of(const kpo_candidate& c) {
+  DetailInfo x;
+  x.name = S(c.name);
+  x.score = c.score;
+  x.overflow = c.overflow_order;
+  x.available = c.available_replicas;
+  x.allocatable = c.allocatable_replicas;
+  return x;
+}
+}  // namespace
+
+void kpo_sort_clusters(const kpo_candidate* c, uint32_t n, int with_avail, uint32_t* order) {
+  vector<uint32_t> idx(n);
+  for (uint32_t i = 0; i < n; i++) idx[i] = i;
+  vector<DetailInfo> d;
+  for (uint32_t i = 0; i < n; i++) d.push_back(detail_of(c[i]));
+  // sortClusters (spreadconstraint/util.go:43-61): overflow asc, score desc, [avail desc], name asc
+  std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+    if (with_avail) return lessDetailAvail(d[a], d[b]);
+    if (d[a].overflow != d[b].overflow) return d[a].overflow < d[b].overflow;
+    if (d[a].score != d[b].score) return d[a].score > d[b].score;
+    return d[a].name < d[b].name;
+  });
+  for (uint32_t i = 0; i < n; i++) order[i] = idx[i];
+}
+
+int kpo_group_clusters(const kp_cluster* clusters, const int64_t* scores, uint32_t n, const kp_binding* b,
+                       int32_t avail, uint32_t* order, int32_t* groups) {
+  vector<Cluster> cl;
+  for (uint32_t i = 0; i < n; i++) {
+    bool ok = true;
+    cl.push_back(convCluster(clusters[i], (int)i, &ok));
+  }
+  Binding bb = convBinding(*b);
+  vector<std::pair<const Cluster*, i64>> scored;
+  vector<i32> est(n, avail);
+  for (uint32_t i = 0; i < n; i++) scored.push_back({&cl[i], scores[i]});
+  Options o;
+  GroupInfoAll info = GroupClustersWithScore(scored, bb, &est, o, KPO_FAST);
+  for (size_t i = 0; i < info.clusters.size(); i++) order[i] = (uint32_t)info.clusters[i].cluster->idx;
+  // generateZoneInfo / generateProviderInfo (group_clusters.go:380-504): computed by the
+  // reference but never read by the selection; their group counts for the unit test
+  std::set<string> zones, providers;
+  if (!isTopologyIgnored(bb)) {
+    for (auto& ci : info.clusters) {
+      if (hasSpreadField(bb, "zone"))
+        for (auto& z : ci.cluster->zones) zones.insert(z);
+      if (hasSpreadField(bb, "provider") && !ci.cluster->provider.empty()) providers.insert(ci.cluster->provider);
+    }
+  }
+  groups[0] = (int32_t)zones.size();
+  groups[1] = (int32_t)info.regions.size();
+  groups[2] = (int32_t)providers.size();
+  return (int)info.clusters.size();
+}
+
+int kpo_select_by_region(const kp_str* region_names, const int64_t* region_scores, const uint32_t* off,
+                         uint32_t n_regions, const kpo_candidate* cands, int64_t rmin, int64_t rmax, int64_t cmin,
+                         int64_t cmax, uint32_t* out) {
+  GroupInfoAll info;
+  info.has_regions = true;
+  std::map<string, vector<uint32_t>> members;
+  for (uint32_t r = 0; r < n_regions; r++) {
+    RegionInfo ri;
+    ri.name = S(region_names[r]);
+    ri.score = region_scores[r];
+    for (uint32_t k = off[r]; k < off[r + 1]; k++) {
+      DetailInfo d = detail_of(cands[k]);
+      d.allocatable = (int32_t)k;  // (carries the candidate index through the selection)
+      ri.clusters.push_back(d);
+      ri.available += d.available;
+    }
+    info.regions[ri.name] = ri;
+  }
+  std::map<string, Spread> scm;
+  scm["region"] = Spread{"region", "", rmax, rmin};
+  scm["cluster"] = Spread{"cluster", "", cmax, cmin};
+  SelectResult res = selectByRegion(scm, info);
+  if (res.err != KP_ERR_NONE) return -res.err;
+  for (size_t i = 0; i < res.clusters.size(); i++) out[i] = (uint32_t)res.clusters[i].allocatable;
+  return (int)res.clusters.size();
+}
+
+int kpo_select_best(const kpo_candidate* cands, uint32_t n, const kp_binding* b, int32_t need_replicas,
+                    uint32_t* out) {
+  GroupInfoAll info;
+  for (uint32_t i = 0; i < n; i++) {
+    DetailInfo d = detail_of(cands[i]);
+    d.allocatable = (int32_t)i;
+    info.clusters.push_back(d);
+  }
+  SelectResult res = SelectBestClusters(convBinding(*b), info, need_replicas);
+  if (res.err != KP_ERR_NONE) return -res.err;
+  for (size_t i = 0; i < res.clusters.size(); i++) out[i] = (uint32_t)res.clusters[i].allocatable;
+  return (int)res.clusters.size();
+}
+
 void kpo_sort_target_clusters(int32_t* replicas, uint32_t* ids, uint32_t n) {
   vector<TargetCluster> v(n);
   for (uint32_t i = 0; i < n; i++) {

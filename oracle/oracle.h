@@ -115,6 +115,25 @@ int64_t kpo_calc_group_score(const kpo_candidate* cands, uint32_t n, const kp_bi
 int kpo_select_clusters(const kp_cluster* clusters, const int64_t* scores, const int32_t* avail,
                         uint32_t n, const kp_binding* b, int32_t need_replicas, uint32_t* out,
                         uint32_t out_cap);
+/* sortClusters (spreadconstraint/util.go:43-61): candidate indices in sorted order;
+ * with_avail adds the AvailableReplicas comparison of generateClustersInfo
+ * (group_clusters.go:370-375). */
+void kpo_sort_clusters(const kpo_candidate* c, uint32_t n, int with_avail, uint32_t* order);
+/* GroupClustersWithScore (group_clusters.go:103-149) with a calAvailableReplicasFunc
+ * answering `avail` for every cluster: order = cluster indices in info.Clusters
+ * order; groups = {#zones, #regions, #providers}. Returns n. */
+int kpo_group_clusters(const kp_cluster* clusters, const int64_t* scores, uint32_t n, const kp_binding* b,
+                       int32_t avail, uint32_t* order, int32_t* groups);
+/* selectBestClustersByRegion (select_clusters_by_region.go:25-64) over a given
+ * GroupClustersInfo: region r has its clusters at candidates [off[r], off[r+1]).
+ * Returns #selected (candidate indices in out) or -KP_ERR_*. */
+int kpo_select_by_region(const kp_str* region_names, const int64_t* region_scores, const uint32_t* off,
+                         uint32_t n_regions, const kpo_candidate* cands, int64_t rmin, int64_t rmax, int64_t cmin,
+                         int64_t cmax, uint32_t* out);
+/* SelectBestClusters (select_clusters.go:28-55) over a given GroupClustersInfo.Clusters
+ * list (in its order, no regions). Returns #selected or -KP_ERR_*. */
+int kpo_select_best(const kpo_candidate* cands, uint32_t n, const kp_binding* b, int32_t need_replicas,
+                    uint32_t* out);
 /* Go 1.26 sort.Sort emulation on TargetClustersList (Less = Replicas desc). */
 void kpo_sort_target_clusters(int32_t* replicas, uint32_t* ids, uint32_t n);
 uint32_t kpo_fnv32a(const char* s, uint32_t len);
