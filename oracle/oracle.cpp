@@ -2456,6 +2456,28 @@ int kpo_select_best(const kpo_candidate* cands, uint32_t n, const kp_binding* b,
   return (int)res.clusters.size();
 }
 
+int kpo_dynamic_divide(const kp_target_cluster* avail, uint32_t n, int32_t available_replicas, int32_t target,
+                       int strategy, const kp_binding* b, int32_t* err_code, kp_target_cluster* out, uint32_t out_cap) {
+  vector<TargetCluster> av;
+  for (uint32_t i = 0; i < n; i++) av.push_back({S(avail[i].name), avail[i].replicas});
+  vector<TargetCluster> scheduled;
+  AssignResult r;
+  const Strategy st = strategy == 2 ? kAggregated : (strategy == 1 ? kDynamic : kNone);
+  if (!dynamicDivide(st, convBinding(*b), av, available_replicas, target, scheduled, &r,
+                     KP_ERR_FRESH_NOT_ENOUGH)) {
+    *err_code = r.err;
+    return -r.status;
+  }
+  *err_code = KP_ERR_NONE;
+  for (size_t i = 0; i < r.targets.size() && i < out_cap; i++) {
+    out[i].replicas = r.targets[i].replicas;
+    out[i].name = kp_str{nullptr, 0};
+    for (uint32_t j = 0; j < n; j++)
+      if (S(avail[j].name) == r.targets[i].name) out[i].name = avail[j].name;
+  }
+  return (int)r.targets.size();
+}
+
 void kpo_sort_target_clusters(int32_t* replicas, uint32_t* ids, uint32_t n) {
   vector<TargetCluster> v(n);
   for (uint32_t i = 0; i < n; i++) {

@@ -134,6 +134,11 @@ int kpo_select_by_region(const kp_str* region_names, const int64_t* region_score
  * list (in its order, no regions). Returns #selected or -KP_ERR_*. */
 int kpo_select_best(const kpo_candidate* cands, uint32_t n, const kp_binding* b, int32_t need_replicas,
                     uint32_t* out);
+/* dynamicDivideReplicas (division_algorithm.go:75-101) over an explicit availableClusters
+ * list (no scheduled clusters); strategy 1 = DynamicWeight, 2 = Aggregated, other =
+ * undefined. Returns #targets or -status (err_code = KP_ERR_*). */
+int kpo_dynamic_divide(const kp_target_cluster* avail, uint32_t n, int32_t available_replicas, int32_t target,
+                       int strategy, const kp_binding* b, int32_t* err_code, kp_target_cluster* out, uint32_t out_cap);
 /* Go 1.26 sort.Sort emulation on TargetClustersList (Less = Replicas desc). */
 void kpo_sort_target_clusters(int32_t* replicas, uint32_t* ids, uint32_t n);
 uint32_t kpo_fnv32a(const char* s, uint32_t len);

@@ -226,8 +226,68 @@ def spread():
     return res
 
 
+def new_cluster(name):  # helper.NewCluster (test/helper/resource.go:680-687)
+    return {"name": name}
+
+
+def detail2(cv, c):
+    """ClusterDetailInfo with every field the assignment reads."""
+    cl = c.get("Cluster")
+    return {"name": cv.ev(c.get("Name", "")), "score": cv.ev(c.get("Score", 0)),
+            "avail": cv.ev(c.get("AvailableReplicas", 0)), "alloc": cv.ev(c.get("AllocatableReplicas", 0)),
+            "ovf": cv.ev(c.get("OverflowOrder", 0)), "cluster": cv.cluster(cl) if cl is not None else None}
+
+
+def core():
+    CORE = "pkg/scheduler/core/"
+    cv = Conv({"helper.NewCluster": new_cluster})
+    res = {"source": []}
+    # Test_DistributionOfReplicas: genericScheduler.assignReplicas over ClusterDetailInfo lists
+    rows, line = table(read(CORE + "generic_scheduler_test.go"), "Test_DistributionOfReplicas")
+    res["distribution"] = [{"name": r.get("name"), "clusters": [detail2(cv, c) for c in r.get("clusters").values()],
+                            "binding": cv.spec(r.get("object")), "want": cv.targets(r.get("result"))} for r in rows]
+    res["source"].append(CORE + "generic_scheduler_test.go:%d (Test_DistributionOfReplicas)" % line)
+    # TestAssignReplicas
+    rows, line = table(read(CORE + "common_test.go"), "TestAssignReplicas")
+    res["assign"] = [{"name": r.get("name"), "clusters": [detail2(cv, c) for c in r.get("clusters").values()],
+                      "binding": cv.spec(r.get("spec"), r.get("status")),
+                      "want": cv.targets(r.get("expectedResult")) if r.get("expectedResult") is not None else None,
+                      "wantErr": bool(r.get("expectedError"))} for r in rows]
+    res["source"].append(CORE + "common_test.go:%d (TestAssignReplicas)" % line)
+    # TestSelectClusters: SelectClusters over scored clusters; no cluster has a ResourceSummary
+    # and no spec has replicas, so calAvailableReplicas answers 0 for every cluster
+    rows, line = table(read(CORE + "common_test.go"), "TestSelectClusters")
+    cases = []
+    for r in rows:
+        b = cv.spec(r.get("spec"), r.get("status"))
+        b["placement"] = cv.placement(r.get("placement"))
+        cases.append({"name": r.get("name"), "binding": b,
+                      "clusters": [cv.cluster(x.get("Cluster")) for x in r.get("clustersScore").values()],
+                      "scores": [cv.ev(x.get("Score", 0)) for x in r.get("clustersScore").values()],
+                      "want": sorted(cv.cluster(x)["name"] for x in (r.get("expectedResult").values()
+                                                                     if r.get("expectedResult") else [])),
+                      "wantErr": bool(r.get("expectedError"))})
+    res["select"] = cases
+    res["source"].append(CORE + "common_test.go:%d (TestSelectClusters)" % line)
+    # Test_dynamicDivideReplicas
+    cv2 = Conv({"DynamicWeightStrategy": 1, "AggregatedStrategy": 2, "StaticWeightStrategy": 3,
+                "DuplicatedStrategy": 4})
+    rows, line = table(read(CORE + "division_algorithm_test.go"), "Test_dynamicDivideReplicas")
+    cases = []
+    for r in rows:
+        st = r.get("state")
+        cases.append({"name": r.get("name"), "available": cv2.targets(st.get("availableClusters")),
+                      "target": cv2.ev(st.get("targetReplicas", 0)),
+                      "availableReplicas": cv2.ev(st.get("availableReplicas", 0)),
+                      "strategy": cv2.ev(st.get("strategyType")), "binding": cv2.spec(st.get("spec")),
+                      "want": cv2.targets(r.get("want")), "wantErr": bool(r.get("wantErr"))})
+    res["dynamic_divide"] = cases
+    res["source"].append(CORE + "division_algorithm_test.go:%d (Test_dynamicDivideReplicas)" % line)
+    return res
+
+
 def main():
-    outs = {"plugins.json": plugins(), "spread.json": spread()}
+    outs = {"plugins.json": plugins(), "spread.json": spread(), "core.json": core()}
     for name, data in outs.items():
         with open(os.path.join(OUT, name), "w") as f:
             json.dump(data, f, indent=1)
