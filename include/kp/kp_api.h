@@ -23,6 +23,7 @@
  *        kp_filter_batch            <- framework.FilterPlugin.Filter for the in-tree filter set
  *                                      (pkg/scheduler/framework/interface.go:85-98,
  *                                       pkg/scheduler/framework/runtime/framework.go:93-122)
+ *        kp_filter_reasons          <- framework.FitError's Diagnosis (framework/types.go:56-90)
  *        kp_score_batch             <- framework.ScorePlugin.Score summed by RunScorePlugins
  *                                      (pkg/scheduler/framework/interface.go:215-232,
  *                                       pkg/scheduler/framework/runtime/framework.go:126-170)
@@ -398,6 +399,28 @@ int kp_schedule_affinities(kp_engine* e, const kp_snapshot* s, const kp_binding*
  * out_mask: n_bindings * ceil(n_clusters/64) words, bit c%64 of word c/64 set
  * when cluster c (caller order) fits. */
 int kp_filter_batch(kp_engine* e, kp_batch* b, uint64_t* out_mask);
+
+/* FitError diagnosis (framework/types.go:56-90; findClustersThatFit,
+ * generic_scheduler.go:119-163): per pair the Result of RunFilterPlugins
+ * (runtime/framework.go:93-105, plugins in canonical order), n_bindings*n_clusters
+ * words in caller cluster order: bits [7:0] = KP_REASON_*, bits [31:8] = argument.
+ * KP_REASON_FIT pairs fit; KP_REASON_DELETING clusters are skipped before the
+ * plugins run and are absent from Diagnosis.ClusterToResultMap. The argument of
+ * KP_REASON_TAINT is the index of the untolerated taint among the cluster's
+ * NoSchedule/NoExecute taints in spec.taints order (FindMatchingUntoleratedTaint);
+ * 0 otherwise. */
+enum {
+  KP_REASON_FIT = 0,
+  KP_REASON_API = 1,             /* api_enablement.go:77 "cluster(s) did not have the API resource" */
+  KP_REASON_TAINT = 2,           /* taint_toleration.go:83 "cluster(s) had untolerated taint {%s}" */
+  KP_REASON_AFFINITY = 3,        /* cluster_affinity.go:89 "...did not match the placement cluster affinity constraint" */
+  KP_REASON_SPREAD_PROVIDER = 4, /* spread_constraint.go:57 "cluster(s) did not have provider property" */
+  KP_REASON_SPREAD_REGION = 5,   /* spread_constraint.go:59 "cluster(s) did not have region property" */
+  KP_REASON_SPREAD_ZONES = 6,    /* spread_constraint.go:61 "cluster(s) did not have zones property" */
+  KP_REASON_EVICTION = 7,        /* cluster_eviction.go:53 "cluster(s) is in the process of eviction" */
+  KP_REASON_DELETING = 255       /* generic_scheduler.go:138-142 (skipped) */
+};
+int kp_filter_reasons(kp_engine* e, kp_batch* b, uint32_t* out_reasons);
 
 /* ScorePlugin boundary: summed score (RunScorePlugins) per pair; n_bindings*n_clusters. */
 int kp_score_batch(kp_engine* e, kp_batch* b, int64_t* out_scores);

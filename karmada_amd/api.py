@@ -159,6 +159,49 @@ PLUGIN_CLUSTER_EVICTION = 1 << 5
 PLUGIN_ALL = 0x3F
 
 STATUS_OK, STATUS_FIT_ERROR, STATUS_UNSCHEDULABLE, STATUS_ERROR = 0, 1, 2, 3
+
+# kp_filter_reasons codes (kp_api.h KP_REASON_*) and the Result reasons the plugins return
+REASON_FIT, REASON_API, REASON_TAINT, REASON_AFFINITY = 0, 1, 2, 3
+REASON_SPREAD_PROVIDER, REASON_SPREAD_REGION, REASON_SPREAD_ZONES, REASON_EVICTION = 4, 5, 6, 7
+REASON_DELETING = 255
+REASON_TEXT = {
+    REASON_API: "cluster(s) did not have the API resource",                              # api_enablement.go:77
+    REASON_TAINT: "cluster(s) had untolerated taint {%s}",                               # taint_toleration.go:83
+    REASON_AFFINITY: "cluster(s) did not match the placement cluster affinity constraint",  # cluster_affinity.go:89
+    REASON_SPREAD_PROVIDER: "cluster(s) did not have provider property",                 # spread_constraint.go:57
+    REASON_SPREAD_REGION: "cluster(s) did not have region property",                     # spread_constraint.go:59
+    REASON_SPREAD_ZONES: "cluster(s) did not have zones property",                       # spread_constraint.go:61
+    REASON_EVICTION: "cluster(s) is in the process of eviction",                         # cluster_eviction.go:53
+}
+
+
+def taint_string(t: dict) -> str:
+    """corev1.Taint.ToString()."""
+    if not t.get("value"):
+        return "%s:%s" % (t.get("key", ""), t.get("effect", ""))
+    return "%s=%s:%s" % (t.get("key", ""), t.get("value", ""), t.get("effect", ""))
+
+
+def reason_text(code: int, cluster: dict) -> str:
+    """The Result reason of one kp_filter_reasons word for `cluster` (its dict form)."""
+    kind, arg = code & 0xFF, code >> 8
+    if kind == REASON_TAINT:
+        taints = [t for t in cluster.get("taints", []) if t.get("effect") in ("NoSchedule", "NoExecute")]
+        return REASON_TEXT[kind] % taint_string(taints[arg])
+    return REASON_TEXT[kind]
+
+
+def fit_error_message(num_all_clusters: int, reasons: dict) -> str:
+    """FitError.Error() (framework/types.go:67-91): reasons = {cluster name: reason text or
+    list of texts} for the clusters of Diagnosis.ClusterToResultMap."""
+    if num_all_clusters == 0 or not reasons:
+        return "0/%d clusters are available: %s." % (num_all_clusters, "no cluster exists")
+    hist = {}
+    for rs in reasons.values():
+        for r in ([rs] if isinstance(rs, str) else rs):
+            hist[r] = hist.get(r, 0) + 1
+    return "0/%d clusters are available: %s." % (num_all_clusters,
+                                                   ", ".join(sorted("%d %s" % (v, k) for k, v in hist.items())))
 ERR_NAMES = {
     0: "none", 1: "fit", 2: "region_min_groups", 3: "region_cluster_min", 4: "cluster_min_groups",
     5: "cluster_resource", 6: "spread_unsupported", 7: "no_clusters", 8: "unsupported_strategy",

@@ -174,6 +174,12 @@ int region_groups(stream_t, const RegionOut* rout, const int32_t* rstat, const B
   return 0;
 }
 
+int reasons(stream_t, const SnapView& s, const BatchView& bv, uint32_t* out) {
+  const uint64_t n = (uint64_t)bv.B * (uint64_t)s.C;
+  for (uint64_t i = 0; i < n; i++) body_reasons(s, bv, i, out);
+  return 0;
+}
+
 int compact(stream_t, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
             const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n) {
   int64_t red[8];

@@ -961,9 +961,14 @@ struct Packer {
     std::string rst = b.has_replica_scheduling ? S(b.replica_scheduling_type) : std::string("Duplicated");
     std::string div = S(b.replica_division_preference);
     bool hasRegion = false, hasCluster = false;
+    int n_order = 0;
     for (uint32_t i = 0; i < b.n_spread_constraints; i++) {
       const kp_spread_constraint& sc = b.spread_constraints[i];
       std::string fld = S(sc.spread_by_field);
+      const int code = fld == "provider" ? 1 : fld == "region" ? 2 : fld == "zone" ? 3 : 0;
+      bool seen = false;
+      for (int k = 0; k < n_order; k++) seen = seen || ((h.spread_order >> (2 * k)) & 3) == code;
+      if (code && !seen) h.spread_order |= code << (2 * n_order++);
       if (fld == "provider") f |= BF_NEED_PROVIDER;
       if (fld == "region") {
         f |= BF_NEED_REGION;
@@ -1766,10 +1771,13 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   HIPCHK(dev::stream_wait(sp, e->ev[0]));  // the fills above precede every kernel
   const int fast = getenv("KP_PAIR_GENERIC") || !bt->fast_ok ? EST_GENERIC : s->est_kind;
   const int md_cap = md_cap_of(s);
-  // SEL_ALL bindings take the fused pair + select kernel when the batch runs a fast
-  // estimator instance and its LDS fits: their rows never leave LDS. The pair
-  // kernel then covers only the cluster/region-spread bindings, on stream2 beside it.
-  const bool fused = fast != EST_GENERIC && !bt->l_all.empty() && !getenv("KP_NO_FUSE") &&
+  // KP_FUSE=1: SEL_ALL bindings take the fused pair + select kernel (fast estimator
+  // instance, LDS fits): their rows never leave LDS, and the pair kernel covers only
+  // the cluster/region-spread bindings, on stream2 beside it. Opt-in: on MI355X the
+  // fused kernel's LDS footprint (4 workgroups/CU) costs more than the row round trip
+  // saves (config 3: 10.2 vs 8.2 ms/step).
+  const char* fz = getenv("KP_FUSE");
+  const bool fused = fast != EST_GENERIC && !bt->l_all.empty() && fz && fz[0] == '1' &&
                      fused_lds_bytes(s->Cp, md_cap) <= e->max_lds;
   SelectExtra sx;
   sx.rout = bt->rout;
@@ -2002,6 +2010,26 @@ int kp_filter_batch(kp_engine* e, kp_batch* bt, uint64_t* out_mask) {
         uint32_t c = s->perm[r];
         out_mask[(size_t)b * Wc + (c >> 6)] |= 1ull << (c & 63);
       }
+  return KP_OK;
+}
+
+int kp_filter_reasons(kp_engine* e, kp_batch* bt, uint32_t* out_reasons) {
+  if (!e || !bt || !out_reasons) return KP_EINVAL;
+  (void)dev::set_device(e->device);
+  kp_snapshot* s = bt->snap;
+  if (bt->B == 0 || s->C == 0) return KP_OK;
+  uint32_t* d = nullptr;
+  const size_t n = (size_t)bt->B * s->C;
+  HIPCHK(dev::alloc((void**)&d, 4 * n));
+  std::vector<uint32_t> h(n);
+  int rc = (dev::reasons(e->stream, s->view, bt->view, d) || dev::d2h(h.data(), d, 4 * n, e->stream) ||
+            dev::sync(e->stream))
+               ? KP_EDEVICE
+               : KP_OK;
+  dev::release(d);
+  if (rc) return rc;
+  for (int b = 0; b < bt->B; b++)
+    for (int r = 0; r < s->C; r++) out_reasons[(size_t)b * s->C + s->perm[r]] = h[(size_t)b * s->C + r];
   return KP_OK;
 }
 

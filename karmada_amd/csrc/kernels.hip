@@ -11,6 +11,7 @@
 // k_compact       per-binding results gathered into CSR order.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "kp_dev.h"
@@ -112,6 +113,10 @@ extern "C" __global__ void __launch_bounds__(kSlowBlock) k_slow(KArgs a, unsigne
                                                                 int cap, int lds_area, int lds_sort) {
   KP_SMEM;
   body_slow(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, (int)gridDim.x, smem, a, scratch, slot_bytes, cap, lds_area, lds_sort);
+}
+extern "C" __global__ void __launch_bounds__(256) k_reasons(SnapView s, BatchView bv, uint64_t n, uint32_t* out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    body_reasons(s, bv, i, out);
 }
 extern "C" __global__ void __launch_bounds__(64) k_compact(const uint64_t* start, const uint32_t* count,
                                                            const uint64_t* offsets, const uint32_t* in_idx,
@@ -276,6 +281,14 @@ int region_groups(stream_t st, const RegionOut* rout, const int32_t* rstat, cons
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_region_groups, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)st, rout, rstat, hdr, list, n,
                      R, rsel, rnsel, nhost);
+  return chk(hipGetLastError());
+}
+
+int reasons(stream_t st, const SnapView& s, const BatchView& bv, uint32_t* out) {
+  const uint64_t n = (uint64_t)bv.B * (uint64_t)s.C;
+  if (n == 0) return 0;
+  const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_reasons, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)st, s, bv, n, out);
   return chk(hipGetLastError());
 }
 

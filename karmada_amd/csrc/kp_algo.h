@@ -25,6 +25,12 @@ KP_HD inline bool list_has(const int32_t* p, int n, int32_t x) {
     if (p[i] == x) return true;
   return false;
 }
+// col[c] with a 32-bit byte offset (c < 2^28): with a uniform column base the
+// load takes the scalar-base + vector-offset form, no 64-bit address math per lane.
+template <class T>
+KP_HD inline T ldcol(const T* col, int c) {
+  return *(const T*)((const char*)col + (uint32_t)c * (uint32_t)sizeof(T));
+}
 KP_HD inline bool bit_test(const uint32_t* bits, int c) { return (bits[c >> 5] >> (c & 31)) & 1u; }
 KP_HD inline bool mask_test(const uint64_t* row, int c) { return (row[c >> 6] >> (c & 63)) & 1ull; }
 KP_HD inline int32_t wrap32(int64_t x) { return (int32_t)(uint32_t)(uint64_t)x; }
@@ -185,12 +191,12 @@ KP_HD inline bool prog_match(const SnapView& s, const BatchView& bv, int32_t pro
 template <int U>
 KP_HD inline void prog_eval_u(const SnapView& s, const BatchView& bv, int32_t prog_id, const int (&c)[U],
                               bool (&res)[U]) {
-  const Prog p = bv.progs[prog_id];
+  const Prog p = kp_ldu(bv.progs + prog_id);
   bool ok[U];
 KP_UNROLL
   for (int u = 0; u < U; u++) ok[u] = true;
   for (int i = 0; i < p.ins_cnt; i++) {
-    const Instr in = bv.instrs[p.ins_off + i];
+    const Instr in = kp_ldu(bv.instrs + p.ins_off + i);
     const int32_t* lst = bv.ipool + (in.op == OP_EXCLUDE || in.op == OP_NAMES ? in.a : in.b);
     const int nl = in.op == OP_EXCLUDE || in.op == OP_NAMES ? in.b : in.c;
     switch (in.op) {
@@ -206,7 +212,7 @@ KP_UNROLL
 KP_UNROLL
         for (int u = 0; u < U; u++) hit[u] = false;
         for (int k = 0; k < nl; k++) {
-          const int32_t x = lst[k];
+          const int32_t x = kp_ldu(lst + k);
 KP_UNROLL
           for (int u = 0; u < U; u++) hit[u] = hit[u] | (x == c[u]);
         }
@@ -224,11 +230,11 @@ KP_UNROLL
         bool hit[U];
 KP_UNROLL
         for (int u = 0; u < U; u++) {
-          v[u] = col[c[u]];
+          v[u] = ldcol(col, c[u]);
           hit[u] = false;
         }
         for (int k = 0; k < nl; k++) {
-          const int32_t x = lst[k];
+          const int32_t x = kp_ldu(lst + k);
 KP_UNROLL
           for (int u = 0; u < U; u++) hit[u] = hit[u] | (x == v[u]);
         }
@@ -246,7 +252,7 @@ KP_UNROLL
         const bool ex = in.op == OP_LBL_EXISTS || in.op == OP_FLD_EXISTS;
 KP_UNROLL
         for (int u = 0; u < U; u++) {
-          const int32_t v = col[c[u]];
+          const int32_t v = ldcol(col, c[u]);
           ok[u] = ok[u] & (ex ? v >= 0 : v < 0);
         }
         break;
@@ -274,7 +280,7 @@ KP_UNROLL
           } else {
             bool hit = false;
             for (int z = z0; z < z1; z++)
-              for (int k = 0; k < nl; k++) hit = hit | (lst[k] == s.zone_ids[z]);
+              for (int k = 0; k < nl; k++) hit = hit | (kp_ldu(lst + k) == s.zone_ids[z]);
             ok[u] = ok[u] & (in.op == OP_ZONE_IN ? ((z1 > z0) & hit) : !hit);
           }
         }
@@ -313,6 +319,51 @@ KP_HD inline bool taints_tolerated(const SnapView& s, const BatchView& bv, const
     if (!tol) return false;
   }
   return true;
+}
+
+// FitError diagnosis of one pair (kp_filter_reasons): findClustersThatFit's skip of
+// deleting clusters, then the Result of the first failing plugin of RunFilterPlugins
+// (runtime/framework.go:93-105) as KP_REASON_* | arg << 8. Reads spec.Clusters and
+// the eviction list from the pools (no LDS bitsets): a diagnosis path, not the hot one.
+KP_HD inline uint32_t pair_reason(const SnapView& s, const BatchView& bv, const BindHdr& h, int c) {
+  const uint32_t f = s.flags[c];
+  if (f & CF_DELETING) return 255u;  // KP_REASON_DELETING
+  const int en = h.enabled;
+  bool in_t = false;  // TargetContains (binding_types_helper.go:102-110)
+  for (int j = 0; j < h.tgt_cnt && !in_t; j++) in_t = bv.ipool[h.tgt_off + 2 * j] == c;
+  if ((en & 1) && !in_t) {  // APIEnablement (api_enablement.go:51-78)
+    if (h.gvk < 0 || !((s.api_bits[(size_t)(h.gvk >> 6) * s.Cp + c] >> (h.gvk & 63)) & 1ull)) return 1u;
+  }
+  if ((en & 2) && !in_t) {  // TaintToleration: FindMatchingUntoleratedTaint (taint_toleration.go:65-83)
+    const int t0 = s.taint_off[c], t1 = s.taint_off[c + 1];
+    for (int t = t0; t < t1; t++) {
+      const int32_t k = s.taint_key[t], v = s.taint_val[t], e = s.taint_eff[t];
+      bool tol = false;
+      for (int j = 0; j < h.tol_cnt && !tol; j++) {
+        const Tol tl = bv.tols[h.tol_off + j];
+        tol = (tl.eff == EFF_ANY || tl.eff == e) && (tl.key < 0 || tl.key == k) && (tl.op == TOL_EXISTS || tl.val == v);
+      }
+      if (!tol) return 2u | (uint32_t)(t - t0) << 8;
+    }
+  }
+  if ((en & 4) && !(h.flags & BF_AFF_ALL)) {  // ClusterAffinity (cluster_affinity.go:51-94)
+    bool m = false;
+    for (int j = 0; j < h.filt_cnt && !m; j++) m = prog_match(s, bv, bv.ipool[h.filt_off + j], c);
+    if (!m) return 3u;
+  }
+  if (en & 8) {  // SpreadConstraint (spread_constraint.go:49-66): constraints in spec order
+    for (int k = 0; k < 3; k++) {
+      const int fld = (h.spread_order >> (2 * k)) & 3;
+      if (fld == 1 && !(f & CF_HAS_PROVIDER)) return 4u;
+      if (fld == 2 && !(f & CF_HAS_REGION)) return 5u;
+      if (fld == 3 && !(f & CF_HAS_ZONES)) return 6u;
+    }
+  }
+  if (en & 32) {  // ClusterEviction (cluster_eviction.go:50-57)
+    for (int j = 0; j < h.evict_cnt; j++)
+      if (bv.ipool[h.evict_off + j] == c) return 7u;
+  }
+  return 0u;
 }
 
 // findClustersThatFit skip-deleting + RunFilterPlugins over the enabled plugins.
@@ -405,7 +456,7 @@ template <int Fast = EST_GENERIC>
 KP_HD inline EstOps est_load(const SnapView& s, const BatchView& bv, const BindHdr& h, int c, uint32_t f) {
   EstOps o;
   o.f = f;
-  o.allowed = s.allowed[c];
+  o.allowed = ldcol(s.allowed, c);
   const bool rr = (h.flags & BF_HAS_RR) != 0;
   const bool model = rr;
   const int jh = rr && Fast < EST_MODEL8 ? (h.sreq_cnt < kReqUnroll ? h.sreq_cnt : kReqUnroll) : 0;
@@ -413,7 +464,7 @@ KP_HD inline EstOps est_load(const SnapView& s, const BatchView& bv, const BindH
 KP_UNROLL
     for (int t = 0; t < kTmplDense; t++) {
       o.mt[t] = 0;
-      if (t < Fast && model) o.mt[t] = s.mt_cnt[(size_t)t * s.Cp + c];
+      if (t < Fast && model) o.mt[t] = ldcol(s.mt_cnt + (size_t)t * s.Cp, c);
     }
   } else if (Fast == EST_SUMMARY) {
   } else if (Fast == EST_MIXED) {
@@ -421,7 +472,7 @@ KP_UNROLL
 KP_UNROLL
     for (int t = 0; t < kTmplDense; t++) {
       o.mt[t] = 0;
-      if (t < th) o.mt[t] = s.mt_cnt[(size_t)t * s.Cp + c];
+      if (t < th) o.mt[t] = ldcol(s.mt_cnt + (size_t)t * s.Cp, c);
     }
   } else {
     const int kh = model ? (s.kmax < kEstUnroll ? s.kmax : kEstUnroll) : 0;
@@ -439,8 +490,8 @@ KP_UNROLL
   for (int j = 0; j < kReqUnroll; j++) {
     o.av[j] = 0;
     if (j < jh) {
-      const int32_t rid = bv.ipool[h.sreq_off + j];
-      if (rid >= 0) o.av[j] = s.avail[(size_t)rid * s.Cp + c];
+      const int32_t rid = Fast != EST_GENERIC ? kp_ldu(bv.ipool + h.sreq_off + j) : bv.ipool[h.sreq_off + j];
+      if (rid >= 0) o.av[j] = ldcol(s.avail + (size_t)rid * s.Cp, c);
     }
   }
   return o;
@@ -575,9 +626,9 @@ KP_UNROLL
 KP_UNROLL
     for (int j = 0; j < kReqUnroll; j++) {
       if (j < h.sreq_cnt) {  // uniform
-        const bool z = bv.ipool[h.sreq_off + j] < 0 || o.av[j] <= 0;
+        const bool z = kp_ldu(bv.ipool + h.sreq_off + j) < 0 || o.av[j] <= 0;
         const int64_t lim = num < m ? num : m;
-        const int64_t d = floor_div_bf(z ? 1 : o.av[j], bv.lpool[h.sreq_q_off + j], lim);
+        const int64_t d = floor_div_bf(z ? 1 : o.av[j], kp_ldu(bv.lpool + h.sreq_q_off + j), lim);
         zero = zero | z;
         num = d < num ? d : num;
       }
@@ -647,7 +698,7 @@ KP_HD inline int32_t pair_eval(const SnapView& s, const BatchView& bv, const Bin
     // uniform loop over the affinity terms (scalar program loads), no early exit
     if ((en & 4) && !(h.flags & BF_AFF_ALL) && s.C > 0) {
       aff = false;
-      for (int j = 0; j < h.filt_cnt; j++) aff = aff | prog_eval_u(s, bv, bv.ipool[h.filt_off + j], c);
+      for (int j = 0; j < h.filt_cnt; j++) aff = aff | prog_eval_u(s, bv, kp_ldu(bv.ipool + h.filt_off + j), c);
     }
   } else if ((en & 4) && !(h.flags & BF_AFF_ALL) && c < s.C) {  // (zone lists are [C+1])
     aff = false;
@@ -691,11 +742,11 @@ KP_HD inline void pair_eval_fast(const SnapView& s, const BatchView& bv, const B
   EstOps o[U];
 KP_UNROLL
   for (int u = 0; u < U; u++) {
-    f[u] = s.flags[c[u]];
+    f[u] = ldcol(s.flags, c[u]);
     aw[u] = 0;
-    if (api_on) aw[u] = s.api_bits[(size_t)(h.gvk >> 6) * s.Cp + c[u]];
+    if (api_on) aw[u] = ldcol(s.api_bits + (size_t)(h.gvk >> 6) * s.Cp, c[u]);
     ts[u] = 0;
-    if (en & 2) ts[u] = s.taint_set[c[u]];
+    if (en & 2) ts[u] = ldcol(s.taint_set, c[u]);
     if (est_on) o[u] = est_load<Fast>(s, bv, h, c[u], f[u]);
   }
   bool aff[U];
@@ -707,7 +758,7 @@ KP_UNROLL
     for (int u = 0; u < U; u++) aff[u] = false;
     for (int j = 0; j < h.filt_cnt; j++) {
       bool m[U];
-      prog_eval_u<U>(s, bv, bv.ipool[h.filt_off + j], c, m);
+      prog_eval_u<U>(s, bv, kp_ldu(bv.ipool + h.filt_off + j), c, m);
 KP_UNROLL
       for (int u = 0; u < U; u++) aff[u] = aff[u] | m[u];
     }

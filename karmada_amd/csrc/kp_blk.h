@@ -354,6 +354,19 @@ KP_HD inline int32_t kp_uniform(int32_t v) {
 #endif
 }
 
+// A load at a block-uniform address of read-only global memory (batch pools in
+// HBM, written before the launch): through the constant address space, so the
+// compiler issues a scalar load instead of a vector load plus readfirstlane.
+// Never for LDS-staged pools or data the running kernel writes.
+template <class T>
+KP_HD inline T kp_ldu(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(const __attribute__((address_space(4))) T*)(p);
+#else
+  return *p;
+#endif
+}
+
 // Atomics on LDS/global memory, usable from both builds.
 template <class T>
 KP_HD inline T kp_atomic_add(T* p, T v) {

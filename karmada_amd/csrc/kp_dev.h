@@ -57,6 +57,8 @@ int pair_list(stream_t st, const SnapView& s, const BatchView& bv, const int32_t
 // step writes them; *nhost counts the bindings left to the host (kGroupsHost).
 int region_groups(stream_t st, const RegionOut* rout, const int32_t* rstat, const BindHdr* hdr, const int32_t* list,
                   int n, int R, int32_t* rsel, int32_t* rnsel, uint32_t* nhost);
+// kp_filter_reasons: out[b * C + r] = pair_reason of binding b, cluster rank r.
+int reasons(stream_t st, const SnapView& s, const BatchView& bv, uint32_t* out);
 int compact(stream_t st, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
             const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n);
 

@@ -713,6 +713,14 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
   }
 }
 
+// kp_filter_reasons: one thread per (binding, cluster) pair, grid-strided;
+// out[b * C + r] for cluster rank r < C.
+KP_HD inline void body_reasons(const SnapView& s, const BatchView& bv, uint64_t i, uint32_t* out) {
+  const uint64_t C = (uint64_t)s.C;
+  const int b = (int)(i / C), r = (int)(i % C);
+  out[i] = pair_reason(s, bv, bv.hdr[b], r);
+}
+
 // Gathers per-binding results into CSR order (offsets computed on the host).
 template <class BLK>
 KP_FI void body_compact(const BLK& B, int blk, const uint64_t* start, const uint32_t* count, const uint64_t* offsets,

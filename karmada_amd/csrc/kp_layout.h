@@ -121,7 +121,7 @@ struct alignas(16) BindHdr {
   int32_t enabled;               // KP_PLUGIN_* mask
   int64_t cluster_min, cluster_max, region_min, region_max;
   int32_t need_replicas;         // SelectBestClusters needReplicas (-1 = ignore resources)
-  int32_t pad0;
+  int32_t spread_order;          // SpreadConstraint fields in first-appearance order, 2 bits each (1 provider, 2 region, 3 zone)
   uint64_t out_cap;
   // this binding's slices of the pools (staged into LDS by the pair kernel)
   int32_t ip_beg, ip_end, pr_beg, pr_end, in_beg, in_end;

@@ -34,7 +34,7 @@ EXPORTS = (
     "kp_abi_version", "kp_engine_create", "kp_engine_destroy", "kp_last_error", "kp_snapshot_create",
     "kp_snapshot_destroy", "kp_snapshot_export", "kp_snapshot_import", "kp_snapshot_update", "kp_batch_create",
     "kp_batch_destroy",
-    "kp_schedule_batch", "kp_schedule_affinities", "kp_filter_batch", "kp_score_batch", "kp_max_available_replicas", "kp_last_stage_times",
+    "kp_schedule_batch", "kp_schedule_affinities", "kp_filter_batch", "kp_filter_reasons", "kp_score_batch", "kp_max_available_replicas", "kp_last_stage_times",
 )
 
 KP_OK, KP_EINVAL, KP_ENOMEM, KP_EDEVICE, KP_ENOTSUP, KP_ESTATE = 0, -1, -2, -3, -4, -5
@@ -68,6 +68,7 @@ def load_library(path: str = LIB_PATH):
                                          C.POINTER(api.kp_affinity_results)]
     L.kp_filter_batch.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
     L.kp_score_batch.argtypes = [vp, vp, C.POINTER(C.c_int64)]
+    L.kp_filter_reasons.argtypes = [vp, vp, C.POINTER(C.c_uint32)]
     L.kp_max_available_replicas.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint32), C.c_uint64,
                                             C.POINTER(C.c_int32)]
     L.kp_last_stage_times.argtypes = [vp, C.POINTER(api.kp_stage_times)]
@@ -299,6 +300,25 @@ class GenericScheduler:
             out.append([self.snapshot.names[c] for c in range(C_) if (m[i * W + (c >> 6)] >> (c & 63)) & 1])
         b.close()
         return out
+
+    def filter_reasons(self, bindings: Sequence[dict]) -> List[List[int]]:
+        """kp_filter_reasons: the KP_REASON_* word of every (binding, cluster) pair."""
+        b = Batch(self.snapshot, bindings)
+        eng = self.snapshot.engine
+        C_ = len(self.snapshot.names)
+        r = (C.c_uint32 * max(1, b.n * C_))()
+        eng._check(eng.L.kp_filter_reasons(eng.h, b.h, r), "kp_filter_reasons")
+        out = [[int(r[i * C_ + c]) for c in range(C_)] for i in range(b.n)]
+        b.close()
+        return out
+
+    def fit_error(self, binding: dict, clusters: Sequence[dict]) -> str:
+        """FitError{NumAllClusters, Diagnosis}.Error() for one binding (generic_scheduler.go:84-89);
+        `clusters` are the snapshot's cluster dicts in its caller order."""
+        codes = self.filter_reasons([binding])[0]
+        reasons = {cl["name"]: api.reason_text(code, cl) for cl, code in zip(clusters, codes)
+                   if code not in (api.REASON_FIT, api.REASON_DELETING)}
+        return api.fit_error_message(len(clusters), reasons)
 
     def score(self, bindings: Sequence[dict]) -> List[List[int]]:
         """Summed plugin scores per (binding, cluster) (prioritizeClusters)."""

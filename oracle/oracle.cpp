@@ -842,6 +842,37 @@ uint32_t RunFilterPlugins(const Binding& b, const Cluster& c, const Options& o) 
   return 0;
 }
 
+// The Result of RunFilterPlugins as a kp_filter_reasons word (KP_REASON_* | arg << 8):
+// findClustersThatFit's skip of deleting clusters (generic_scheduler.go:138-142), then
+// the first failing plugin's reason (api_enablement.go:77, taint_toleration.go:83 with
+// the FindMatchingUntoleratedTaint taint among the NoSchedule/NoExecute ones,
+// cluster_affinity.go:89, spread_constraint.go:55-62 per constraint in spec order,
+// cluster_eviction.go:53).
+uint32_t RunFilterPluginsReason(const Binding& b, const Cluster& c, const Options& o) {
+  if (c.deleting) return 255;
+  if ((o.plugins & KP_PLUGIN_API_ENABLEMENT) && !FilterAPIEnablement(b, c)) return 1;
+  if ((o.plugins & KP_PLUGIN_TAINT_TOLERATION) && !TargetContains(b, c.name)) {
+    uint32_t k = 0;
+    for (auto& taint : c.taints) {
+      if (!(taint.effect == "NoSchedule" || taint.effect == "NoExecute")) continue;
+      bool tol = false;
+      for (auto& t : b.tolerations) tol = tol || ToleratesTaint(t, taint);
+      if (!tol) return 2u | k << 8;
+      k++;
+    }
+  }
+  if ((o.plugins & KP_PLUGIN_CLUSTER_AFFINITY) && !FilterClusterAffinity(b, c)) return 3;
+  if (o.plugins & KP_PLUGIN_SPREAD_CONSTRAINT) {
+    for (auto& sc : b.spreads) {
+      if (sc.field == "provider" && c.provider.empty()) return 4;
+      if (sc.field == "region" && c.region.empty()) return 5;
+      if (sc.field == "zone" && c.zones.empty()) return 6;
+    }
+  }
+  if ((o.plugins & KP_PLUGIN_CLUSTER_EVICTION) && !FilterClusterEviction(b, c)) return 7;
+  return 0;
+}
+
 // RunScorePlugins summed (framework.go:126-170, generic_scheduler.go:185-191):
 // ClusterLocality (cluster_locality.go:50-61) + ClusterAffinity = 0 (cluster_affinity.go:97-100)
 i64 ScoreCluster(const Binding& b, const Cluster& c, const Options& o) {
@@ -2203,6 +2234,11 @@ uint32_t kpo_filter(const kp_cluster* c, const kp_binding* b, const kp_options* 
   bool ok = true;
   Cluster cl = convCluster(*c, 0, &ok);
   return RunFilterPlugins(convBinding(*b), cl, convOptions(opts));
+}
+uint32_t kpo_filter_reason(const kp_cluster* c, const kp_binding* b, const kp_options* opts) {
+  bool ok = true;
+  Cluster cl = convCluster(*c, 0, &ok);
+  return RunFilterPluginsReason(convBinding(*b), cl, convOptions(opts));
 }
 
 int64_t kpo_score(const kp_cluster* c, const kp_binding* b, const kp_options* opts) {

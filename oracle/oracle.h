@@ -78,6 +78,8 @@ int kpo_cluster_matches(const kp_cluster* c, const kp_cluster_affinity* a);
 /* Filter plugins in canonical order; returns 0 when the cluster fits, else the
  * KP_PLUGIN_* bit of the first failing plugin. */
 uint32_t kpo_filter(const kp_cluster* c, const kp_binding* b, const kp_options* opts);
+/* The same pair as a kp_filter_reasons word (KP_REASON_* | arg << 8). */
+uint32_t kpo_filter_reason(const kp_cluster* c, const kp_binding* b, const kp_options* opts);
 int64_t kpo_score(const kp_cluster* c, const kp_binding* b, const kp_options* opts);
 int32_t kpo_max_available_replicas(const kp_cluster* c, const kp_binding* b,
                                    const kp_options* opts, int mode);

@@ -21,18 +21,18 @@ def engine():
     e.close()
 
 
-def run(engine, u, opts, lo=0, hi=None, fuse=True, times=None):
-    """Schedules bindings [lo, hi); fuse=False forces the two-kernel SEL_ALL path
-    (KP_NO_FUSE), times (a list) receives the call's kp_stage_times."""
+def run(engine, u, opts, lo=0, hi=None, fuse=False, times=None):
+    """Schedules bindings [lo, hi); fuse=True takes the fused SEL_ALL kernel
+    (KP_FUSE=1), times (a list) receives the call's kp_stage_times."""
     hi = u.n_bindings if hi is None else hi
     snap = Snapshot.from_structs(engine, u.clusters, u.n_clusters, u.names, opts)
     b = Batch(snap, structs=u.binding_slice(lo, hi))
-    if not fuse:
-        os.environ["KP_NO_FUSE"] = "1"
+    if fuse:
+        os.environ["KP_FUSE"] = "1"
     try:
         out = b.schedule()
     finally:
-        os.environ.pop("KP_NO_FUSE", None)
+        os.environ.pop("KP_FUSE", None)
     if times is not None:
         times.append(engine.stage_times())
     b.close()

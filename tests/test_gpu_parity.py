@@ -91,6 +91,24 @@ def test_schedule_parity(engine, config, seed, n_clusters, n_bindings):
     compare(gpu_schedule(engine, u, opts), oracle_schedule(u, opts), f"config {config} seed {seed}")
 
 
+@pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
+    (3, 3, 500, 1000), (2, 2, 1000, 1000), (5, 5, 3000, 1200), (7, 17, 2000, 1000), (3, 3, 5000, 1000),
+])
+def test_schedule_parity_fused(engine, config, seed, n_clusters, n_bindings):
+    """The opt-in fused pair + SEL_ALL kernel (KP_FUSE=1, k_fused_all*)."""
+    import os
+    u = synth.Universe(config, seed, n_clusters, 0, n_bindings)
+    opts = api.options()
+    os.environ["KP_FUSE"] = "1"
+    try:
+        got = gpu_schedule(engine, u, opts)
+        fused = engine.stage_times()["fused"]
+    finally:
+        os.environ.pop("KP_FUSE", None)
+    compare(got, oracle_schedule(u, opts), f"fused config {config} seed {seed}")
+    assert fused == 1
+
+
 @pytest.mark.parametrize("prop,plugins,gate", [
     (True, api.PLUGIN_ALL, True),
     (False, api.PLUGIN_ALL & ~api.PLUGIN_TAINT_TOLERATION, True),
