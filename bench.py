@@ -5,10 +5,16 @@ GeneralEstimator with 8 resource-model grades, 50% DynamicWeight / 50%
 Aggregated (synthetic universe of SURVEY.md §8(d), seed 3). A step = one
 kp_schedule_batch over the whole batch: filter -> score -> estimate -> select ->
 divide, results copied back to the host as CSR. Packed inputs are resident in
-HBM before the timed region (snapshot and binding packing are reported
-separately). Multi-GPU: one process per GPU, each schedules its own contiguous
-binding range of the universe against its own snapshot replica (weak scaling,
-no data-path collective).
+HBM before the timed region; `end_to_end_value` times binding packing + upload +
+schedule together (the snapshot is packed once per cache generation). Multi-GPU:
+one process per GPU, each schedules its own contiguous binding range of the
+universe against its own snapshot replica (weak scaling, no data-path
+collective); the per-rank CSR results are all-gathered after the timed region.
+
+Roofline: the dominant kernel of the step (by its HIP-event time) against HBM
+peak with compulsory bytes, plus the counter-derived DRAM bytes
+(FETCH_SIZE x2 on gfx950 + WRITE_SIZE) and VALU issue fraction of the same
+kernel from the committed PMC summary (profiles/r02_pmc_config<N>.json).
 """
 import argparse
 import json
@@ -21,41 +27,67 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 instruction per 2 cycles per SIMD
-# at 2.4 GHz (MI355X_MICROARCH.md, "issues each VALU instruction over 2 cycles")
+# at 2.4 GHz (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles")
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # 1228.8 G wave-instructions/s
-# SURVEY.md §8(d) streamed-row model, config 3: B_row = 140 filter + 52 summary + 192 grades
-B_ROW = {2: 184, 3: 384, 4: 192, 5: 384, 6: 384, 1: 184}
+# Per-binding input record: BindHdr (160 B) + its pool slices (~96 B on these workloads)
 B_BIND = 256
 # pair kernel instance per kp_stage_times.pair_kind (kp_algo.h EST_*)
 PAIR_KERNELS = {0: "k_pair", 1: "k_pair_fast", 2: "k_pair_fast_summary", 8: "k_pair_fast_m8", 16: "k_pair_fast_m16"}
 
 
-def pair_bytes_per_binding(config, n_clusters):
-    """Algorithmic bytes of the pair kernel per binding: B_bind + C*B_row + C/8 + 4*C."""
-    C = n_clusters
-    return B_BIND + C * B_ROW[config] + C / 8.0 + 4.0 * C
+def compulsory_bytes(n_bind, n_all, n_clusters, n_targets, snap_bytes):
+    """Compulsory HBM bytes per launch:
+    pair         = snapshot once + binding records + the est row (4*Cp) and feasibility
+                   mask (Cp/8) it writes per binding;
+    k_select_all = its bindings' rows and records read back + their results (cluster u32
+                   + replicas i32 per target, status/err/arg/start/count per binding)."""
+    Cp = (n_clusters + 63) // 64 * 64
+    row = 4.0 * Cp + Cp / 8.0
+    pair = snap_bytes + n_bind * (B_BIND + row)
+    sel = n_all * (B_BIND + row + 28) + 8.0 * n_targets
+    return pair, sel
+
+
+def load_pmc(config, kernel):
+    """Per-launch PMC figures of `kernel` from the committed summary (same bench
+    command, default sizes): {hbm_bytes (FETCH_SIZE*2 + WRITE_SIZE), valu_insts, ...}."""
+    try:
+        with open(os.path.join(ROOT, "profiles", f"r02_pmc_config{config}.json")) as f:
+            return json.load(f).get("kernels", {}).get(kernel)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_threads():
+    """Host threads for the CPU baseline: the CPUs this process may run on
+    (sched_getaffinity), or KP_CPU_THREADS."""
+    if os.environ.get("KP_CPU_THREADS"):
+        return max(1, int(os.environ["KP_CPU_THREADS"]))
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def cpu_baseline(u, opts, budget_s):
-    """Oracle (faithful C++ restatement, REFSHAPE mode) on a bounded sample, rank 0 only."""
+    """Oracle (faithful C++ restatement, REFSHAPE mode) on a bounded sample, rank 0 only,
+    at 1 thread and at every CPU the process may use."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    threads = int(os.environ.get("KP_CPU_THREADS", "16"))
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    threads = cpu_threads()
     out = {}
     for th, share in ((1, 0.35), (threads, 0.65)):
-        n, done, t_used = 16, 0, 0.0
+        n = 16
         while True:
             n = min(n, u.n_bindings)
             ba, _ = u.binding_slice(0, n)
             t0 = time.perf_counter()
             O.schedule_c(u.clusters, u.n_clusters, ba, n, opts, O.REFSHAPE, th)
             dt = time.perf_counter() - t0
-            done, t_used = n, dt
             if dt >= budget_s * share / 3 or n >= u.n_bindings:
                 break
             n *= 2
-        out[th] = (done / t_used, done, t_used)
+        out[th] = (n / dt, n, dt)
     rate, n, dt = out[threads]
     r1, n1, dt1 = out[1]
     return {
@@ -66,14 +98,14 @@ def cpu_baseline(u, opts, budget_s):
                    "closed form (the literal FF loop is intractable here), so a lower bound on the "
                    "reference's cost"),
         "single_thread_value": round(r1, 3),
+        "os_cpu_count": os.cpu_count(),
     }
 
 
-def parity_check(u, r, opts, n_check, seed):
+def parity_check(u, res, opts, n_check, seed):
     """Oracle (FAST mode) on n_check bindings sampled from the timed batch, compared
     with the engine's results of the last timed step (status, error, multiset of
     targets). Test infrastructure, after the timed region."""
-    import ctypes as C
     import random
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
@@ -83,41 +115,9 @@ def parity_check(u, r, opts, n_check, seed):
         return 0, 0
     idx = sorted(random.Random(seed).sample(range(u.n_bindings), n))
     arr = (api.kp_binding * n)(*[u.bindings[i] for i in idx])
-    want = O.schedule_c(u.clusters, u.n_clusters, arr, n, opts, O.FAST, min(16, os.cpu_count() or 1))
-    got = api.results_to_python(r.status, r.err_code, r.err_arg, r.offsets, r.cluster_idx, r.replicas, r.n_bindings)
-    bad = sum(1 for k, i in enumerate(idx) if got[i] != want[k])
+    want = O.schedule_c(u.clusters, u.n_clusters, arr, n, opts, O.FAST, min(16, cpu_threads()))
+    bad = sum(1 for k, i in enumerate(idx) if res[i] != want[k])
     return n, bad
-
-
-def load_traffic(config, kernel):
-    """Per-launch PMC figures of the pair kernel instance from the committed profile,
-    if any: (HBM bytes = FETCH_SIZE + WRITE_SIZE, VALU wave-instructions)."""
-    p = os.path.join(ROOT, "profiles", f"traffic_config{config}.json")
-    try:
-        with open(p) as f:
-            d = json.load(f)
-        if d.get("kernel", "k_pair") != kernel:
-            return None, None  # profiled another instance
-        return d.get("k_pair_bytes_per_launch"), d.get("k_pair_valu_per_launch")
-    except (OSError, ValueError):
-        return None, None
-
-
-def select_bytes(n_bindings, n_clusters, n_targets):
-    """Algorithmic bytes of the select stage per batch: each binding reads its feasibility
-    bitmask (C/8) and its calAvailableReplicas row (4*C) plus its packed header, and the
-    results are written as (cluster_idx u32, replicas i32) pairs."""
-    Cp = (n_clusters + 63) // 64 * 64
-    return n_bindings * (Cp / 8.0 + 4.0 * Cp + 144) + 8.0 * n_targets
-
-
-def load_select_pmc(config):
-    """k_select_all's per-launch HBM bytes (FETCH_SIZE + WRITE_SIZE) from the committed PMC summary."""
-    try:
-        with open(os.path.join(ROOT, "profiles", f"r01_pmc_config{config}.json")) as f:
-            return json.load(f).get("k_select_all", {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
 
 
 def main():
@@ -133,10 +133,12 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", type=int, default=1000,
                     help="bindings of the timed batch re-checked against the oracle after timing (0: off)")
+    ap.add_argument("--e2e-reps", type=int, default=5, help="timed pack+upload+schedule repetitions (0: off)")
     ap.add_argument("--lib", default=None, help="engine library (default karmada_amd/libkp.so)")
     args = ap.parse_args()
 
     from karmada_amd import api, synth
+    from karmada_amd.dist import Csr
     from karmada_amd.engine import Batch, Engine, Snapshot
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -178,6 +180,7 @@ def main():
         snap = Snapshot.from_structs(eng, u.clusters, u.n_clusters, u.names, opts) if rank == 0 else None
         snap = broadcast_snapshot(eng, snap, u.names)
     snap_s = time.perf_counter() - t0
+    snap_bytes = len(snap.to_bytes())
     t0 = time.perf_counter()
     batch = Batch(snap, structs=u.binding_slice(0, u.n_bindings))
     pack_s = time.perf_counter() - t0
@@ -191,48 +194,78 @@ def main():
     for _ in range(args.warmup):
         batch.schedule_raw()
     barrier_sync()
-    pair_ms, sel_ms, host_ms = [], [], []
+    st_all = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         r = batch.schedule_raw()
-        st = eng.stage_times()
-        pair_ms.append(st["pair_kernel_ms"])
-        sel_ms.append(st["select_kernel_ms"])
-        host_ms.append(st["host_ms"])
-        n_slow = st["n_slow"]
-        launches = max(1, st["pair_launches"])
-        kind = st["pair_kind"]
+        st_all.append(eng.stage_times())
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    n_ok = sum(1 for i in range(r.n_bindings) if r.status[i] == 0)
-    n_targets = n_targets_rank = int(r.n_targets)
+    # ---- after the timed region ----
+    csr = Csr.from_results(r)
+    res = csr.to_python()
+    n_ok = int((csr.status == 0).sum())
+    n_targets_rank = n_targets = csr.n_targets
     if dist is not None:
         import torch
+        from karmada_amd.dist import gather_csr
         t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        # per-rank result counts, all-gathered (after the timed region)
-        c = torch.tensor([n_ok, n_targets], dtype=torch.int64, device=tdev)
-        parts = [torch.zeros_like(c) for _ in range(world)]
-        dist.all_gather(parts, c)
-        n_ok = int(sum(p[0].item() for p in parts))
-        n_targets = int(sum(p[1].item() for p in parts))
+        whole = gather_csr(csr)  # two-phase CSR all-gather (counts, then padded arrays)
+        n_ok = int((whole.status == 0).sum())
+        n_targets = whole.n_targets
 
-    n_chk, n_bad = parity_check(u, r, opts, args.check, 1000 + rank) if args.check > 0 else (0, 0)
+    n_chk, n_bad = parity_check(u, res, opts, args.check, 1000 + rank) if args.check > 0 else (0, 0)
     if dist is not None:
         t = torch.tensor([n_chk, n_bad], dtype=torch.int64, device=tdev)
         dist.all_reduce(t)
         n_chk, n_bad = int(t[0].item()), int(t[1].item())
+
+    # end to end: binding packing + upload + schedule + results to host, per batch
+    batch.close()
+    e2e = None
+    if args.e2e_reps > 0:
+        ts = []
+        for _ in range(args.e2e_reps):
+            t1 = time.perf_counter()
+            b2 = Batch(snap, structs=u.binding_slice(0, u.n_bindings))
+            b2.schedule_raw()
+            ts.append(time.perf_counter() - t1)
+            b2.close()
+        e2e = sum(ts) / len(ts)
+        if dist is not None:
+            t = torch.tensor([e2e], dtype=torch.float64, device=tdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            e2e = float(t.item())
+
+    def avg(k):
+        return sum(x[k] for x in st_all) / len(st_all)
     ms_per_step = 1e3 * elapsed / args.steps
     value = (B * world) / (elapsed / args.steps)
-    avg_pair_ms = sum(pair_ms) / len(pair_ms)  # all pair launches of one step
-    achieved = pair_bytes_per_binding(cfg, C_) * B / (avg_pair_ms * 1e-3) / 1e9
-    launch_ms = avg_pair_ms / launches
-    avg_sel_ms = sum(sel_ms) / len(sel_ms)
-    sel_gbs = select_bytes(B, C_, n_targets_rank) / (avg_sel_ms * 1e-3) / 1e9
-    # the committed PMC figures are per launch at the config's default sizes only
+    last = st_all[-1]
+    pair_ms, sel_ms = avg("pair_kernel_ms"), avg("select_kernel_ms")
+    sel_all_ms, fused_ms = avg("sel_all_kernel_ms"), avg("fused_kernel_ms")
+    fused = last["fused"] == 1
+    pair_b, sel_b = compulsory_bytes(B, int(last["n_sel_all"]), C_, n_targets_rank, snap_bytes)
+    cands = [(PAIR_KERNELS.get(last["pair_kind"], "k_pair"), pair_ms, pair_b)]
+    if not fused:
+        cands.append(("k_select_all", sel_all_ms, sel_b))
+    kname, kms, kbytes = max(cands, key=lambda x: x[1])
+    achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     profiled = (C_, B) == tuple(synth.CONFIGS[cfg])
-    traffic, valu = load_traffic(cfg, PAIR_KERNELS.get(kind, "k_pair")) if profiled else (None, None)
+    pmc = load_pmc(cfg, kname) if profiled else None
+
+    def pmc_frac(key, peak):
+        if not pmc or not pmc.get(key) or kms <= 0:
+            return None
+        return round(pmc[key] / (kms * 1e-3) / 1e9 / peak, 4)
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc.get("hbm_bytes") if pmc else None,
+            "kernel": kname, "kernel_ms": round(kms, 4), "algorithmic_bytes": round(kbytes),
+            "dram_frac": pmc_frac("hbm_bytes", HBM_PEAK_GBS), "valu_frac": pmc_frac("valu_insts", VALU_PEAK_GINST)}
+    step_bytes = pair_b + (0.0 if fused else sel_b)
+    step_gbs = step_bytes / (ms_per_step * 1e-3) / 1e9
     line = {
         "metric": "ResourceBindings scheduled/sec at 100k bindings x 5k clusters",
         "value": round(value, 1),
@@ -250,29 +283,20 @@ def main():
                                "resource-model grades, DynamicWeight/Aggregated" if cfg == 3 else
                    f"config{cfg}: {B} bindings/GPU x {C_} clusters, seed {seed}",
                    "bindings_per_gpu": B, "clusters": C_, "parallelism": f"binding-shard x{world}"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": PAIR_KERNELS.get(kind, "k_pair"), "kernel_ms": round(launch_ms, 4),
-                     "launches_per_step": launches,
-                     # SURVEY §8(d) streamed-row model: every binding re-reads every cluster
-                     # row. The packed snapshot (~2 MB) stays in each XCD's L2, so that
-                     # exceeds HBM peak; what bounds the kernel is instruction issue:
-                     "dram_gbs": round(traffic / (launch_ms * 1e-3) / 1e9, 1) if traffic else None,
-                     "valu": ({"achieved": round(valu / (launch_ms * 1e-3) / 1e9, 1), "peak": VALU_PEAK_GINST,
-                               "unit": "G wave-inst/s", "frac": round(valu / (launch_ms * 1e-3) / 1e9 / VALU_PEAK_GINST, 4)}
-                              if valu else None)},
-        # the select stage (k_select_all + k_slow + k_compact, HIP events after the last pair
-        # launch) is the larger share of the step; its byte roofline beside the pair kernel's
-        "select_roofline": {"bound": "hbm", "achieved": round(sel_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": round(sel_gbs / HBM_PEAK_GBS, 4), "traffic": load_select_pmc(cfg) if profiled else None,
-                            "kernel": "k_select_all", "stage_ms": round(avg_sel_ms, 4)},
-        "stages_ms": {"pair_kernel": round(avg_pair_ms, 3), "select_kernels": round(sum(sel_ms) / len(sel_ms), 3),
-                      "host_region": round(sum(host_ms) / len(host_ms), 3)},
+        "roofline": roof,
+        # compulsory bytes of the whole step (every kernel) over the whole step's time
+        "step_roofline": {"achieved": round(step_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(step_gbs / HBM_PEAK_GBS, 4), "bytes": round(step_bytes)},
+        "stages_ms": {"pair_kernel": round(pair_ms, 3), "select_kernels": round(sel_ms, 3),
+                      "sel_all_kernel": round(sel_all_ms, 3), "fused_kernel": round(fused_ms, 3),
+                      "host_region": round(avg("host_ms"), 3)},
+        "end_to_end_value": round(B * world / e2e, 1) if e2e else None,
+        "end_to_end_ms": round(1e3 * e2e, 2) if e2e else None,
         "setup_s": {"generate": round(gen_s, 2), "snapshot_pack_upload": round(snap_s, 3),
                     "binding_pack_upload": round(pack_s, 3)},
         "scheduled_ok": n_ok,
         "result_targets": n_targets,
-        "slow_path_bindings": n_slow,
+        "slow_path_bindings": int(last["n_slow"]),
         # bindings of the timed batch (sampled over all ranks) re-checked against the oracle
         "parity_checked": n_chk,
         "parity_bad": n_bad,
@@ -281,7 +305,6 @@ def main():
         line["cpu_baseline"] = cpu_baseline(u, opts, args.cpu_budget)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    batch.close()
     snap.close()
     eng.close()
     if dist is not None:

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 5
+#define KP_ABI_VERSION 6
 
 /* ------------------------------------------------------------------------- */
 /* Object model                                                              */
@@ -329,6 +329,8 @@ typedef struct kp_stage_times {
   uint32_t pair_kind;     /* pair kernel instance: 0 generic, 1 mixed, 2 summary-only, 8/16 model-only */
   float fused_kernel_ms;  /* fused pair + SEL_ALL select kernel (HIP events), 0 when not run */
   uint32_t fused;         /* 1: the SEL_ALL bindings took the fused kernel (rows kept in LDS) */
+  float sel_all_kernel_ms; /* the two-kernel path's SEL_ALL select kernel alone (HIP events) */
+  uint32_t n_sel_all;      /* bindings of the SEL_ALL select kernel (SelectBestClusters selects all) */
 } kp_stage_times;
 
 /* ------------------------------------------------------------------------- */

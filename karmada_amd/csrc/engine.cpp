@@ -631,9 +631,18 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
 // ============================================================================
 // Binding packing
 // ============================================================================
+// Host-side pools of packed bindings (kp_batch's, or one packing thread's).
+struct Pools {
+  std::vector<int32_t> ipool;
+  std::vector<int64_t> lpool;
+  std::vector<Tol> tols;
+  std::vector<Prog> progs;
+  std::vector<Instr> instrs;
+};
+
 struct Packer {
   kp_snapshot* s;
-  kp_batch* bt;
+  Pools* bt;  // this packer's pools (one per packing thread, merged by kp_batch_create)
 
   int32_t list(const std::vector<int32_t>& v) {
     int32_t off = (int32_t)bt->ipool.size();
@@ -826,16 +835,16 @@ struct Packer {
     // spec.Clusters
     h.n_targets_all = (int32_t)b.n_clusters;
     {
-      std::vector<int32_t> t;
-      std::vector<char> seen(s->C, 0);
+      std::vector<int32_t> t, rk;
       for (uint32_t i = 0; i < b.n_clusters; i++) {
         auto it = s->rank_of.find(S(b.clusters[i].name));
         if (it == s->rank_of.end()) continue;
-        if (seen[it->second]) f |= BF_DUP_TARGETS;
-        seen[it->second] = 1;
+        rk.push_back(it->second);
         t.push_back(it->second);
         t.push_back(b.clusters[i].replicas);
       }
+      std::sort(rk.begin(), rk.end());
+      if (std::adjacent_find(rk.begin(), rk.end()) != rk.end()) f |= BF_DUP_TARGETS;
       h.tgt_off = list(t);
       h.tgt_cnt = (int32_t)t.size() / 2;
       if (b.n_clusters > 0 && (o.enabled_plugins & KP_PLUGIN_CLUSTER_LOCALITY)) f |= BF_SCORE_LOCALITY;
@@ -1586,6 +1595,76 @@ int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_sna
   return KP_OK;
 }
 
+// Packs bindings [0, n) into bt->hdr and bt's pools on T host threads: thread t
+// packs a contiguous chunk into its own Pools (the Packer only reads the snapshot's
+// dictionaries), then the chunks are concatenated and every pool reference is
+// rebased: header offsets, program ids in the ipool lists, Prog::ins_off and the
+// list offsets inside Instr. The result equals a sequential pack (test_abi).
+// Threads: KP_PACK_THREADS, else hardware_concurrency, one per 4096 bindings at most.
+bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* bt) {
+  int T = (int)std::thread::hardware_concurrency();
+  if (const char* v = getenv("KP_PACK_THREADS")) T = atoi(v);
+  T = std::max(1, std::min(T, n / 4096));
+  std::vector<Pools> pl(T);
+  std::vector<int> lo(T + 1);
+  for (int t = 0; t <= T; t++) lo[t] = (int)((int64_t)n * t / T);
+  auto run = [&](int t) {
+    Packer pk{s, &pl[t]};
+    for (int i = lo[t]; i < lo[t + 1]; i++) pk.pack(bindings[i], bt->hdr[i]);
+  };
+  if (T == 1) {
+    run(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++) th.emplace_back(run, t);
+    for (auto& x : th) x.join();
+  }
+  size_t ni = 0, nl = 0, nt = 0, np = 0, nn = 0;
+  for (auto& q : pl) ni += q.ipool.size(), nl += q.lpool.size(), nt += q.tols.size(), np += q.progs.size(),
+                     nn += q.instrs.size();
+  if (ni > (size_t)INT32_MAX || nl > (size_t)INT32_MAX || nt > (size_t)INT32_MAX || np > (size_t)INT32_MAX ||
+      nn > (size_t)INT32_MAX)
+    return false;  // pool offsets are int32
+  bt->ipool.reserve(ni);
+  bt->lpool.reserve(nl);
+  bt->tols.reserve(nt);
+  bt->progs.reserve(np);
+  bt->instrs.reserve(nn);
+  for (int t = 0; t < T; t++) {
+    Pools& q = pl[t];
+    const int32_t bi = (int32_t)bt->ipool.size(), bl = (int32_t)bt->lpool.size(), bo = (int32_t)bt->tols.size(),
+                  bp = (int32_t)bt->progs.size(), bn = (int32_t)bt->instrs.size();
+    if (t > 0) {
+      for (int i = lo[t]; i < lo[t + 1]; i++) {
+        BindHdr& h = bt->hdr[i];
+        for (int j = 0; j < h.filt_cnt; j++) q.ipool[h.filt_off + j] += bp;
+        for (int j = 0; j < h.ovf_cnt; j++) q.ipool[h.ovf_off + j] += bp;
+        for (int j = 0; j < h.sw_cnt; j++) q.ipool[h.sw_off + j] += bp;
+        h.tgt_off += bi, h.evict_off += bi, h.filt_off += bi, h.ovf_off += bi, h.sw_off += bi;
+        h.sreq_off += bi, h.mreq_off += bi, h.ip_beg += bi, h.ip_end += bi;
+        h.sw_w_off += bl, h.sreq_q_off += bl, h.mreq_q_off += bl;
+        h.tol_off += bo;
+        h.pr_beg += bp, h.pr_end += bp;
+        h.in_beg += bn, h.in_end += bn;
+      }
+      for (Prog& p : q.progs) p.ins_off += bn;
+      for (Instr& x : q.instrs) {
+        if (x.op == OP_EXCLUDE || x.op == OP_NAMES) x.a += bi;
+        else if (x.op == OP_LBL_IN || x.op == OP_LBL_NOTIN || x.op == OP_FLD_IN || x.op == OP_FLD_NOTIN ||
+                 x.op == OP_ZONE_IN || x.op == OP_ZONE_NOTIN)
+          x.b += bi;
+      }
+    }
+    bt->ipool.insert(bt->ipool.end(), q.ipool.begin(), q.ipool.end());
+    bt->lpool.insert(bt->lpool.end(), q.lpool.begin(), q.lpool.end());
+    bt->tols.insert(bt->tols.end(), q.tols.begin(), q.tols.end());
+    bt->progs.insert(bt->progs.end(), q.progs.begin(), q.progs.end());
+    bt->instrs.insert(bt->instrs.end(), q.instrs.begin(), q.instrs.end());
+    q = Pools();
+  }
+  return true;
+}
+
 int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindings, uint64_t n, kp_batch** out) {
   if (!e || !sc || !out || (n && !bindings)) return KP_EINVAL;
   if (n > (uint64_t)INT32_MAX) return KP_ENOTSUP;
@@ -1596,9 +1675,12 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   bt->snap = s;
   bt->B = (int)n;
   bt->hdr.resize(n);
-  Packer pk{s, bt};
+  const auto tp0 = std::chrono::steady_clock::now();
+  if (!pack_parallel(s, bindings, (int)n, bt)) {
+    e->err = "batch pools exceed 2^31 entries";
+    return KP_ENOTSUP;
+  }
   for (uint64_t i = 0; i < n; i++) {
-    pk.pack(bindings[i], bt->hdr[i]);
     bt->out_cap += bt->hdr[i].out_cap;
     const BindHdr& h = bt->hdr[i];
     if (h.sel == SEL_CLUSTER) bt->l_cluster.push_back((int32_t)i);
@@ -1695,7 +1777,9 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->rnsel, std::max(1, nr));
   a.add(&bt->nhost, 1);
   a.add(&bt->slow_scratch, bt->slow_slot * bt->slow_grid);
+  const auto tp1 = std::chrono::steady_clock::now();
   HIPCHK(a.alloc());
+  const auto tp2 = std::chrono::steady_clock::now();
   auto up = [&](void* d, const void* h, size_t bytes) {
     return dev::h2d(d, h, bytes, e->stream);
   };
@@ -1711,6 +1795,12 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   HIPCHK(up(bt->d_cs, bt->l_cs.data(), 4 * bt->l_cs.size()));
   HIPCHK(dev::fill(bt->slow, 0, 4 * (size_t)B, e->stream));
   HIPCHK(dev::sync(e->stream));
+  if (getenv("KP_PACK_TIMING")) {
+    const auto tp3 = std::chrono::steady_clock::now();
+    auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+    fprintf(stderr, "kp_batch_create: pack %.1f ms, alloc %.1f ms, upload %.1f ms\n", ms(tp0, tp1), ms(tp1, tp2),
+            ms(tp2, tp3));
+  }
   BatchView& v = bt->view;
   v.B = bt->B;
   v.hdr = d_hdr;
@@ -1812,6 +1902,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     k.n = (int)bt->l_all.size();
     HIPCHK(dev::select(st, SEL_LAUNCH_ALL, k, smem_all(s), cap, sx));
   }
+  HIPCHK(dev::event_record(e->ev[7], st));  // k_select_all alone: ev[1] -> ev[7]
   if (!bt->l_cluster.empty()) {
     KArgs k = ka;
     k.list = bt->d_cluster;
@@ -1948,6 +2039,8 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   tm.pair_kernel_ms = ms_pair;
   tm.select_kernel_ms = ms_sel;
   tm.fused_kernel_ms = ms_fused;
+  tm.sel_all_kernel_ms = dev::event_ms(e->ev[1], e->ev[7]);
+  tm.n_sel_all = (uint32_t)bt->l_all.size();
   tm.fused = fused ? 1u : 0u;
   tm.n_slow = bt->h_stats[0];
 #ifdef KP_STAMPS

@@ -90,3 +90,23 @@ def test_cpusim_overflow_tiers_large_c(engine):
     ba, n = u.binding_slice(0, 4000)
     want = O.schedule_c(u.clusters, u.n_clusters, ba, n, opts, O.FAST, 8)
     compare(run(engine, u, opts, 0, 4000), want, "config 6 seed 13 C=5000")
+
+
+def test_cpusim_parallel_packing(engine):
+    """kp_batch_create packs on several host threads (one per 4096 bindings) and
+    rebases every pool reference: the results equal a one-thread pack and the oracle."""
+    u = synth.Universe(6, 41, 60, 0, 20000)
+    opts = api.options()
+    os.environ["KP_PACK_THREADS"] = "1"
+    try:
+        one = run(engine, u, opts)
+    finally:
+        os.environ.pop("KP_PACK_THREADS", None)
+    os.environ["KP_PACK_THREADS"] = "5"
+    try:
+        many = run(engine, u, opts)
+    finally:
+        os.environ.pop("KP_PACK_THREADS", None)
+    assert many == one
+    ba, n = u.binding_slice(0, u.n_bindings)
+    compare(many, O.schedule_c(u.clusters, u.n_clusters, ba, n, opts, O.FAST, 8), "parallel packing")
