@@ -60,13 +60,22 @@ def load_pmc(config, kernel):
 
 def cpu_threads():
     """Host threads for the CPU baseline: the CPUs this process may run on
-    (sched_getaffinity), or KP_CPU_THREADS."""
+    (sched_getaffinity), capped by its cgroup CPU quota (cpu.max) when one is set,
+    or KP_CPU_THREADS."""
     if os.environ.get("KP_CPU_THREADS"):
         return max(1, int(os.environ["KP_CPU_THREADS"]))
     try:
-        return max(1, len(os.sched_getaffinity(0)))
+        n = len(os.sched_getaffinity(0))
     except AttributeError:
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
 
 
 def cpu_baseline(u, opts, budget_s):

@@ -109,8 +109,7 @@ int pair(stream_t, const SnapView& s, const BatchView& bv, const int32_t* list, 
 
 int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x) {
   switch (which) {
-    case SEL_LAUNCH_ALL:
-    case SEL_LAUNCH_ALL_REG: {  // the host runs the LDS form; size its scratch here
+    case SEL_LAUNCH_ALL: {
       const size_t need = kRedBytes + 4 * (size_t)((((a.s.Cp + 31) >> 5) + 3) & ~3) + 8 * (size_t)a.s.Cp + 3072 +
                           8 * (size_t)sel_all_ecap(a.s.Cp) + 64;
       grid(a.n, need > smem ? need : smem,

@@ -365,35 +365,6 @@ KP_FI void body_fused_all(const BLK& B, int blk, unsigned char* smem, const KArg
   select_all_common(B, a, x, RowCands{fit, row, s.C, B.tid(), B.nth()}, F, ss);
 }
 
-// Candidates in registers: thread t owns clusters t + nth*j, j < J (C <= nth*J).
-template <int J, class BLK>
-KP_FI void body_select_all_reg(const BLK& B, int blk, unsigned char* smem, const KArgs& a) {
-  if (blk >= a.n) return;
-  const int b = a.list[blk];
-  const int words = (a.s.Cp + 31) >> 5;
-  uint32_t* tgt = (uint32_t*)(smem + kRedBytes);
-  const SelScratch ss = carve_sel_scratch((unsigned char*)(tgt + ((words + 3) & ~3)), a.s.Cp);
-  const BindHdr* h = &a.bv.hdr[b];
-  build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
-  SelCtx x = make_ctx(a, b, tgt);
-  const bool weights = h->strategy == ST_STATIC && h->sel == SEL_ALL;
-  RegCands<J> cs;
-  cs.tid = B.tid();
-  cs.nth = B.nth();
-  cs.fm = 0;
-KP_UNROLL
-  for (int j = 0; j < J; j++) {
-    const int c = cs.tid + cs.nth * j;
-    cs.v[j] = 0;
-    if (c < a.s.C && mask_test(x.frow, c)) {
-      cs.fm |= 1ull << j;
-      cs.v[j] = weights ? static_vote(x, c) : x.erow[c];
-    }
-  }
-  const int F = (int)B.sum64(popc64(cs.fm));
-  select_all_common(B, a, x, cs, F, ss);
-}
-
 // ---------------------------------------------------------------------------
 // Select stage: SEL_CLUSTER
 // ---------------------------------------------------------------------------

@@ -27,8 +27,7 @@ enum : int {
   SEL_LAUNCH_CLUSTER,
   SEL_LAUNCH_REGION_A,
   SEL_LAUNCH_REGION_B,
-  SEL_LAUNCH_SLOW,
-  SEL_LAUNCH_ALL_REG  // SEL_LAUNCH_ALL with candidates in registers (GPU)
+  SEL_LAUNCH_SLOW
 };
 
 struct SelectExtra {
@@ -55,12 +54,6 @@ constexpr int kTsetMax = 4096;    // distinct taint lists answered once per bind
 #define KP_ECAP_MAX 1024
 #endif
 KP_HD inline int sel_all_ecap(int Cp) { return Cp / 2 < 64 ? 64 : (Cp / 2 > KP_ECAP_MAX ? KP_ECAP_MAX : Cp / 2); }
-// Register-resident SEL_ALL: slots per thread for C clusters (0 = use the LDS form).
-KP_HD inline int sel_all_slots(int C) {
-  for (int J = 4; J <= 64; J *= 2)
-    if (C <= kBlock * J) return J;
-  return 0;
-}
 
 // LDS bytes of the pair stage's per-binding tail (evict bits | md table | predicate
 // stage | taint-list bits; kp_kernels.h PairLds).

@@ -69,22 +69,6 @@ struct LdsCands {  // candidates compacted in LDS (gather)
   KP_FI uint64_t okey(const SelCtx& x, uint32_t rk, int32_t v0) const { return cand_order_key(x, rk, v0); }
   static constexpr bool kExact = false;  // okey is sort.Sort's output order only for <= 12 (stable insertion)
 };
-template <int J>
-struct RegCands {  // slot j of thread t is cluster t + nth*j; votes live in registers
-  int32_t v[J];
-  uint64_t fm;  // bit j: slot j is a candidate
-  int tid, nth;
-  template <class Fn>
-  KP_FI void each(Fn fn) const {
-KP_UNROLL
-    for (int j = 0; j < J; j++)
-      if ((fm >> j) & 1ull) fn((uint32_t)(tid + nth * j), v[j]);
-  }
-  KP_FI uint64_t okey(const SelCtx& x, uint32_t rk, int32_t v0) const { return cand_order_key(x, rk, v0); }
-  static constexpr bool kExact = false;
-  static constexpr bool kSettable = false;
-};
-
 // The fused pair + select kernel's candidates: the clusters whose feasibility
 // bit is set in the LDS bitset `fit` (u64 words, the fmask row layout), with
 // v = row[c] (calAvailableReplicas, or the StaticWeight vote) in LDS. Thread t
@@ -192,6 +176,54 @@ KP_FI void emit_each(const BLK& B, const SelCtx& x, const CS& cs, RepFn rep, boo
       o++;
     }
   });
+}
+
+// Block-parallel emission from a compacted party list pl[0, np) ((rank << 32) |
+// votes; rep(rank, votes) gives the replicas, emitted when > 0) plus, when
+// `targets`, the binding's spec.Clusters entries that are candidates with
+// trep(rank) > 0 (0 for those the list already holds).
+template <class BLK, class RepFn, class TRepFn>
+KP_FI void emit_lists(const BLK& B, const SelCtx& x, const uint64_t* pl, int np, RepFn rep, bool targets,
+                      TRepFn trep) {
+  const BindHdr& h = *x.h;
+  const int nt = targets ? h.tgt_cnt : 0;
+  auto trank = [&](int j) { return (uint32_t)x.bv->ipool[h.tgt_off + 2 * j]; };
+  int32_t mine = 0;
+  for (int i = B.tid(); i < np; i += B.nth())
+    if (rep((uint32_t)(pl[i] >> 32), (int64_t)(uint32_t)pl[i]) > 0) mine++;
+  for (int j = B.tid(); j < nt; j += B.nth())
+    if (mask_test(x.frow, (int)trank(j)) && trep(trank(j)) > 0) mine++;
+  int32_t tot;
+  const int32_t off = B.excl_scan(mine, &tot);
+  unsigned long long base = 0;
+  if (B.tid() == 0) {
+    base = tot > 0 ? kp_atomic_add(x.sink.counter, (unsigned long long)tot) : 0ull;
+    x.sink.status[x.b] = KP_STATUS_OK;
+    x.sink.err[x.b] = KP_ERR_NONE;
+    x.sink.arg[x.b] = 0;
+    x.sink.start[x.b] = base;
+    x.sink.count[x.b] = (uint32_t)tot;
+  }
+  uint64_t o = (uint64_t)B.bcast(base) + (uint64_t)off;
+  for (int i = B.tid(); i < np; i += B.nth()) {
+    const uint32_t rk = (uint32_t)(pl[i] >> 32);
+    const int32_t r = rep(rk, (int64_t)(uint32_t)pl[i]);
+    if (r > 0) {
+      x.sink.out_idx[o] = x.s->perm[rk];
+      x.sink.out_rep[o] = r;
+      o++;
+    }
+  }
+  for (int j = B.tid(); j < nt; j += B.nth()) {
+    const uint32_t rk = trank(j);
+    if (!mask_test(x.frow, (int)rk)) continue;
+    const int32_t r = trep(rk);
+    if (r > 0) {
+      x.sink.out_idx[o] = x.s->perm[rk];
+      x.sink.out_rep[o] = r;
+      o++;
+    }
+  }
 }
 
 // dynamicScaleDown (division_algorithm.go:103-119) for SEL_ALL bindings: the
@@ -468,6 +500,27 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
   };
   WebRes w = webster_par(B, parties, target, desc, ss);
   KP_STAMP(x, 4);
+  if (w.mode == 2 && w.compact && !prop) {
+    // Only parties take seats, and every party with a seat is in Webster's compacted
+    // list (votes >= Lb <= t*): emit from it, plus the prior targets outside it
+    // whose merged replicas are > 0 (MergeTargetClusters), instead of walking every
+    // candidate. Same multiset as the full walk below.
+    auto in_list = [&](uint32_t rk) {
+      const int32_t v0 = x.erow[rk];
+      const int64_t v = vote32(rk, v0);
+      return member(rk, v, v0) && v >= w.Lb;
+    };
+    emit_lists(
+        B, x, w.pl, w.np,
+        [&](uint32_t rk, int64_t v) {
+          int32_t r = web_seats(w, v, rk);
+          if (merge && tgt(rk)) r = add32(r, sched_rep_of(x, rk));
+          return r;
+        },
+        merge, [&](uint32_t rk) { return in_list(rk) ? (int32_t)0 : sched_rep_of(x, rk); });
+    KP_STAMP(x, 5);
+    return SLOW_NONE;
+  }
   emit_each(
       B, x, cs,
       [&](uint32_t rk, int32_t v0) {

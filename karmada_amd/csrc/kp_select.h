@@ -631,6 +631,12 @@ struct WebRes {
   uint64_t tie;   // tie-key threshold (inclusive)
   int32_t N;
   bool desc;
+  // mode 2 with compact: every party with a seat is among the np entries of pl
+  // ((rank << 32) | votes, votes >= Lb); the list stays valid after the return.
+  bool compact = false;
+  int32_t np = 0;
+  int64_t Lb = 1;
+  const uint64_t* pl = nullptr;
 };
 KP_HD inline uint64_t tie_key(int64_t base, uint32_t rank, bool desc) {
   return ((uint64_t)base << kRankBits) | (desc ? (uint64_t)(kRankMask - rank) : (uint64_t)rank);
@@ -891,6 +897,10 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     tstar = bitsd(rank_select(B, sc.buf, E, (int64_t)N - chi, true, (uint64_t*)sc.whist));
   }
   r.t = tstar;
+  r.compact = compact;
+  r.np = np;
+  r.Lb = Lb;
+  r.pl = pl;
   KP_STAMPD(sc.dbg, 12);
   // seats strictly above t*, then the tie group at t* ordered by (k asc, name)
   int64_t S = 0, T = 0;
@@ -934,7 +944,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     r.tie = tlo;
   }
   KP_STAMPD(sc.dbg, 14);
-  B.sync();  // pl / buf / whist are free again for the caller
+  B.sync();  // buf[0, 64) / whist are free again for the caller; pl stays
   return r;
 }
 
