@@ -31,6 +31,8 @@
  *                                      for the GeneralEstimator
  *                                      (pkg/estimator/client/interface.go:39-71,
  *                                       pkg/estimator/client/general.go:57-108)
+ *        kp_max_available_component_sets <- ReplicaEstimator.MaxAvailableComponentSets
+ *                                      (general.go:154-292)
  *        kp_snapshot_create         <- cache.Cache.Snapshot (pkg/scheduler/cache/cache.go:124-139)
  *        kp_schedule_affinities     <- Scheduler.scheduleResourceBindingWithClusterAffinities
  *                                      (pkg/scheduler/scheduler.go:584-585,618-684)
@@ -48,7 +50,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 6
+#define KP_ABI_VERSION 7
 
 /* ------------------------------------------------------------------------- */
 /* Object model                                                              */
@@ -234,6 +236,18 @@ typedef struct kp_cluster {
   uint32_t n_allocatable_modelings;
 } kp_cluster;
 
+/* workv1alpha2.Component (pkg/apis/work/v1alpha2/binding_types.go): one pod template
+ * of a multi-template workload; ReplicaRequirements.ResourceRequest only (the
+ * NodeClaim never filters the estimator's model nodes, which carry no Node object,
+ * scheduling_simulator_components.go:149-153). */
+typedef struct kp_component {
+  kp_str name;
+  int32_t replicas;
+  uint8_t has_replica_requirements;
+  const kp_resource* resource_request;
+  uint32_t n_resource_request;
+} kp_component;
+
 /* In-tree plugin names (pkg/scheduler/framework/plugins/registry.go:33-50). */
 enum {
   KP_PLUGIN_API_ENABLEMENT = 1u << 0,
@@ -250,6 +264,7 @@ enum {
 typedef struct kp_options {
   uint8_t enable_empty_workload_propagation;   /* --enable-empty-workload-propagation */
   uint8_t customized_cluster_resource_modeling; /* feature gate, default on */
+  uint8_t multiple_pod_templates_scheduling;    /* feature gate MultiplePodTemplatesScheduling, alpha, default off */
   uint32_t enabled_plugins;                     /* KP_PLUGIN_* bitmask (--plugins) */
 } kp_options;
 
@@ -432,6 +447,21 @@ int kp_score_batch(kp_engine* e, kp_batch* b, int64_t* out_scores);
  * estimator answer per cluster in input order (general.go:57-64). */
 int kp_max_available_replicas(kp_engine* e, kp_batch* b, uint64_t binding,
                               const uint32_t* cluster_idx, uint64_t n, int32_t* out);
+
+/* ReplicaEstimator.MaxAvailableComponentSets for the GeneralEstimator
+ * (estimator/client/general.go:154-292): for one component list (one set = every
+ * component's Replicas), the number of complete sets each cluster cluster_idx[i]
+ * (caller order) holds, written to out[i]: the pod and resource-summary bounds
+ * (quantityAsInt64 by each Quantity's format), then, with the
+ * CustomizedClusterResourceModeling gate and models, the first-fit simulation over
+ * the model-grade nodes (SchedulingSimulator.SimulateScheduling,
+ * scheduling_simulator_components.go:51-131). Assumed workloads are empty
+ * (SchedulingOvercommitProtection off). KP_ENOTSUP when the snapshot's options
+ * have the MultiplePodTemplatesScheduling gate off (the scheduler then never calls
+ * it, core/util.go:113-118), or when a cluster's simulation exceeds the device
+ * run capacity (kp_last_error says which). */
+int kp_max_available_component_sets(kp_engine* e, const kp_snapshot* s, const kp_component* components,
+                                    uint32_t n_components, const uint32_t* cluster_idx, uint64_t n, int32_t* out);
 
 /* Last schedule call's stage timings. */
 int kp_last_stage_times(const kp_engine* e, kp_stage_times* out);

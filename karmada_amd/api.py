@@ -125,9 +125,15 @@ class kp_cluster(C.Structure):
     ]
 
 
+class kp_component(C.Structure):
+    _fields_ = [("name", kp_str), ("replicas", i32), ("has_replica_requirements", u8),
+                ("resource_request", C.POINTER(kp_resource)), ("n_resource_request", u32)]
+
+
 class kp_options(C.Structure):
     _fields_ = [("enable_empty_workload_propagation", u8),
                 ("customized_cluster_resource_modeling", u8),
+                ("multiple_pod_templates_scheduling", u8),
                 ("enabled_plugins", u32)]
 
 
@@ -211,8 +217,11 @@ ERR_NAMES = {
 }
 
 
-def options(empty_workload_propagation=False, models_gate=True, plugins=PLUGIN_ALL) -> kp_options:
-    return kp_options(int(empty_workload_propagation), int(models_gate), plugins)
+def options(empty_workload_propagation=False, models_gate=True, plugins=PLUGIN_ALL,
+            multi_templates=False) -> kp_options:
+    return kp_options(enable_empty_workload_propagation=int(empty_workload_propagation),
+                      customized_cluster_resource_modeling=int(models_gate),
+                      multiple_pod_templates_scheduling=int(multi_templates), enabled_plugins=plugins)
 
 
 class World:
@@ -241,6 +250,16 @@ class World:
 
     def resources(self, rl: Optional[Dict[str, str]]):
         return self.arr(kp_resource, [kp_resource(self.s(k), self.s(str(v))) for k, v in (rl or {}).items()])
+
+    def components(self, comps):
+        """[{name, replicas, replicaRequirements?: {resourceRequest}}] -> (kp_component array, n)."""
+        out = []
+        for c in comps or []:
+            rr = c.get("replicaRequirements")
+            ra, nr = self.resources((rr or {}).get("resourceRequest"))
+            out.append(kp_component(self.s(c.get("name", "")), int(c.get("replicas", 0)), 1 if rr is not None else 0,
+                                    ra, nr))
+        return self.arr(kp_component, out)
 
     def requirements(self, exprs):
         out = []

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "kp_dev.h"
+#include "kp_sets.h"
 #include "kp_kernels.h"
 
 namespace kp {
@@ -170,6 +171,12 @@ int region_groups(stream_t, const RegionOut* rout, const int32_t* rstat, const B
     if (k == kGroupsHost) ++*nhost;
     rnsel[j] = k;
   }
+  return 0;
+}
+
+int component_sets(stream_t, const SnapView& s, const SetsArgs* A, const int32_t* ranks, const int64_t* off,
+                   uint64_t n, int64_t* scratch, int32_t* out) {
+  for (uint64_t i = 0; i < n; i++) body_sets(s, A, ranks, off, i, scratch, out);
   return 0;
 }
 

@@ -24,6 +24,7 @@
 #include "kp_launch.h"
 #include "kp_paths.h"
 #include "kp_pdq.h"
+#include "kp_sets.h"
 
 using namespace kp;
 
@@ -132,6 +133,7 @@ struct kp_snapshot {
   std::vector<int32_t> provider, region, region_idx, zone_off, zone_ids, label_val, taint_off, taint_key, taint_val,
       taint_eff, mgrp_off, mgrp_tid, mg_tid, mg_cnt;
   std::vector<int64_t> provider_int, region_int, allowed, avail, mgrp_cnt, tmpl;
+  std::vector<int64_t> qa;  // [R][Cp] quantityAsInt64 availability, kQaAbsent where not allocatable
   std::vector<uint64_t> api_bits;
   Arena dev;
   SnapView view{};
@@ -224,6 +226,7 @@ struct ClusterRow {
   std::vector<int32_t> gvks;
   int64_t allowed = 0;
   std::vector<std::pair<int32_t, int64_t>> avail;   // (resource id, available)
+  std::vector<std::pair<int32_t, int64_t>> qa;      // (resource id, quantityAsInt64 availability)
   std::vector<std::pair<int32_t, int64_t>> groups;  // (template id, node count), grades ascending
 };
 
@@ -288,6 +291,11 @@ int pack_row(kp_engine* e, kp_snapshot* s, const kp_cluster& c, std::map<std::ve
       int64_t v = k8s::value(q);
       int64_t d = v <= 0 ? 0 : (kv.first == "cpu" ? k8s::milli(q) : v);
       w.avail.push_back({s->res.add(kv.first), d});
+      // availableResourceMap (general.go:403-415): Sub keeps the allocatable's format
+      k8s::Qty a = kv.second;
+      if ((x = ad.find(kv.first)) != ad.end()) k8s::qsub(a, x->second);
+      if ((x = ag.find(kv.first)) != ag.end()) k8s::qsub(a, x->second);
+      w.qa.push_back({s->res.add(kv.first), k8s::as_int64(a)});
     }
     // buildModelNodes (general.go:296-361)
     if (s->opts.customized_cluster_resource_modeling && c.n_allocatable_modelings > 0 && c.n_resource_models > 0) {
@@ -369,6 +377,7 @@ void apply_rows(kp_snapshot* s, const std::vector<ClusterRow>& rows,
   s->api_bits.assign((size_t)std::max(AW, 1) * Cp, 0);
   s->allowed.assign(Cp, 0);
   s->avail.assign((size_t)std::max(R, 1) * Cp, 0);
+  s->qa.assign((size_t)std::max(R, 1) * Cp, kQaAbsent);
   s->zone_off.assign(C + 1, 0);
   s->taint_off.assign(C + 1, 0);
   s->mgrp_off.assign(C + 1, 0);
@@ -398,6 +407,7 @@ void apply_rows(kp_snapshot* s, const std::vector<ClusterRow>& rows,
     for (int32_t g : w.gvks) s->api_bits[(size_t)(g >> 6) * Cp + r] |= 1ull << (g & 63);
     s->allowed[r] = w.allowed;
     for (auto& kv : w.avail) s->avail[(size_t)kv.first * Cp + r] = kv.second;
+    for (auto& kv : w.qa) s->qa[(size_t)kv.first * Cp + r] = kv.second;
     for (auto& g : w.groups) {
       s->mgrp_tid.push_back(g.first);
       s->mgrp_cnt.push_back(g.second);
@@ -430,7 +440,7 @@ void apply_rows(kp_snapshot* s, const std::vector<ClusterRow>& rows,
 }
 
 int build_snapshot(kp_engine* e, const kp_cluster* cl, uint64_t n, const kp_options* o, kp_snapshot* s) {
-  s->opts = o ? *o : kp_options{0, 1, KP_PLUGIN_ALL};
+  s->opts = o ? *o : kp_options{0, 1, 0, KP_PLUGIN_ALL};
   if (n > (uint64_t)kMaxClusters) {
     e->err = "too many clusters";
     return KP_ENOTSUP;
@@ -508,7 +518,7 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
   Arena& a = s->dev;
   uint32_t *d_flags, *d_perm;
   int32_t *d_prov, *d_reg, *d_regidx, *d_zoff, *d_zid, *d_lbl, *d_toff, *d_tk, *d_tv, *d_te, *d_mtid, *d_mcnt;
-  int64_t *d_pint, *d_rint, *d_allowed, *d_avail, *d_tmpl;
+  int64_t *d_pint, *d_rint, *d_allowed, *d_avail, *d_tmpl, *d_qa;
   uint64_t* d_api;
   // taint lists deduplicated: one TaintToleration answer per distinct list and binding
   std::vector<int32_t> tset(Cp, 0), trep;
@@ -569,6 +579,7 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
   a.add(&d_rint, Cp);
   a.add(&d_allowed, Cp);
   a.add(&d_avail, s->avail.size());
+  a.add(&d_qa, s->qa.size());
   a.add(&d_tmpl, s->tmpl.size());
   a.add(&d_api, s->api_bits.size());
   HIPCHK(a.alloc());
@@ -596,6 +607,7 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
   HIPCHK(up(d_rint, s->region_int.data(), 8 * Cp));
   HIPCHK(up(d_allowed, s->allowed.data(), 8 * Cp));
   HIPCHK(up(d_avail, s->avail.data(), 8 * s->avail.size()));
+  HIPCHK(up(d_qa, s->qa.data(), 8 * s->qa.size()));
   HIPCHK(up(d_tmpl, s->tmpl.data(), 8 * s->tmpl.size()));
   HIPCHK(up(d_api, s->api_bits.data(), 8 * s->api_bits.size()));
   HIPCHK(dev::sync(e->stream));
@@ -619,6 +631,7 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
   v.api_bits = d_api;
   v.allowed = d_allowed;
   v.avail = d_avail;
+  v.qa = d_qa;
   v.kmax = kmax;
   v.mg_tid = d_mtid;
   v.mg_cnt = d_mcnt;
@@ -1197,7 +1210,7 @@ int snapshot_est_kind(const kp_snapshot* s) {
 // Packed-snapshot bytes: pack once on one rank, broadcast the bytes, import on
 // the others. Host-endian; same engine build on every rank.
 namespace {
-const char kSnapMagic[8] = {'K', 'P', 'S', 'N', 'A', 'P', '0', '2'};
+const char kSnapMagic[8] = {'K', 'P', 'S', 'N', 'A', 'P', '0', '3'};
 struct Wr {
   std::vector<unsigned char>& b;
   void raw(const void* p, size_t n) { b.insert(b.end(), (const unsigned char*)p, (const unsigned char*)p + n); }
@@ -1289,7 +1302,7 @@ bool snapshot_consistent(const kp_snapshot* s) {
                    s->provider_int.size(), s->region_int.size(), s->allowed.size()})
     if (n != Cp) return false;
   if (s->label_val.size() != (size_t)std::max(K, 1) * Cp || s->api_bits.size() != (size_t)std::max(AW, 1) * Cp ||
-      s->avail.size() != (size_t)std::max(R, 1) * Cp || s->tmpl.size() != (size_t)std::max(T, 1) * std::max(R, 1) ||
+      s->avail.size() != (size_t)std::max(R, 1) * Cp || s->qa.size() != (size_t)std::max(R, 1) * Cp || s->tmpl.size() != (size_t)std::max(T, 1) * std::max(R, 1) ||
       s->mg_tid.size() != (size_t)std::max(km, 1) * Cp || s->mg_cnt.size() != s->mg_tid.size())
     return false;
   if (s->taint_val.size() != s->taint_key.size() || s->taint_eff.size() != s->taint_key.size() ||
@@ -1410,6 +1423,8 @@ ClusterRow row_of(const kp_snapshot* s, int r) {
   for (int j = 0; j < R; j++) {
     const int64_t a = s->avail[(size_t)j * Cp + r];
     if (a != 0) w.avail.push_back({j, a});
+    const int64_t q = s->qa[(size_t)j * Cp + r];
+    if (q != kQaAbsent) w.qa.push_back({j, q});
   }
   for (int g = s->mgrp_off[r]; g < s->mgrp_off[r + 1]; g++) w.groups.push_back({s->mgrp_tid[g], s->mgrp_cnt[g]});
   return w;
@@ -1521,6 +1536,7 @@ int kp_snapshot_export(const kp_snapshot* cs, const void** bytes, uint64_t* n_by
   w.vec(s->region_int);
   w.vec(s->allowed);
   w.vec(s->avail);
+  w.vec(s->qa);
   w.vec(s->tmpl);
   w.vec(s->api_bits);
   *bytes = s->blob.data();
@@ -1578,6 +1594,7 @@ int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_sna
   s->region_int = r.vec<int64_t>();
   s->allowed = r.vec<int64_t>();
   s->avail = r.vec<int64_t>();
+  s->qa = r.vec<int64_t>();
   s->tmpl = r.vec<int64_t>();
   s->api_bits = r.vec<uint64_t>();
   if (!r.ok || r.p != r.end || !snapshot_consistent(s)) {
@@ -2123,6 +2140,107 @@ int kp_filter_reasons(kp_engine* e, kp_batch* bt, uint32_t* out_reasons) {
   if (rc) return rc;
   for (int b = 0; b < bt->B; b++)
     for (int r = 0; r < s->C; r++) out_reasons[(size_t)b * s->C + s->perm[r]] = h[(size_t)b * s->C + r];
+  return KP_OK;
+}
+
+int kp_max_available_component_sets(kp_engine* e, const kp_snapshot* sc, const kp_component* comps, uint32_t K,
+                                    const uint32_t* cluster_idx, uint64_t n, int32_t* out) {
+  if (!e || !sc || (K && !comps) || (n && (!cluster_idx || !out))) return KP_EINVAL;
+  (void)dev::set_device(e->device);
+  kp_snapshot* s = const_cast<kp_snapshot*>(sc);
+  if (!s->opts.multiple_pod_templates_scheduling) {
+    e->err = "MaxAvailableComponentSets: the MultiplePodTemplatesScheduling gate is off";
+    return KP_ENOTSUP;
+  }
+  if (K > (uint32_t)kSetsComp) {
+    e->err = "MaxAvailableComponentSets: more than 16 components";
+    return KP_ENOTSUP;
+  }
+  SetsArgs A;
+  memset(&A, 0, sizeof(A));
+  A.K = (int32_t)K;
+  std::map<std::string, int64_t> per;       // perSetRequirement (general.go:389-401), wrapping int64
+  std::vector<std::map<std::string, int64_t>> nr(K);  // util.NewResource of each request
+  std::vector<std::string> slots;
+  int64_t pps = 0;
+  for (uint32_t k = 0; k < K; k++) {
+    A.replicas[k] = comps[k].replicas;
+    pps += comps[k].replicas;  // podsInSet
+    if (!comps[k].has_replica_requirements) continue;
+    QtyMap rq;
+    if (!qmap(comps[k].resource_request, comps[k].n_resource_request, &rq)) {
+      e->err = "MaxAvailableComponentSets: unparsable quantity";
+      return KP_EINVAL;
+    }
+    for (auto& kv : rq) {
+      const std::string& nm = kv.first;
+      per[nm] = (int64_t)((uint64_t)per[nm] + (uint64_t)k8s::as_int64(kv.second) * (uint64_t)(int64_t)comps[k].replicas);
+      int64_t v;
+      if (nm == "cpu") v = k8s::milli(kv.second);
+      else if (nm == "memory" || nm == "ephemeral-storage" || (nm != "pods" && k8s::scalar_resource(nm)))
+        v = k8s::value(kv.second);
+      else continue;  // pods: requiredPerReplica.AllowedPodNumber = 1
+      nr[k][nm] += v;
+      if (std::find(slots.begin(), slots.end(), nm) == slots.end()) slots.push_back(nm);
+    }
+  }
+  if (slots.size() + 1 > (size_t)kSetsSlots || per.size() > (size_t)kSetsPer) {
+    e->err = "MaxAvailableComponentSets: too many distinct resources";
+    return KP_ENOTSUP;
+  }
+  A.NS = (int32_t)slots.size() + 1;
+  for (size_t j = 0; j < slots.size(); j++) A.slot_rid[j] = s->res.get(slots[j]);
+  A.slot_rid[slots.size()] = -2;  // pods
+  for (uint32_t k = 0; k < K; k++) {
+    for (size_t j = 0; j < slots.size(); j++) {
+      auto it = nr[k].find(slots[j]);
+      const int64_t v = it == nr[k].end() ? 0 : it->second;
+      A.req[k][j] = v;
+      A.pos[k][j] = v > 0 ? v : 0;
+    }
+    A.req[k][slots.size()] = 1;
+    A.pos[k][slots.size()] = 1;
+  }
+  A.pods_per_set = pps;
+  for (auto& kv : per) {
+    A.per_rid[A.nper] = s->res.get(kv.first);
+    A.per_req[A.nper] = kv.second;
+    A.per_nonzero |= kv.second != 0 ? 1 : 0;
+    A.nper++;
+  }
+  std::vector<int32_t> ranks(n);
+  std::vector<int64_t> off(n + 1, 0);  // runs per cluster: its model node count (a run holds >= 1 node)
+  for (uint64_t i = 0; i < n; i++) {
+    if (cluster_idx[i] >= (uint32_t)s->C) return KP_EINVAL;
+    const int r = s->inv[cluster_idx[i]];
+    ranks[i] = r;
+    int64_t nodes = 0;
+    for (int g = s->mgrp_off[r]; g < s->mgrp_off[r + 1]; g++) nodes += s->mgrp_cnt[g];
+    off[i + 1] = off[i] + std::max<int64_t>(1, std::min<int64_t>(nodes, kSetsRunsMax));
+  }
+  if (n == 0) return KP_OK;
+  Arena a;
+  SetsArgs* dA;
+  int32_t *dr, *dout;
+  int64_t *doff, *scratch;
+  a.add(&dA, 1);
+  a.add(&dr, n);
+  a.add(&doff, n + 1);
+  a.add(&dout, n);
+  a.add(&scratch, (size_t)off[n] * (1 + kSetsSlots));
+  HIPCHK(a.alloc());
+  HIPCHK(dev::h2d(dA, &A, sizeof(A), e->stream));
+  HIPCHK(dev::h2d(dr, ranks.data(), 4 * n, e->stream));
+  HIPCHK(dev::h2d(doff, off.data(), 8 * (n + 1), e->stream));
+  HIPCHK(dev::component_sets(e->stream, s->view, dA, dr, doff, n, scratch, dout));
+  HIPCHK(dev::d2h(out, dout, 4 * n, e->stream));
+  HIPCHK(dev::sync(e->stream));
+  for (uint64_t i = 0; i < n; i++)
+    if (out[i] == kSetsOverflow) {
+      e->err = "MaxAvailableComponentSets: cluster " + s->names[ranks[i]] + " needs more than " +
+               std::to_string(kSetsRunsMax) + " node runs";
+      return KP_ENOTSUP;
+    }
   return KP_OK;
 }
 

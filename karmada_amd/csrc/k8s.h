@@ -18,6 +18,7 @@ typedef __int128 i128;
 // Exact quantity value in units of 1e-9 (ParseQuantity rounds to Nano away from zero).
 struct Qty {
   i128 nano = 0;
+  int fmt = 0;  // resource.Format: 0 DecimalSI, 1 BinarySI, 2 DecimalExponent
 };
 
 inline i128 p10(int k) {
@@ -31,11 +32,20 @@ inline int64_t round_away(i128 nano, i128 div) {
 }
 inline int64_t value(const Qty& q) { return round_away(q.nano, (i128)1000000000); }
 inline int64_t milli(const Qty& q) { return round_away(q.nano, (i128)1000000); }
+// quantityAsInt64 (estimator/client/general.go:417-427): DecimalSI/DecimalExponent ->
+// MilliValue, BinarySI -> Value
+inline int64_t as_int64(const Qty& q) { return q.fmt == 1 ? value(q) : milli(q); }
+// Quantity.Sub: a zero receiver takes the subtrahend's format
+inline void qsub(Qty& a, const Qty& y) {
+  if (a.nano == 0) a.fmt = y.fmt;
+  a.nano -= y.nano;
+}
 
 inline bool parse_quantity(const std::string& str, Qty* out) {
   if (str.empty()) return false;
   if (str == "0") {
     out->nano = 0;
+    out->fmt = 0;
     return true;
   }
   size_t pos = 0, end = str.size();
@@ -84,6 +94,7 @@ inline bool parse_quantity(const std::string& str, Qty* out) {
       binary = true;
       found = true;
     }
+  int fmt = binary ? 1 : 0;
   if (!found) {
     if (suf.size() > 1 && (suf[0] == 'e' || suf[0] == 'E')) {
       const char* p = suf.c_str() + 1;
@@ -91,6 +102,7 @@ inline bool parse_quantity(const std::string& str, Qty* out) {
       long long v = strtoll(p, &e, 10);
       if (e == p || *e) return false;
       ex = (int32_t)v;
+      fmt = 2;
     } else {
       return false;
     }
@@ -125,6 +137,7 @@ inline bool parse_quantity(const std::string& str, Qty* out) {
   }
   if (nano > lim) return false;
   out->nano = positive ? nano : -nano;
+  out->fmt = fmt;
   return true;
 }
 

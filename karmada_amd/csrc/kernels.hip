@@ -16,6 +16,7 @@
 
 #include "kp_dev.h"
 #include "kp_kernels.h"
+#include "kp_sets.h"
 
 using namespace kp;
 
@@ -113,6 +114,11 @@ extern "C" __global__ void __launch_bounds__(kSlowBlock) k_slow(KArgs a, unsigne
                                                                 int cap, int lds_area, int lds_sort) {
   KP_SMEM;
   body_slow(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, (int)gridDim.x, smem, a, scratch, slot_bytes, cap, lds_area, lds_sort);
+}
+extern "C" __global__ void __launch_bounds__(64) k_sets(SnapView s, const SetsArgs* A, const int32_t* ranks, const int64_t* off,
+                                                       uint64_t n, int64_t* scratch, int32_t* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) body_sets(s, A, ranks, off, i, scratch, out);
 }
 extern "C" __global__ void __launch_bounds__(256) k_reasons(SnapView s, BatchView bv, uint64_t n, uint32_t* out) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
@@ -281,6 +287,13 @@ int region_groups(stream_t st, const RegionOut* rout, const int32_t* rstat, cons
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_region_groups, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)st, rout, rstat, hdr, list, n,
                      R, rsel, rnsel, nhost);
+  return chk(hipGetLastError());
+}
+
+int component_sets(stream_t st, const SnapView& s, const SetsArgs* A, const int32_t* ranks, const int64_t* off,
+                   uint64_t n, int64_t* scratch, int32_t* out) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_sets, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)st, s, A, ranks, off, n, scratch, out);
   return chk(hipGetLastError());
 }
 

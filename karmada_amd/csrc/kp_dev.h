@@ -12,6 +12,7 @@
 #include "kp_launch.h"
 
 namespace kp {
+struct SetsArgs;
 namespace dev {
 
 typedef void* stream_t;
@@ -57,6 +58,10 @@ int pair_list(stream_t st, const SnapView& s, const BatchView& bv, const int32_t
 // step writes them; *nhost counts the bindings left to the host (kGroupsHost).
 int region_groups(stream_t st, const RegionOut* rout, const int32_t* rstat, const BindHdr* hdr, const int32_t* list,
                   int n, int R, int32_t* rsel, int32_t* rnsel, uint32_t* nhost);
+// kp_max_available_component_sets: out[i] = sets_one for cluster rank ranks[i]
+// (A, ranks and off in device memory; cluster i's runs at scratch[off[i], off[i+1])).
+int component_sets(stream_t st, const SnapView& s, const SetsArgs* A, const int32_t* ranks, const int64_t* off,
+                   uint64_t n, int64_t* scratch, int32_t* out);
 // kp_filter_reasons: out[b * C + r] = pair_reason of binding b, cluster rank r.
 int reasons(stream_t st, const SnapView& s, const BatchView& bv, uint32_t* out);
 int compact(stream_t st, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,

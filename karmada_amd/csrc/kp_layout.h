@@ -128,6 +128,7 @@ struct alignas(16) BindHdr {
 };
 
 // ---- snapshot device view -----------------------------------------------------
+constexpr int64_t kQaAbsent = INT64_MIN;
 struct SnapView {
   int32_t C, Cp, W;              // clusters, padded clusters, ceil(C/64)
   int32_t n_label_keys, api_words, n_res, n_tmpl, n_regions;
@@ -151,6 +152,8 @@ struct SnapView {
   const uint64_t* api_bits;      // [api_words][Cp]
   const int64_t* allowed;        // [Cp] getAllowedPodNumber
   const int64_t* avail;          // [n_res][Cp] summary path available (milli for cpu), <=0 -> 0
+  const int64_t* qa;             // [n_res][Cp] quantityAsInt64(allocatable - allocated - allocating)
+                                 // (general.go:403-427), kQaAbsent where not allocatable
   const int32_t* mg_tid;         // [kmax][Cp] model node group: template id (grade ascending)
   const int32_t* mg_cnt;         // [kmax][Cp] node count, clamped to MaxInt32 (0 = no group)
   const int64_t* tmpl;           // [n_tmpl][n_res] model template values

@@ -25,7 +25,7 @@ from karmada_amd import api
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libkp.so")
-KP_ABI_VERSION = 6
+KP_ABI_VERSION = 7
 
 _LIBS = {}
 
@@ -34,7 +34,8 @@ EXPORTS = (
     "kp_abi_version", "kp_engine_create", "kp_engine_destroy", "kp_last_error", "kp_snapshot_create",
     "kp_snapshot_destroy", "kp_snapshot_export", "kp_snapshot_import", "kp_snapshot_update", "kp_batch_create",
     "kp_batch_destroy",
-    "kp_schedule_batch", "kp_schedule_affinities", "kp_filter_batch", "kp_filter_reasons", "kp_score_batch", "kp_max_available_replicas", "kp_last_stage_times",
+    "kp_schedule_batch", "kp_schedule_affinities", "kp_filter_batch", "kp_filter_reasons", "kp_score_batch", "kp_max_available_replicas", "kp_max_available_component_sets",
+    "kp_last_stage_times",
 )
 
 KP_OK, KP_EINVAL, KP_ENOMEM, KP_EDEVICE, KP_ENOTSUP, KP_ESTATE = 0, -1, -2, -3, -4, -5
@@ -71,6 +72,8 @@ def load_library(path: str = LIB_PATH):
     L.kp_filter_reasons.argtypes = [vp, vp, C.POINTER(C.c_uint32)]
     L.kp_max_available_replicas.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint32), C.c_uint64,
                                             C.POINTER(C.c_int32)]
+    L.kp_max_available_component_sets.argtypes = [vp, vp, C.POINTER(api.kp_component), C.c_uint32,
+                                                  C.POINTER(C.c_uint32), C.c_uint64, C.POINTER(C.c_int32)]
     L.kp_last_stage_times.argtypes = [vp, C.POINTER(api.kp_stage_times)]
     L.kp_snapshot_export.argtypes = [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
     L.kp_snapshot_import.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(vp)]
@@ -330,6 +333,19 @@ class GenericScheduler:
         out = [[int(s[i * C_ + c]) for c in range(C_)] for i in range(b.n)]
         b.close()
         return out
+
+    def max_available_component_sets(self, components: Sequence[dict], clusters: Sequence[str]) -> List[int]:
+        """GeneralEstimator.MaxAvailableComponentSets (general.go:154-162) for one
+        component list; raises EngineError (KP_ENOTSUP) with the gate off."""
+        eng = self.snapshot.engine
+        w = api.World()
+        ca, nc = w.components(components)
+        idx = {n: i for i, n in enumerate(self.snapshot.names)}
+        ci = (C.c_uint32 * max(1, len(clusters)))(*[idx[n] for n in clusters])
+        out = (C.c_int32 * max(1, len(clusters)))()
+        eng._check(eng.L.kp_max_available_component_sets(eng.h, self.snapshot.h, ca, nc, ci, len(clusters), out),
+                   "kp_max_available_component_sets")
+        return [int(out[i]) for i in range(len(clusters))]
 
     def max_available_replicas(self, binding: dict, clusters: Sequence[str]) -> List[int]:
         """GeneralEstimator.MaxAvailableReplicas for one binding's request."""

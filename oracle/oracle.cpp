@@ -47,6 +47,7 @@ inline i64 mul64(i64 a, i64 b) { return (i64)((uint64_t)a * (uint64_t)b); }
 // ===========================================================================
 struct Quantity {
   i128 nano = 0;
+  int fmt = 0;  // resource.Format: 0 DecimalSI, 1 BinarySI, 2 DecimalExponent (quantity.go:113-119)
 };
 
 i128 pow10_128(int k) {
@@ -69,8 +70,9 @@ const i128 kQMax = (i128)1 << 100;  // beyond this we refuse (never produced by 
 // ParseQuantity (quantity.go:161-394).
 bool ParseQuantity(const string& str, Quantity* out) {
   if (str.empty()) return false;
-  if (str == "0") {
+  if (str == "0") {  // quantity.go: the "0" fast path is DecimalSI
     out->nano = 0;
+    out->fmt = 0;
     return true;
   }
   bool positive = true;
@@ -161,6 +163,7 @@ bool ParseQuantity(const string& str, Quantity* out) {
   int base = 10;
   i64 exponent = 0;
   bool binary = false;
+  int fmt = 0;
   static const std::map<string, int> dec = {{"n", -9}, {"u", -6}, {"m", -3}, {"", 0},  {"k", 3},
                                             {"M", 6},  {"G", 9},  {"T", 12}, {"P", 15}, {"E", 18}};
   static const std::map<string, int> bin = {{"Ki", 10}, {"Mi", 20}, {"Gi", 30},
@@ -174,6 +177,7 @@ bool ParseQuantity(const string& str, Quantity* out) {
       base = 2;
       exponent = b->second;
       binary = true;
+      fmt = 1;
     } else if (suf.size() > 1 && (suf[0] == 'E' || suf[0] == 'e')) {
       // strconv.ParseInt(suffix[1:], 10, 64), then int32(parsed)
       const char* p = suf.c_str() + 1;
@@ -183,6 +187,7 @@ bool ParseQuantity(const string& str, Quantity* out) {
       if (errno != 0 || *endp != 0 || endp == p) return false;
       if (p[0] == ' ') return false;
       exponent = (i32)v;
+      fmt = 2;
     } else {
       return false;  // ErrSuffix
     }
@@ -235,6 +240,7 @@ bool ParseQuantity(const string& str, Quantity* out) {
   }
   if (nano > kQMax) return false;
   out->nano = positive ? nano : -nano;
+  out->fmt = fmt;
   return true;
 }
 
@@ -1089,6 +1095,201 @@ i32 maxAvailableReplicas(const Cluster& c, const Binding& b, const Options& o, i
   i64 num = getMaximumReplicasBasedOnClusterSummary(c, b.request);
   if (num < maximum) maximum = num;
   return (i32)maximum;
+}
+
+// ===========================================================================
+// GeneralEstimator.MaxAvailableComponentSets (general.go:154-292), assumed
+// workloads empty (SchedulingOvercommitProtection off).
+// ===========================================================================
+struct Component {
+  i32 replicas = 0;
+  bool has_rr = false;
+  ResourceList request;
+};
+
+// quantityAsInt64 (general.go:417-427): DecimalSI / DecimalExponent -> MilliValue,
+// BinarySI -> Value.
+i64 quantityAsInt64(const Quantity& q) { return q.fmt == 1 ? QValue(q) : QMilli(q); }
+// Quantity.Sub: a zero receiver takes the subtrahend's format (quantity.go Sub).
+void QSub(Quantity& a, const Quantity& y) {
+  if (a.nano == 0) a.fmt = y.fmt;
+  a.nano -= y.nano;
+}
+i64 wrapmul(i64 a, i64 b) { return (i64)((uint64_t)a * (uint64_t)b); }
+i32 toI32(i64 v) { return (i32)(uint32_t)(uint64_t)v; }  // int32(x) of an int64
+
+// util.Resource of a per-replica request (requiredPerReplica, AllowedPodNumber = 1)
+// and the positive part MaxDivided reads (Resource.ResourceList keeps fields > 0).
+void replicaRequest(const Component& k, Resource* req, Resource* pos) {
+  *req = Resource();
+  if (k.has_rr) req->Add(k.request);
+  req->AllowedPodNumber = 1;
+  *pos = Resource();
+  pos->MilliCPU = req->MilliCPU > 0 ? req->MilliCPU : 0;
+  pos->Memory = req->Memory > 0 ? req->Memory : 0;
+  pos->EphemeralStorage = req->EphemeralStorage > 0 ? req->EphemeralStorage : 0;
+  pos->AllowedPodNumber = 1;
+  for (auto& kv : req->Scalar)
+    if (kv.second > 0) pos->Scalar[kv.first] = kv.second;
+}
+Resource scaled(const Resource& r, i64 f) {  // Clone().Multiply(f) (resource.go:77-93)
+  Resource o = r;
+  o.MilliCPU = wrapmul(o.MilliCPU, f);
+  o.Memory = wrapmul(o.Memory, f);
+  o.EphemeralStorage = wrapmul(o.EphemeralStorage, f);
+  o.AllowedPodNumber = wrapmul(o.AllowedPodNumber, f);
+  for (auto& kv : o.Scalar) kv.second = wrapmul(kv.second, f);
+  return o;
+}
+
+// SchedulingSimulator.SimulateScheduling (scheduling_simulator_components.go:51-131)
+// over the model nodes of `groups`, literally: every node, every set, first fit.
+i32 simulateFF(const vector<std::pair<Resource, i64>>& groups, const vector<Component>& comps, i32 upper) {
+  vector<Resource> nodes;
+  for (auto& g : groups)
+    for (i64 i = 0; i < g.second; i++) nodes.push_back(g.first);
+  vector<Resource> req(comps.size()), pos(comps.size());
+  for (size_t k = 0; k < comps.size(); k++) replicaRequest(comps[k], &req[k], &pos[k]);
+  i32 complete = 0;
+  while (complete < upper) {
+    bool ok = true;
+    for (size_t k = 0; k < comps.size() && ok; k++) {  // scheduleComponentSet
+      i32 remaining = comps[k].replicas;
+      bool done = false;
+      for (auto& n : nodes) {  // scheduleComponent
+        i64 alloc = n.MaxDivided(pos[k]);
+        if (alloc == 0) continue;
+        if ((i64)remaining < alloc) alloc = remaining;
+        n.Sub(scaled(req[k], alloc));
+        remaining -= (i32)alloc;
+        if (remaining == 0) {
+          done = true;
+          break;
+        }
+      }
+      if (!done && remaining != 0) ok = false;
+    }
+    if (!ok) break;
+    complete++;
+  }
+  return complete;
+}
+
+// The same simulation over runs of identical nodes (the engine's device form):
+// identical consecutive nodes absorb the same amount, so a run of cnt nodes that
+// each take m replicas is one step, and a partial fill splits a run into at most
+// three. Runs before ptr[k] can no longer hold component k (capacity only drops),
+// so each component's scan resumes there. Same answer as simulateFF.
+i32 simulateRuns(const vector<std::pair<Resource, i64>>& groups, const vector<Component>& comps, i32 upper) {
+  struct Run {
+    Resource cap;
+    i64 cnt;
+  };
+  vector<Run> runs;
+  for (auto& g : groups)
+    if (g.second > 0) runs.push_back({g.first, g.second});
+  const size_t K = comps.size();
+  vector<Resource> req(K), pos(K);
+  for (size_t k = 0; k < K; k++) replicaRequest(comps[k], &req[k], &pos[k]);
+  vector<size_t> ptr(K, 0);
+  i32 complete = 0;
+  while (complete < upper) {
+    bool ok = true;
+    for (size_t k = 0; k < K && ok; k++) {
+      i64 rem = comps[k].replicas;
+      if (rem == 0) continue;  // succeeds at the first node that fits or at the end
+      bool lead = true;
+      size_t i = ptr[k];
+      for (; i < runs.size() && rem > 0; i++) {
+        const i64 m = runs[i].cap.MaxDivided(pos[k]);
+        if (m <= 0) {
+          if (lead) ptr[k] = i + 1;
+          continue;
+        }
+        lead = false;
+        const i128 all = (i128)m * runs[i].cnt;
+        if ((i128)rem >= all) {
+          runs[i].cap.Sub(scaled(req[k], m));
+          rem -= (i64)all;
+          continue;
+        }
+        const i64 q = rem / m, r = rem % m, rest = runs[i].cnt - q - (r > 0 ? 1 : 0);
+        vector<Run> parts;
+        if (q > 0) {
+          Run a = runs[i];
+          a.cap.Sub(scaled(req[k], m));
+          a.cnt = q;
+          parts.push_back(a);
+        }
+        if (r > 0) {
+          Run b = runs[i];
+          b.cap.Sub(scaled(req[k], r));
+          b.cnt = 1;
+          parts.push_back(b);
+        }
+        if (rest > 0) {
+          Run c = runs[i];
+          c.cnt = rest;
+          parts.push_back(c);
+        }
+        const size_t add = parts.size() - 1;
+        runs.erase(runs.begin() + i);
+        runs.insert(runs.begin() + i, parts.begin(), parts.end());
+        for (size_t j = 0; j < K; j++)
+          if (j != k && ptr[j] > i) ptr[j] += add;
+        rem = 0;
+      }
+      if (rem > 0) ok = false;
+    }
+    if (!ok) break;
+    complete++;
+  }
+  return complete;
+}
+
+// maxAvailableComponentSets (general.go:163-199) with resourceBoundedSets,
+// applyResourceModelBound and getMaximumSetsBasedOnResourceModels (:218-292).
+i32 maxAvailableComponentSets(const Cluster& c, const vector<Component>& comps, const Options& o, int mode) {
+  if (!c.has_summary) return 0;
+  std::map<string, i64> available;  // availableResourceMap (general.go:403-415)
+  for (auto& kv : c.allocatable) {
+    Quantity a = kv.second;
+    auto ad = c.allocated.find(kv.first);
+    if (ad != c.allocated.end()) QSub(a, ad->second);
+    auto ag = c.allocating.find(kv.first);
+    if (ag != c.allocating.end()) QSub(a, ag->second);
+    available[kv.first] = quantityAsInt64(a);
+  }
+  const i64 allowedPods = getAllowedPodNumber(c);
+  if (allowedPods <= 0) return 0;
+  i64 podsPerSet = 0;  // podsInSet
+  for (auto& k : comps) podsPerSet += (i64)k.replicas;
+  if (podsPerSet <= 0) return toI32(allowedPods);
+  const i32 podBound = toI32(allowedPods / podsPerSet);
+  std::map<string, i64> perSet;  // perSetRequirement
+  for (auto& k : comps) {
+    if (!k.has_rr) continue;
+    for (auto& kv : k.request) perSet[kv.first] = (i64)((uint64_t)perSet[kv.first] + (uint64_t)wrapmul(quantityAsInt64(kv.second), k.replicas));
+  }
+  i32 maxSets = podBound;  // resourceBoundedSets
+  bool allZero = true;
+  for (auto& kv : perSet) allZero = allZero && kv.second == 0;
+  if (!perSet.empty() && !allZero) {
+    for (auto& kv : perSet) {
+      if (kv.second <= 0) continue;
+      auto it = available.find(kv.first);
+      const i64 av = it == available.end() ? 0 : it->second;
+      if (av <= 0) return 0;
+      const i32 rb = toI32(av / kv.second);
+      if (rb < maxSets) maxSets = rb;
+    }
+  }
+  // applyResourceModelBound
+  if (!o.models_gate || c.modelings.empty()) return maxSets;
+  vector<std::pair<Resource, i64>> groups;
+  if (!buildModelNodes(c, &groups)) return maxSets;  // error -> the summary bound
+  const i32 num = mode == KPO_FAITHFUL ? simulateFF(groups, comps, maxSets) : simulateRuns(groups, comps, maxSets);
+  return num < maxSets ? num : maxSets;
 }
 
 // calAvailableReplicas (pkg/scheduler/core/util.go:57-110) with the general estimator only.
@@ -2234,6 +2435,47 @@ uint32_t kpo_filter(const kp_cluster* c, const kp_binding* b, const kp_options* 
   bool ok = true;
   Cluster cl = convCluster(*c, 0, &ok);
   return RunFilterPlugins(convBinding(*b), cl, convOptions(opts));
+}
+static bool convComponents(const kp_component* comps, uint32_t n, vector<Component>* v);
+int32_t kpo_max_available_component_sets(const kp_cluster* c, const kp_component* comps, uint32_t n,
+                                         const kp_options* opts, int mode) {
+  bool ok = true;
+  Cluster cl = convCluster(*c, 0, &ok);
+  vector<Component> v;
+  if (!convComponents(comps, n, &v)) return -1;
+  return maxAvailableComponentSets(cl, v, convOptions(opts), mode);
+}
+static bool convComponents(const kp_component* comps, uint32_t n, vector<Component>* v) {
+  v->assign(n, Component());
+  for (uint32_t i = 0; i < n; i++) {
+    (*v)[i].replicas = comps[i].replicas;
+    (*v)[i].has_rr = comps[i].has_replica_requirements != 0;
+    if (!parseList(comps[i].resource_request, comps[i].n_resource_request, &(*v)[i].request)) return false;
+  }
+  return true;
+}
+int32_t kpo_max_sets_models(const kp_cluster* c, const kp_component* comps, uint32_t n, int32_t upper, int mode) {
+  bool ok = true;
+  Cluster cl = convCluster(*c, 0, &ok);
+  vector<Component> v;
+  if (!convComponents(comps, n, &v)) return -2;
+  vector<std::pair<Resource, i64>> groups;
+  if (!buildModelNodes(cl, &groups)) return -1;  // getMaximumSetsBasedOnResourceModels' error
+  return mode == KPO_FAITHFUL ? simulateFF(groups, v, upper) : simulateRuns(groups, v, upper);
+}
+int32_t kpo_simulate_sets(const kp_cluster* nodes, uint32_t n_nodes, const kp_component* comps, uint32_t n,
+                          int32_t upper, int mode) {
+  vector<std::pair<Resource, i64>> groups;
+  for (uint32_t i = 0; i < n_nodes; i++) {  // createNodeInfo: Allocatable = NewResource(allocatable)
+    ResourceList rl;
+    if (!parseList(nodes[i].allocatable, nodes[i].n_allocatable, &rl)) return -2;
+    Resource r;
+    r.Add(rl);
+    groups.push_back({r, 1});
+  }
+  vector<Component> v;
+  if (!convComponents(comps, n, &v)) return -2;
+  return mode == KPO_FAITHFUL ? simulateFF(groups, v, upper) : simulateRuns(groups, v, upper);
 }
 uint32_t kpo_filter_reason(const kp_cluster* c, const kp_binding* b, const kp_options* opts) {
   bool ok = true;

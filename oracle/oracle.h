@@ -78,6 +78,16 @@ int kpo_cluster_matches(const kp_cluster* c, const kp_cluster_affinity* a);
 /* Filter plugins in canonical order; returns 0 when the cluster fits, else the
  * KP_PLUGIN_* bit of the first failing plugin. */
 uint32_t kpo_filter(const kp_cluster* c, const kp_binding* b, const kp_options* opts);
+/* GeneralEstimator.maxAvailableComponentSets (general.go:163-292) for one cluster;
+ * mode FAITHFUL runs the literal first-fit over every model node, FAST the run form. */
+int32_t kpo_max_available_component_sets(const kp_cluster* c, const kp_component* comps, uint32_t n,
+                                         const kp_options* opts, int mode);
+/* getMaximumSetsBasedOnResourceModels (general.go:262-292): -1 on its error. */
+int32_t kpo_max_sets_models(const kp_cluster* c, const kp_component* comps, uint32_t n, int32_t upper, int mode);
+/* SchedulingSimulator.SimulateScheduling over explicit nodes (each node = a cluster
+ * struct's resource_summary.allocatable, createNodeInfo of the reference's test). */
+int32_t kpo_simulate_sets(const kp_cluster* nodes, uint32_t n_nodes, const kp_component* comps, uint32_t n,
+                          int32_t upper, int mode);
 /* The same pair as a kp_filter_reasons word (KP_REASON_* | arg << 8). */
 uint32_t kpo_filter_reason(const kp_cluster* c, const kp_binding* b, const kp_options* opts);
 int64_t kpo_score(const kp_cluster* c, const kp_binding* b, const kp_options* opts);

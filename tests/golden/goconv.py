@@ -21,6 +21,7 @@ CONST = {
     "corev1.TaintEffectPreferNoSchedule": "PreferNoSchedule",
     "corev1.ResourceCPU": "cpu", "corev1.ResourceMemory": "memory", "corev1.ResourcePods": "pods",
     "corev1.ResourceEphemeralStorage": "ephemeral-storage",
+    "uint": lambda x: x,
     "corev1.NodeSelectorOpIn": "In", "corev1.NodeSelectorOpNotIn": "NotIn",
     "corev1.NodeSelectorOpExists": "Exists", "corev1.NodeSelectorOpDoesNotExist": "DoesNotExist",
     "corev1.NodeSelectorOpGt": "Gt", "corev1.NodeSelectorOpLt": "Lt",
@@ -188,6 +189,21 @@ class Conv:
             d["schedulerObservedAffinityName"] = self.ev(status.get("SchedulerObservedAffinityName", ""))
         return d
 
+    # -- components ----------------------------------------------------------------------
+    def components(self, v):
+        """[]workv1alpha2.Component -> [{name, replicas, replicaRequirements?: {resourceRequest}}]."""
+        out = []
+        for c in (v.values() if v is not None else []):
+            if isinstance(c, Call) and c.fn in self.syms and callable(self.syms[c.fn]):
+                out.append(self.syms[c.fn](*c.args))
+                continue
+            d = {"name": self.ev(c.get("Name", "")), "replicas": self.ev(c.get("Replicas", 0))}
+            rr = c.get("ReplicaRequirements")
+            if rr is not None:
+                d["replicaRequirements"] = {"resourceRequest": self.qmap(rr.get("ResourceRequest"))}
+            out.append(d)
+        return out
+
     # -- cluster -------------------------------------------------------------------------
     def cluster(self, c):
         if isinstance(c, dict):
@@ -212,6 +228,12 @@ class Conv:
             d["taints"] = [{"key": self.ev(t.get("Key", "")), "value": self.ev(t.get("Value", "")),
                             "effect": self.ev(t.get("Effect", ""))}
                            for t in (sp.get("Taints").values() if sp.get("Taints") is not None else [])]
+            d["resourceModels"] = [
+                {"grade": self.ev(m.get("Grade", 0)),
+                 "ranges": [{"name": self.key(r.get("Name", "")), "min": str(self.ev(r.get("Min", "0"))),
+                             "max": str(self.ev(r.get("Max", "0")))}
+                            for r in (m.get("Ranges").values() if m.get("Ranges") is not None else [])]}
+                for m in (sp.get("ResourceModels").values() if sp.get("ResourceModels") is not None else [])]
         st = c.get("Status")
         if st is not None:
             ae = []
@@ -224,5 +246,9 @@ class Conv:
             if rs is not None:
                 d["resourceSummary"] = {"allocatable": self.qmap(rs.get("Allocatable")),
                                         "allocated": self.qmap(rs.get("Allocated")),
-                                        "allocating": self.qmap(rs.get("Allocating"))}
+                                        "allocating": self.qmap(rs.get("Allocating")),
+                                        "allocatableModelings": [
+                                            {"grade": self.ev(m.get("Grade", 0)), "count": self.ev(m.get("Count", 0))}
+                                            for m in (rs.get("AllocatableModelings").values()
+                                                      if rs.get("AllocatableModelings") is not None else [])]}
         return d

@@ -18,7 +18,7 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 
 
 def read(path):
-    with open(os.path.join(REF, path)) as f:
+    with open(os.path.join(REF, path), encoding="utf-8") as f:
         return f.read()
 
 
@@ -286,8 +286,52 @@ def core():
     return res
 
 
+def sets():
+    """GeneralEstimator component-set tables (estimator/client/general_test.go) and the
+    FF simulator table (estimator/scheduling_simulator_components_test.go)."""
+    res = {"source": []}
+    GEN = "pkg/estimator/client/general_test.go"
+    src = read(GEN)
+    cv = Conv({"GPU": "nvidia.com/gpu", "BIGU": 100, "q": lambda x: x})
+
+    def comp(name, replicas, rl):  # general_test.go:251-259
+        return {"name": cv.ev(name), "replicas": cv.ev(replicas),
+                "replicaRequirements": {"resourceRequest": cv.qmap(rl)}}
+    cv.syms["comp"] = comp
+    rows, line = table(src, "TestGetMaximumSetsBasedOnResourceModels")
+    res["models"] = [{"name": r.get("name"), "cluster": cv.cluster(r.get("cluster")),
+                      "components": cv.components(r.get("components")), "upperBound": cv.ev(r.get("upperBound")),
+                      "expectError": bool(cv.ev(r.get("expectError", False))),
+                      "expectedSets": cv.ev(r.get("expectedSets"))} for r in rows]
+    res["source"].append(GEN + ":%d (TestGetMaximumSetsBasedOnResourceModels)" % line)
+    rows, line = table(src, "TestGetMaxAvailableComponentSetsGeneral")
+    res["general"] = [{"name": r.get("name"), "cluster": cv.cluster(r.get("cluster") or Comp(None, [])),
+                       "components": cv.components(r.get("components")), "expected": cv.ev(r.get("expected"))}
+                      for r in rows]
+    res["source"].append(GEN + ":%d (TestGetMaxAvailableComponentSetsGeneral)" % line)
+    SIM = "pkg/estimator/scheduling_simulator_components_test.go"
+    ssrc = read(SIM).replace("(&pb.ComponentReplicaRequirements{}).MustSetResourceRequest(", "RR(")
+    cs = Conv({"RR": lambda rl: cs.qmap(rl), "createNodeInfo": lambda name, rl: {"name": name, "allocatable": rl}})
+    rows, line = table(ssrc, "TestSchedulingSimulator_SimulateSchedulingFF")
+    ff = []
+    for r in rows:
+        nodes = [{"name": cs.ev(n.args[0]), "allocatable": cs.qmap(n.args[1])} for n in r.get("nodes").values()]
+        comps = []
+        for c in r.get("components").values():
+            rr = c.get("ReplicaRequirements")
+            d = {"name": cs.ev(c.get("Name", "")), "replicas": cs.ev(c.get("Replicas", 0))}
+            if rr is not None:
+                d["replicaRequirements"] = {"resourceRequest": cs.qmap(rr.args[0]) if isinstance(rr, Call) else {}}
+            comps.append(d)
+        ff.append({"name": r.get("name"), "nodes": nodes, "components": comps,
+                   "upperBound": cs.ev(r.get("upperBound")), "expectedSets": cs.ev(r.get("expectedSets"))})
+    res["ff"] = ff
+    res["source"].append(SIM + ":%d (TestSchedulingSimulator_SimulateSchedulingFF)" % line)
+    return res
+
+
 def main():
-    outs = {"plugins.json": plugins(), "spread.json": spread(), "core.json": core()}
+    outs = {"plugins.json": plugins(), "spread.json": spread(), "core.json": core(), "sets.json": sets()}
     for name, data in outs.items():
         with open(os.path.join(OUT, name), "w") as f:
             json.dump(data, f, indent=1)
