@@ -231,22 +231,44 @@ def main():
         dist.all_reduce(t)
         n_chk, n_bad = int(t[0].item()), int(t[1].item())
 
-    # end to end: binding packing + upload + schedule + results to host, per batch
+    # end to end: binding packing + upload + schedule + results to host, per batch.
+    # serial: one batch at a time; pipelined: two engines on this GPU, each packing
+    # its next batch on the host while the other's batch runs on the device (a
+    # scheduler draining its queue), timed over 2 x e2e_reps batches.
     batch.close()
-    e2e = None
+    e2e = e2e_pipe = None
     if args.e2e_reps > 0:
+        structs = u.binding_slice(0, u.n_bindings)
         ts = []
         for _ in range(args.e2e_reps):
             t1 = time.perf_counter()
-            b2 = Batch(snap, structs=u.binding_slice(0, u.n_bindings))
+            b2 = Batch(snap, structs=structs)
             b2.schedule_raw()
             ts.append(time.perf_counter() - t1)
             b2.close()
         e2e = sum(ts) / len(ts)
+        import threading
+        eng2 = Engine(local, lib_path=os.path.join(ROOT, args.lib)) if args.lib else Engine(local)
+        snap2 = Snapshot.from_bytes(eng2, snap.to_bytes(), u.names)
+
+        def drain(sn):
+            for _ in range(args.e2e_reps):
+                b3 = Batch(sn, structs=structs)
+                b3.schedule_raw()
+                b3.close()
+        t1 = time.perf_counter()
+        th = [threading.Thread(target=drain, args=(sn,)) for sn in (snap, snap2)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        e2e_pipe = (time.perf_counter() - t1) / (2 * args.e2e_reps)
+        snap2.close()
+        eng2.close()
         if dist is not None:
-            t = torch.tensor([e2e], dtype=torch.float64, device=tdev)
+            t = torch.tensor([e2e, e2e_pipe], dtype=torch.float64, device=tdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            e2e = float(t.item())
+            e2e, e2e_pipe = float(t[0].item()), float(t[1].item())
 
     def avg(k):
         return sum(x[k] for x in st_all) / len(st_all)
@@ -299,8 +321,11 @@ def main():
         "stages_ms": {"pair_kernel": round(pair_ms, 3), "select_kernels": round(sel_ms, 3),
                       "sel_all_kernel": round(sel_all_ms, 3), "fused_kernel": round(fused_ms, 3),
                       "host_region": round(avg("host_ms"), 3)},
-        "end_to_end_value": round(B * world / e2e, 1) if e2e else None,
-        "end_to_end_ms": round(1e3 * e2e, 2) if e2e else None,
+        # bindings/s including host packing + upload: pipelined over two engines (the
+        # value), and one batch at a time (end_to_end_serial_ms per batch)
+        "end_to_end_value": round(B * world / e2e_pipe, 1) if e2e_pipe else None,
+        "end_to_end_ms": round(1e3 * e2e_pipe, 2) if e2e_pipe else None,
+        "end_to_end_serial_ms": round(1e3 * e2e, 2) if e2e else None,
         "setup_s": {"generate": round(gen_s, 2), "snapshot_pack_upload": round(snap_s, 3),
                     "binding_pack_upload": round(pack_s, 3)},
         "scheduled_ok": n_ok,

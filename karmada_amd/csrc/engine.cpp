@@ -14,6 +14,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -31,12 +32,21 @@ using namespace kp;
 namespace {
 
 std::string S(const kp_str& s) { return (s.ptr && s.len) ? std::string(s.ptr, s.len) : std::string(); }
+std::string_view SV(const kp_str& s) { return (s.ptr && s.len) ? std::string_view(s.ptr, s.len) : std::string_view(); }
 double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// std::string-keyed hash table with string_view lookups (no key copy per probe).
+struct SvHash {
+  using is_transparent = void;
+  size_t operator()(std::string_view v) const { return std::hash<std::string_view>()(v); }
+};
+template <class V>
+using SvMap = std::unordered_map<std::string, V, SvHash, std::equal_to<>>;
+
 struct Dict {
-  std::unordered_map<std::string, int32_t> m;
+  SvMap<int32_t> m;
   std::vector<std::string> names;
   int32_t add(const std::string& s) {
     auto it = m.find(s);
@@ -46,7 +56,7 @@ struct Dict {
     names.push_back(s);
     return id;
   }
-  int32_t get(const std::string& s) const {
+  int32_t get(std::string_view s) const {
     auto it = m.find(s);
     return it == m.end() ? -1 : it->second;
   }
@@ -120,7 +130,7 @@ struct kp_snapshot {
   kp_options opts{};
   int C = 0, Cp = 0, W = 0;
   Dict str, keys, gvk, res, regions;
-  std::unordered_map<std::string, int32_t> rank_of;  // cluster name -> rank
+  SvMap<int32_t> rank_of;  // cluster name -> rank
   std::vector<uint32_t> perm;                        // rank -> caller index
   std::vector<int32_t> inv;                          // caller index -> rank
   int32_t rid_cpu = -1, rid_mem = -1, rid_eph = -1;
@@ -665,7 +675,7 @@ struct Packer {
   std::vector<int32_t> ranks(const kp_str* names, uint32_t n) {
     std::vector<int32_t> r;
     for (uint32_t i = 0; i < n; i++) {
-      auto it = s->rank_of.find(S(names[i]));
+      auto it = s->rank_of.find(SV(names[i]));
       if (it != s->rank_of.end()) r.push_back(it->second);
     }
     return r;
@@ -673,7 +683,7 @@ struct Packer {
   std::vector<int32_t> vals(const kp_str* v, uint32_t n) {
     std::vector<int32_t> r;
     for (uint32_t i = 0; i < n; i++) {
-      int32_t id = s->str.get(S(v[i]));
+      int32_t id = s->str.get(SV(v[i]));
       if (id >= 0) r.push_back(id);
     }
     return r;
@@ -850,7 +860,7 @@ struct Packer {
     {
       std::vector<int32_t> t, rk;
       for (uint32_t i = 0; i < b.n_clusters; i++) {
-        auto it = s->rank_of.find(S(b.clusters[i].name));
+        auto it = s->rank_of.find(SV(b.clusters[i].name));
         if (it == s->rank_of.end()) continue;
         rk.push_back(it->second);
         t.push_back(it->second);
@@ -881,7 +891,7 @@ struct Packer {
       else if ((x.key = s->str.get(key)) < 0) continue;
       if (op.empty() || op == "Equal") {
         x.op = TOL_EQUAL;
-        if ((x.val = s->str.get(S(t.value))) < 0) continue;
+        if ((x.val = s->str.get(SV(t.value))) < 0) continue;
       } else if (op == "Exists") {
         x.op = TOL_EXISTS;
         x.val = -1;
@@ -945,12 +955,26 @@ struct Packer {
     }
     // requests
     {
-      QtyMap rq;
-      if (!qmap(b.resource_request, b.n_resource_request, &rq)) f |= BF_BAD;
+      // the ResourceList as (name, quantity) in name order, a repeated name's last
+      // entry winning (the map the reference decodes), without per-entry allocation
+      std::vector<std::pair<std::string_view, k8s::Qty>> rq;
+      for (uint32_t i = 0; i < b.n_resource_request; i++) {
+        k8s::Qty q;
+        if (!k8s::parse_quantity(SV(b.resource_request[i].quantity), &q)) f |= BF_BAD;
+        const std::string_view nm = SV(b.resource_request[i].name);
+        bool dup = false;
+        for (auto& kv : rq)
+          if (kv.first == nm) {
+            kv.second = q;
+            dup = true;
+          }
+        if (!dup) rq.push_back({nm, q});
+      }
+      std::sort(rq.begin(), rq.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
       std::vector<int32_t> sr, mr;
       std::vector<int64_t> sq, mq;
       for (auto& kv : rq) {
-        const std::string& nm = kv.first;
+        const std::string_view nm = kv.first;
         int64_t v = k8s::value(kv.second);
         if (v > 0) {  // summary path: every resource name (general.go:467-471)
           sr.push_back(s->res.get(nm));
@@ -963,7 +987,7 @@ struct Packer {
             mr.push_back(s->res.get(nm));
             mq.push_back(m);
           }
-        } else if (nm == "memory" || nm == "ephemeral-storage" || (nm != "pods" && k8s::scalar_resource(nm))) {
+        } else if (nm == "memory" || nm == "ephemeral-storage" || (nm != "pods" && k8s::scalar_resource(std::string(nm)))) {
           if (v > 0) {
             mr.push_back(s->res.get(nm));
             mq.push_back(v);
@@ -1108,6 +1132,21 @@ std::vector<int> select_groups(std::vector<G> groups, int64_t minC, int64_t maxC
   std::vector<int> out;
   for (int i : fin->g) out.push_back(groups[i].id);
   return out;
+}
+
+// Hardware threads, capped by the cgroup v2 CPU quota (cpu.max "quota period") when set.
+int host_cpus() {
+  int n = (int)std::max(1u, std::thread::hardware_concurrency());
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long long period = 0;
+    if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+      const long long quota = atoll(q);
+      n = std::min<long long>(n, std::max<long long>(1, (quota + period - 1) / period));
+    }
+    fclose(f);
+  }
+  return n;
 }
 
 template <class F>
@@ -1617,9 +1656,10 @@ int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_sna
 // dictionaries), then the chunks are concatenated and every pool reference is
 // rebased: header offsets, program ids in the ipool lists, Prog::ins_off and the
 // list offsets inside Instr. The result equals a sequential pack (test_abi).
-// Threads: KP_PACK_THREADS, else hardware_concurrency, one per 4096 bindings at most.
+// Threads: KP_PACK_THREADS, else the CPUs this process may use (hardware threads,
+// capped by a cgroup CPU quota), one per 4096 bindings at most.
 bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* bt) {
-  int T = (int)std::thread::hardware_concurrency();
+  int T = host_cpus();
   if (const char* v = getenv("KP_PACK_THREADS")) T = atoi(v);
   T = std::max(1, std::min(T, n / 4096));
   std::vector<Pools> pl(T);

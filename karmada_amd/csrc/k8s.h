@@ -9,6 +9,7 @@
 
 #include <cstring>
 #include <string>
+#include <string_view>
 
 namespace kp {
 namespace k8s {
@@ -41,7 +42,7 @@ inline void qsub(Qty& a, const Qty& y) {
   a.nano -= y.nano;
 }
 
-inline bool parse_quantity(const std::string& str, Qty* out) {
+inline bool parse_quantity(std::string_view str, Qty* out) {
   if (str.empty()) return false;
   if (str == "0") {
     out->nano = 0;
@@ -55,7 +56,7 @@ inline bool parse_quantity(const std::string& str, Qty* out) {
     pos = 1;
   }
   while (pos < end && str[pos] == '0') pos++;
-  std::string num, denom, suf;
+  std::string_view num, denom, suf;
   size_t i = pos;
   while (i < end && str[i] >= '0' && str[i] <= '9') i++;
   num = str.substr(pos, i - pos);
@@ -96,11 +97,13 @@ inline bool parse_quantity(const std::string& str, Qty* out) {
     }
   int fmt = binary ? 1 : 0;
   if (!found) {
-    if (suf.size() > 1 && (suf[0] == 'e' || suf[0] == 'E')) {
-      const char* p = suf.c_str() + 1;
+    if (suf.size() > 1 && suf.size() < 32 && (suf[0] == 'e' || suf[0] == 'E')) {
+      char buf[32];
+      memcpy(buf, suf.data() + 1, suf.size() - 1);
+      buf[suf.size() - 1] = 0;
       char* e = nullptr;
-      long long v = strtoll(p, &e, 10);
-      if (e == p || *e) return false;
+      long long v = strtoll(buf, &e, 10);
+      if (e == buf || *e) return false;
       ex = (int32_t)v;
       fmt = 2;
     } else {
@@ -109,10 +112,11 @@ inline bool parse_quantity(const std::string& str, Qty* out) {
   }
   const i128 lim = (i128)1 << 100;
   i128 m = 0;
-  for (char c : num + denom) {
-    if (m > lim) return false;
-    m = m * 10 + (c - '0');
-  }
+  for (std::string_view part : {num, denom})
+    for (char c : part) {
+      if (m > lim) return false;
+      m = m * 10 + (c - '0');
+    }
   i128 nano;
   if (!binary) {
     int64_t sc = 9 + ex - (int64_t)denom.size();
