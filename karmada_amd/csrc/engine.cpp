@@ -110,8 +110,9 @@ struct Arena {
 struct kp_engine {
   int device = 0;
   dev::stream_t stream = nullptr;   // select kernels, copies (the batch's result order)
-  dev::stream_t stream2 = nullptr;  // pair kernels, one launch per chunk ahead of the selects
-  dev::event_t ev[8] = {};
+  dev::stream_t stream2 = nullptr;  // pair kernel, then the SEL_ALL select kernel
+  dev::stream_t stream3 = nullptr;  // the cluster-spread select kernel, beside the other selects
+  dev::event_t ev[12] = {};
   std::string err;
   kp_stage_times times{};
   struct {  // kp_schedule_affinities results
@@ -1390,7 +1391,8 @@ int kp_engine_create(int device, kp_engine** out) {
   if (device < 0 || dev::device_count() <= device) return KP_EDEVICE;
   auto* e = new kp_engine();
   e->device = device;
-  if (dev::set_device(device) || dev::stream_create(&e->stream) || dev::stream_create(&e->stream2)) {
+  if (dev::set_device(device) || dev::stream_create(&e->stream) || dev::stream_create(&e->stream2) ||
+      dev::stream_create(&e->stream3)) {
     delete e;
     return KP_EDEVICE;
   }
@@ -1409,6 +1411,7 @@ void kp_engine_destroy(kp_engine* e) {
     if (ev) dev::event_destroy(ev);
   if (e->stream) dev::stream_destroy(e->stream);
   if (e->stream2) dev::stream_destroy(e->stream2);
+  if (e->stream3) dev::stream_destroy(e->stream3);
   delete e;
 }
 
@@ -1953,19 +1956,26 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   }
   HIPCHK(dev::stream_wait(st, e->ev[4]));  // every pair row precedes the rest
   HIPCHK(dev::event_record(e->ev[1], st));
+  // The three selection kinds touch disjoint bindings: SEL_ALL on stream2 (after the
+  // pair kernel there), cluster spread on stream3, the region chain on stream, so a
+  // latency-bound kernel shares the CUs with the others instead of running alone.
+  HIPCHK(dev::event_record(e->ev[7], sp));
   if (!fused && !bt->l_all.empty()) {
     KArgs k = ka;
     k.list = bt->d_all;
     k.n = (int)bt->l_all.size();
-    HIPCHK(dev::select(st, SEL_LAUNCH_ALL, k, smem_all(s), cap, sx));
+    HIPCHK(dev::select(sp, SEL_LAUNCH_ALL, k, smem_all(s), cap, sx));
   }
-  HIPCHK(dev::event_record(e->ev[7], st));  // k_select_all alone: ev[1] -> ev[7]
+  HIPCHK(dev::event_record(e->ev[8], sp));  // k_select_all alone: ev[7] -> ev[8]
+  dev::stream_t s3 = e->stream3;
+  HIPCHK(dev::stream_wait(s3, e->ev[4]));
   if (!bt->l_cluster.empty()) {
     KArgs k = ka;
     k.list = bt->d_cluster;
     k.n = (int)bt->l_cluster.size();
-    HIPCHK(dev::select(st, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sx));
+    HIPCHK(dev::select(s3, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sx));
   }
+  HIPCHK(dev::event_record(e->ev[9], s3));
   double th0 = 0, th1 = 0;
   if (!bt->l_region.empty()) {
     const int nr = (int)bt->l_region.size(), R = s->view.n_regions;
@@ -2030,6 +2040,8 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     }
     HIPCHK(dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sx));
   }
+  HIPCHK(dev::stream_wait(st, e->ev[8]));  // every fast-path flag precedes k_slow
+  HIPCHK(dev::stream_wait(st, e->ev[9]));
   if (fused)  // HBM rows of the bindings the fused kernel flagged for k_slow
     HIPCHK(dev::pair_list(st, s->view, bt->view, bt->d_slowlist, bt->stats, (int)bt->l_slow.size(), bt->fmask, bt->est,
                           md_cap, smem_pair(s, md_cap)));
@@ -2096,7 +2108,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   tm.pair_kernel_ms = ms_pair;
   tm.select_kernel_ms = ms_sel;
   tm.fused_kernel_ms = ms_fused;
-  tm.sel_all_kernel_ms = dev::event_ms(e->ev[1], e->ev[7]);
+  tm.sel_all_kernel_ms = dev::event_ms(e->ev[7], e->ev[8]);
   tm.n_sel_all = (uint32_t)bt->l_all.size();
   tm.fused = fused ? 1u : 0u;
   tm.n_slow = bt->h_stats[0];
