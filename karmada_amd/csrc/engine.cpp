@@ -976,21 +976,23 @@ struct Packer {
       std::vector<int64_t> sq, mq;
       for (auto& kv : rq) {
         const std::string_view nm = kv.first;
+        const bool cpu = nm == "cpu", mem = nm == "memory";
+        const int32_t rid = cpu ? s->rid_cpu : (mem ? s->rid_mem : s->res.get(nm));
         int64_t v = k8s::value(kv.second);
         if (v > 0) {  // summary path: every resource name (general.go:467-471)
-          sr.push_back(s->res.get(nm));
-          sq.push_back(nm == "cpu" ? k8s::milli(kv.second) : v);
+          sr.push_back(rid);
+          sq.push_back(cpu ? k8s::milli(kv.second) : v);
         }
         // model path: util.NewResource classes (resource.go:46-75)
-        if (nm == "cpu") {
+        if (cpu) {
           int64_t m = k8s::milli(kv.second);
           if (m > 0) {
-            mr.push_back(s->res.get(nm));
+            mr.push_back(rid);
             mq.push_back(m);
           }
-        } else if (nm == "memory" || nm == "ephemeral-storage" || (nm != "pods" && k8s::scalar_resource(std::string(nm)))) {
+        } else if (mem || nm == "ephemeral-storage" || (nm != "pods" && k8s::scalar_resource(std::string(nm)))) {
           if (v > 0) {
-            mr.push_back(s->res.get(nm));
+            mr.push_back(rid);
             mq.push_back(v);
           }
         }
