@@ -35,16 +35,26 @@ B_BIND = 256
 PAIR_KERNELS = {0: "k_pair", 1: "k_pair_fast", 2: "k_pair_fast_summary", 8: "k_pair_fast_m8", 16: "k_pair_fast_m16"}
 
 
-def compulsory_bytes(n_bind, n_all, n_clusters, n_targets, snap_bytes):
-    """Compulsory HBM bytes per launch:
-    pair         = snapshot once + binding records + the est row (4*Cp) and feasibility
-                   mask (Cp/8) it writes per binding;
-    k_select_all = its bindings' rows and records read back + their results (cluster u32
-                   + replicas i32 per target, status/err/arg/start/count per binding)."""
+def compulsory_bytes(n_bind, n_all, n_clusters, n_targets, snap_bytes, n_classes):
+    """Compulsory HBM bytes per launch.
+    bits mode (n_classes > 0):
+      filter stage = snapshot (incl. its bitset rows) once + binding records + the
+                     feasibility row (Cp/8) written per binding + the estimator-class
+                     rows (4*Cp each) written once;
+      k_select_all = its bindings' records and feasibility rows read back, the class
+                     rows once, their results (cluster u32 + replicas i32 per target,
+                     status/err/arg/start/count per binding).
+    pair-row mode: the pair kernel writes a 4*Cp est row per binding and k_select_all
+    reads it back."""
     Cp = (n_clusters + 63) // 64 * 64
-    row = 4.0 * Cp + Cp / 8.0
-    pair = snap_bytes + n_bind * (B_BIND + row)
-    sel = n_all * (B_BIND + row + 28) + 8.0 * n_targets
+    if n_classes:
+        cls = 4.0 * Cp * n_classes
+        pair = snap_bytes + n_bind * (B_BIND + Cp / 8.0) + cls
+        sel = n_all * (B_BIND + Cp / 8.0 + 28) + cls + 8.0 * n_targets
+    else:
+        row = 4.0 * Cp + Cp / 8.0
+        pair = snap_bytes + n_bind * (B_BIND + row)
+        sel = n_all * (B_BIND + row + 28) + 8.0 * n_targets
     return pair, sel
 
 
@@ -276,12 +286,12 @@ def main():
     value = (B * world) / (elapsed / args.steps)
     last = st_all[-1]
     pair_ms, sel_ms = avg("pair_kernel_ms"), avg("select_kernel_ms")
-    sel_all_ms, fused_ms = avg("sel_all_kernel_ms"), avg("fused_kernel_ms")
-    fused = last["fused"] == 1
-    pair_b, sel_b = compulsory_bytes(B, int(last["n_sel_all"]), C_, n_targets_rank, snap_bytes)
-    cands = [(PAIR_KERNELS.get(last["pair_kind"], "k_pair"), pair_ms, pair_b)]
-    if not fused:
-        cands.append(("k_select_all", sel_all_ms, sel_b))
+    sel_all_ms, filter_ms = avg("sel_all_kernel_ms"), avg("filter_kernel_ms")
+    bits = last["bits"] == 1
+    pair_b, sel_b = compulsory_bytes(B, int(last["n_sel_all"]), C_, n_targets_rank, snap_bytes,
+                                     int(last["n_classes"]) if bits else 0)
+    stage = "k_est_class+k_filter" if bits else PAIR_KERNELS.get(last["pair_kind"], "k_pair")
+    cands = [(stage, pair_ms, pair_b), ("k_select_all", sel_all_ms, sel_b)]
     kname, kms, kbytes = max(cands, key=lambda x: x[1])
     achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     profiled = (C_, B) == tuple(synth.CONFIGS[cfg])
@@ -295,7 +305,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc.get("hbm_bytes") if pmc else None,
             "kernel": kname, "kernel_ms": round(kms, 4), "algorithmic_bytes": round(kbytes),
             "dram_frac": pmc_frac("hbm_bytes", HBM_PEAK_GBS), "valu_frac": pmc_frac("valu_insts", VALU_PEAK_GINST)}
-    step_bytes = pair_b + (0.0 if fused else sel_b)
+    step_bytes = pair_b + sel_b
     step_gbs = step_bytes / (ms_per_step * 1e-3) / 1e9
     line = {
         "metric": "ResourceBindings scheduled/sec at 100k bindings x 5k clusters",
@@ -318,9 +328,12 @@ def main():
         # compulsory bytes of the whole step (every kernel) over the whole step's time
         "step_roofline": {"achieved": round(step_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(step_gbs / HBM_PEAK_GBS, 4), "bytes": round(step_bytes)},
-        "stages_ms": {"pair_kernel": round(pair_ms, 3), "select_kernels": round(sel_ms, 3),
-                      "sel_all_kernel": round(sel_all_ms, 3), "fused_kernel": round(fused_ms, 3),
+        # filter stage: k_est_class + k_filter (bits mode) or the pair kernel
+        "stages_ms": {"filter_stage": round(pair_ms, 3), "filter_kernel": round(filter_ms, 3),
+                      "select_kernels": round(sel_ms, 3), "sel_all_kernel": round(sel_all_ms, 3),
                       "host_region": round(avg("host_ms"), 3)},
+        "filter_mode": "bitset filter + estimator classes" if bits else "per-binding pair rows",
+        "estimator_classes": int(last["n_classes"]) if bits else None,
         # bindings/s including host packing + upload: pipelined over two engines (the
         # value), and one batch at a time (end_to_end_serial_ms per batch)
         "end_to_end_value": round(B * world / e2e_pipe, 1) if e2e_pipe else None,

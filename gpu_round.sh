@@ -18,7 +18,7 @@ for s in "$@"; do
     bench_small) step bench_small 300 python bench.py --steps 3 --warmup 1 --bindings 5000 --no-cpu ;;
     bench) step bench 600 python bench.py ;;
     benchq) step benchq 300 python bench.py --steps 100 --warmup 2 --no-cpu --check 300 ;;
-    bench_fuse) KP_FUSE=1 step bench_fuse 300 python bench.py --steps 100 --warmup 2 --no-cpu --check 300 ;;
+    bench_rows) KP_PAIR_ROWS=1 step bench_rows 300 python bench.py --steps 100 --warmup 2 --no-cpu --check 300 --e2e-reps 0 ;;
     sweep) for t in 256 512; do KP_SEL_THREADS=$t step sweep_$t 300 python bench.py --steps 3 --warmup 1 --no-cpu; done ;;
     chunks) for c in 4096 8192 16384 32768 200000; do KP_CHUNK=$c step chunk_$c 300 python bench.py --steps 5 --warmup 1 --no-cpu; done ;;
     configs) for c in 2 4 6; do step bench_config$c 300 python bench.py --config $c --steps 3 --warmup 1 --no-cpu; done

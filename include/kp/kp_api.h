@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 7
+#define KP_ABI_VERSION 8
 
 /* ------------------------------------------------------------------------- */
 /* Object model                                                              */
@@ -332,20 +332,21 @@ typedef struct kp_affinity_results {
 /* Per-stage timing of the last kp_schedule_batch call (milliseconds, host clock
  * around device work; kernel-only numbers come from rocprof). */
 typedef struct kp_stage_times {
-  double pair_ms;      /* filter + score + estimate kernel (rows to HBM) */
-  double select_ms;    /* candidate/group/select/divide kernels after the pair and fused kernels */
+  double pair_ms;      /* filter + estimate stage: k_est_class + k_filter, or the pair kernel */
+  double select_ms;    /* candidate/group/select/divide kernels after the filter stage */
   double host_ms;      /* host group-combination (region DFS) */
   double copy_ms;      /* device -> host result copies */
   double total_ms;
-  float pair_kernel_ms;   /* sum of the pair kernel launches' HIP event times */
-  float select_kernel_ms; /* select kernels after the last pair launch (HIP events) */
+  float pair_kernel_ms;   /* filter + estimate stage kernels (HIP events) */
+  float select_kernel_ms; /* select kernels after the filter stage (HIP events) */
   uint64_t n_slow;        /* bindings that took the exact serial path */
-  uint32_t pair_launches; /* pair kernel launches in the batch (0 or 1) */
-  uint32_t pair_kind;     /* pair kernel instance: 0 generic, 1 mixed, 2 summary-only, 8/16 model-only */
-  float fused_kernel_ms;  /* fused pair + SEL_ALL select kernel (HIP events), 0 when not run */
-  uint32_t fused;         /* 1: the SEL_ALL bindings took the fused kernel (rows kept in LDS) */
+  uint32_t pair_launches; /* filter-stage kernel launches (2: k_est_class + k_filter, 1: pair kernel) */
+  uint32_t pair_kind;     /* estimator instance: 0 generic, 1 mixed, 2 summary-only, 8/16 model-only */
+  float filter_kernel_ms; /* k_filter alone (HIP events), 0 with the pair kernel */
+  uint32_t bits;          /* 1: bitset filter + estimator-class rows; 0: per-binding pair rows */
   float sel_all_kernel_ms; /* the two-kernel path's SEL_ALL select kernel alone (HIP events) */
   uint32_t n_sel_all;      /* bindings of the SEL_ALL select kernel (SelectBestClusters selects all) */
+  uint32_t n_classes;      /* estimator-class rows computed (bits == 1; row 0 = non-workload) */
 } kp_stage_times;
 
 /* ------------------------------------------------------------------------- */

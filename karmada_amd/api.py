@@ -153,8 +153,9 @@ class kp_stage_times(C.Structure):
                 ("copy_ms", C.c_double), ("total_ms", C.c_double),
                 ("pair_kernel_ms", C.c_float), ("select_kernel_ms", C.c_float), ("n_slow", u64),
                 ("pair_launches", C.c_uint32), ("pair_kind", C.c_uint32),
-                ("fused_kernel_ms", C.c_float), ("fused", C.c_uint32),
-                ("sel_all_kernel_ms", C.c_float), ("n_sel_all", C.c_uint32)]
+                ("filter_kernel_ms", C.c_float), ("bits", C.c_uint32),
+                ("sel_all_kernel_ms", C.c_float), ("n_sel_all", C.c_uint32),
+                ("n_classes", C.c_uint32)]
 
 
 PLUGIN_API_ENABLEMENT = 1 << 0

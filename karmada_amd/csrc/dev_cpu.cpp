@@ -108,6 +108,26 @@ int pair(stream_t, const SnapView& s, const BatchView& bv, const int32_t* list, 
   return 0;
 }
 
+int est_class(stream_t, const SnapView& s, const BatchView& bv, const int32_t* rep, int n_rows, int32_t* rows,
+              int fast) {
+  grid(n_rows, 4 * kTmplDense, [&](int k, unsigned char* sm) {
+    const CpuBlk B{(int64_t*)sm};
+    switch (fast) {
+      case EST_MIXED: body_est_class<EST_MIXED>(B, k, sm, s, bv, rep, rows); break;
+      case EST_SUMMARY: body_est_class<EST_SUMMARY>(B, k, sm, s, bv, rep, rows); break;
+      case EST_MODEL8: body_est_class<EST_MODEL8>(B, k, sm, s, bv, rep, rows); break;
+      case EST_MODEL16: body_est_class<EST_MODEL16>(B, k, sm, s, bv, rep, rows); break;
+      default: break;
+    }
+  });
+  return fast == EST_MIXED || fast == EST_SUMMARY || fast == EST_MODEL8 || fast == EST_MODEL16 ? 0 : -1;
+}
+
+int filter(stream_t, const SnapView& s, const BatchView& bv, uint64_t* fmask) {
+  grid(bv.B, 0, [&](int b, unsigned char* sm) { body_filter(CpuBlk{(int64_t*)sm}, b, s, bv, fmask); });
+  return 0;
+}
+
 int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x) {
   switch (which) {
     case SEL_LAUNCH_ALL: {
@@ -138,29 +158,6 @@ int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const Sele
     default:
       return -1;
   }
-  return 0;
-}
-
-int fused_all(stream_t, const KArgs& a, size_t smem, int md_cap, int fast) {
-  grid(a.n, smem, [&](int blk, unsigned char* sm) {
-    const CpuBlk B{(int64_t*)sm};
-    switch (fast) {
-      case EST_MIXED: body_fused_all<EST_MIXED>(B, blk, sm, a, md_cap); break;
-      case EST_SUMMARY: body_fused_all<EST_SUMMARY>(B, blk, sm, a, md_cap); break;
-      case EST_MODEL8: body_fused_all<EST_MODEL8>(B, blk, sm, a, md_cap); break;
-      case EST_MODEL16: body_fused_all<EST_MODEL16>(B, blk, sm, a, md_cap); break;
-      default: break;
-    }
-  });
-  return fast == EST_MIXED || fast == EST_SUMMARY || fast == EST_MODEL8 || fast == EST_MODEL16 ? 0 : -1;
-}
-
-int pair_list(stream_t, const SnapView& s, const BatchView& bv, const int32_t* list, const uint32_t* count, int max_n,
-              uint64_t* fmask, int32_t* est, int md_cap, size_t smem) {
-  const int n = (int)*count < max_n ? (int)*count : max_n;
-  grid(n, smem, [&](int blk, unsigned char* sm) {
-    body_pair_list<EST_GENERIC>(CpuBlk{(int64_t*)sm}, blk, n, sm, s, bv, list, count, max_n, fmask, est, md_cap);
-  });
   return 0;
 }
 

@@ -165,7 +165,11 @@ struct kp_batch {
   BatchView view{};
   // device work buffers
   uint64_t* fmask = nullptr;
-  int32_t* est = nullptr;
+  int32_t* est = nullptr;  // [B][Cp] per-binding rows (allocated on first use: rows mode, diagnosis entries)
+  // estimator classes (kp_filter.h): class of each binding (0 = non-workload) and
+  // a representative binding per class; their raw GeneralEstimator rows [n][Cp]
+  std::vector<int32_t> bcls, crep;
+  int32_t *d_bcls = nullptr, *d_crep = nullptr, *cls_rows = nullptr;
   int32_t *d_all = nullptr, *d_cluster = nullptr, *d_region = nullptr, *d_slowlist = nullptr, *d_cs = nullptr;
   int32_t *status = nullptr, *errc = nullptr, *slow = nullptr;
   int64_t* arg = nullptr;
@@ -200,6 +204,7 @@ struct kp_batch {
   ~kp_batch() {
     dev::host_release(h_cidx);
     dev::host_release(h_crep);
+    if (est) dev::release(est);
   }
   std::vector<RegionOut> h_rout;
 };
@@ -553,6 +558,72 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
     if (trep.empty()) trep.push_back(0);
   }
   int32_t *d_tset, *d_trep, *d_mt = nullptr;
+  // Cluster bitsets of the filter predicates (kp_filter.h; SnapView::bits).
+  std::vector<uint64_t> bits, bkey;
+  std::vector<int32_t> bval;
+  int32_t n_bits = 0, br_api = 0, br_tset = 0, br_lex = 0;
+  const int W = s->W;
+  if (W > 0 && (int)trep.size() <= kTsetRowsMax) {
+    const int G = (int)s->gvk.names.size();
+    std::unordered_map<uint64_t, int32_t> row_of;
+    std::vector<std::pair<uint64_t, int32_t>> order;  // (key, cluster) in row-assignment order
+    br_api = BR_FIXED;
+    br_tset = br_api + G;
+    br_lex = br_tset + (int)trep.size();
+    int32_t next = br_lex + K;
+    auto key_row = [&](uint64_t key) {
+      auto it = row_of.find(key);
+      if (it != row_of.end()) return it->second;
+      row_of.emplace(key, next);
+      return next++;
+    };
+    std::vector<std::pair<int32_t, int>> sets;  // (row, cluster) of the hashed rows
+    for (int k = 0; k < K; k++)
+      for (int r = 0; r < C; r++) {
+        const int32_t v = s->label_val[(size_t)k * Cp + r];
+        if (v >= 0) sets.push_back({key_row(bits_key(BK_LABEL, (uint32_t)k, v)), r});
+      }
+    for (int r = 0; r < C; r++) {
+      if (s->provider[r] >= 0) sets.push_back({key_row(bits_key(BK_PROVIDER, 0, s->provider[r])), r});
+      if (s->region[r] >= 0) sets.push_back({key_row(bits_key(BK_REGION, 0, s->region[r])), r});
+      for (int z = s->zone_off[r]; z < s->zone_off[r + 1]; z++)
+        sets.push_back({key_row(bits_key(BK_ZONE, 0, s->zone_ids[z])), r});
+    }
+    // within budget: the rows stay a small fraction of HBM even at large C
+    if ((uint64_t)next * (uint64_t)W * 8 <= ((uint64_t)256 << 20)) {
+      n_bits = next;
+      bits.assign((size_t)n_bits * W, 0);
+      auto set = [&](int32_t row, int r) { bits[(size_t)row * W + (r >> 6)] |= 1ull << (r & 63); };
+      for (int r = 0; r < C; r++) {
+        const uint32_t f = s->flags[r];
+        if (!(f & CF_DELETING)) set(BR_BASE, r);
+        if (f & CF_HAS_PROVIDER) set(BR_HAS_PROVIDER, r);
+        if (f & CF_HAS_REGION) set(BR_HAS_REGION, r);
+        if (f & CF_HAS_ZONES) set(BR_HAS_ZONES, r);
+        if (s->provider[r] >= 0) set(BR_PROV_SET, r);
+        if (s->region[r] >= 0) set(BR_REG_SET, r);
+        if (s->zone_off[r + 1] > s->zone_off[r]) set(BR_ZONE_ANY, r);
+        for (int g = 0; g < G; g++)
+          if ((s->api_bits[(size_t)(g >> 6) * Cp + r] >> (g & 63)) & 1ull) set(br_api + g, r);
+        set(br_tset + tset[r], r);
+        for (int k = 0; k < K; k++)
+          if (s->label_val[(size_t)k * Cp + r] >= 0) set(br_lex + k, r);
+      }
+      for (auto& x : sets) set(x.first, x.second);
+      size_t tsz = 16;
+      while (tsz < 2 * row_of.size()) tsz <<= 1;
+      bkey.assign(tsz, kBitsEmpty);
+      bval.assign(tsz, -1);
+      for (auto& kv : row_of) {
+        uint32_t i = bits_hash(kv.first) & (uint32_t)(tsz - 1);
+        while (bkey[i] != kBitsEmpty) i = (i + 1) & (uint32_t)(tsz - 1);
+        bkey[i] = kv.first;
+        bval[i] = kv.second;
+      }
+    }
+  }
+  uint64_t *d_bits = nullptr, *d_bkey = nullptr;
+  int32_t* d_bval = nullptr;
   // model node counts per (template, cluster): the fast estimator's dense form
   std::vector<int32_t> mt;
   {
@@ -593,6 +664,11 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
   a.add(&d_qa, s->qa.size());
   a.add(&d_tmpl, s->tmpl.size());
   a.add(&d_api, s->api_bits.size());
+  if (n_bits) {
+    a.add(&d_bits, bits.size());
+    a.add(&d_bkey, bkey.size());
+    a.add(&d_bval, bval.size());
+  }
   HIPCHK(a.alloc());
   std::vector<uint32_t> permp(Cp, 0);
   for (int r = 0; r < C; r++) permp[r] = s->perm[r];
@@ -621,6 +697,11 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
   HIPCHK(up(d_qa, s->qa.data(), 8 * s->qa.size()));
   HIPCHK(up(d_tmpl, s->tmpl.data(), 8 * s->tmpl.size()));
   HIPCHK(up(d_api, s->api_bits.data(), 8 * s->api_bits.size()));
+  if (n_bits) {
+    HIPCHK(up(d_bits, bits.data(), 8 * bits.size()));
+    HIPCHK(up(d_bkey, bkey.data(), 8 * bkey.size()));
+    HIPCHK(up(d_bval, bval.data(), 4 * bval.size()));
+  }
   HIPCHK(dev::sync(e->stream));
   v.flags = d_flags;
   v.perm = d_perm;
@@ -648,6 +729,14 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
   v.mg_cnt = d_mcnt;
   v.tmpl = d_tmpl;
   v.mt_cnt = d_mt;
+  v.bits = d_bits;
+  v.n_bits = n_bits;
+  v.br_api = br_api;
+  v.br_tset = br_tset;
+  v.br_lex = br_lex;
+  v.bkey = d_bkey;
+  v.bval = d_bval;
+  v.bmask = n_bits ? (uint32_t)(bkey.size() - 1) : 0u;
   s->est_kind = snapshot_est_kind(s);
   return KP_OK;
 }
@@ -1663,6 +1752,26 @@ int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_sna
 // list offsets inside Instr. The result equals a sequential pack (test_abi).
 // Threads: KP_PACK_THREADS, else the CPUs this process may use (hardware threads,
 // capped by a cgroup CPU quota), one per 4096 bindings at most.
+// Estimator class key of a packed binding: everything the GeneralEstimator reads
+// from it (est_load / est_compute_bf / template_md, kp_algo.h): whether it has
+// ReplicaRequirements and its summary and model requests (resource id, divisor).
+void est_key(const BindHdr& h, const Pools& p, std::string* k) {
+  k->clear();
+  auto put = [&](const void* v, size_t n) { k->append((const char*)v, n); };
+  const uint32_t rr = h.flags & BF_HAS_RR;
+  put(&rr, 4);
+  put(&h.sreq_cnt, 4);
+  for (int j = 0; j < h.sreq_cnt; j++) {
+    put(&p.ipool[h.sreq_off + j], 4);
+    put(&p.lpool[h.sreq_q_off + j], 8);
+  }
+  put(&h.mreq_cnt, 4);
+  for (int j = 0; j < h.mreq_cnt; j++) {
+    put(&p.ipool[h.mreq_off + j], 4);
+    put(&p.lpool[h.mreq_q_off + j], 8);
+  }
+}
+
 bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* bt) {
   int T = host_cpus();
   if (const char* v = getenv("KP_PACK_THREADS")) T = atoi(v);
@@ -1670,9 +1779,27 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
   std::vector<Pools> pl(T);
   std::vector<int> lo(T + 1);
   for (int t = 0; t <= T; t++) lo[t] = (int)((int64_t)n * t / T);
+  // estimator classes: thread-local ids (bt->bcls) and keys, unified below
+  bt->bcls.assign(n, 0);
+  std::vector<std::vector<std::string>> tkeys(T);
   auto run = [&](int t) {
     Packer pk{s, &pl[t]};
-    for (int i = lo[t]; i < lo[t + 1]; i++) pk.pack(bindings[i], bt->hdr[i]);
+    std::unordered_map<std::string, int32_t> ids;
+    std::string key;
+    for (int i = lo[t]; i < lo[t + 1]; i++) {
+      pk.pack(bindings[i], bt->hdr[i]);
+      if (bt->hdr[i].flags & BF_NONWORKLOAD_EST) {
+        bt->bcls[i] = -1;
+        continue;
+      }
+      est_key(bt->hdr[i], pl[t], &key);
+      auto it = ids.find(key);
+      if (it == ids.end()) {
+        it = ids.emplace(key, (int32_t)tkeys[t].size()).first;
+        tkeys[t].push_back(key);
+      }
+      bt->bcls[i] = it->second;
+    }
   };
   if (T == 1) {
     run(0);
@@ -1723,6 +1850,22 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
     bt->progs.insert(bt->progs.end(), q.progs.begin(), q.progs.end());
     bt->instrs.insert(bt->instrs.end(), q.instrs.begin(), q.instrs.end());
     q = Pools();
+  }
+  // global class ids (1-based; 0 = non-workload) and one representative per class
+  std::unordered_map<std::string, int32_t> gid;
+  bt->crep.assign(1, 0);
+  for (int t = 0; t < T; t++) {
+    std::vector<int32_t> remap(tkeys[t].size());
+    for (size_t j = 0; j < tkeys[t].size(); j++) {
+      auto it = gid.emplace(tkeys[t][j], (int32_t)gid.size() + 1).first;
+      remap[j] = it->second;
+      if ((size_t)it->second == bt->crep.size()) bt->crep.push_back(-1);
+    }
+    for (int i = lo[t]; i < lo[t + 1]; i++) {
+      const int32_t g = bt->bcls[i] < 0 ? 0 : remap[bt->bcls[i]];
+      bt->bcls[i] = g;
+      if (g && bt->crep[g] < 0) bt->crep[g] = i;
+    }
   }
   return true;
 }
@@ -1811,7 +1954,9 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&d_progs, bt->progs.size());
   a.add(&d_instrs, bt->instrs.size());
   a.add(&bt->fmask, (size_t)B * s->W);
-  a.add(&bt->est, (size_t)B * s->Cp);
+  a.add(&bt->d_bcls, B);
+  a.add(&bt->d_crep, bt->crep.size());
+  a.add(&bt->cls_rows, bt->crep.size() * (size_t)s->Cp);
   a.add(&bt->d_all, std::max<size_t>(1, bt->l_all.size()));
   a.add(&bt->d_cluster, std::max<size_t>(1, bt->l_cluster.size()));
   a.add(&bt->d_region, std::max<size_t>(1, bt->l_region.size()));
@@ -1851,6 +1996,8 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   HIPCHK(up(d_tols, bt->tols.data(), sizeof(Tol) * bt->tols.size()));
   HIPCHK(up(d_progs, bt->progs.data(), sizeof(Prog) * bt->progs.size()));
   HIPCHK(up(d_instrs, bt->instrs.data(), sizeof(Instr) * bt->instrs.size()));
+  HIPCHK(up(bt->d_bcls, bt->bcls.data(), 4 * bt->bcls.size()));
+  HIPCHK(up(bt->d_crep, bt->crep.data(), 4 * bt->crep.size()));
   HIPCHK(up(bt->d_all, bt->l_all.data(), 4 * bt->l_all.size()));
   HIPCHK(up(bt->d_cluster, bt->l_cluster.data(), 4 * bt->l_cluster.size()));
   HIPCHK(up(bt->d_region, bt->l_region.data(), 4 * bt->l_region.size()));
@@ -1876,6 +2023,19 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
 }
 
 void kp_batch_destroy(kp_batch* b) { delete b; }
+
+// The per-binding [B][Cp] calAvailableReplicas rows, allocated on first use (the
+// pair-row mode and the diagnosis entry points; the default path never needs them).
+static int ensure_rows(kp_engine* e, kp_batch* bt) {
+  if (bt->est) return 0;
+  void* p = nullptr;
+  if (dev::alloc(&p, 4 * (size_t)std::max(1, bt->B) * (size_t)bt->snap->Cp)) {
+    e->err = std::string("per-binding estimate rows: ") + dev::last_error();
+    return -1;
+  }
+  bt->est = (int32_t*)p;
+  return 0;
+}
 
 int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   if (!e || !bt || !out) return KP_EINVAL;
@@ -1923,14 +2083,14 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   HIPCHK(dev::stream_wait(sp, e->ev[0]));  // the fills above precede every kernel
   const int fast = getenv("KP_PAIR_GENERIC") || !bt->fast_ok ? EST_GENERIC : s->est_kind;
   const int md_cap = md_cap_of(s);
-  // KP_FUSE=1: SEL_ALL bindings take the fused pair + select kernel (fast estimator
-  // instance, LDS fits): their rows never leave LDS, and the pair kernel covers only
-  // the cluster/region-spread bindings, on stream2 beside it. Opt-in: on MI355X the
-  // fused kernel's LDS footprint (4 workgroups/CU) costs more than the row round trip
-  // saves (config 3: 10.2 vs 8.2 ms/step).
-  const char* fz = getenv("KP_FUSE");
-  const bool fused = fast != EST_GENERIC && !bt->l_all.empty() && fz && fz[0] == '1' &&
-                     fused_lds_bytes(s->Cp, md_cap) <= e->max_lds;
+  // Feasibility and calAvailableReplicas: by default (fast estimator instance and
+  // the snapshot's bitset rows built) the filter runs as bitset algebra (k_filter)
+  // and the estimator once per estimator class (k_est_class), kp_filter.h; else
+  // (or KP_PAIR_ROWS=1) the pair kernel writes every binding's rows.
+  const bool bits = fast != EST_GENERIC && s->view.n_bits > 0 && !getenv("KP_PAIR_ROWS");
+  if (!bits && ensure_rows(e, bt)) return KP_EDEVICE;
+  ka.est = bits ? bt->cls_rows : bt->est;
+  ka.bcls = bits ? bt->d_bcls : nullptr;
   SelectExtra sx;
   sx.rout = bt->rout;
   sx.rstat = bt->rstat;
@@ -1942,27 +2102,23 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   sx.lds_area = bt->slow_lds;
   sx.lds_sort = bt->slow_sort;
   const int cap = kSmallMax + kTgtSmallMax + 16;
-  const int n_pair = fused ? (int)bt->l_cs.size() : B;
   HIPCHK(dev::event_record(e->ev[3], sp));
-  if (n_pair > 0)
-    HIPCHK(dev::pair(sp, s->view, bt->view, fused ? bt->d_cs : nullptr, 0, n_pair, bt->fmask, bt->est, nullptr, 0,
-                     md_cap, smem_pair(s, md_cap), fast));
-  HIPCHK(dev::event_record(e->ev[4], sp));
-  if (fused) {
-    KArgs k = ka;
-    k.list = bt->d_all;
-    k.n = (int)bt->l_all.size();
-    HIPCHK(dev::event_record(e->ev[5], st));
-    HIPCHK(dev::fused_all(st, k, fused_lds_bytes(s->Cp, md_cap), md_cap, fast));
-    HIPCHK(dev::event_record(e->ev[6], st));
+  if (bits) {
+    HIPCHK(dev::est_class(sp, s->view, bt->view, bt->d_crep, (int)bt->crep.size(), bt->cls_rows, fast));
+    HIPCHK(dev::event_record(e->ev[5], sp));
+    HIPCHK(dev::filter(sp, s->view, bt->view, bt->fmask));
+  } else {
+    HIPCHK(dev::pair(sp, s->view, bt->view, nullptr, 0, B, bt->fmask, bt->est, nullptr, 0, md_cap, smem_pair(s, md_cap),
+                     fast));
   }
+  HIPCHK(dev::event_record(e->ev[4], sp));
   HIPCHK(dev::stream_wait(st, e->ev[4]));  // every pair row precedes the rest
   HIPCHK(dev::event_record(e->ev[1], st));
   // The three selection kinds touch disjoint bindings: SEL_ALL on stream2 (after the
   // pair kernel there), cluster spread on stream3, the region chain on stream, so a
   // latency-bound kernel shares the CUs with the others instead of running alone.
   HIPCHK(dev::event_record(e->ev[7], sp));
-  if (!fused && !bt->l_all.empty()) {
+  if (!bt->l_all.empty()) {
     KArgs k = ka;
     k.list = bt->d_all;
     k.n = (int)bt->l_all.size();
@@ -2044,9 +2200,6 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   }
   HIPCHK(dev::stream_wait(st, e->ev[8]));  // every fast-path flag precedes k_slow
   HIPCHK(dev::stream_wait(st, e->ev[9]));
-  if (fused)  // HBM rows of the bindings the fused kernel flagged for k_slow
-    HIPCHK(dev::pair_list(st, s->view, bt->view, bt->d_slowlist, bt->stats, (int)bt->l_slow.size(), bt->fmask, bt->est,
-                          md_cap, smem_pair(s, md_cap)));
   if (!bt->l_slow.empty()) {
     KArgs k = ka;
     k.list = bt->d_slowlist;
@@ -2099,20 +2252,21 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   }
   HIPCHK(dev::sync(st));
   double t1 = now_ms();
-  // pair: the pair launch (stream2); fused: the fused SEL_ALL kernel (stream);
-  // select: from the point where both are complete to the end of the last
+  // pair: the pair launch, or k_est_class + k_filter (stream2; filter: k_filter
+  // alone); select: from the point where they are complete to the end of the last
   // select kernel.
   const float ms_pair = dev::event_ms(e->ev[3], e->ev[4]);
-  const float ms_fused = fused ? dev::event_ms(e->ev[5], e->ev[6]) : 0.f;
+  const float ms_filter = bits ? dev::event_ms(e->ev[5], e->ev[4]) : 0.f;
   const float ms_sel = dev::event_ms(e->ev[1], e->ev[2]);
-  tm.pair_launches = n_pair > 0 ? 1 : 0;
+  tm.pair_launches = bits ? 2 : 1;
   tm.pair_kind = (uint32_t)fast;
   tm.pair_kernel_ms = ms_pair;
   tm.select_kernel_ms = ms_sel;
-  tm.fused_kernel_ms = ms_fused;
+  tm.filter_kernel_ms = ms_filter;
   tm.sel_all_kernel_ms = dev::event_ms(e->ev[7], e->ev[8]);
   tm.n_sel_all = (uint32_t)bt->l_all.size();
-  tm.fused = fused ? 1u : 0u;
+  tm.bits = bits ? 1u : 0u;
+  tm.n_classes = bits ? (uint32_t)bt->crep.size() : 0u;
   tm.n_slow = bt->h_stats[0];
 #ifdef KP_STAMPS
   {
@@ -2149,6 +2303,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
 
 // Runs the pair kernel and returns the rank-ordered device row pointers.
 static int run_pair(kp_engine* e, kp_batch* bt, int64_t* score, int est_mode, int b0, int nb) {
+  if (ensure_rows(e, bt)) return KP_EDEVICE;
   kp_snapshot* s = bt->snap;
   HIPCHK(dev::pair(e->stream, s->view, bt->view, nullptr, b0, nb, bt->fmask, bt->est, score, est_mode, md_cap_of(s),
                      smem_pair(s, md_cap_of(s))));
@@ -2161,8 +2316,12 @@ int kp_filter_batch(kp_engine* e, kp_batch* bt, uint64_t* out_mask) {
   (void)dev::set_device(e->device);
   kp_snapshot* s = bt->snap;
   if (bt->B == 0) return KP_OK;
-  int rc = run_pair(e, bt, nullptr, 0, 0, bt->B);
-  if (rc) return rc;
+  if (s->view.n_bits > 0 && !getenv("KP_PAIR_ROWS")) {  // the schedule path's bitset filter
+    HIPCHK(dev::filter(e->stream, s->view, bt->view, bt->fmask));
+  } else {
+    int rc = run_pair(e, bt, nullptr, 0, 0, bt->B);
+    if (rc) return rc;
+  }
   std::vector<uint64_t> m((size_t)bt->B * s->W);
   HIPCHK(dev::d2h(m.data(), bt->fmask, 8 * m.size(), e->stream));
   HIPCHK(dev::sync(e->stream));

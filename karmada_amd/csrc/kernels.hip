@@ -54,29 +54,23 @@ KP_PAIR_FAST(k_pair_fast, EST_MIXED)
 KP_PAIR_FAST(k_pair_fast_summary, EST_SUMMARY)
 KP_PAIR_FAST(k_pair_fast_m8, EST_MODEL8)
 KP_PAIR_FAST(k_pair_fast_m16, EST_MODEL16)
-// Fused pair + SEL_ALL select, one instance per estimator kind (fast batches only).
-#ifndef KP_FUSED_THREADS
-#define KP_FUSED_THREADS 256
-#endif
-#ifndef KP_FUSED_MIN_WAVES
-#define KP_FUSED_MIN_WAVES 1
-#endif
-#define KP_FUSED(NAME, KIND)                                                                             \
-  extern "C" __global__ void __launch_bounds__(KP_FUSED_THREADS, KP_FUSED_MIN_WAVES) NAME(KArgs a, int md_cap) { \
-    KP_SMEM;                                                                                             \
-    body_fused_all<KIND>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, md_cap);                      \
+// Estimator-class rows (kp_filter.h), one instance per estimator kind.
+#define KP_EST_CLASS(NAME, KIND)                                                                              \
+  extern "C" __global__ void __launch_bounds__(kBlock) NAME(SnapView s, BatchView bv, const int32_t* rep,      \
+                                                             int32_t* rows) {                                 \
+    KP_SMEM;                                                                                                  \
+    body_est_class<KIND>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, rep, rows);                    \
   }
-KP_FUSED(k_fused_all, EST_MIXED)
-KP_FUSED(k_fused_all_summary, EST_SUMMARY)
-KP_FUSED(k_fused_all_m8, EST_MODEL8)
-KP_FUSED(k_fused_all_m16, EST_MODEL16)
-// Pair rows of the bindings flagged for k_slow (persistent grid over the device list).
-extern "C" __global__ void __launch_bounds__(kBlock) k_pair_list(SnapView s, BatchView bv, const int32_t* list,
-                                                                 const uint32_t* count, int max_n, uint64_t* fmask,
-                                                                 int32_t* est, int md_cap) {
-  KP_SMEM;
-  body_pair_list<EST_GENERIC>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, (int)gridDim.x, smem, s, bv, list, count, max_n,
-                              fmask, est, md_cap);
+KP_EST_CLASS(k_est_class, EST_MIXED)
+KP_EST_CLASS(k_est_class_summary, EST_SUMMARY)
+KP_EST_CLASS(k_est_class_m8, EST_MODEL8)
+KP_EST_CLASS(k_est_class_m16, EST_MODEL16)
+// Feasibility rows by bitset algebra: one wave64 per binding, kFilterWaves per workgroup.
+constexpr int kFilterWaves = 4;
+extern "C" __global__ void __launch_bounds__(64 * kFilterWaves) k_filter(SnapView s, BatchView bv, uint64_t* fmask) {
+  const int b = (int)(blockIdx.x * kFilterWaves + (threadIdx.x >> 6));
+  if (b >= bv.B) return;  // wave-uniform
+  body_filter(GpuBlk{nullptr}, b, s, bv, fmask);
 }
 extern "C" __global__ void __launch_bounds__(KP_SEL_MAX_THREADS, KP_SEL_MIN_WAVES) k_select_all(KArgs a) {
   KP_SMEM;
@@ -227,6 +221,26 @@ int pair(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* lis
   return chk(hipGetLastError());
 }
 
+int est_class(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* rep, int n_rows, int32_t* rows,
+              int fast) {
+  if (n_rows <= 0) return 0;
+  auto* k = fast == EST_MIXED     ? k_est_class
+            : fast == EST_SUMMARY ? k_est_class_summary
+            : fast == EST_MODEL8  ? k_est_class_m8
+            : fast == EST_MODEL16 ? k_est_class_m16
+                                  : nullptr;
+  if (!k) return chk(hipErrorInvalidValue);
+  hipLaunchKernelGGL(k, dim3(n_rows), dim3(kBlock), kRedBytes + 4 * kTmplDense, (hipStream_t)st, s, bv, rep, rows);
+  return chk(hipGetLastError());
+}
+
+int filter(stream_t st, const SnapView& s, const BatchView& bv, uint64_t* fmask) {
+  if (bv.B <= 0 || s.W <= 0) return 0;
+  hipLaunchKernelGGL(k_filter, dim3((bv.B + kFilterWaves - 1) / kFilterWaves), dim3(64 * kFilterWaves), 0,
+                     (hipStream_t)st, s, bv, fmask);
+  return chk(hipGetLastError());
+}
+
 int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x) {
   if (a.n <= 0) return 0;
   hipStream_t h = (hipStream_t)st;
@@ -256,29 +270,6 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
     default:
       return chk(hipErrorInvalidValue);
   }
-  return chk(hipGetLastError());
-}
-
-int fused_all(stream_t st, const KArgs& a, size_t smem, int md_cap, int fast) {
-  if (a.n <= 0) return 0;
-  auto* kf = fast == EST_MIXED     ? k_fused_all
-             : fast == EST_SUMMARY ? k_fused_all_summary
-             : fast == EST_MODEL8  ? k_fused_all_m8
-             : fast == EST_MODEL16 ? k_fused_all_m16
-                                   : nullptr;
-  if (!kf) return chk(hipErrorInvalidValue);
-  if (smem > 65536 && chk(hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)))
-    return -1;
-  hipLaunchKernelGGL(kf, dim3(a.n), dim3(KP_FUSED_THREADS), smem, (hipStream_t)st, a, md_cap);
-  return chk(hipGetLastError());
-}
-
-int pair_list(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* list, const uint32_t* count,
-              int max_n, uint64_t* fmask, int32_t* est, int md_cap, size_t smem) {
-  if (max_n <= 0) return 0;
-  const int grid = max_n < 256 ? max_n : 256;
-  hipLaunchKernelGGL(k_pair_list, dim3(grid), dim3(kBlock), smem, (hipStream_t)st, s, bv, list, count, max_n, fmask,
-                     est, md_cap);
   return chk(hipGetLastError());
 }
 

@@ -46,14 +46,14 @@ int fill(void* dst, int value, size_t bytes, stream_t s);
 // Pair rows of bindings list[b0 + i] (or b0 + i when list is null), i < nb.
 int pair(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* list, int b0, int nb, uint64_t* fmask,
          int32_t* est, int64_t* score, int est_mode, int md_cap, size_t smem, int fast = 0);
+// Estimator-class rows: rows[k][Cp] for k < n_rows (body_est_class; row 0 MaxInt32),
+// class k's representative binding rep[k]; fast = EST_* kind (not EST_GENERIC).
+int est_class(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* rep, int n_rows, int32_t* rows,
+              int fast);
+// Feasibility rows fmask[b][W] of every binding by bitset algebra (body_filter;
+// requires s.n_bits > 0).
+int filter(stream_t st, const SnapView& s, const BatchView& bv, uint64_t* fmask);
 int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x);
-// Fused pair + SEL_ALL select over a.list[0, a.n) (body_fused_all); fast = EST_* kind
-// (not EST_GENERIC).
-int fused_all(stream_t st, const KArgs& a, size_t smem, int md_cap, int fast);
-// Pair rows (fmask/est) of list[0, *count) (device count, at most max_n): the
-// bindings the fused kernel flagged for k_slow.
-int pair_list(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* list, const uint32_t* count,
-              int max_n, uint64_t* fmask, int32_t* est, int md_cap, size_t smem);
 // selectGroups for n region bindings (one thread each): rsel/rnsel as the host
 // step writes them; *nhost counts the bindings left to the host (kGroupsHost).
 int region_groups(stream_t st, const RegionOut* rout, const int32_t* rstat, const BindHdr* hdr, const int32_t* list,

@@ -16,6 +16,7 @@
 #include "kp_launch.h"
 #include "kp_paths.h"
 #include "kp_pdq.h"
+#include "kp_filter.h"
 
 namespace kp {
 
@@ -26,7 +27,16 @@ KP_HD inline SelCtx make_ctx(const KArgs& a, int b, const uint32_t* tgt_bits) {
   x.h = &a.bv.hdr[b];
   x.b = b;
   x.frow = a.fmask + (size_t)b * a.s.W;
-  x.erow = a.est + (size_t)b * a.s.Cp;
+  if (a.bcls) {
+    const int32_t k = a.bcls[b];
+    x.erow = a.est + (size_t)k * a.s.Cp;
+    x.mrep = k ? x.h->replicas : kInt32Max;
+    x.merge = true;
+  } else {
+    x.erow = a.est + (size_t)b * a.s.Cp;
+    x.mrep = kInt32Max;
+    x.merge = false;
+  }
   x.tgt_bits = tgt_bits;
   x.sink = a.sink;
   x.dbg = a.dbg;
@@ -232,6 +242,28 @@ KP_FI void pair_one(const BLK& B, int b, unsigned char* smem, const SnapView& s,
   }
 }
 
+// k_est_class: row k of the estimator classes' raw GeneralEstimator answers
+// (est_compute_bf, the pair kernel's arithmetic) for every cluster, from the
+// class's representative binding rep[k]; row 0 (non-workload bindings, whose
+// calAvailableReplicas is MaxInt32, core/util.go:69-73) is MaxInt32.
+template <int Fast, class BLK>
+KP_FI void body_est_class(const BLK& B, int k, unsigned char* smem, const SnapView& s, const BatchView& bv,
+                          const int32_t* rep, int32_t* rows) {
+  int32_t* row = rows + (size_t)k * s.Cp;
+  if (k == 0) {
+    for (int c = B.tid(); c < s.Cp; c += B.nth()) row[c] = kInt32Max;
+    return;
+  }
+  const BindHdr h = bv.hdr[rep[k]];
+  int32_t* md = (int32_t*)(smem + kRedBytes);  // MaxDivided per template, zero past n_tmpl
+  const bool rr = (h.flags & BF_HAS_RR) != 0;
+  for (int t = B.tid(); t < kTmplDense; t += B.nth()) md[t] = rr && t < s.n_tmpl ? template_md(s, bv, h, t) : 0;
+  B.sync();
+  const MdTab mdt = md_regs(md);
+  for (int c = B.tid(); c < s.Cp; c += B.nth())
+    row[c] = est_compute_bf<Fast>(s, bv, h, c, mdt.v, est_load<Fast>(s, bv, h, c, ldcol(s.flags, c)));
+}
+
 // Pair stage for binding list[b0 + blk] (b0 + blk without a list): each wave evaluates 64 consecutive clusters
 // (coalesced SoA columns), stores their feasibility as one u64 word and
 // calAvailableReplicas per cluster. est_mode 1: raw GeneralEstimator answers for
@@ -241,20 +273,6 @@ KP_FI void body_pair(const BLK& B, int blk, unsigned char* smem, const SnapView&
                      const int32_t* list, int b0, uint64_t* fmask, int32_t* est, int64_t* score, int est_mode,
                      int md_cap) {
   pair_one<Fast>(B, list ? list[b0 + blk] : b0 + blk, smem, s, bv, fmask, est, score, est_mode, md_cap);
-}
-
-// Pair stage for the bindings flagged for k_slow (list entries [0, *count),
-// appended on the device by the select kernels), persistent over the grid:
-// the fused SEL_ALL kernel keeps its rows in LDS, and k_slow reads them from HBM.
-template <int Fast, class BLK>
-KP_FI void body_pair_list(const BLK& B, int blk, int grid, unsigned char* smem, const SnapView& s,
-                          const BatchView& bv, const int32_t* list, const uint32_t* count, int max_n, uint64_t* fmask,
-                          int32_t* est, int md_cap) {
-  const int n = (int)*(const volatile uint32_t*)count;
-  for (int i = blk; i < n && i < max_n; i += grid) {
-    B.sync();  // the previous binding's LDS readers are done
-    pair_one<Fast>(B, list[i], smem, s, bv, fmask, est, nullptr, 0, md_cap);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -312,57 +330,6 @@ KP_FI void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
   KP_STAMP(x, 1);
   LdsCands cs{&cd, B.tid(), B.nth()};
   select_all_common(B, a, x, cs, cd.F, ss);
-}
-
-// ---------------------------------------------------------------------------
-// Fused pair + SEL_ALL select (k_fused_all): one workgroup per SEL_ALL binding.
-// The pair stage leaves the binding's feasibility bits and per-cluster votes
-// (calAvailableReplicas, or the StaticWeight vote) in LDS, and the assignment
-// reads them there: no per-pair row is written to HBM and read back. Bindings
-// the fast assignment refuses are flagged for k_slow; k_pair_list writes their
-// HBM rows (the same pair body) before k_slow reads them.
-// LDS: [red | tgt bits | fit u64[W] | row i32[Cp] | union{ pair: PairLds tail ; select: SelScratch }]
-// ---------------------------------------------------------------------------
-template <int Fast, class BLK>
-KP_FI void body_fused_all(const BLK& B, int blk, unsigned char* smem, const KArgs& a, int md_cap) {
-  if (blk >= a.n) return;
-  KP_STAMP_INIT
-  const int b = a.list[blk];
-  const SnapView& s = a.s;
-  const BindHdr h = a.bv.hdr[b];
-  const int words = (s.Cp + 31) >> 5;
-  uint32_t* tgt = (uint32_t*)(smem + kRedBytes);
-  uint64_t* fit = (uint64_t*)(tgt + ((words + 3) & ~3));
-  int32_t* row = (int32_t*)(fit + ((s.W + 1) & ~1));
-  unsigned char* un = (unsigned char*)(row + s.Cp);
-  const PairLds L = pair_lds_carve(tgt, un, s.Cp, md_cap);
-  bool use_md, use_ts;
-  (void)pair_setup(B, s, a.bv, h, L, 0, md_cap, &use_md, &use_ts, false);
-  const MdTab mdt = md_regs(L.md);
-  // StaticWeight SEL_ALL bindings vote with their static weights: the estimator is
-  // not evaluated for them (getStaticWeightInfoList, division_algorithm.go:38-72).
-  const bool weights = h.strategy == ST_STATIC && h.sel == SEL_ALL;
-  BindHdr hp = h;
-  if (weights) hp.flags |= BF_NONWORKLOAD_EST;
-  KP_STAMPD(a.dbg, 0);  // pair setup
-  int32_t mine = 0;
-  pair_loop_fast<Fast>(B, s, a.bv, hp, L, mdt, [&](int c, bool ok, int32_t v) {
-    if (weights && ok) v = static_vote_u(s, a.bv, h, c);
-    B.mask_store(fit, c, ok, s.W);
-    row[c] = v;
-    mine += ok ? 1 : 0;
-  });
-  const int F = (int)B.sum64(mine);  // (its barrier also publishes fit and row)
-  KP_STAMPD(a.dbg, 15);  // pair loop
-  SelCtx x = make_ctx(a, b, tgt);
-  x.frow = fit;
-  x.erow = row;
-  const SelScratch ss = carve_sel_scratch(un, s.Cp);  // the pair state is dead now
-#ifdef KP_EXP_NOSEL  // timing experiments only (tuning variants, wrong answers)
-  if (B.tid() == 0) sink_error(x, KP_STATUS_OK, 0, F);
-  return;
-#endif
-  select_all_common(B, a, x, RowCands{fit, row, s.C, B.tid(), B.nth()}, F, ss);
 }
 
 // ---------------------------------------------------------------------------

@@ -14,7 +14,11 @@ struct KArgs {
   const int32_t* list;    // binding ids handled by this launch
   int32_t n;
   const uint64_t* fmask;  // [B][W]
-  const int32_t* est;     // [B][Cp]
+  // calAvailableReplicas rows: [B][Cp] merged per binding (bcls == nullptr), or
+  // [n_classes][Cp] raw GeneralEstimator rows of the estimator classes, binding b
+  // reading row bcls[b] (row 0: non-workload bindings, MaxInt32).
+  const int32_t* est;
+  const int32_t* bcls;
   Sink sink;
   int32_t* slow;          // [B] SLOW_* reason the binding needs k_slow for (0: none)
   int32_t* slow_ids;      // bindings flagged for k_slow, [0, stats[0]) (append order)
@@ -60,13 +64,5 @@ KP_HD inline int sel_all_ecap(int Cp) { return Cp / 2 < 64 ? 64 : (Cp / 2 > KP_E
 KP_HD inline size_t pair_lds_tail_bytes(int Cp, int md_cap) {  // evict | md | stage | tolb
   const int words = (Cp + 31) >> 5;
   return 4 * (size_t)((words + 3) & ~3) + 4 * (size_t)((md_cap + 3) & ~3) + kPairStage + kTsetMax / 8;
-}
-// Dynamic LDS of k_fused_all (kp_kernels.h body_fused_all).
-KP_HD inline size_t fused_lds_bytes(int Cp, int md_cap) {
-  const int words = (Cp + 31) >> 5, W = Cp / 64;
-  const size_t pair_tail = pair_lds_tail_bytes(Cp, md_cap);
-  const size_t sel = 3072 + 8 * (size_t)sel_all_ecap(Cp);
-  return kRedBytes + 4 * (size_t)((words + 3) & ~3) + 8 * (size_t)((W + 1) & ~1) + 4 * (size_t)Cp +
-         (pair_tail > sel ? pair_tail : sel) + 64;
 }
 }  // namespace kp

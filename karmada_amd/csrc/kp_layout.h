@@ -14,6 +14,7 @@
 #include <stdint.h>
 
 #include "../../include/kp/kp_api.h"
+#include "kp_blk.h"
 
 namespace kp {
 
@@ -160,7 +161,42 @@ struct SnapView {
   const int32_t* mt_cnt;         // [n_tmpl][Cp] model nodes per template, clamped to MaxInt32, or
                                  // nullptr (n_tmpl > kTmplDense or a negative template value)
   const uint32_t* perm;          // rank -> caller index
+  // Cluster bitsets ("postings" of every filter predicate, bit c of word c >> 6;
+  // kp_filter.h): fixed rows (BR_*), the API-enablement row of each GVK, the row of
+  // each taint list, then one row per (label key, value), provider, region and zone
+  // value, found through an open-addressed table keyed by bits_key(). n_bits == 0:
+  // not built (over budget, or more than kTsetRowsMax taint lists).
+  const uint64_t* bits;          // [n_bits][W]
+  int32_t n_bits;
+  int32_t br_api, br_tset, br_lex;  // first row of: GVK rows, taint-list rows, label-exists rows
+  const uint64_t* bkey;          // [bmask + 1] table keys (kBitsEmpty = free)
+  const int32_t* bval;           // [bmask + 1] row of the key
+  uint32_t bmask;
 };
+
+// Fixed bitset rows.
+enum : int32_t {
+  BR_BASE = 0,      // c < C and not deleting (findClustersThatFit, generic_scheduler.go:140-143)
+  BR_HAS_PROVIDER,  // CF_HAS_PROVIDER (SpreadConstraint filter)
+  BR_HAS_REGION,
+  BR_HAS_ZONES,
+  BR_PROV_SET,      // provider string id >= 0 (field selector Exists)
+  BR_REG_SET,
+  BR_ZONE_ANY,      // at least one zone (matchZones Exists)
+  BR_FIXED
+};
+enum : uint64_t { BK_LABEL = 1, BK_PROVIDER = 2, BK_REGION = 3, BK_ZONE = 4 };
+constexpr uint64_t kBitsEmpty = ~0ull;
+constexpr int kTsetRowsMax = 64;  // taint lists answered by one ballot word per binding
+KP_HD inline uint64_t bits_key(uint64_t kind, uint32_t slot, int32_t vid) {
+  return (kind << 60) | ((uint64_t)slot << 32) | (uint64_t)(uint32_t)vid;
+}
+KP_HD inline uint32_t bits_hash(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  return (uint32_t)k;
+}
 
 struct BatchView {
   int32_t B;

@@ -28,7 +28,7 @@ KP_HD inline uint64_t cand_key(const SelCtx& x, const Cands& cd, int i, int32_t 
 KP_HD inline Item item_from_key(const SelCtx& x, uint64_t k) {
   Item it;
   it.rank = key_rank(k);
-  it.alloc = x.erow[it.rank];
+  it.alloc = est_at(x, (int)it.rank);
   it.avail = key_avail(k);
   it.ovf = key_ovf(k);
   it.pad = 0;
@@ -69,29 +69,6 @@ struct LdsCands {  // candidates compacted in LDS (gather)
   KP_FI uint64_t okey(const SelCtx& x, uint32_t rk, int32_t v0) const { return cand_order_key(x, rk, v0); }
   static constexpr bool kExact = false;  // okey is sort.Sort's output order only for <= 12 (stable insertion)
 };
-// The fused pair + select kernel's candidates: the clusters whose feasibility
-// bit is set in the LDS bitset `fit` (u64 words, the fmask row layout), with
-// v = row[c] (calAvailableReplicas, or the StaticWeight vote) in LDS. Thread t
-// owns clusters t + nth*j.
-struct RowCands {
-  const uint64_t* fit;
-  int32_t* row;
-  int C, tid, nth;
-  template <class Fn>
-  KP_FI void each(Fn fn) const {
-    for (int c = tid; c < C; c += nth)
-      if ((fit[c >> 6] >> (c & 63)) & 1ull) fn((uint32_t)c, row[c]);
-  }
-  template <class Fn>
-  KP_FI void each_set(Fn fn) const {
-    for (int c = tid; c < C; c += nth)
-      if ((fit[c >> 6] >> (c & 63)) & 1ull) row[c] = fn((uint32_t)c, row[c]);
-  }
-  static constexpr bool kSettable = true;
-  KP_FI uint64_t okey(const SelCtx& x, uint32_t rk, int32_t v0) const { return cand_order_key(x, rk, v0); }
-  static constexpr bool kExact = false;
-};
-
 // Gathered candidates (any memory) whose sort.Sort output order is known:
 // pos[rank] = position after the emulated sort (k_slow, kp_pdq.h).
 struct PosCands {
@@ -246,7 +223,7 @@ KP_HD inline bool scale_down_targets(const SelCtx& x, unsigned char* mem, size_t
     if (!mask_test(x.frow, (int)r)) continue;
     assigned = add32(assigned, x.bv->ipool[h.tgt_off + 2 * j + 1]);
     items[n].rank = r;
-    items[n].alloc = x.erow[r];
+    items[n].alloc = est_at(x, (int)r);
     items[n].avail = 0;
     items[n].ovf = 0;
     items[n].pad = 0;
@@ -506,7 +483,7 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
     // whose merged replicas are > 0 (MergeTargetClusters), instead of walking every
     // candidate. Same multiset as the full walk below.
     auto in_list = [&](uint32_t rk) {
-      const int32_t v0 = x.erow[rk];
+      const int32_t v0 = est_at(x, (int)rk);
       const int64_t v = vote32(rk, v0);
       return member(rk, v, v0) && v >= w.Lb;
     };

@@ -76,11 +76,19 @@ struct SelCtx {
   const BindHdr* h;
   int b;
   const uint64_t* frow;
+  // calAvailableReplicas of cluster c = est_at(x, c): erow is either the binding's
+  // own merged row (merge == false) or its estimator class's raw GeneralEstimator
+  // row, merged here with spec.Replicas (mrep) as cal_merge_bf does.
   const int32_t* erow;
+  int32_t mrep;
+  bool merge;
   const uint32_t* tgt_bits;
   Sink sink;
   unsigned long long* dbg;  // diagnostic build only (KP_STAMPS): per-phase cycle sums
 };
+
+KP_HD inline int32_t est_merge(const SelCtx& x, int32_t r) { return x.merge ? cal_merge_bf(x.mrep, r) : r; }
+KP_HD inline int32_t est_at(const SelCtx& x, int c) { return est_merge(x, x.erow[c]); }
 
 // Diagnostic phase stamps (a separate -DKP_STAMPS build; never in libkp.so).
 #if defined(KP_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
@@ -589,7 +597,7 @@ KP_UNROLL
       for (int q = 0; q < 4; q++)
         if ((fm[j] >> q) & 1u) {
           cd.r[pos] = (uint32_t)(4 * (tid + nth * j) + q);
-          cd.v[pos] = ev[j].v[q];
+          cd.v[pos] = est_merge(x, ev[j].v[q]);
           pos++;
         }
     B.sync();
@@ -610,7 +618,7 @@ KP_UNROLL
   for (int c = tid; c < s.C; c += nth)
     if (mask_test(x.frow, c)) {
       cd.r[pos] = (uint32_t)c | ((uint32_t)overflow_order(s, *x.bv, h, c) << kRankBits);
-      cd.v[pos] = weights ? static_vote(x, c) : x.erow[c];
+      cd.v[pos] = weights ? static_vote(x, c) : est_at(x, c);
       pos++;
     }
   B.sync();

@@ -21,18 +21,19 @@ def engine():
     e.close()
 
 
-def run(engine, u, opts, lo=0, hi=None, fuse=False, times=None):
-    """Schedules bindings [lo, hi); fuse=True takes the fused SEL_ALL kernel
-    (KP_FUSE=1), times (a list) receives the call's kp_stage_times."""
+def run(engine, u, opts, lo=0, hi=None, rows=False, times=None):
+    """Schedules bindings [lo, hi); rows=True forces the per-binding pair rows
+    (KP_PAIR_ROWS=1) instead of the bitset filter + estimator classes, times (a
+    list) receives the call's kp_stage_times."""
     hi = u.n_bindings if hi is None else hi
     snap = Snapshot.from_structs(engine, u.clusters, u.n_clusters, u.names, opts)
     b = Batch(snap, structs=u.binding_slice(lo, hi))
-    if fuse:
-        os.environ["KP_FUSE"] = "1"
+    if rows:
+        os.environ["KP_PAIR_ROWS"] = "1"
     try:
         out = b.schedule()
     finally:
-        os.environ.pop("KP_FUSE", None)
+        os.environ.pop("KP_PAIR_ROWS", None)
     if times is not None:
         times.append(engine.stage_times())
     b.close()
@@ -50,21 +51,21 @@ def compare(got, want, label):
         pytest.fail("\n".join(msg))
 
 
-@pytest.mark.parametrize("fuse", [True, False], ids=["fused", "two-kernel"])
+@pytest.mark.parametrize("rows", [False, True], ids=["bits", "rows"])
 @pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
     (1, 1, 10, 1000), (2, 2, 300, 400), (3, 3, 200, 300), (4, 4, 400, 500),
     (6, 6, 120, 1500), (6, 7, 40, 1500), (6, 8, 1, 200), (6, 9, 257, 600),
     (7, 17, 300, 400), (7, 18, 13, 300), (5, 5, 500, 600),
 ])
-def test_cpusim_schedule_parity(engine, config, seed, n_clusters, n_bindings, fuse):
+def test_cpusim_schedule_parity(engine, config, seed, n_clusters, n_bindings, rows):
     u = synth.Universe(config, seed, n_clusters, 0, n_bindings)
     opts = api.options()
     ba, n = u.binding_slice(0, n_bindings)
     want = O.schedule_c(u.clusters, u.n_clusters, ba, n, opts, O.FAST, 8)
     times = []
-    compare(run(engine, u, opts, fuse=fuse, times=times), want, f"config {config} seed {seed}")
-    if config in (2, 3, 5, 7):  # fast estimator instances with SEL_ALL bindings
-        assert times[0]["fused"] == int(fuse)
+    compare(run(engine, u, opts, rows=rows, times=times), want, f"config {config} seed {seed}")
+    if config in (2, 3, 5, 7):  # fast estimator instances
+        assert times[0]["bits"] == int(not rows)
 
 
 @pytest.mark.parametrize("prop,plugins,gate", [

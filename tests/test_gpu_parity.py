@@ -94,19 +94,21 @@ def test_schedule_parity(engine, config, seed, n_clusters, n_bindings):
 @pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
     (3, 3, 500, 1000), (2, 2, 1000, 1000), (5, 5, 3000, 1200), (7, 17, 2000, 1000), (3, 3, 5000, 1000),
 ])
-def test_schedule_parity_fused(engine, config, seed, n_clusters, n_bindings):
-    """The opt-in fused pair + SEL_ALL kernel (KP_FUSE=1, k_fused_all*)."""
+def test_schedule_parity_pair_rows(engine, config, seed, n_clusters, n_bindings):
+    """The per-binding pair-row route (KP_PAIR_ROWS=1: k_pair_fast_* writes every
+    binding's feasibility and calAvailableReplicas rows) beside the default
+    bitset filter + estimator classes."""
     import os
     u = synth.Universe(config, seed, n_clusters, 0, n_bindings)
     opts = api.options()
-    os.environ["KP_FUSE"] = "1"
+    os.environ["KP_PAIR_ROWS"] = "1"
     try:
         got = gpu_schedule(engine, u, opts)
-        fused = engine.stage_times()["fused"]
+        bits = engine.stage_times()["bits"]
     finally:
-        os.environ.pop("KP_FUSE", None)
-    compare(got, oracle_schedule(u, opts), f"fused config {config} seed {seed}")
-    assert fused == 1
+        os.environ.pop("KP_PAIR_ROWS", None)
+    compare(got, oracle_schedule(u, opts), f"pair rows config {config} seed {seed}")
+    assert bits == 0
 
 
 @pytest.mark.parametrize("prop,plugins,gate", [
