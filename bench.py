@@ -331,7 +331,8 @@ def main():
         # filter stage: k_est_class + k_filter (bits mode) or the pair kernel
         "stages_ms": {"filter_stage": round(pair_ms, 3), "filter_kernel": round(filter_ms, 3),
                       "select_kernels": round(sel_ms, 3), "sel_all_kernel": round(sel_all_ms, 3),
-                      "host_region": round(avg("host_ms"), 3)},
+                      "host_region": round(avg("host_ms"), 3), "copy_back": round(avg("copy_ms"), 3),
+                      "call_total": round(avg("total_ms"), 3)},
         "filter_mode": "bitset filter + estimator classes" if bits else "per-binding pair rows",
         "estimator_classes": int(last["n_classes"]) if bits else None,
         # bindings/s including host packing + upload: pipelined over two engines (the

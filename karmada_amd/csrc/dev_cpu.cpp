@@ -137,6 +137,9 @@ int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const Sele
            [&](int blk, unsigned char* sm) { body_select_all(CpuBlk{(int64_t*)sm}, blk, sm, a); });
       break;
     }
+    case SEL_LAUNCH_ALL_STREAM:
+      grid(a.n, smem, [&](int blk, unsigned char* sm) { body_select_all_stream(CpuBlk{(int64_t*)sm}, blk, sm, a); });
+      break;
     case SEL_LAUNCH_CLUSTER:
       grid(a.n, smem,
            [&](int blk, unsigned char* sm) { body_select_cluster(CpuBlk{(int64_t*)sm}, blk, sm, a, cap); });
@@ -180,6 +183,14 @@ int component_sets(stream_t, const SnapView& s, const SetsArgs* A, const int32_t
 int reasons(stream_t, const SnapView& s, const BatchView& bv, uint32_t* out) {
   const uint64_t n = (uint64_t)bv.B * (uint64_t)s.C;
   for (uint64_t i = 0; i < n; i++) body_reasons(s, bv, i, out);
+  return 0;
+}
+
+int offsets(stream_t, const int32_t* status, const uint32_t* count, int n, uint64_t* off, uint64_t* part) {
+  int64_t red[8];
+  const int nb = (n + kOffChunk - 1) / kOffChunk;
+  for (int k = 0; k < nb; k++) body_offsets_a(CpuBlk{red}, k, status, count, n, off, part);
+  for (int k = 0; k < nb; k++) body_offsets_b(CpuBlk{red}, k, nb, n, off, part);
   return 0;
 }
 

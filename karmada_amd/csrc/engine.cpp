@@ -160,6 +160,7 @@ struct kp_batch {
   std::vector<Prog> progs;
   std::vector<Instr> instrs;
   std::vector<int32_t> l_all, l_cluster, l_region, l_slow, l_cs;  // l_cs: cluster + region bindings
+  int n_all_dyn = 0;  // l_all = [other strategies | StaticWeight]: the first n_all_dyn are not StaticWeight
   uint64_t out_cap = 0;
   Arena dev;
   BatchView view{};
@@ -182,6 +183,7 @@ struct kp_batch {
   uint32_t* out_idx = nullptr;
   int32_t* out_rep = nullptr;
   uint64_t* offsets_d = nullptr;
+  uint64_t* off_part = nullptr;  // per-chunk totals of the offsets scan
   uint32_t* cidx_d = nullptr;
   int32_t* crep_d = nullptr;
   RegionOut* rout = nullptr;
@@ -1892,6 +1894,10 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
     else if (h.sel == SEL_REGION) bt->l_region.push_back((int32_t)i);
     else bt->l_all.push_back((int32_t)i);
   }
+  // SEL_ALL bindings: StaticWeight last (they take the streamed-candidate kernel, kp_kernels.h)
+  bt->n_all_dyn = (int)(std::stable_partition(bt->l_all.begin(), bt->l_all.end(),
+                                              [&](int32_t i) { return bt->hdr[i].strategy != ST_STATIC; }) -
+                        bt->l_all.begin());
   bt->l_slow = bt->l_all;
   bt->l_slow.insert(bt->l_slow.end(), bt->l_cluster.begin(), bt->l_cluster.end());
   bt->l_cs = bt->l_cluster;
@@ -1976,6 +1982,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->out_idx, std::max<uint64_t>(1, bt->out_cap));
   a.add(&bt->out_rep, std::max<uint64_t>(1, bt->out_cap));
   a.add(&bt->offsets_d, B + 1);
+  a.add(&bt->off_part, (size_t)(B + kOffChunk - 1) / kOffChunk);
   a.add(&bt->cidx_d, std::max<uint64_t>(1, bt->out_cap));
   a.add(&bt->crep_d, std::max<uint64_t>(1, bt->out_cap));
   a.add(&bt->rout, (size_t)std::max(1, nr) * R);
@@ -2122,7 +2129,25 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     KArgs k = ka;
     k.list = bt->d_all;
     k.n = (int)bt->l_all.size();
-    HIPCHK(dev::select(sp, SEL_LAUNCH_ALL, k, smem_all(s), cap, sx));
+    // Candidates gathered into LDS (k_select_all), or, in bits mode, streamed from
+    // the feasibility and class rows (k_select_all_stream): for the StaticWeight
+    // bindings (votes from per-rule bitsets), and for all when the gathered
+    // candidates would leave one workgroup per CU (C ~ 8.6k+). KP_SEL_GATHER=1 /
+    // KP_SEL_STREAM=1 force one kernel for all.
+    const bool stream_all = bits && (getenv("KP_SEL_STREAM") || smem_all(s) > 80 * 1024) && !getenv("KP_SEL_GATHER");
+    const bool stream_w = bits && !getenv("KP_SEL_GATHER");
+    const int na = stream_all ? 0 : (stream_w ? bt->n_all_dyn : k.n);
+    if (na > 0) {
+      KArgs g = k;
+      g.n = na;
+      HIPCHK(dev::select(sp, SEL_LAUNCH_ALL, g, smem_all(s), cap, sx));
+    }
+    if (k.n - na > 0) {
+      KArgs g = k;
+      g.list = bt->d_all + na;
+      g.n = k.n - na;
+      HIPCHK(dev::select(sp, SEL_LAUNCH_ALL_STREAM, g, sel_stream_lds_bytes(s->Cp), cap, sx));
+    }
   }
   HIPCHK(dev::event_record(e->ev[8], sp));  // k_select_all alone: ev[7] -> ev[8]
   dev::stream_t s3 = e->stream3;
@@ -2209,30 +2234,22 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
                        bt->slow_cap, sx));
   }
   HIPCHK(dev::event_record(e->ev[2], st));
-  // results -> host, compacted to CSR
+  // results -> host, compacted to CSR: offsets scanned and results compacted on
+  // the device, then the per-binding arrays and the CSR copied back
+  HIPCHK(dev::offsets(st, bt->status, bt->count, B, bt->offsets_d, bt->off_part));
+  HIPCHK(dev::compact(st, bt->start, bt->count, bt->offsets_d, bt->out_idx, bt->out_rep, bt->cidx_d, bt->crep_d, B));
   bt->h_status.resize(B);
   bt->h_err.resize(B);
   bt->h_arg.resize(B);
-  bt->h_start.resize(B);
-  bt->h_count.resize(B);
+  bt->h_offsets.resize(B + 1);
   HIPCHK(dev::d2h(bt->h_status.data(), bt->status, 4 * (size_t)B, st));
   HIPCHK(dev::d2h(bt->h_err.data(), bt->errc, 4 * (size_t)B, st));
   HIPCHK(dev::d2h(bt->h_arg.data(), bt->arg, 8 * (size_t)B, st));
-  HIPCHK(dev::d2h(bt->h_count.data(), bt->count, 4 * (size_t)B, st));
+  HIPCHK(dev::d2h(bt->h_offsets.data(), bt->offsets_d, 8 * (size_t)(B + 1), st));
   HIPCHK(dev::d2h(bt->h_stats, bt->stats, sizeof(bt->h_stats), st));
   HIPCHK(dev::sync(st));
   double tc0 = now_ms();
-  bt->h_offsets.resize(B + 1);
-  uint64_t tot = 0;
-  for (int i = 0; i < B; i++) {
-    bt->h_offsets[i] = tot;
-    tot += bt->h_status[i] == KP_STATUS_OK ? bt->h_count[i] : 0;
-    if (bt->h_status[i] != KP_STATUS_OK) bt->h_count[i] = 0;
-  }
-  bt->h_offsets[B] = tot;
-  HIPCHK(dev::h2d(bt->offsets_d, bt->h_offsets.data(), 8 * (size_t)(B + 1), st));
-  HIPCHK(dev::h2d(bt->count, bt->h_count.data(), 4 * (size_t)B, st));
-  HIPCHK(dev::compact(st, bt->start, bt->count, bt->offsets_d, bt->out_idx, bt->out_rep, bt->cidx_d, bt->crep_d, B));
+  const uint64_t tot = bt->h_offsets[B];
   if (tot > bt->h_res_cap || !bt->h_cidx) {
     dev::host_release(bt->h_cidx);
     dev::host_release(bt->h_crep);

@@ -76,21 +76,38 @@ extern "C" __global__ void __launch_bounds__(KP_SEL_MAX_THREADS, KP_SEL_MIN_WAVE
   KP_SMEM;
   body_select_all(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a);
 }
+// SEL_ALL over streamed candidates: ~15 KB LDS at C = 5k, so LDS no longer bounds
+// the workgroups per CU; KP_STREAM_MIN_WAVES waves per SIMD bounds the VGPRs.
+#ifndef KP_STREAM_THREADS
+#define KP_STREAM_THREADS 256
+#endif
+#ifndef KP_STREAM_MIN_WAVES
+#define KP_STREAM_MIN_WAVES 6
+#endif
+extern "C" __global__ void __launch_bounds__(KP_STREAM_THREADS, KP_STREAM_MIN_WAVES) k_select_all_stream(KArgs a) {
+  KP_SMEM;
+  body_select_all_stream(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a);
+}
 // Large snapshots (C ~ 10k): the candidate arrays alone take 8 B per cluster, so a
 // single workgroup fits a CU; 1024 threads then keep 16 waves in flight instead of 8.
 extern "C" __global__ void __launch_bounds__(1024) k_select_all_wide(KArgs a) {
   KP_SMEM;
   body_select_all(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a);
 }
-extern "C" __global__ void __launch_bounds__(kBlock) k_select_cluster(KArgs a, int cap) {
+// Spread-constraint selection kernels: workgroup size (their LDS, ~8 B per cluster
+// of gathered candidates, bounds the workgroups per CU; wider ones hide latency).
+#ifndef KP_REG_THREADS
+#define KP_REG_THREADS 256
+#endif
+extern "C" __global__ void __launch_bounds__(KP_REG_THREADS) k_select_cluster(KArgs a, int cap) {
   KP_SMEM;
   body_select_cluster(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, cap);
 }
-extern "C" __global__ void __launch_bounds__(kBlock) k_region_a(KArgs a, RegionOut* rout, int32_t* rstat) {
+extern "C" __global__ void __launch_bounds__(KP_REG_THREADS) k_region_a(KArgs a, RegionOut* rout, int32_t* rstat) {
   KP_SMEM;
   body_region_a(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, rout, rstat);
 }
-extern "C" __global__ void __launch_bounds__(kBlock) k_region_b(KArgs a, const int32_t* rsel, const int32_t* rnsel,
+extern "C" __global__ void __launch_bounds__(KP_REG_THREADS) k_region_b(KArgs a, const int32_t* rsel, const int32_t* rnsel,
                                                                 int cap) {
   KP_SMEM;
   body_region_b(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, rsel, rnsel, cap);
@@ -117,6 +134,15 @@ extern "C" __global__ void __launch_bounds__(64) k_sets(SnapView s, const SetsAr
 extern "C" __global__ void __launch_bounds__(256) k_reasons(SnapView s, BatchView bv, uint64_t n, uint32_t* out) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     body_reasons(s, bv, i, out);
+}
+extern "C" __global__ void __launch_bounds__(kOffThreads) k_offsets_a(const int32_t* status, const uint32_t* count, int n,
+                                                                    uint64_t* offsets, uint64_t* part) {
+  __shared__ int64_t red[128];
+  body_offsets_a(GpuBlk{red}, (int)blockIdx.x, status, count, n, offsets, part);
+}
+extern "C" __global__ void __launch_bounds__(kOffThreads) k_offsets_b(int n, uint64_t* offsets, const uint64_t* part) {
+  __shared__ int64_t red[128];
+  body_offsets_b(GpuBlk{red}, (int)blockIdx.x, (int)gridDim.x, n, offsets, part);
 }
 extern "C" __global__ void __launch_bounds__(64) k_compact(const uint64_t* start, const uint32_t* count,
                                                            const uint64_t* offsets, const uint32_t* in_idx,
@@ -251,14 +277,17 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
       else
         hipLaunchKernelGGL(k_select_all, dim3(a.n), dim3(sel_threads()), smem, h, a);
       break;
+    case SEL_LAUNCH_ALL_STREAM:
+      hipLaunchKernelGGL(k_select_all_stream, dim3(a.n), dim3(KP_STREAM_THREADS), smem, h, a);
+      break;
     case SEL_LAUNCH_CLUSTER:
-      hipLaunchKernelGGL(k_select_cluster, dim3(a.n), dim3(kBlock), smem, h, a, cap);
+      hipLaunchKernelGGL(k_select_cluster, dim3(a.n), dim3(KP_REG_THREADS), smem, h, a, cap);
       break;
     case SEL_LAUNCH_REGION_A:
-      hipLaunchKernelGGL(k_region_a, dim3(a.n), dim3(kBlock), smem, h, a, x.rout, x.rstat);
+      hipLaunchKernelGGL(k_region_a, dim3(a.n), dim3(KP_REG_THREADS), smem, h, a, x.rout, x.rstat);
       break;
     case SEL_LAUNCH_REGION_B:
-      hipLaunchKernelGGL(k_region_b, dim3(a.n), dim3(kBlock), smem, h, a, x.rsel, x.rnsel, cap);
+      hipLaunchKernelGGL(k_region_b, dim3(a.n), dim3(KP_REG_THREADS), smem, h, a, x.rsel, x.rnsel, cap);
       break;
     case SEL_LAUNCH_SLOW:
       if (smem > 65536 &&
@@ -293,6 +322,14 @@ int reasons(stream_t st, const SnapView& s, const BatchView& bv, uint32_t* out) 
   if (n == 0) return 0;
   const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
   hipLaunchKernelGGL(k_reasons, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)st, s, bv, n, out);
+  return chk(hipGetLastError());
+}
+
+int offsets(stream_t st, const int32_t* status, const uint32_t* count, int n, uint64_t* off, uint64_t* part) {
+  if (n <= 0) return 0;
+  const int nb = (n + kOffChunk - 1) / kOffChunk;
+  hipLaunchKernelGGL(k_offsets_a, dim3(nb), dim3(kOffThreads), 0, (hipStream_t)st, status, count, n, off, part);
+  hipLaunchKernelGGL(k_offsets_b, dim3(nb), dim3(kOffThreads), 0, (hipStream_t)st, n, off, (const uint64_t*)part);
   return chk(hipGetLastError());
 }
 

@@ -64,6 +64,9 @@ int component_sets(stream_t st, const SnapView& s, const SetsArgs* A, const int3
                    uint64_t n, int64_t* scratch, int32_t* out);
 // kp_filter_reasons: out[b * C + r] = pair_reason of binding b, cluster rank r.
 int reasons(stream_t st, const SnapView& s, const BatchView& bv, uint32_t* out);
+// CSR offsets[n + 1] of the per-binding results (counts of OK bindings), on the device;
+// part: ceil(n / kOffChunk) u64 of scratch.
+int offsets(stream_t st, const int32_t* status, const uint32_t* count, int n, uint64_t* off, uint64_t* part);
 int compact(stream_t st, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
             const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n);
 

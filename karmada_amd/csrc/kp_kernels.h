@@ -326,10 +326,85 @@ KP_FI void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
   SelCtx x = make_ctx(a, b, tgt);
   KP_STAMP(x, 0);
   const bool weights = h->strategy == ST_STATIC && h->sel == SEL_ALL;
+  if (h->sel == SEL_ERR_UNSUPPORTED || (h->flags & BF_BAD)) {  // errors: only F (FitError first) is needed
+    int64_t F = 0;
+    for (int w = B.tid(); w < a.s.W; w += B.nth()) F += popc64(x.frow[w]);
+    cd.F = (int)B.sum64(F);
+    select_all_common(B, a, x, LdsCands{&cd, B.tid(), B.nth()}, cd.F, ss);
+    return;
+  }
   cd.F = gather(B, x, cd, weights, [&] { build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2); });
   KP_STAMP(x, 1);
   LdsCands cs{&cd, B.tid(), B.nth()};
   select_all_common(B, a, x, cs, cd.F, ss);
+}
+
+// ---------------------------------------------------------------------------
+// SEL_ALL over streamed candidates (k_select_all_stream, the bits-mode path): no
+// per-binding candidate arrays in LDS. Every pass walks the binding's feasibility
+// row (fmask, k_filter) and reads each candidate's calAvailableReplicas from its
+// estimator-class row (est_at; the class rows are shared by every binding of the
+// class and stay in L2), or its StaticWeight vote from per-rule cluster bitsets
+// built once in LDS (prog_word, kp_filter.h). The LDS left is the TargetContains
+// bits and the selection scratch, so several times more workgroups share a CU.
+// LDS: [red | tgt bits | rule bits kSwRules x W | SelScratch]
+// ---------------------------------------------------------------------------
+struct StreamCands {
+  const SelCtx* x;
+  int C, tid, nth;
+  bool weights;
+  const uint64_t* swb;  // weights && swb: [nsw][W] rule bitsets
+  int nsw;
+  KP_FI int32_t vote(int c) const {
+    if (!weights) return est_at(*x, c);
+    if (!swb) return static_vote(*x, c);
+    const BindHdr& h = *x->h;
+    if (!(h.flags & BF_HAS_WP)) return 1;
+    int64_t wt = 0;
+    for (int j = 0; j < nsw; j++)
+      if ((swb[(size_t)j * x->s->W + (c >> 6)] >> (c & 63)) & 1ull) {
+        const int64_t rw = kp_ldu(x->bv->lpool + h.sw_w_off + j);
+        wt = rw > wt ? rw : wt;
+      }
+    return (int32_t)(wt > kInt32Max ? kInt32Max : wt);
+  }
+  template <class Fn>
+  KP_FI void each(Fn fn) const {
+    for (int c = tid; c < C; c += nth) {
+      const uint64_t m = x->frow[c >> 6];  // wave-uniform word
+      if ((m >> (c & 63)) & 1ull) fn((uint32_t)c, vote(c));
+    }
+  }
+  static constexpr bool kSettable = false;
+  KP_FI uint64_t okey(const SelCtx& xx, uint32_t rk, int32_t v0) const { return cand_order_key(xx, rk, v0); }
+  static constexpr bool kExact = false;
+};
+template <class BLK>
+KP_FI void body_select_all_stream(const BLK& B, int blk, unsigned char* smem, const KArgs& a) {
+  if (blk >= a.n) return;
+  KP_STAMP_INIT
+  const int b = a.list[blk];
+  const SnapView& s = a.s;
+  const int words = (s.Cp + 31) >> 5;
+  uint32_t* tgt = (uint32_t*)(smem + kRedBytes);
+  uint64_t* swb = (uint64_t*)(tgt + ((words + 3) & ~3));
+  SelScratch ss = carve_sel_scratch((unsigned char*)(swb + (size_t)kSwRules * s.W), s.Cp);
+  ss.dbg = a.dbg;
+  const BindHdr* h = &a.bv.hdr[b];
+  build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
+  SelCtx x = make_ctx(a, b, tgt);
+  const bool weights = h->strategy == ST_STATIC && h->sel == SEL_ALL;
+  const bool rules = weights && (h->flags & BF_HAS_WP) && h->sw_cnt <= kSwRules && s.n_bits > 0;
+  if (rules) {  // getStaticWeightInfoList's ClusterMatches per rule, as cluster bitsets
+    for (int i = B.tid(); i < h->sw_cnt * s.W; i += B.nth())
+      swb[i] = prog_word(s, a.bv, kp_ldu(a.bv.ipool + h->sw_off + i / s.W), i % s.W);
+  }
+  int64_t F = 0;
+  for (int w = B.tid(); w < s.W; w += B.nth()) F += popc64(x.frow[w]);
+  F = B.sum64(F);  // (its barrier also publishes tgt and swb)
+  KP_STAMP(x, 1);
+  const StreamCands cs{&x, s.C, B.tid(), B.nth(), weights, rules ? swb : nullptr, rules ? h->sw_cnt : 0};
+  select_all_common(B, a, x, cs, (int)F, ss);
 }
 
 // ---------------------------------------------------------------------------
@@ -659,13 +734,46 @@ KP_HD inline void body_reasons(const SnapView& s, const BatchView& bv, uint64_t 
   out[i] = pair_reason(s, bv, bv.hdr[b], r);
 }
 
-// Gathers per-binding results into CSR order (offsets computed on the host).
+// CSR offsets of the per-binding results: offsets[b] = sum of the counts of the
+// bindings before b whose status is OK (the others report no targets),
+// offsets[n] = total. Two launches over chunks of kOffChunk bindings: pass A
+// writes each chunk's local exclusive offsets and its total; pass B adds the
+// totals of the chunks before it (and the last chunk writes offsets[n]).
+template <class BLK>
+KP_FI void body_offsets_a(const BLK& B, int blk, const int32_t* status, const uint32_t* count, int n,
+                          uint64_t* offsets, uint64_t* part) {
+  const int per = kOffChunk / B.nth();  // entries per thread (kOffPer on the GPU)
+  const int lo = blk * kOffChunk + B.tid() * per;
+  auto cnt = [&](int i) { return i < n && status[i] == KP_STATUS_OK ? count[i] : 0u; };
+  int64_t mine = 0;
+  for (int q = 0; q < per; q++) mine += cnt(lo + q);
+  int32_t tlo, thi;  // 64-bit exclusive scan as two 32-bit ones (low 16 bits, the rest)
+  const int32_t blo = B.excl_scan((int32_t)(mine & 0xffff), &tlo);
+  const int32_t bhi = B.excl_scan((int32_t)(mine >> 16), &thi);
+  uint64_t o = (uint64_t)(uint32_t)blo + ((uint64_t)(uint32_t)bhi << 16);
+  for (int q = 0; q < per; q++) {
+    if (lo + q < n) offsets[lo + q] = o;
+    o += cnt(lo + q);
+  }
+  if (B.tid() == 0) part[blk] = (uint64_t)(uint32_t)tlo + ((uint64_t)(uint32_t)thi << 16);
+}
+template <class BLK>
+KP_FI void body_offsets_b(const BLK& B, int blk, int nblk, int n, uint64_t* offsets, const uint64_t* part) {
+  int64_t base = 0;
+  for (int k = B.tid(); k < blk; k += B.nth()) base += (int64_t)part[k];
+  base = B.sum64(base);
+  const int lo = blk * kOffChunk, hi = lo + kOffChunk < n ? lo + kOffChunk : n;
+  for (int i = lo + B.tid(); i < hi; i += B.nth()) offsets[i] += (uint64_t)base;
+  if (blk == nblk - 1 && B.tid() == 0) offsets[n] = (uint64_t)base + part[blk];
+}
+
+// Gathers per-binding results into CSR order (offsets from body_offsets).
 template <class BLK>
 KP_FI void body_compact(const BLK& B, int blk, const uint64_t* start, const uint32_t* count, const uint64_t* offsets,
                         const uint32_t* in_idx, const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n) {
   if (blk >= n) return;
   uint64_t s = start[blk], o = offsets[blk];
-  uint32_t c = count[blk];
+  uint32_t c = (uint32_t)(offsets[blk + 1] - o);  // 0 unless the status is OK (body_offsets)
   for (uint32_t i = B.tid(); i < c; i += B.nth()) {
     out_idx[o + i] = in_idx[s + i];
     out_rep[o + i] = in_rep[s + i];

@@ -31,7 +31,8 @@ enum : int {
   SEL_LAUNCH_CLUSTER,
   SEL_LAUNCH_REGION_A,
   SEL_LAUNCH_REGION_B,
-  SEL_LAUNCH_SLOW
+  SEL_LAUNCH_SLOW,
+  SEL_LAUNCH_ALL_STREAM  // SEL_ALL over streamed candidates (bits mode)
 };
 
 struct SelectExtra {
@@ -64,5 +65,13 @@ KP_HD inline int sel_all_ecap(int Cp) { return Cp / 2 < 64 ? 64 : (Cp / 2 > KP_E
 KP_HD inline size_t pair_lds_tail_bytes(int Cp, int md_cap) {  // evict | md | stage | tolb
   const int words = (Cp + 31) >> 5;
   return 4 * (size_t)((words + 3) & ~3) + 4 * (size_t)((md_cap + 3) & ~3) + kPairStage + kTsetMax / 8;
+}
+constexpr int kOffThreads = 256, kOffChunk = 4 * kOffThreads;  // CSR offsets scan (body_offsets_a/b)
+constexpr int kSwRules = 4;  // StaticWeight rules kept as LDS bitsets (more: per-cluster static_vote)
+// Dynamic LDS of k_select_all_stream (kp_kernels.h body_select_all_stream).
+KP_HD inline size_t sel_stream_lds_bytes(int Cp) {
+  const int words = (Cp + 31) >> 5, W = Cp / 64;
+  return kRedBytes + 4 * (size_t)((words + 3) & ~3) + 8 * (size_t)kSwRules * W + 3072 + 8 * (size_t)sel_all_ecap(Cp) +
+         64;
 }
 }  // namespace kp

@@ -545,21 +545,6 @@ KP_HD inline int32_t static_vote(const SelCtx& x, int c) {
   return (int32_t)(wt > kInt32Max ? kInt32Max : wt);
 }
 
-// static_vote with the uniform program evaluation of the fast kernels (c < C).
-KP_HD inline int32_t static_vote_u(const SnapView& s, const BatchView& bv, const BindHdr& h, int c) {
-  int64_t wt = 0;
-  if (!(h.flags & BF_HAS_WP)) {
-    wt = 1;
-  } else {
-    for (int j = 0; j < h.sw_cnt; j++) {
-      const bool m = prog_eval_u(s, bv, bv.ipool[h.sw_off + j], c);
-      const int64_t rw = bv.lpool[h.sw_w_off + j];
-      if (m && rw > wt) wt = rw;
-    }
-  }
-  return (int32_t)(wt > kInt32Max ? kInt32Max : wt);
-}
-
 // ----------------------------------------------------------------------------
 // Candidate gather: feasible clusters of the binding in rank order.
 // ----------------------------------------------------------------------------
