@@ -1279,12 +1279,12 @@ size_t smem_cluster(const kp_snapshot* s, int cap) {
 size_t smem_region_a(const kp_snapshot* s) {
   int words = (s->Cp + 31) >> 5;
   size_t R = s->view.n_regions;
-  return kRedBytes + 80 * R + 4 * (size_t)((words + 3) & ~3) + 8 * (size_t)s->Cp + 64;
+  return kRedBytes + 80 * R + 4 * (size_t)((words + 3) & ~3) + 10 * (size_t)s->Cp + 64;
 }
 size_t smem_region_b(const kp_snapshot* s, int cap) {
   int words = (s->Cp + 31) >> 5;
   size_t R = s->view.n_regions;
-  size_t area = std::max(8 * (size_t)s->Cp, serial_scratch_bytes(cap));
+  size_t area = std::max(10 * (size_t)s->Cp, serial_scratch_bytes(cap));  // cand r/v/g, then the serial scratch
   return kRedBytes + 1024 + sizeof(Item) * 2 * kSmallMax + 16 * kSmallMax + 8 * R + 4 * ((R + 3) & ~3) +
          4 * (size_t)((words + 3) & ~3) + area + 64;
 }
@@ -2291,7 +2291,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     HIPCHK(dev::d2h(h, bt->dbg, sizeof(h), st));
     HIPCHK(dev::sync(st));
     fprintf(stderr, "kp stamps (s_memtime ticks, summed over workgroups):");
-    for (int i = 0; i < 16; i++) fprintf(stderr, " [%d]=%llu", i, h[i]);
+    for (int i = 0; i < 32; i++) fprintf(stderr, " [%d]=%llu", i, h[i]);
     fprintf(stderr, "\n");
   }
 #endif

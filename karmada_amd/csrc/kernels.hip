@@ -96,22 +96,25 @@ extern "C" __global__ void __launch_bounds__(1024) k_select_all_wide(KArgs a) {
 }
 // Spread-constraint selection kernels: workgroup size (their LDS, ~8 B per cluster
 // of gathered candidates, bounds the workgroups per CU; wider ones hide latency).
-#ifndef KP_REG_THREADS
-#define KP_REG_THREADS 256
-#endif
-extern "C" __global__ void __launch_bounds__(KP_REG_THREADS) k_select_cluster(KArgs a, int cap) {
-  KP_SMEM;
-  body_select_cluster(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, cap);
-}
-extern "C" __global__ void __launch_bounds__(KP_REG_THREADS) k_region_a(KArgs a, RegionOut* rout, int32_t* rstat) {
-  KP_SMEM;
-  body_region_a(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, rout, rstat);
-}
-extern "C" __global__ void __launch_bounds__(KP_REG_THREADS) k_region_b(KArgs a, const int32_t* rsel, const int32_t* rnsel,
-                                                                int cap) {
-  KP_SMEM;
-  body_region_b(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, rsel, rnsel, cap);
-}
+// Two instances each: 256 threads while the LDS leaves several workgroups per CU
+// (C up to ~8.6k; fewer waves per barrier), 512 when it leaves one (wider hides
+// latency). 4 / 3 waves per SIMD bound the VGPRs at 128 / 168.
+#define KP_SPREAD_KERNELS(SUF, T, MINW)                                                                          \
+  extern "C" __global__ void __launch_bounds__(T, MINW) k_select_cluster##SUF(KArgs a, int cap) {              \
+    KP_SMEM;                                                                                                   \
+    body_select_cluster(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, cap);                                \
+  }                                                                                                            \
+  extern "C" __global__ void __launch_bounds__(T, MINW) k_region_a##SUF(KArgs a, RegionOut* rout, int32_t* rstat) { \
+    KP_SMEM;                                                                                                   \
+    body_region_a(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, rout, rstat);                              \
+  }                                                                                                            \
+  extern "C" __global__ void __launch_bounds__(T, MINW) k_region_b##SUF(KArgs a, const int32_t* rsel,           \
+                                                                      const int32_t* rnsel, int cap) {         \
+    KP_SMEM;                                                                                                   \
+    body_region_b(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, rsel, rnsel, cap);                         \
+  }
+KP_SPREAD_KERNELS(, 256, 3)
+KP_SPREAD_KERNELS(_wide, 512, 4)
 extern "C" __global__ void __launch_bounds__(256) k_region_groups(const RegionOut* rout, const int32_t* rstat,
                                                                   const BindHdr* hdr, const int32_t* list, int n, int R,
                                                                   int32_t* rsel, int32_t* rnsel, uint32_t* nhost) {
@@ -281,13 +284,22 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
       hipLaunchKernelGGL(k_select_all_stream, dim3(a.n), dim3(KP_STREAM_THREADS), smem, h, a);
       break;
     case SEL_LAUNCH_CLUSTER:
-      hipLaunchKernelGGL(k_select_cluster, dim3(a.n), dim3(KP_REG_THREADS), smem, h, a, cap);
+      if (smem > kLdsPerCu / 2)
+        hipLaunchKernelGGL(k_select_cluster_wide, dim3(a.n), dim3(512), smem, h, a, cap);
+      else
+        hipLaunchKernelGGL(k_select_cluster, dim3(a.n), dim3(256), smem, h, a, cap);
       break;
     case SEL_LAUNCH_REGION_A:
-      hipLaunchKernelGGL(k_region_a, dim3(a.n), dim3(KP_REG_THREADS), smem, h, a, x.rout, x.rstat);
+      if (smem > kLdsPerCu / 2)
+        hipLaunchKernelGGL(k_region_a_wide, dim3(a.n), dim3(512), smem, h, a, x.rout, x.rstat);
+      else
+        hipLaunchKernelGGL(k_region_a, dim3(a.n), dim3(256), smem, h, a, x.rout, x.rstat);
       break;
     case SEL_LAUNCH_REGION_B:
-      hipLaunchKernelGGL(k_region_b, dim3(a.n), dim3(KP_REG_THREADS), smem, h, a, x.rsel, x.rnsel, cap);
+      if (smem > kLdsPerCu / 2)
+        hipLaunchKernelGGL(k_region_b_wide, dim3(a.n), dim3(512), smem, h, a, x.rsel, x.rnsel, cap);
+      else
+        hipLaunchKernelGGL(k_region_b, dim3(a.n), dim3(256), smem, h, a, x.rsel, x.rnsel, cap);
       break;
     case SEL_LAUNCH_SLOW:
       if (smem > 65536 &&

@@ -801,6 +801,7 @@ struct Cands {
   uint32_t* r;  // rank | overflow << kRankBits
   int32_t* v;   // AllocatableReplicas (or static weight for SEL_ALL StaticWeight)
   int32_t F;
+  int16_t* g = nullptr;  // region-spread kernels: region index of candidate i (LDS; -1 none)
 };
 KP_HD inline uint32_t c_rank(const Cands& cd, int i) { return cd.r[i] & kRankMask; }
 KP_HD inline int32_t c_ovf(const Cands& cd, int i) { return (int32_t)(cd.r[i] >> kRankBits); }

@@ -65,6 +65,14 @@ KP_FI const T* rebase(const T* p, int64_t bias) {
   return (const T*)((uintptr_t)p - (uintptr_t)bias * sizeof(T));
 }
 
+// Region index of every gathered candidate into cd.g (one global load each, in
+// parallel; the region kernels' passes then read LDS only).
+template <class BLK>
+KP_FI void region_of_cands(const BLK& B, const SnapView& s, const Cands& cd) {
+  for (int i = B.tid(); i < cd.F; i += B.nth()) cd.g[i] = (int16_t)s.region_idx[c_rank(cd, i)];
+  B.sync();
+}
+
 // Status of bindings that never reach selection.
 template <class BLK>
 KP_FI bool pre_checks(const BLK& B, const SelCtx& x, int F) {
@@ -300,14 +308,6 @@ KP_FI void select_all_common(const BLK& B, const KArgs& a, const SelCtx& x, cons
   if (why != SLOW_NONE && B.tid() == 0) flag_slow(a, b, why);
 }
 
-KP_HD inline SelScratch carve_sel_scratch(unsigned char* p, int Cp) {
-  SelScratch ss;
-  ss.whist = (unsigned long long*)p;
-  ss.hist = (uint32_t*)(ss.whist + 256);
-  ss.buf = (uint64_t*)(ss.hist + 256);
-  ss.cap = sel_all_ecap(Cp);
-  return ss;
-}
 
 // Candidates compacted in LDS (any block policy; the only form for CpuBlk).
 template <class BLK>
@@ -413,6 +413,7 @@ KP_FI void body_select_all_stream(const BLK& B, int blk, unsigned char* smem, co
 template <class BLK>
 KP_FI void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const KArgs& a, int scratch_cap) {
   if (blk >= a.n) return;
+  KP_STAMP_INIT
   const int b = a.list[blk];
   const int words = (a.s.Cp + 31) >> 5;
   uint32_t* hist = (uint32_t*)(smem + kRedBytes);
@@ -426,9 +427,13 @@ KP_FI void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const
   const BindHdr* h = &a.bv.hdr[b];
   build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
   SelCtx x = make_ctx(a, b, tgt);
+  KP_STAMP(x, 26);
   cd.F = gather(B, x, cd, false);
+  KP_STAMP(x, 27);
   if (pre_checks(B, x, cd.F)) return;
-  if (!sel_cluster_fast(B, x, cd, hist, items, keys, area, scratch_cap)) {
+  const size_t area_bytes = 8 * (size_t)a.s.Cp > serial_scratch_bytes(scratch_cap) ? 8 * (size_t)a.s.Cp
+                                                                                    : serial_scratch_bytes(scratch_cap);
+  if (!sel_cluster_fast(B, x, cd, hist, items, keys, area, scratch_cap, area_bytes)) {
     if (B.tid() == 0) flag_slow(a, b, SLOW_CLUSTER);
   }
 }
@@ -440,6 +445,7 @@ KP_FI void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const
 template <class BLK>
 KP_FI void body_region_a(const BLK& B, int blk, unsigned char* smem, const KArgs& a, RegionOut* rout, int32_t* rstat) {
   if (blk >= a.n) return;
+  KP_STAMP_INIT
   const int b = a.list[blk];
   const int words = (a.s.Cp + 31) >> 5;
   const int R = a.s.n_regions;
@@ -474,15 +480,20 @@ KP_FI void body_region_a(const BLK& B, int blk, unsigned char* smem, const KArgs
   Cands cd;
   cd.r = (uint32_t*)p;
   cd.v = (int32_t*)(cd.r + a.s.Cp);
+  cd.g = (int16_t*)(cd.v + a.s.Cp);
   const BindHdr* h = &a.bv.hdr[b];
   build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
   SelCtx x = make_ctx(a, b, tgt);
+  KP_STAMP(x, 22);
   cd.F = gather(B, x, cd, false);
+  region_of_cands(B, a.s, cd);
+  KP_STAMP(x, 23);
   if (pre_checks(B, x, cd.F)) {
     if (B.tid() == 0) rstat[blk] = -1;
     return;
   }
   region_a(B, x, cd, L, rout + (size_t)blk * R);
+  KP_STAMP(x, 24);
   if (B.tid() == 0) rstat[blk] = 0;
 }
 
@@ -492,6 +503,7 @@ template <class BLK>
 KP_FI void body_region_b(const BLK& B, int blk, unsigned char* smem, const KArgs& a, const int32_t* rsel,
                          const int32_t* rnsel, int scratch_cap) {
   if (blk >= a.n) return;
+  KP_STAMP_INIT
   const int b = a.list[blk];
   const int nsel = rnsel[blk];
   if (nsel == -1000) return;
@@ -513,6 +525,7 @@ KP_FI void body_region_b(const BLK& B, int blk, unsigned char* smem, const KArgs
   Cands cd;
   cd.r = (uint32_t*)p;
   cd.v = (int32_t*)(cd.r + a.s.Cp);
+  cd.g = (int16_t*)(cd.v + a.s.Cp);
   const BindHdr* h = &a.bv.hdr[b];
   build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
   SelCtx x = make_ctx(a, b, tgt);
@@ -524,8 +537,13 @@ KP_FI void body_region_b(const BLK& B, int blk, unsigned char* smem, const KArgs
     if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, -1);
     return;
   }
+  KP_STAMP(x, 16);
   cd.F = gather(B, x, cd, false);
-  region_b(B, x, cd, rsel + (size_t)blk * R, nsel, hist, heads, rs, items, keys, p, scratch_cap);
+  region_of_cands(B, a.s, cd);
+  KP_STAMP(x, 17);
+  const size_t area_bytes = 8 * (size_t)a.s.Cp > serial_scratch_bytes(scratch_cap) ? 8 * (size_t)a.s.Cp
+                                                                                    : serial_scratch_bytes(scratch_cap);
+  region_b(B, x, cd, rsel + (size_t)blk * R, nsel, hist, heads, rs, items, keys, p, scratch_cap, area_bytes);
 }
 
 // ---------------------------------------------------------------------------

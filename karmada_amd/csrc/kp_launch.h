@@ -52,13 +52,6 @@ constexpr int kSlowBlock = 512;  // k_slow: wider for the LDS bitonic sort
 constexpr int kPairStage = 4096;  // bytes of per-binding predicate data staged in LDS
 constexpr int kTsetMax = 4096;    // distinct taint lists answered once per binding (LDS bits)
 
-// Enumeration capacity (u64 entries) of the SEL_ALL selection buffer.
-// 1024 entries (8 KB) keep k_select_all's LDS under a third of the CU's 160 KB at
-// C = 5k; larger party sets fall back to the uncompacted (exact) Webster passes.
-#ifndef KP_ECAP_MAX
-#define KP_ECAP_MAX 1024
-#endif
-KP_HD inline int sel_all_ecap(int Cp) { return Cp / 2 < 64 ? 64 : (Cp / 2 > KP_ECAP_MAX ? KP_ECAP_MAX : Cp / 2); }
 
 // LDS bytes of the pair stage's per-binding tail (evict bits | md table | predicate
 // stage | taint-list bits; kp_kernels.h PairLds).

@@ -512,10 +512,53 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
 }
 
 // ----------------------------------------------------------------------------
-// Small selected list -> serial AssignReplicas (thread 0) -> sink.
+// Small selected list -> AssignReplicas -> sink.
+// The selected clusters (spread selection's output, in the order AssignReplicas
+// receives them) as a candidate set for the block-parallel assignment
+// (sel_all_fast): v = AllocatableReplicas, or the StaticWeight vote; sort.Sort's
+// input position is the position in the list.
 // ----------------------------------------------------------------------------
+struct ItemCands {
+  const Item* it;
+  int n, tid, nth;
+  const SelCtx* x;
+  bool weights;
+  template <class Fn>
+  KP_FI void each(Fn fn) const {
+    for (int i = tid; i < n; i += nth) fn(it[i].rank, weights ? static_vote(*x, (int)it[i].rank) : it[i].alloc);
+  }
+  static constexpr bool kSettable = false;
+  KP_FI uint64_t okey(const SelCtx&, uint32_t rk, int32_t) const {
+    for (int i = 0; i < n; i++)
+      if (it[i].rank == rk) return (uint64_t)i;
+    return ~0ull;
+  }
+  static constexpr bool kExact = false;
+};
+// The block-parallel AssignReplicas over the selected list, with the candidate
+// bitset (scheduledClusters = spec.Clusters entries among the selected ones) in
+// scratch; the exact serial emulation (thread 0) for what it refuses (Aggregated
+// ties at the cut in lists > 12, overflow tiers, wrap hazards, ...).
+// scratch: at least area_bytes of LDS.
 template <class BLK>
-KP_FI void assign_small(const BLK& B, const SelCtx& x, const Item* items, int n, void* scratch, int cap) {
+KP_FI void assign_small(const BLK& B, const SelCtx& x, const Item* items, int n, void* scratch, int cap,
+                        size_t area_bytes) {
+  const int W = x.s->W;
+  if (n > 0 && 8 * (size_t)W + 3072 + 8 * (size_t)sel_all_ecap(x.s->Cp) + 64 <= area_bytes) {
+    uint64_t* selb = (uint64_t*)scratch;
+    uint32_t* sel32 = (uint32_t*)scratch;
+    for (int w = B.tid(); w < W; w += B.nth()) selb[w] = 0;
+    B.sync();
+    for (int i = B.tid(); i < n; i += B.nth()) kp_atomic_or(&sel32[items[i].rank >> 5], 1u << (items[i].rank & 31));
+    B.sync();
+    SelCtx y = x;
+    y.frow = selb;
+    const SelScratch ss = carve_sel_scratch((unsigned char*)(selb + W), x.s->Cp);
+    const bool weights = x.h->strategy == ST_STATIC;
+    const int why = sel_all_fast(B, y, ItemCands{items, n, B.tid(), B.nth(), &y, weights}, ss);
+    B.sync();
+    if (why == SLOW_NONE) return;
+  }
   if (B.tid() == 0) {
     SerialScratch sc = serial_scratch_carve(scratch, cap);
     SerialAssign sa{x, sc, (x.h->flags & BF_UID_DESC) != 0};
@@ -531,7 +574,7 @@ KP_FI void assign_small(const BLK& B, const SelCtx& x, const Item* items, int n,
 // ----------------------------------------------------------------------------
 template <class BLK>
 KP_FI bool sel_cluster_fast(const BLK& B, const SelCtx& x, const Cands& cd, uint32_t* hist, Item* items,
-                            uint64_t* keys, void* scratch, int cap) {
+                            uint64_t* keys, void* scratch, int cap, size_t area_bytes) {
   const BindHdr& h = *x.h;
   const int F = cd.F;
   if ((int64_t)F < h.cluster_min) {
@@ -549,9 +592,11 @@ KP_FI bool sel_cluster_fast(const BLK& B, const SelCtx& x, const Cands& cd, uint
     }
     return true;
   }
+  KP_STAMP_INIT
   auto key = [&](int i) { return cand_key(x, cd, i, cd.v[i]); };
   auto all = [&](int) { return true; };
   uint64_t kth = radix_select(B, hist, F, all, key, needCnt);
+  KP_STAMP(x, 28);
   // compact the selected keys
   int n = 0;
   for (int t0 = 0; t0 < F; t0 += B.nth()) {
@@ -664,7 +709,9 @@ KP_FI bool sel_cluster_fast(const BLK& B, const SelCtx& x, const Cands& cd, uint
       if (!ok) return true;
     }
   }
-  assign_small(B, x, items, n, scratch, cap);
+  KP_STAMP(x, 29);
+  assign_small(B, x, items, n, scratch, cap, area_bytes);
+  KP_STAMP(x, 30);
   return true;
 }
 
@@ -872,8 +919,7 @@ KP_FI void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L,
   B.sync();
   const bool dup = (h.flags & BF_GROUP_DUP) != 0;
   for (int i = B.tid(); i < cd.F; i += B.nth()) {
-    uint32_t rk = c_rank(cd, i);
-    int r = x.s->region_idx[rk];
+    int r = cd.g[i];
     if (r < 0) continue;
     uint64_t k = cand_key(x, cd, i, cd.v[i]);
     int64_t av = key_avail(k), sc = key_score(k);
@@ -913,8 +959,7 @@ KP_FI void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L,
     }
     if (!B.any(any)) break;
     for (int i = B.tid(); i < cd.F; i += B.nth()) {
-      uint32_t rk = c_rank(cd, i);
-      int r = x.s->region_idx[rk];
+      int r = cd.g[i];
       if (r < 0 || L.done[r]) continue;
       uint64_t k = cand_key(x, cd, i, cd.v[i]);
       if (L.wcnt[r] > 0 && k <= L.last[r]) continue;
@@ -964,7 +1009,9 @@ KP_FI void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L,
 // ----------------------------------------------------------------------------
 template <class BLK>
 KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_t* sel, int nsel, uint32_t* hist,
-                    unsigned long long* heads, int32_t* rsel, Item* items, uint64_t* keys, void* scratch, int cap) {
+                    unsigned long long* heads, int32_t* rsel, Item* items, uint64_t* keys, void* scratch, int cap,
+                    size_t area_bytes) {
+  KP_STAMP_INIT
   const BindHdr& h = *x.h;
   const int R = x.s->n_regions;
   for (int r = B.tid(); r < R; r += B.nth()) {
@@ -981,7 +1028,7 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
   // `keys` (2*kSmallMax entries) when they fit.
   const int kc = 2 * kSmallMax;
   auto in_sel = [&](int i) {
-    const int r = x.s->region_idx[c_rank(cd, i)];
+    const int r = cd.g[i];
     return r >= 0 && rsel[r] >= 0;
   };
   int32_t mine = 0;
@@ -990,11 +1037,12 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
   for (int i = B.tid(); i < cd.F; i += B.nth()) {
     if (!in_sel(i)) continue;
     const uint64_t k = cand_key(x, cd, i, cd.v[i]);
-    kp_atomic_min_u64(&heads[x.s->region_idx[c_rank(cd, i)]], k);
+    kp_atomic_min_u64(&heads[cd.g[i]], k);
     if (pos < kc) keys[pos] = k;
     pos++;
   }
   B.sync();
+  KP_STAMP(x, 18);
   const int64_t total = *ctr;
   int64_t needCnt = total < h.cluster_max ? total : h.cluster_max;
   int64_t restCnt = needCnt - nsel;
@@ -1007,23 +1055,25 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
     for (int j = 0; j < nsel; j++) items[n++] = item_from_key(x, heads[sel[j]]);
   n = nsel;
   B.sync();
-  if (restCnt > 0 && total <= kc && restCnt <= 64) {
-    // the restCnt smallest non-head keys, ascending: one block minimum per pick
-    uint64_t prev = 0;
-    for (int64_t q = 0; q < restCnt; q++) {
-      uint64_t m = ~0ull;
-      for (int i = B.tid(); i < (int)total; i += B.nth()) {
-        const uint64_t k = keys[i];
-        if ((q == 0 || k > prev) && k < m && k != heads[x.s->region_idx[key_rank(k)]]) m = k;
-      }
-      prev = B.minu64(m);
-      if (B.tid() == 0) items[nsel + q] = item_from_key(x, prev);
+  if (restCnt > 0 && total <= kc) {
+    // the restCnt smallest non-head keys, ascending: heads drop out of the list
+    // (~0), then each key's position is the count of smaller keys (keys are
+    // distinct: the rank is in the low bits)
+    for (int i = B.tid(); i < (int)total; i += B.nth())
+      if (keys[i] == heads[x.s->region_idx[key_rank(keys[i])]]) keys[i] = ~0ull;
+    B.sync();
+    for (int i = B.tid(); i < (int)total; i += B.nth()) {
+      const uint64_t k = keys[i];
+      if (k == ~0ull) continue;
+      int64_t pos = 0;
+      for (int j = 0; j < (int)total; j++) pos += keys[j] < k ? 1 : 0;
+      if (pos < restCnt) items[nsel + pos] = item_from_key(x, k);
     }
     n = nsel + (int)restCnt;
     B.sync();
   } else if (restCnt > 0) {
     auto incand = [&](int i) {
-      int r = x.s->region_idx[c_rank(cd, i)];
+      int r = cd.g[i];
       return r >= 0 && rsel[r] >= 0 && cand_key(x, cd, i, cd.v[i]) != heads[r];
     };
     auto key = [&](int i) { return cand_key(x, cd, i, cd.v[i]); };
@@ -1058,7 +1108,9 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
     n = nsel + m;
     B.sync();
   }
-  assign_small(B, x, items, n, scratch, cap);
+  KP_STAMP(x, 19);
+  assign_small(B, x, items, n, scratch, cap, area_bytes);
+  KP_STAMP(x, 20);
 }
 
 }  // namespace kp

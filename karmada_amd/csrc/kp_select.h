@@ -651,6 +651,22 @@ struct SelScratch {
   unsigned long long* dbg = nullptr;  // diagnostic build only (KP_STAMPS)
 };
 
+// Enumeration capacity (u64 entries) of the SEL_ALL selection buffer.
+// 1024 entries (8 KB) keep k_select_all's LDS under a third of the CU's 160 KB at
+// C = 5k; larger party sets fall back to the uncompacted (exact) Webster passes.
+#ifndef KP_ECAP_MAX
+#define KP_ECAP_MAX 1024
+#endif
+KP_HD inline int sel_all_ecap(int Cp) { return Cp / 2 < 64 ? 64 : (Cp / 2 > KP_ECAP_MAX ? KP_ECAP_MAX : Cp / 2); }
+KP_HD inline SelScratch carve_sel_scratch(unsigned char* p, int Cp) {
+  SelScratch ss;
+  ss.whist = (unsigned long long*)p;
+  ss.hist = (uint32_t*)(ss.whist + 256);
+  ss.buf = (uint64_t*)(ss.hist + 256);
+  ss.cap = sel_all_ecap(Cp);
+  return ss;
+}
+
 template <class BLK, class Pred, class Key>
 KP_FI uint64_t radix_select(const BLK& B, uint32_t* hist, int F, Pred pred, Key key, int64_t k);
 
