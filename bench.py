@@ -11,6 +11,11 @@ one process per GPU, each schedules its own contiguous binding range of the
 universe against its own snapshot replica (weak scaling, no data-path
 collective); the per-rank CSR results are all-gathered after the timed region.
 
+In flight: --inflight engines (default 4), each with its own HIP streams and its
+own copy of the batch, are driven by as many host threads over the K steps, so one
+batch's host steps and result copy-back overlap another batch's kernels (a
+scheduler keeping two batches in flight); `serial_value` is one batch at a time.
+
 Roofline: the dominant kernel of the step (by its HIP-event time) against HBM
 peak with compulsory bytes, plus the counter-derived DRAM bytes
 (FETCH_SIZE x2 on gfx950 + WRITE_SIZE) and VALU issue fraction of the same
@@ -142,7 +147,7 @@ def parity_check(u, res, opts, n_check, seed):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--clusters", type=int, default=None)
@@ -154,6 +159,9 @@ def main():
                     help="bindings of the timed batch re-checked against the oracle after timing (0: off)")
     ap.add_argument("--e2e-reps", type=int, default=5, help="timed pack+upload+schedule repetitions (0: off)")
     ap.add_argument("--lib", default=None, help="engine library (default karmada_amd/libkp.so)")
+    ap.add_argument("--inflight", type=int, default=4,
+                    help="batches in flight per GPU: engines (own HIP streams) driven by as many host threads, "
+                         "so one batch's result copy-back and host steps overlap another's kernels")
     args = ap.parse_args()
 
     from karmada_amd import api, synth
@@ -210,16 +218,60 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
+    # in-flight batches: engine k schedules the same packed bindings (its own snapshot
+    # replica and batch); steps are split over them, each step = one whole batch
+    import threading
+    lanes = [(eng, snap, batch)]
+    for _ in range(1, max(1, args.inflight)):
+        e2 = Engine(local, lib_path=os.path.join(ROOT, args.lib)) if args.lib else Engine(local)
+        s2 = Snapshot.from_bytes(e2, snap.to_bytes(), u.names)
+        lanes.append((e2, s2, Batch(s2, structs=u.binding_slice(0, u.n_bindings))))
     for _ in range(args.warmup):
-        batch.schedule_raw()
-    barrier_sync()
+        for _, _, bt in lanes:
+            bt.schedule_raw()
     st_all = []
+    results = [None] * len(lanes)
+
+    def drive(k, n):
+        e_k, _, b_k = lanes[k]
+        st = []
+        for _ in range(n):
+            results[k] = b_k.schedule_raw()
+            st.append(e_k.stage_times())
+        st_all.extend(st)
+
+    per = [args.steps // len(lanes) + (1 if k < args.steps % len(lanes) else 0) for k in range(len(lanes))]
+    barrier_sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        r = batch.schedule_raw()
-        st_all.append(eng.stage_times())
+    if len(lanes) == 1:
+        drive(0, per[0])
+    else:
+        th = [threading.Thread(target=drive, args=(k, per[k])) for k in range(len(lanes)) if per[k] > 0]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
     barrier_sync()
     elapsed = time.perf_counter() - t0
+    r = results[0]
+    # one batch at a time (no overlap), for reference: a short serial run on engine 0
+    serial_ms = None
+    if len(lanes) > 1:
+        n_ser = max(1, min(args.steps, 50))
+        barrier_sync()
+        t1 = time.perf_counter()
+        st_ser = []
+        for _ in range(n_ser):
+            r = batch.schedule_raw()
+            st_ser.append(eng.stage_times())
+        barrier_sync()
+        st_all = st_ser  # per-stage HIP event times without another batch's kernels beside them
+        serial_ms = 1e3 * (time.perf_counter() - t1) / n_ser
+        if dist is not None:
+            import torch
+            t = torch.tensor([serial_ms], dtype=torch.float64, device=tdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            serial_ms = float(t.item())
     # ---- after the timed region ----
     csr = Csr.from_results(r)
     res = csr.to_python()
@@ -245,6 +297,10 @@ def main():
     # serial: one batch at a time; pipelined: two engines on this GPU, each packing
     # its next batch on the host while the other's batch runs on the device (a
     # scheduler draining its queue), timed over 2 x e2e_reps batches.
+    for e_k, s_k, b_k in lanes[1:]:
+        b_k.close()
+        s_k.close()
+        e_k.close()
     batch.close()
     e2e = e2e_pipe = None
     if args.e2e_reps > 0:
@@ -315,6 +371,10 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
+        "inflight": len(lanes),
+        # one batch at a time on one engine (nothing overlapped): ms per batch and the rate
+        "serial_ms_per_step": round(serial_ms, 3) if serial_ms else round(ms_per_step, 3),
+        "serial_value": round(B * world / (serial_ms * 1e-3), 1) if serial_ms else round(value, 1),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

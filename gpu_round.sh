@@ -27,7 +27,7 @@ for s in "$@"; do
     lib_*) n=${s#lib_}; step bench_$n 300 python bench.py --lib karmada_amd/libkp_$n.so --steps 50 --warmup 2 --no-cpu --check 200 ;;
     libst_*) n=${s#libst_}; step stamps_$n 300 python bench.py --lib karmada_amd/libkp_$n.so --steps 2 --warmup 1 --no-cpu --check 0 ;;
     prof_sq) step prof_sq 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --output-format csv -d $ROOT/gpurun_out/prof_sq -o sq -- python3 $ROOT/bench.py --steps 1 --warmup 0 --no-cpu" ;;
-    prof_kt) step prof_kt 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/prof_kt -o kt -- python3 $ROOT/bench.py --steps 5 --warmup 1 --no-cpu" ;;
+    prof_kt) step prof_kt 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/prof_kt -o kt -- python3 $ROOT/bench.py --steps 5 --warmup 1 --no-cpu --inflight 1 --e2e-reps 0" ;;
     prof_fetch) step prof_fetch 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --pmc FETCH_SIZE --output-format csv -d $ROOT/gpurun_out/prof_fetch -o f -- python3 $ROOT/bench.py --steps 2 --warmup 0 --no-cpu" ;;
     prof_write) step prof_write 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --pmc WRITE_SIZE --output-format csv -d $ROOT/gpurun_out/prof_write -o w -- python3 $ROOT/bench.py --steps 2 --warmup 0 --no-cpu" ;;
     dist2) KP_DIST_BACKEND=gloo step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --bindings 20000 ;;

@@ -13,7 +13,7 @@ for pass in \
   "FETCH_SIZE" \
   "WRITE_SIZE" ; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $pass --output-format csv -d $ROOT/gpurun_out/pmc_$tag/p$i -o p -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu --check 0 "$@" > $ROOT/gpurun_out/pmc_${tag}_p$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $pass --output-format csv -d $ROOT/gpurun_out/pmc_$tag/p$i -o p -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu --check 0 --inflight 1 --e2e-reps 0 "$@" > $ROOT/gpurun_out/pmc_${tag}_p$i.log 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi
