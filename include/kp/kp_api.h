@@ -33,6 +33,10 @@
  *                                       pkg/estimator/client/general.go:57-108)
  *        kp_max_available_component_sets <- ReplicaEstimator.MaxAvailableComponentSets
  *                                      (general.go:154-292)
+ *        kp_model_grades            <- getAllocatableModelings over modeling.AddToResourceSummary
+ *                                      (pkg/controllers/status/cluster_status_controller.go:642-677)
+ *        kp_node_max_replicas       <- noderesource.nodeResourceEstimator.Estimate (estimator server,
+ *                                      pkg/estimator/server/framework/plugins/noderesource)
  *        kp_snapshot_create         <- cache.Cache.Snapshot (pkg/scheduler/cache/cache.go:124-139)
  *        kp_schedule_affinities     <- Scheduler.scheduleResourceBindingWithClusterAffinities
  *                                      (pkg/scheduler/scheduler.go:584-585,618-684)
@@ -50,7 +54,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 8
+#define KP_ABI_VERSION 9
 
 /* ------------------------------------------------------------------------- */
 /* Object model                                                              */
@@ -463,6 +467,59 @@ int kp_max_available_replicas(kp_engine* e, kp_batch* b, uint64_t binding,
  * run capacity (kp_last_error says which). */
 int kp_max_available_component_sets(kp_engine* e, const kp_snapshot* s, const kp_component* components,
                                     uint32_t n_components, const uint32_t* cluster_idx, uint64_t n, int32_t* out);
+
+/* ---- member-cluster nodes ------------------------------------
+ * A member cluster's node as the cluster status controller and the estimator
+ * server see it: corev1.Node plus the non-terminal pods bound to it. `requested`
+ * is their summed effective requests (util.Resource.AddPodRequest: cpu, memory,
+ * ephemeral-storage and scalar resources), n_pods their count. */
+typedef struct kp_node {
+  kp_str name;
+  const kp_label* labels;
+  uint32_t n_labels;
+  const kp_taint* taints;
+  uint32_t n_taints;
+  int32_t unschedulable; /* node.Spec.Unschedulable */
+  const kp_resource* allocatable; /* node.Status.Allocatable */
+  uint32_t n_allocatable;
+  const kp_resource* requested;
+  uint32_t n_requested;
+  uint32_t n_pods;
+} kp_node;
+
+/* The resource-model grade histogram of a cluster: getAllocatableModelings
+ * (controllers/status/cluster_status_controller.go:642-677) over
+ * modeling.InitSummary / AddToResourceSummary (pkg/modeling/modeling.go:75-223).
+ * Each node's available resources (getNodeAvailable, :613-639; the walk stops at
+ * the first node with no pod room, as the reference's `break` does) go to the grade
+ * getIndex picks (searchLastLessElement per resource name, the minimum over names);
+ * out_counts[k] = AllocatableModeling.Count of models[k]. KP_EINVAL for
+ * InitSummary's error and for models without ranges. Replaces the Go function
+ * getAllocatableModelings. */
+int kp_model_grades(kp_engine* e, const kp_resource_model* models, uint32_t n_models, const kp_node* nodes,
+                    uint64_t n_nodes, int64_t* out_counts);
+
+/* pb.NodeClaim of the estimator request: nodeSelector and tolerations (required
+ * node-affinity terms are not modeled: has_node_affinity != 0 -> KP_ENOTSUP). */
+typedef struct kp_node_claim {
+  const kp_label* node_selector;
+  uint32_t n_node_selector;
+  const kp_toleration* tolerations;
+  uint32_t n_tolerations;
+  int32_t has_node_affinity;
+} kp_node_claim;
+
+/* The accurate estimator's per-node path: nodeResourceEstimator.Estimate
+ * (estimator/server/framework/plugins/noderesource/noderesource.go:70-131) with no
+ * assumed workloads: the sum over the nodes that MatchNode accepts (nodeSelector,
+ * tolerations incl. the unschedulable taint, filter.go:38-90) of int32(MaxDivided)
+ * of the node's available resources (allocatable - requested, clamped at 0; pods
+ * = allocatable pods - n_pods, util/resource.go:96-115,221-248) for `request`.
+ * claim may be NULL (no NodeClaim). *out = the int32 sum (Go's atomic int32 adds
+ * wrap). Replaces AccurateSchedulerEstimatorServer.EstimateReplicas for one request
+ * (estimate.go:33-76; 0 when there are no nodes). */
+int kp_node_max_replicas(kp_engine* e, const kp_node* nodes, uint64_t n_nodes, const kp_resource* request,
+                         uint32_t n_request, const kp_node_claim* claim, int32_t* out);
 
 /* Last schedule call's stage timings. */
 int kp_last_stage_times(const kp_engine* e, kp_stage_times* out);

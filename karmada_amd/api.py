@@ -104,6 +104,19 @@ class kp_resource_model(C.Structure):
     _fields_ = [("grade", u32), ("ranges", C.POINTER(kp_model_range)), ("n_ranges", u32)]
 
 
+class kp_node(C.Structure):
+    _fields_ = [("name", kp_str), ("labels", C.POINTER(kp_label)), ("n_labels", u32),
+                ("taints", C.POINTER(kp_taint)), ("n_taints", u32), ("unschedulable", i32),
+                ("allocatable", C.POINTER(kp_resource)), ("n_allocatable", u32),
+                ("requested", C.POINTER(kp_resource)), ("n_requested", u32), ("n_pods", u32)]
+
+
+class kp_node_claim(C.Structure):
+    _fields_ = [("node_selector", C.POINTER(kp_label)), ("n_node_selector", u32),
+                ("tolerations", C.POINTER(kp_toleration)), ("n_tolerations", u32),
+                ("has_node_affinity", i32)]
+
+
 class kp_allocatable_modeling(C.Structure):
     _fields_ = [("grade", u32), ("count", i64)]
 
@@ -286,6 +299,49 @@ class World:
         r.cluster_names, r.n_cluster_names = self.strs(a.get("clusterNames"))
         r.exclude_clusters, r.n_exclude_clusters = self.strs(a.get("exclude"))
         return r
+
+    def models(self, ms):
+        """[{grade, ranges: [{name, min, max}]}] -> (kp_resource_model array, n)."""
+        out = []
+        for m in ms or []:
+            rr = [kp_model_range(self.s(r["name"]), self.s(str(r.get("min", "0"))), self.s(str(r.get("max", ""))))
+                  for r in m.get("ranges") or []]
+            ra, nr = self.arr(kp_model_range, rr)
+            out.append(kp_resource_model(m.get("grade", 0), ra, nr))
+        return self.arr(kp_resource_model, out)
+
+    # -- member-cluster node ------------------------------------------------------------
+    def node(self, d: dict) -> kp_node:
+        """{name, labels, taints, unschedulable, allocatable, requested, pods} -> kp_node."""
+        n = kp_node()
+        n.name = self.s(d.get("name", ""))
+        n.labels, n.n_labels = self.arr(kp_label, [kp_label(self.s(k), self.s(v)) for k, v in (d.get("labels") or {}).items()])
+        n.taints, n.n_taints = self.arr(kp_taint, [
+            kp_taint(self.s(t.get("key")), self.s(t.get("value")), self.s(t.get("effect"))) for t in d.get("taints") or []])
+        n.unschedulable = int(bool(d.get("unschedulable")))
+        n.allocatable, n.n_allocatable = self.resources(d.get("allocatable"))
+        n.requested, n.n_requested = self.resources(d.get("requested"))
+        n.n_pods = int(d.get("pods", 0))
+        return n
+
+    def nodes(self, ds):
+        a = (kp_node * max(1, len(ds)))(*[self.node(d) for d in ds])
+        self._keep.append(a)
+        return a, len(ds)
+
+    def node_claim(self, d: Optional[dict]):
+        """{nodeSelector: {k: v}, tolerations: [...], nodeAffinity: any} -> kp_node_claim or None."""
+        if d is None:
+            return None
+        c = kp_node_claim()
+        c.node_selector, c.n_node_selector = self.arr(kp_label, [
+            kp_label(self.s(k), self.s(v)) for k, v in (d.get("nodeSelector") or {}).items()])
+        c.tolerations, c.n_tolerations = self.arr(kp_toleration, [
+            kp_toleration(self.s(t.get("key")), self.s(t.get("operator")), self.s(t.get("value")), self.s(t.get("effect")))
+            for t in d.get("tolerations") or []])
+        c.has_node_affinity = int(d.get("nodeAffinity") is not None)
+        self._keep.append(c)
+        return c
 
     # -- cluster ---------------------------------------------------------------------
     def cluster(self, d: dict) -> kp_cluster:

@@ -180,6 +180,18 @@ int component_sets(stream_t, const SnapView& s, const SetsArgs* A, const int32_t
   return 0;
 }
 
+int grades(stream_t, const GradesArgs& A) {
+  for (uint64_t i = 0; i < A.n; i++) body_grades(A, i);
+  return 0;
+}
+
+int node_est(stream_t, const NodeEstArgs& A) {
+  uint32_t s = 0;
+  for (uint64_t i = 0; i < A.n; i++) s += (uint32_t)node_replicas(A, i);
+  *A.sum += s;
+  return 0;
+}
+
 int reasons(stream_t, const SnapView& s, const BatchView& bv, uint32_t* out) {
   const uint64_t n = (uint64_t)bv.B * (uint64_t)s.C;
   for (uint64_t i = 0; i < n; i++) body_reasons(s, bv, i, out);

@@ -26,6 +26,7 @@
 #include "kp_paths.h"
 #include "kp_pdq.h"
 #include "kp_sets.h"
+#include "kp_nodes.h"
 
 using namespace kp;
 
@@ -2506,6 +2507,309 @@ int kp_max_available_replicas(kp_engine* e, kp_batch* bt, uint64_t binding, cons
     if (cluster_idx[i] >= (uint32_t)s->C) return KP_EINVAL;
     out[i] = row[s->inv[cluster_idx[i]]];
   }
+  return KP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Member-cluster nodes
+// ---------------------------------------------------------------------------
+namespace {
+// util.Resource (util/resource.go:28-93): cpu in milli, the rest in units; scalar
+// resources only under IsScalarResourceName.
+struct NodeRes {
+  int64_t cpu = 0, mem = 0, eph = 0, pods = 0;
+  std::map<std::string, int64_t> sc;
+};
+void res_add(NodeRes& r, const QtyMap& rl) {
+  for (auto& kv : rl) {
+    const std::string& n = kv.first;
+    if (n == "cpu") r.cpu += k8s::milli(kv.second);
+    else if (n == "memory") r.mem += k8s::value(kv.second);
+    else if (n == "pods") r.pods += k8s::value(kv.second);
+    else if (n == "ephemeral-storage") r.eph += k8s::value(kv.second);
+    else if (k8s::scalar_resource(n)) r.sc[n] += k8s::value(kv.second);
+  }
+}
+k8s::Qty qty_of(int64_t v, int64_t unit_nano, int fmt) {
+  k8s::Qty q;
+  q.nano = (k8s::i128)v * unit_nano;
+  q.fmt = fmt;
+  return q;
+}
+// getNodeAvailable (cluster_status_controller.go:613-639); false: no pod room
+// (the caller's walk stops there).
+bool node_available(const kp_node& nd, QtyMap* out) {
+  QtyMap alloc;
+  if (!qmap(nd.allocatable, nd.n_allocatable, &alloc)) return false;
+  if (nd.n_pods == 0) {  // no pods on the node: nodePodResourcesMap has no entry
+    *out = alloc;
+    return true;
+  }
+  QtyMap req;
+  qmap(nd.requested, nd.n_requested, &req);
+  NodeRes pr;
+  res_add(pr, req);
+  pr.pods += nd.n_pods;  // AddResourcePods
+  QtyMap al;  // Resource.ResourceList(): the positive fields
+  if (pr.cpu > 0) al["cpu"] = qty_of(pr.cpu, 1000000, 0);
+  if (pr.mem > 0) al["memory"] = qty_of(pr.mem, 1000000000, 1);
+  if (pr.eph > 0) al["ephemeral-storage"] = qty_of(pr.eph, 1000000000, 1);
+  if (pr.pods > 0) al["pods"] = qty_of(pr.pods, 1000000000, 0);
+  for (auto& kv : pr.sc)
+    if (kv.second > 0) al[kv.first] = qty_of(kv.second, 1000000000, kv.first.rfind("hugepages-", 0) == 0 ? 1 : 0);
+  auto pods_of = [](const QtyMap& m) {
+    auto it = m.find("pods");
+    return it == m.end() ? (int64_t)0 : k8s::value(it->second);
+  };
+  if (pods_of(alloc) - pods_of(al) <= 0) return false;
+  for (auto& kv : al) {
+    auto it = alloc.find(kv.first);
+    if (it != alloc.end()) k8s::qsub(it->second, kv.second);
+  }
+  *out = alloc;
+  return true;
+}
+void split128(k8s::i128 v, int64_t* hi, uint64_t* lo) {
+  *hi = (int64_t)(v >> 64);
+  *lo = (uint64_t)v;
+}
+}  // namespace
+
+int kp_model_grades(kp_engine* e, const kp_resource_model* models, uint32_t n_models, const kp_node* nodes,
+                    uint64_t n_nodes, int64_t* out_counts) {
+  if (!e || (n_models && !models) || (n_nodes && !nodes) || (n_models && !out_counts)) return KP_EINVAL;
+  (void)dev::set_device(e->device);
+  if (n_models == 0) return KP_OK;  // getAllocatableModelings returns nil
+  // modeling.InitSummary (modeling.go:75-102)
+  std::vector<std::string> rs_name;
+  std::vector<QtyMap> rs_list;
+  for (uint32_t g = 0; g < n_models; g++) {
+    QtyMap tmp;
+    for (uint32_t j = 0; j < models[g].n_ranges; j++) {
+      const kp_model_range& it = models[g].ranges[j];
+      if (rs_name.size() != models[g].n_ranges) rs_name.push_back(S(it.name));
+      k8s::Qty q;
+      if (!k8s::parse_quantity(S(it.min), &q)) {
+        e->err = "kp_model_grades: unparsable range minimum";
+        return KP_EINVAL;
+      }
+      tmp[S(it.name)] = q;
+    }
+    rs_list.push_back(tmp);
+  }
+  if (!rs_name.empty() && rs_name.size() != rs_list[0].size()) {
+    e->err = "the number of resourceName is not equal the number of resourceList";
+    return KP_EINVAL;
+  }
+  if (rs_name.empty()) {  // getIndex would index RMs[MaxInt]
+    e->err = "kp_model_grades: resource models without ranges";
+    return KP_EINVAL;
+  }
+  const int K = (int)n_models, NR = (int)rs_name.size();
+  std::vector<int64_t> mh((size_t)NR * K), vh;
+  std::vector<uint64_t> ml((size_t)NR * K), vl;
+  for (int r = 0; r < NR; r++)
+    for (int g = 0; g < K; g++) {
+      auto it = rs_list[g].find(rs_name[r]);
+      split128(it == rs_list[g].end() ? (k8s::i128)0 : it->second.nano, &mh[(size_t)r * K + g], &ml[(size_t)r * K + g]);
+    }
+  // the nodes' available resources, up to the first without pod room
+  uint64_t n = 0;
+  vh.reserve((size_t)n_nodes * NR);
+  vl.reserve((size_t)n_nodes * NR);
+  for (; n < n_nodes; n++) {
+    QtyMap av;
+    if (!node_available(nodes[n], &av)) break;
+    for (int r = 0; r < NR; r++) {
+      auto it = av.find(rs_name[r]);
+      int64_t h;
+      uint64_t l;
+      split128(it == av.end() ? (k8s::i128)0 : it->second.nano, &h, &l);
+      vh.push_back(h);
+      vl.push_back(l);
+    }
+  }
+  Arena a;
+  int64_t *d_mh, *d_vh;
+  uint64_t *d_ml, *d_vl;
+  unsigned long long* d_cnt;
+  a.add(&d_mh, mh.size());
+  a.add(&d_ml, ml.size());
+  a.add(&d_vh, std::max<size_t>(1, vh.size()));
+  a.add(&d_vl, std::max<size_t>(1, vl.size()));
+  a.add(&d_cnt, K);
+  HIPCHK(a.alloc());
+  dev::stream_t st = e->stream;
+  HIPCHK(dev::h2d(d_mh, mh.data(), 8 * mh.size(), st));
+  HIPCHK(dev::h2d(d_ml, ml.data(), 8 * ml.size(), st));
+  HIPCHK(dev::h2d(d_vh, vh.data(), 8 * vh.size(), st));
+  HIPCHK(dev::h2d(d_vl, vl.data(), 8 * vl.size(), st));
+  HIPCHK(dev::fill(d_cnt, 0, 8 * (size_t)K, st));
+  GradesArgs A{K, NR, d_mh, d_ml, d_vh, d_vl, n, d_cnt};
+  HIPCHK(dev::grades(st, A));
+  std::vector<unsigned long long> c(K);
+  HIPCHK(dev::d2h(c.data(), d_cnt, 8 * (size_t)K, st));
+  HIPCHK(dev::sync(st));
+  for (int g = 0; g < K; g++) out_counts[g] = (int64_t)c[g];
+  return KP_OK;
+}
+
+int kp_node_max_replicas(kp_engine* e, const kp_node* nodes, uint64_t n_nodes, const kp_resource* request,
+                         uint32_t n_request, const kp_node_claim* claim, int32_t* out) {
+  if (!e || !out || (n_nodes && !nodes) || (n_request && !request)) return KP_EINVAL;
+  (void)dev::set_device(e->device);
+  *out = 0;
+  if (claim && claim->has_node_affinity) {
+    e->err = "kp_node_max_replicas: required node-affinity terms are not modeled";
+    return KP_ENOTSUP;
+  }
+  QtyMap rq;
+  if (!qmap(request, n_request, &rq)) {
+    e->err = "kp_node_max_replicas: unparsable resource request";
+    return KP_EINVAL;
+  }
+  if (n_nodes == 0) return KP_OK;  // estimate.go:43-45
+  // MaxDivided's dividing entries (resource.go:221-248): cpu milli, memory,
+  // ephemeral-storage, scalar resources, each > 0
+  std::vector<std::string> qn;
+  std::vector<int64_t> qv;
+  for (auto& kv : rq) {
+    const std::string& nm = kv.first;
+    int64_t v = 0;
+    if (nm == "cpu") v = k8s::milli(kv.second);
+    else if (nm == "memory" || nm == "ephemeral-storage" || k8s::scalar_resource(nm)) v = k8s::value(kv.second);
+    else continue;
+    if (v > 0) {
+      qn.push_back(nm);
+      qv.push_back(v);
+    }
+  }
+  const int NQ = (int)qn.size();
+  Dict d;  // strings of this call
+  std::vector<int64_t> avail, pods, lbl, sel;
+  std::vector<uint32_t> flags;
+  std::vector<int32_t> lbl_off{0}, tnt_off{0}, tnt;
+  for (uint64_t i = 0; i < n_nodes; i++) {
+    const kp_node& nd = nodes[i];
+    QtyMap al, rqd;
+    if (!qmap(nd.allocatable, nd.n_allocatable, &al) || !qmap(nd.requested, nd.n_requested, &rqd)) {
+      e->err = "kp_node_max_replicas: unparsable node quantity";
+      return KP_EINVAL;
+    }
+    NodeRes a, r;  // getNodeAvailableResource (noderesource.go:135-144)
+    res_add(a, al);
+    res_add(r, rqd);
+    for (int j = 0; j < NQ; j++) {
+      int64_t x;
+      if (qn[j] == "cpu") x = std::max<int64_t>(a.cpu - r.cpu, 0);
+      else if (qn[j] == "memory") x = std::max<int64_t>(a.mem - r.mem, 0);
+      else if (qn[j] == "ephemeral-storage") x = std::max<int64_t>(a.eph - r.eph, 0);
+      else {
+        auto ia = a.sc.find(qn[j]);
+        auto ir = r.sc.find(qn[j]);
+        x = ia == a.sc.end() ? 0 : (ir == r.sc.end() ? ia->second : std::max<int64_t>(ia->second - ir->second, 0));
+      }
+      avail.push_back(x);
+    }
+    pods.push_back(std::max<int64_t>(std::max<int64_t>(a.pods - r.pods, 0) - (int64_t)nd.n_pods, 0));
+    flags.push_back(nd.unschedulable ? 1u : 0u);
+    std::map<std::string, std::string> lm;
+    for (uint32_t j = 0; j < nd.n_labels; j++) lm[S(nd.labels[j].key)] = S(nd.labels[j].value);
+    for (auto& kv : lm) lbl.push_back(((int64_t)d.add(kv.first) << 32) | (int64_t)(uint32_t)d.add(kv.second));
+    lbl_off.push_back((int32_t)lbl.size());
+    for (uint32_t j = 0; j < nd.n_taints; j++) {
+      const std::string ef = S(nd.taints[j].effect);
+      if (ef != "NoSchedule" && ef != "NoExecute") continue;  // DoNotScheduleTaintsFilterFunc
+      tnt.push_back(d.add(S(nd.taints[j].key)));
+      tnt.push_back(d.add(S(nd.taints[j].value)));
+      tnt.push_back(ef == "NoSchedule" ? EFF_NOSCHEDULE : EFF_NOEXECUTE);
+    }
+    tnt_off.push_back((int32_t)(tnt.size() / 3));
+  }
+  std::vector<Tol> tols;
+  int32_t tol_unsched = 0;
+  if (claim) {
+    std::map<std::string, std::string> sm;  // SelectorFromSet: one requirement per key
+    for (uint32_t j = 0; j < claim->n_node_selector; j++)
+      sm[S(claim->node_selector[j].key)] = S(claim->node_selector[j].value);
+    for (auto& kv : sm) sel.push_back(((int64_t)d.add(kv.first) << 32) | (int64_t)(uint32_t)d.add(kv.second));
+    for (uint32_t j = 0; j < claim->n_tolerations; j++) {
+      const kp_toleration& t = claim->tolerations[j];
+      const std::string ef = S(t.effect), key = S(t.key), op = S(t.op), val = S(t.value);
+      // TolerationsTolerateTaint for {node.kubernetes.io/unschedulable, NoSchedule}
+      if ((ef.empty() || ef == "NoSchedule") && (key.empty() || key == "node.kubernetes.io/unschedulable") &&
+          (op == "Exists" || ((op.empty() || op == "Equal") && val.empty())))
+        tol_unsched = 1;
+      Tol x;
+      if (ef.empty()) x.eff = EFF_ANY;
+      else if (ef == "NoSchedule") x.eff = EFF_NOSCHEDULE;
+      else if (ef == "NoExecute") x.eff = EFF_NOEXECUTE;
+      else continue;
+      x.key = key.empty() ? -1 : d.add(key);
+      if (op.empty() || op == "Equal") {
+        x.op = TOL_EQUAL;
+        x.val = d.add(val);
+      } else if (op == "Exists") {
+        x.op = TOL_EXISTS;
+        x.val = -1;
+      } else {
+        continue;  // Lt/Gt disabled, unknown operators never tolerate
+      }
+      tols.push_back(x);
+    }
+  }
+  Arena ar;
+  int64_t *d_avail, *d_q, *d_pods, *d_lbl, *d_sel;
+  uint32_t *d_flags, *d_sum;
+  int32_t *d_loff, *d_toff, *d_tnt;
+  Tol* d_tols;
+  ar.add(&d_avail, std::max<size_t>(1, avail.size()));
+  ar.add(&d_q, std::max<size_t>(1, qv.size()));
+  ar.add(&d_pods, pods.size());
+  ar.add(&d_flags, flags.size());
+  ar.add(&d_loff, lbl_off.size());
+  ar.add(&d_lbl, std::max<size_t>(1, lbl.size()));
+  ar.add(&d_toff, tnt_off.size());
+  ar.add(&d_tnt, std::max<size_t>(1, tnt.size()));
+  ar.add(&d_sel, std::max<size_t>(1, sel.size()));
+  ar.add(&d_tols, std::max<size_t>(1, tols.size()));
+  ar.add(&d_sum, 1);
+  HIPCHK(ar.alloc());
+  dev::stream_t st = e->stream;
+  auto up = [&](void* dd, const void* h, size_t bytes) { return dev::h2d(dd, h, bytes, st); };
+  HIPCHK(up(d_avail, avail.data(), 8 * avail.size()));
+  HIPCHK(up(d_q, qv.data(), 8 * qv.size()));
+  HIPCHK(up(d_pods, pods.data(), 8 * pods.size()));
+  HIPCHK(up(d_flags, flags.data(), 4 * flags.size()));
+  HIPCHK(up(d_loff, lbl_off.data(), 4 * lbl_off.size()));
+  HIPCHK(up(d_lbl, lbl.data(), 8 * lbl.size()));
+  HIPCHK(up(d_toff, tnt_off.data(), 4 * tnt_off.size()));
+  HIPCHK(up(d_tnt, tnt.data(), 4 * tnt.size()));
+  HIPCHK(up(d_sel, sel.data(), 8 * sel.size()));
+  HIPCHK(up(d_tols, tols.data(), sizeof(Tol) * tols.size()));
+  HIPCHK(dev::fill(d_sum, 0, 4, st));
+  NodeEstArgs A;
+  A.n = n_nodes;
+  A.NQ = NQ;
+  A.avail = d_avail;
+  A.q = d_q;
+  A.pods = d_pods;
+  A.flags = d_flags;
+  A.lbl_off = d_loff;
+  A.lbl = d_lbl;
+  A.tnt_off = d_toff;
+  A.tnt = d_tnt;
+  A.sel = d_sel;
+  A.n_sel = (int32_t)sel.size();
+  A.tols = d_tols;
+  A.n_tols = (int32_t)tols.size();
+  A.tol_unsched = tol_unsched;
+  A.sum = d_sum;
+  HIPCHK(dev::node_est(st, A));
+  uint32_t sum = 0;
+  HIPCHK(dev::d2h(&sum, d_sum, 4, st));
+  HIPCHK(dev::sync(st));
+  *out = (int32_t)sum;
   return KP_OK;
 }
 

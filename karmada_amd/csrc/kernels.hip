@@ -134,6 +134,17 @@ extern "C" __global__ void __launch_bounds__(64) k_sets(SnapView s, const SetsAr
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) body_sets(s, A, ranks, off, i, scratch, out);
 }
+extern "C" __global__ void __launch_bounds__(256) k_grades(GradesArgs A) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < A.n) body_grades(A, i);
+}
+extern "C" __global__ void __launch_bounds__(256) k_node_est(NodeEstArgs A) {
+  __shared__ int64_t red[128];
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const GpuBlk B{red};
+  const int64_t s = B.sum64(i < A.n ? (int64_t)(uint32_t)node_replicas(A, i) : 0);
+  if (threadIdx.x == 0) atomicAdd(A.sum, (uint32_t)(uint64_t)s);  // mod 2^32: Go's wrapping int32 adds
+}
 extern "C" __global__ void __launch_bounds__(256) k_reasons(SnapView s, BatchView bv, uint64_t n, uint32_t* out) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     body_reasons(s, bv, i, out);
@@ -326,6 +337,18 @@ int component_sets(stream_t st, const SnapView& s, const SetsArgs* A, const int3
                    uint64_t n, int64_t* scratch, int32_t* out) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(k_sets, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)st, s, A, ranks, off, n, scratch, out);
+  return chk(hipGetLastError());
+}
+
+int grades(stream_t st, const GradesArgs& A) {
+  if (A.n == 0) return 0;
+  hipLaunchKernelGGL(k_grades, dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, (hipStream_t)st, A);
+  return chk(hipGetLastError());
+}
+
+int node_est(stream_t st, const NodeEstArgs& A) {
+  if (A.n == 0) return 0;
+  hipLaunchKernelGGL(k_node_est, dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, (hipStream_t)st, A);
   return chk(hipGetLastError());
 }
 

@@ -13,6 +13,8 @@
 
 namespace kp {
 struct SetsArgs;
+struct GradesArgs;
+struct NodeEstArgs;
 namespace dev {
 
 typedef void* stream_t;
@@ -62,6 +64,10 @@ int region_groups(stream_t st, const RegionOut* rout, const int32_t* rstat, cons
 // (A, ranks and off in device memory; cluster i's runs at scratch[off[i], off[i+1])).
 int component_sets(stream_t st, const SnapView& s, const SetsArgs* A, const int32_t* ranks, const int64_t* off,
                    uint64_t n, int64_t* scratch, int32_t* out);
+// kp_model_grades: A.counts[grade] += 1 per node (body_grades); A's arrays in device memory.
+int grades(stream_t st, const GradesArgs& A);
+// kp_node_max_replicas: *A.sum += int32 sum of node_replicas over the nodes (wrapping).
+int node_est(stream_t st, const NodeEstArgs& A);
 // kp_filter_reasons: out[b * C + r] = pair_reason of binding b, cluster rank r.
 int reasons(stream_t st, const SnapView& s, const BatchView& bv, uint32_t* out);
 // CSR offsets[n + 1] of the per-binding results (counts of OK bindings), on the device;

@@ -17,6 +17,7 @@
 #include "kp_paths.h"
 #include "kp_pdq.h"
 #include "kp_filter.h"
+#include "kp_nodes.h"
 
 namespace kp {
 

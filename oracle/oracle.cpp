@@ -2771,4 +2771,161 @@ void kpo_sort_target_clusters(int32_t* replicas, uint32_t* ids, uint32_t n) {
 
 uint32_t kpo_fnv32a(const char* s, uint32_t len) { return fnv32a(string(s, len)); }
 
+
+// ---------------------------------------------------------------------------
+// Member-cluster nodes
+// ---------------------------------------------------------------------------
+static ResourceList rl_of(const kp_resource* r, uint32_t n, bool* ok) {
+  ResourceList m;
+  for (uint32_t i = 0; i < n; i++) {
+    Quantity q;
+    if (!ParseQuantity(S(r[i].quantity), &q)) *ok = false;
+    m[S(r[i].name)] = q;
+  }
+  return m;
+}
+
+// modeling.searchLastLessElement (modeling.go:123-145)
+static int SearchLastLessElement(const vector<Quantity>& nums, const Quantity& target) {
+  int low = 0, high = (int)nums.size() - 1;
+  while (low <= high) {
+    int mid = low + ((high - low) >> 1);
+    int diff1 = nums[mid].nano < target.nano ? -1 : (nums[mid].nano > target.nano ? 1 : 0);
+    int diff2 = 0;
+    if (mid != (int)nums.size() - 1)
+      diff2 = nums[mid + 1].nano < target.nano ? -1 : (nums[mid + 1].nano > target.nano ? 1 : 0);
+    if (diff1 < 1) {
+      if (mid == (int)nums.size() - 1 || diff2 == 1) return mid;
+      low = mid + 1;
+    } else {
+      high = mid - 1;
+    }
+  }
+  return -1;
+}
+
+// getAllocatableModelings (cluster_status_controller.go:642-677) with
+// modeling.InitSummary (modeling.go:75-102), getIndex (:112-121) and
+// AddToResourceSummary (:163-223; only the per-grade Quantity is observable).
+int kpo_model_grades(const kp_resource_model* models, uint32_t n_models, const kp_node* nodes, uint64_t n_nodes,
+                     int64_t* out) {
+  if (n_models == 0) return 0;
+  vector<string> rsName;
+  vector<ResourceList> rsList;
+  bool ok = true;
+  for (uint32_t g = 0; g < n_models; g++) {
+    ResourceList tmp;
+    for (uint32_t j = 0; j < models[g].n_ranges; j++) {
+      const kp_model_range& it = models[g].ranges[j];
+      if (rsName.size() != models[g].n_ranges) rsName.push_back(S(it.name));
+      Quantity q;
+      if (!ParseQuantity(S(it.min), &q)) ok = false;
+      tmp[S(it.name)] = q;
+    }
+    rsList.push_back(tmp);
+  }
+  if (!ok) return -1;
+  if (!rsName.empty() && !rsList.empty() && rsName.size() != rsList[0].size()) return -1;  // InitSummary error
+  if (rsName.empty()) return -1;  // getIndex -> MaxInt: RMs[MaxInt] panics
+  vector<vector<Quantity>> sortings(rsName.size());
+  for (size_t g = 0; g < rsList.size(); g++)
+    for (size_t i = 0; i < rsName.size(); i++) {
+      auto it = rsList[g].find(rsName[i]);
+      sortings[i].push_back(it == rsList[g].end() ? Quantity() : it->second);
+    }
+  for (uint32_t g = 0; g < n_models; g++) out[g] = 0;
+  for (uint64_t k = 0; k < n_nodes; k++) {
+    const kp_node& nd = nodes[k];
+    ResourceList alloc = rl_of(nd.allocatable, nd.n_allocatable, &ok);
+    if (!ok) return -1;
+    // getNodeAvailable (:613-639); nodePodResourcesMap has no entry without pods
+    if (nd.n_pods > 0) {
+      Resource pr;
+      pr.Add(rl_of(nd.requested, nd.n_requested, &ok));
+      ResourceList pods1;
+      pods1["pods"].nano = (i128)nd.n_pods * 1000000000;
+      pr.Add(pods1);  // AddResourcePods
+      ResourceList al;  // Resource.ResourceList (resource.go:250-280)
+      if (pr.MilliCPU > 0) al["cpu"] = Quantity{(i128)pr.MilliCPU * 1000000, 0};
+      if (pr.Memory > 0) al["memory"] = Quantity{(i128)pr.Memory * 1000000000, 1};
+      if (pr.EphemeralStorage > 0) al["ephemeral-storage"] = Quantity{(i128)pr.EphemeralStorage * 1000000000, 1};
+      if (pr.AllowedPodNumber > 0) al["pods"] = Quantity{(i128)pr.AllowedPodNumber * 1000000000, 0};
+      for (auto& kv : pr.Scalar)
+        if (kv.second > 0) al[kv.first] = Quantity{(i128)kv.second * 1000000000, kv.first.rfind("hugepages-", 0) == 0 ? 1 : 0};
+      auto podsv = [](const ResourceList& m) {
+        auto it = m.find("pods");
+        return it == m.end() ? (i64)0 : QValue(it->second);
+      };
+      if (podsv(alloc) - podsv(al) <= 0) break;  // nodeAvailable == nil: the walk stops
+      for (auto& kv : al) {
+        auto it = alloc.find(kv.first);
+        if (it != alloc.end()) it->second.nano -= kv.second.nano;  // Quantity.Sub
+      }
+    }
+    int index = INT32_MAX;  // getIndex
+    for (size_t i = 0; i < rsName.size(); i++) {
+      auto it = alloc.find(rsName[i]);
+      int t = SearchLastLessElement(sortings[i], it == alloc.end() ? Quantity() : it->second);
+      if (t < index) index = t;
+    }
+    if (index == -1) continue;  // no appropriate grade
+    out[index] += 1;
+  }
+  return 0;
+}
+
+// nodeResourceEstimator.Estimate (noderesource.go:70-131), no assumed workloads:
+// MatchNode (filter.go:60-90) then the int32 sum of MaxDivided over the nodes'
+// available resources (getNodeAvailableResource, :135-144).
+int kpo_node_max_replicas(const kp_node* nodes, uint64_t n_nodes, const kp_resource* request, uint32_t n_request,
+                          const kp_node_claim* claim, int32_t* out) {
+  *out = 0;
+  if (claim && claim->has_node_affinity) return -2;
+  bool ok = true;
+  Resource req;
+  req.Add(rl_of(request, n_request, &ok));
+  if (!ok) return -1;
+  std::map<string, string> selector;
+  vector<Toleration> tols;
+  if (claim) {
+    for (uint32_t j = 0; j < claim->n_node_selector; j++)
+      selector[S(claim->node_selector[j].key)] = S(claim->node_selector[j].value);
+    for (uint32_t j = 0; j < claim->n_tolerations; j++) {
+      const kp_toleration& t = claim->tolerations[j];
+      tols.push_back(Toleration{S(t.key), S(t.op), S(t.value), S(t.effect)});
+    }
+  }
+  const Taint unsched{"node.kubernetes.io/unschedulable", "", "NoSchedule"};
+  bool tolUnsched = false;
+  for (auto& t : tols) tolUnsched = tolUnsched || ToleratesTaint(t, unsched);
+  uint32_t res = 0;  // atomic.AddInt32 wraps
+  for (uint64_t k = 0; k < n_nodes; k++) {
+    const kp_node& nd = nodes[k];
+    std::map<string, string> labels;
+    for (uint32_t j = 0; j < nd.n_labels; j++) labels[S(nd.labels[j].key)] = S(nd.labels[j].value);
+    bool match = true;
+    for (auto& kv : selector) {  // labels.SelectorFromSet
+      auto it = labels.find(kv.first);
+      if (it == labels.end() || it->second != kv.second) match = false;
+    }
+    if (nd.unschedulable && !tolUnsched) match = false;
+    for (uint32_t j = 0; j < nd.n_taints && match; j++) {
+      const Taint taint{S(nd.taints[j].key), S(nd.taints[j].value), S(nd.taints[j].effect)};
+      if (!(taint.effect == "NoSchedule" || taint.effect == "NoExecute")) continue;
+      bool tol = false;
+      for (auto& t : tols) tol = tol || ToleratesTaint(t, taint);
+      if (!tol) match = false;
+    }
+    if (!match) continue;
+    Resource rest, rq;
+    rest.Add(rl_of(nd.allocatable, nd.n_allocatable, &ok));
+    rq.Add(rl_of(nd.requested, nd.n_requested, &ok));
+    if (!ok) return -1;
+    rest.Sub(rq);
+    rest.AllowedPodNumber = std::max<i64>(rest.AllowedPodNumber - (i64)nd.n_pods, 0);
+    res += (uint32_t)(int32_t)rest.MaxDivided(req);
+  }
+  *out = (int32_t)res;
+  return 0;
+}
 }  // extern "C"

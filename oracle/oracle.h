@@ -154,6 +154,12 @@ int kpo_dynamic_divide(const kp_target_cluster* avail, uint32_t n, int32_t avail
 /* Go 1.26 sort.Sort emulation on TargetClustersList (Less = Replicas desc). */
 void kpo_sort_target_clusters(int32_t* replicas, uint32_t* ids, uint32_t n);
 uint32_t kpo_fnv32a(const char* s, uint32_t len);
+/* getAllocatableModelings' grade counts (0 ok, -1 InitSummary error) and
+ * nodeResourceEstimator.Estimate's sum (0 ok, -1 parse error, -2 node affinity). */
+int kpo_model_grades(const kp_resource_model* models, uint32_t n_models, const kp_node* nodes, uint64_t n_nodes,
+                     int64_t* out);
+int kpo_node_max_replicas(const kp_node* nodes, uint64_t n_nodes, const kp_resource* request, uint32_t n_request,
+                          const kp_node_claim* claim, int32_t* out);
 
 #ifdef __cplusplus
 }
