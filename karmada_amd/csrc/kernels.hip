@@ -286,7 +286,7 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
   hipStream_t h = (hipStream_t)st;
   switch (which) {
     case SEL_LAUNCH_ALL:
-      if (smem > kLdsPerCu / 2 && !getenv("KP_SEL_THREADS"))  // one workgroup per CU: go wide
+      if ((smem > kLdsPerCu / 2 && !getenv("KP_SEL_THREADS")) || getenv("KP_SEL_WIDE"))  // one workgroup per CU: go wide
         hipLaunchKernelGGL(k_select_all_wide, dim3(a.n), dim3(1024), smem, h, a);
       else
         hipLaunchKernelGGL(k_select_all, dim3(a.n), dim3(sel_threads()), smem, h, a);

@@ -242,6 +242,7 @@ KP_HD inline bool scale_down_targets(const SelCtx& x, unsigned char* mem, size_t
 // scheduled replicas > 0 (the prior clusters, if merging) their sum and count.
 struct DivSums {
   int64_t sabs = 0, vmin = 0, vtot = 0, nparty = 0, sp = 0, np = 0;
+  int64_t vmax = 0, P = 0;  // largest vote, votes > 0 (with the octave histogram in ss.hist: WebPre)
   bool valid = false;
 };
 
@@ -302,11 +303,15 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
   // BF_FRESH; the prior-cluster sum is 0 unless some prior has replicas).
   const bool fresh = (h.flags & BF_FRESH) != 0;
   auto tgt = [&](uint32_t rk) { return h.tgt_cnt > 0 && bit_test(x.tgt_bits, (int)rk); };
+  // this pass also takes Webster's vote totals and octave histogram (WebPre)
+  for (int i = B.tid(); i < 256; i += B.nth()) ss.hist[i] = 0;
+  if (B.tid() == 0) *web_ctr(ss) = 0;
   int64_t asum = 0, apos = 0;
   TgtCands{&x, B.tid(), B.nth()}.each([&](uint32_t, int32_t v) {
     asum += v;
-    apos |= v > 0 ? 1 : 0;
+    apos += v > 0 ? 1 : 0;
   });
+  B.sync();
   DivSums ds;
   cs.each([&](uint32_t rk, int32_t v0) {
     int32_t v32 = v0;
@@ -319,18 +324,29 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
     const int64_t v = v32;
     ds.sabs += v < 0 ? -v : v;
     if (v < ds.vmin) ds.vmin = v;
+    if (v > ds.vmax) ds.vmax = v;
     ds.vtot += v;
     ds.nparty++;
+    if (v > 0) {
+      ds.P++;
+      kp_atomic_add(&ss.hist[vote_bin((uint32_t)v)], 1u);
+    }
     if (pr) {
       ds.sp += v;
       ds.np++;
     }
   });
   {
+    // counts < 2^32 share a slot: (apos | P << 32), (nparty | np << 32)
     auto add = [](int64_t p, int64_t q) { return p + q; };
-    B.reduce4(asum, add, 0, apos, [](int64_t p, int64_t q) { return p | q; }, 0, ds.sabs, add, 0, ds.vtot, add, 0);
-    B.reduce4(ds.vmin, [](int64_t p, int64_t q) { return p < q ? p : q; }, 0, ds.nparty, add, 0, ds.sp, add, 0, ds.np,
-              add, 0);
+    int64_t ap = apos + (ds.P << 32), pn = ds.nparty + (ds.np << 32);
+    B.reduce4(asum, add, 0, ap, add, 0, ds.sabs, add, 0, ds.vtot, add, 0);
+    B.reduce4(ds.vmin, [](int64_t p, int64_t q) { return p < q ? p : q; }, 0, pn, add, 0, ds.sp, add, 0, ds.vmax,
+              [](int64_t p, int64_t q) { return p > q ? p : q; }, 0);
+    apos = ap & 0xffffffffll;
+    ds.P = ap >> 32;
+    ds.nparty = pn & 0xffffffffll;
+    ds.np = pn >> 32;
   }
   ds.valid = true;
   const int32_t assigned = wrap32(asum);
@@ -475,7 +491,10 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
       if (member(rk, v, v0)) fn(rk, v);
     });
   };
-  WebRes w = webster_par(B, parties, target, desc, ss);
+  // DynamicWeight: the parties are every candidate with the votes sel_all_fast's pass
+  // summed (vote32), so its totals and histogram stand in for Webster's first pass
+  const WebPre wp{pre ? pre->vtot : 0, pre ? pre->vmax : 0, pre ? pre->P : 0};
+  WebRes w = webster_par(B, parties, target, desc, ss, pre && st != ST_AGGREGATED ? &wp : nullptr);
   KP_STAMP(x, 4);
   if (w.mode == 2 && w.compact && !prop) {
     // Only parties take seats, and every party with a seat is in Webster's compacted

@@ -746,29 +746,40 @@ KP_FI uint64_t rank_select(const BLK& B, const uint64_t* keys, int E, int64_t k,
 // priorities remain, which are enumerated and rank-selected.
 // Seats strictly above t* are exact per party; the tie group at t* is ordered
 // by (seats asc, name) as the heap's tie-breaker orders it (tie_key).
+// Totals of the party votes a caller already took in its own pass (with the octave
+// histogram in sc.hist and the party-list counter zeroed): webster_par skips its first pass.
+struct WebPre {
+  int64_t V, vmax, P;
+};
+KP_HD inline uint32_t* web_ctr(const SelScratch& sc) { return (uint32_t*)sc.whist + 511; }  // party list fill counter
 template <class BLK, class Parties>
-KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc, const SelScratch& sc) {
+KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc, const SelScratch& sc,
+                         const WebPre* pre = nullptr) {
   KP_STAMP_INIT
   WebRes r;
   r.N = N;
   r.desc = desc;
   r.t = 0;
   r.tie = 0;
-  // One pass: totals and the octave histogram of the votes (kth_vote_floor).
-  uint32_t* ctr = (uint32_t*)sc.whist + 511;  // party list fill counter
-  for (int i = B.tid(); i < 256; i += B.nth()) sc.hist[i] = 0;
-  if (B.tid() == 0) *ctr = 0;
-  B.sync();
+  uint32_t* ctr = web_ctr(sc);
   int64_t V = 0, vmax = 0, P = 0, none = 0;
-  all_parties([&](uint32_t, int64_t v) {
-    V += v;
-    if (v > vmax) vmax = v;
-    if (v > 0) {
-      P++;
-      kp_atomic_add(&sc.hist[vote_bin((uint32_t)v)], 1u);
-    }
-  });
-  {
+  if (pre) {
+    V = pre->V;
+    vmax = pre->vmax;
+    P = pre->P;
+  } else {
+    // One pass: totals and the octave histogram of the votes (kth_vote_floor).
+    for (int i = B.tid(); i < 256; i += B.nth()) sc.hist[i] = 0;
+    if (B.tid() == 0) *ctr = 0;
+    B.sync();
+    all_parties([&](uint32_t, int64_t v) {
+      V += v;
+      if (v > vmax) vmax = v;
+      if (v > 0) {
+        P++;
+        kp_atomic_add(&sc.hist[vote_bin((uint32_t)v)], 1u);
+      }
+    });
     auto add = [](int64_t p, int64_t q) { return p + q; };
     B.reduce4(V, add, 0, P, add, 0, vmax, [](int64_t p, int64_t q) { return p > q ? p : q; }, INT64_MIN, none, add, 0);
   }
