@@ -22,18 +22,19 @@ using namespace kp;
 
 #define KP_SMEM extern __shared__ __align__(16) unsigned char smem[]
 // k_select_all: workgroup size bound and minimum waves per SIMD. Its LDS (~53 KB at
-// C = 5k with KP_ECAP_MAX = 1024) allows 3 workgroups of 512 threads per CU, i.e. 6
-// waves per SIMD; asking the compiler for 6 keeps the VGPRs at <= 80 so that those 3
-// workgroups are resident together (89 VGPRs allowed only 2: 5.5 -> 4.2 ms at config 3).
+// C = 5k with KP_ECAP_MAX = 1024) allows 3 workgroups per CU. 256-thread workgroups
+// (3 waves per SIMD, 93 VGPRs, no scratch) ran 3.93 ms at config 3 against 4.01-4.02 ms
+// for 512 threads at 6 waves per SIMD (80 VGPRs + 60 B/lane scratch): fewer waves wait
+// at each of the binding's barriers.
 constexpr size_t kLdsPerCu = 160 * 1024;  // gfx950 LDS per CU
 #ifndef KP_PAIR_MIN_WAVES
 #define KP_PAIR_MIN_WAVES 1
 #endif
 #ifndef KP_SEL_MAX_THREADS
-#define KP_SEL_MAX_THREADS 512
+#define KP_SEL_MAX_THREADS 256
 #endif
 #ifndef KP_SEL_MIN_WAVES
-#define KP_SEL_MIN_WAVES 6
+#define KP_SEL_MIN_WAVES 3
 #endif
 
 extern "C" __global__ void __launch_bounds__(kBlock) k_pair(SnapView s, BatchView bv, const int32_t* list, int b0,
@@ -179,8 +180,8 @@ thread_local hipError_t g_err = hipSuccess;
 int sel_threads() {
   static int n = [] {
     const char* e = getenv("KP_SEL_THREADS");
-    int v = e ? atoi(e) : 512;
-    return (v == 256 || v == 512) && v <= KP_SEL_MAX_THREADS ? v : 512;
+    int v = e ? atoi(e) : KP_SEL_MAX_THREADS;
+    return (v == 128 || v == 256 || v == 512) && v <= KP_SEL_MAX_THREADS ? v : KP_SEL_MAX_THREADS;
   }();
   return n;
 }

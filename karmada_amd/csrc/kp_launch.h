@@ -53,12 +53,6 @@ constexpr int kPairStage = 4096;  // bytes of per-binding predicate data staged 
 constexpr int kTsetMax = 4096;    // distinct taint lists answered once per binding (LDS bits)
 
 
-// LDS bytes of the pair stage's per-binding tail (evict bits | md table | predicate
-// stage | taint-list bits; kp_kernels.h PairLds).
-KP_HD inline size_t pair_lds_tail_bytes(int Cp, int md_cap) {  // evict | md | stage | tolb
-  const int words = (Cp + 31) >> 5;
-  return 4 * (size_t)((words + 3) & ~3) + 4 * (size_t)((md_cap + 3) & ~3) + kPairStage + kTsetMax / 8;
-}
 constexpr int kOffThreads = 256, kOffChunk = 4 * kOffThreads;  // CSR offsets scan (body_offsets_a/b)
 constexpr int kSwRules = 4;  // StaticWeight rules kept as LDS bitsets (more: per-cluster static_vote)
 // Dynamic LDS of k_select_all_stream (kp_kernels.h body_select_all_stream).
