@@ -1889,6 +1889,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
     return KP_ENOTSUP;
   }
   for (uint64_t i = 0; i < n; i++) {
+    bt->hdr[i].out_off = bt->out_cap;  // private result slots: no atomic on the emit path
     bt->out_cap += bt->hdr[i].out_cap;
     const BindHdr& h = bt->hdr[i];
     if (h.sel == SEL_CLUSTER) bt->l_cluster.push_back((int32_t)i);
@@ -1980,12 +1981,13 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
 #ifdef KP_STAMPS
   a.add(&bt->dbg, 32);
 #endif
-  a.add(&bt->out_idx, std::max<uint64_t>(1, bt->out_cap));
-  a.add(&bt->out_rep, std::max<uint64_t>(1, bt->out_cap));
+  // [0, out_cap): per-binding slots; [out_cap, 2 out_cap): serial results past their slot
+  a.add(&bt->out_idx, std::max<uint64_t>(1, 2 * bt->out_cap));
+  a.add(&bt->out_rep, std::max<uint64_t>(1, 2 * bt->out_cap));
   a.add(&bt->offsets_d, B + 1);
   a.add(&bt->off_part, (size_t)(B + kOffChunk - 1) / kOffChunk);
-  a.add(&bt->cidx_d, std::max<uint64_t>(1, bt->out_cap));
-  a.add(&bt->crep_d, std::max<uint64_t>(1, bt->out_cap));
+  a.add(&bt->cidx_d, std::max<uint64_t>(1, 2 * bt->out_cap));
+  a.add(&bt->crep_d, std::max<uint64_t>(1, 2 * bt->out_cap));
   a.add(&bt->rout, (size_t)std::max(1, nr) * R);
   a.add(&bt->rstat, std::max(1, nr));
   a.add(&bt->rsel, (size_t)std::max(1, nr) * R);
@@ -2064,7 +2066,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     return KP_ESTATE;
   }
   if (batch_lds_check(e, s, bt)) return KP_ENOTSUP;
-  HIPCHK(dev::fill(bt->counter, 0, sizeof(unsigned long long), st));
+  HIPCHK(dev::h2d(bt->counter, &bt->out_cap, sizeof(unsigned long long), st));  // the shared area's start
   HIPCHK(dev::fill(bt->stats, 0, 8 * sizeof(uint32_t), st));
   KArgs ka;
   ka.s = s->view;

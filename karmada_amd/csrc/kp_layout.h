@@ -123,7 +123,8 @@ struct alignas(16) BindHdr {
   int64_t cluster_min, cluster_max, region_min, region_max;
   int32_t need_replicas;         // SelectBestClusters needReplicas (-1 = ignore resources)
   int32_t spread_order;          // SpreadConstraint fields in first-appearance order, 2 bits each (1 provider, 2 region, 3 zone)
-  uint64_t out_cap;
+  uint64_t out_cap;               // result entries this binding can emit on the fast paths
+  uint64_t out_off;               // its slot in the batch's result pool (prefix sum of out_cap)
   // this binding's slices of the pools (staged into LDS by the pair kernel)
   int32_t ip_beg, ip_end, pr_beg, pr_end, in_beg, in_end;
 };

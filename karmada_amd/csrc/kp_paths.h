@@ -135,16 +135,16 @@ KP_FI void emit_each(const BLK& B, const SelCtx& x, const CS& cs, RepFn rep, boo
   }
   int32_t tot;
   const int32_t off = B.excl_scan(mine, &tot);
-  unsigned long long base = 0;
+  // the binding's own slot of out_cap entries (the fast paths never exceed it)
+  const uint64_t base = x.h->out_off;
   if (B.tid() == 0) {
-    base = tot > 0 ? kp_atomic_add(x.sink.counter, (unsigned long long)tot) : 0ull;
     x.sink.status[x.b] = KP_STATUS_OK;
     x.sink.err[x.b] = KP_ERR_NONE;
     x.sink.arg[x.b] = 0;
     x.sink.start[x.b] = base;
     x.sink.count[x.b] = (uint32_t)tot;
   }
-  uint64_t o = (uint64_t)B.bcast(base) + (uint64_t)off;
+  uint64_t o = base + (uint64_t)off;
   cs.each([&](uint32_t rk, int32_t v) {
     const int32_t r = CS::kSettable ? v : rep(rk, v);
     if (keep_all || r > 0) {
@@ -172,16 +172,16 @@ KP_FI void emit_lists(const BLK& B, const SelCtx& x, const uint64_t* pl, int np,
     if (mask_test(x.frow, (int)trank(j)) && trep(trank(j)) > 0) mine++;
   int32_t tot;
   const int32_t off = B.excl_scan(mine, &tot);
-  unsigned long long base = 0;
+  // the binding's own slot of out_cap entries (the fast paths never exceed it)
+  const uint64_t base = x.h->out_off;
   if (B.tid() == 0) {
-    base = tot > 0 ? kp_atomic_add(x.sink.counter, (unsigned long long)tot) : 0ull;
     x.sink.status[x.b] = KP_STATUS_OK;
     x.sink.err[x.b] = KP_ERR_NONE;
     x.sink.arg[x.b] = 0;
     x.sink.start[x.b] = base;
     x.sink.count[x.b] = (uint32_t)tot;
   }
-  uint64_t o = (uint64_t)B.bcast(base) + (uint64_t)off;
+  uint64_t o = base + (uint64_t)off;
   for (int i = B.tid(); i < np; i += B.nth()) {
     const uint32_t rk = (uint32_t)(pl[i] >> 32);
     const int32_t r = rep(rk, (int64_t)(uint32_t)pl[i]);

@@ -511,7 +511,10 @@ KP_HD inline void sink_serial(const SelCtx& x, const SerialScratch& sc, const Se
     k.count[b] = 0;
     return;
   }
-  unsigned long long base = kp_atomic_add(k.counter, (unsigned long long)o.n);
+  // the binding's own slot when the list fits it; else (overflow tiers can append the
+  // spec.Clusters entries once per tier) the shared area past every slot
+  unsigned long long base = (uint64_t)o.n <= x.h->out_cap ? (unsigned long long)x.h->out_off
+                                                          : kp_atomic_add(k.counter, (unsigned long long)o.n);
   k.start[b] = base;
   k.count[b] = (uint32_t)o.n;
   for (int i = 0; i < o.n; i++) {
