@@ -814,7 +814,7 @@ KP_HD inline int32_t assigned_of(const BatchView& bv, const BindHdr& h, const ui
   return 0;
 }
 KP_HD inline int64_t locality_score(const BindHdr& h, const uint32_t* tgt_bits, uint32_t rank) {
-  return ((h.flags & BF_SCORE_LOCALITY) && bit_test(tgt_bits, (int)rank)) ? 100 : 0;
+  return ((h.flags & BF_SCORE_LOCALITY) && h.tgt_cnt > 0 && bit_test(tgt_bits, (int)rank)) ? 100 : 0;
 }
 
 // ============================================================================

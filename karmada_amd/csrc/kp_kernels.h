@@ -45,8 +45,11 @@ KP_HD inline SelCtx make_ctx(const KArgs& a, int b, const uint32_t* tgt_bits) {
 }
 
 // Bitset (LDS) of the binding's spec.Clusters ranks (TargetContains, locality).
+// Empty lists leave the bitset untouched (no barrier): every reader tests the
+// list's count first (tgt_cnt / evict_cnt > 0).
 template <class BLK>
 KP_FI void build_bits(const BLK& B, uint32_t* bits, int words, const int32_t* pool, int off, int cnt, int stride) {
+  if (cnt == 0) return;  // block-uniform
   for (int i = B.tid(); i < words; i += B.nth()) bits[i] = 0;
   B.sync();
   for (int j = B.tid(); j < cnt; j += B.nth()) {
