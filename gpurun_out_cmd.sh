@@ -4,6 +4,3 @@ for rep in 1 2; do
   tail -1 gpurun_out/v.log | python3 -c "
 import json,sys; d=json.loads(sys.stdin.read()); print('serial', d['ms_per_step'], d['stages_ms'], d['parity_checked'], d['parity_bad'])"
 done
-timeout -k 10 300 python bench.py --steps 200 --warmup 2 --no-cpu --check 200 --e2e-reps 0 > gpurun_out/v.log 2>&1 || exit $?
-tail -1 gpurun_out/v.log | python3 -c "
-import json,sys; d=json.loads(sys.stdin.read()); print('inflight4', d['ms_per_step'], d['serial_ms_per_step'], d['stages_ms']['sel_all_kernel'])"

@@ -440,16 +440,22 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
       });
     };
     int64_t xmax = -1, xsum = 0;
-    xvals([&](int64_t v) {
-      if (v > xmax) xmax = v;
-      xsum += v;
-    });
-    B.maxsum(xmax, xsum);
+    const bool all_x = pre && nP == 0;  // no prior cluster: X is every candidate, sel_all_fast's sums hold
+    if (all_x) {
+      xmax = pre->vmax;
+      xsum = pre->vtot;
+    } else {
+      xvals([&](int64_t v) {
+        if (v > xmax) xmax = v;
+        xsum += v;
+      });
+      B.maxsum(xmax, xsum);
+    }
     if (xmax < 0 || xsum < tX) {
       noCut = true;  // every element of X is taken
     } else {
       if (tX <= 0) vstar = xmax;  // the first element alone reaches the target
-      else vstar = wsel_max(B, ss.whist, xvals, tX);  // largest v with sum{v_i >= v} >= tX
+      else vstar = wsel_max(B, ss.whist, xvals, tX, xmax);  // largest v with sum{v_i >= v} >= tX
       int64_t sgt = 0, ceq = 0;
       xvals([&](int64_t v) {
         if (v > vstar) sgt += v;

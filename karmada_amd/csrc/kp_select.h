@@ -976,10 +976,16 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
 // it): an 8-bit radix descent with value-weighted bins. `vals(fn)` calls fn(v)
 // for every value the calling thread owns.
 template <class BLK, class Vals>
-KP_FI int64_t wsel_max(const BLK& B, unsigned long long* wh, Vals vals, int64_t target) {
+KP_FI int64_t wsel_max(const BLK& B, unsigned long long* wh, Vals vals, int64_t target, int64_t vmax = -1) {
+  // the highest set bit of the OR of the values is the maximum's: a known maximum
+  // spares the OR pass
   uint64_t on = 0;
-  vals([&](int64_t v) { on |= (uint64_t)v; });
-  on = B.or64(on);
+  if (vmax >= 0) {
+    on = (uint64_t)vmax;
+  } else {
+    vals([&](int64_t v) { on |= (uint64_t)v; });
+    on = B.or64(on);
+  }
   int start = 24;
   while (start > 0 && !(on >> start)) start -= 8;
   uint32_t prefix = 0;
