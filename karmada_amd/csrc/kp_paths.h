@@ -454,14 +454,19 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
     if (xmax < 0 || xsum < tX) {
       noCut = true;  // every element of X is taken
     } else {
+      WselTail wt;
       if (tX <= 0) vstar = xmax;  // the first element alone reaches the target
-      else vstar = wsel_max(B, ss.whist, xvals, tX, xmax);  // largest v with sum{v_i >= v} >= tX
-      int64_t sgt = 0, ceq = 0;
-      xvals([&](int64_t v) {
-        if (v > vstar) sgt += v;
-        if (v == vstar) ceq++;
-      });
-      B.sum2(sgt, ceq);
+      else vstar = wsel_max(B, ss.whist, xvals, tX, xmax, &wt);  // largest v with sum{v_i >= v} >= tX
+      int64_t sgt = wt.sum_gt, ceq = wt.cnt_eq;
+      if (ceq < 0) {  // (not read off the radix: v* from the maximum, or v* = 0)
+        sgt = 0;
+        ceq = 0;
+        xvals([&](int64_t v) {
+          if (v > vstar) sgt += v;
+          if (v == vstar) ceq++;
+        });
+        B.sum2(sgt, ceq);
+      }
       const int64_t need = tX - sgt;
       const int64_t j = need <= 0 ? 1 : (vstar > 0 ? (need + vstar - 1) / vstar : ceq);
       if (j < ceq) {  // the tie group straddles the cut

@@ -975,8 +975,14 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
 // >= v* sum to at least `target` (>= 1; the caller guarantees the total reaches
 // it): an 8-bit radix descent with value-weighted bins. `vals(fn)` calls fn(v)
 // for every value the calling thread owns.
+// sum{v_i > v*} and #{v_i == v*} of wsel_max's answer, read off its last histogram
+// (cnt_eq = -1 when v* = 0: the caller counts).
+struct WselTail {
+  int64_t sum_gt = 0, cnt_eq = -1;
+};
 template <class BLK, class Vals>
-KP_FI int64_t wsel_max(const BLK& B, unsigned long long* wh, Vals vals, int64_t target, int64_t vmax = -1) {
+KP_FI int64_t wsel_max(const BLK& B, unsigned long long* wh, Vals vals, int64_t target, int64_t vmax = -1,
+                       WselTail* tail = nullptr) {
   // the highest set bit of the OR of the values is the maximum's: a known maximum
   // spares the OR pass
   uint64_t on = 0;
@@ -1002,6 +1008,10 @@ KP_FI int64_t wsel_max(const BLK& B, unsigned long long* wh, Vals vals, int64_t 
     const int bin = B.find_bin(wh, target - above, &before, true);
     above += before;
     prefix |= (uint32_t)bin << shift;
+    if (shift == 0 && tail) {  // the last round's bins are single values: bin = v*
+      tail->sum_gt = above;
+      tail->cnt_eq = prefix ? (int64_t)(wh[bin] / prefix) : -1;
+    }
   }
   return (int64_t)prefix;
 }
