@@ -160,14 +160,16 @@ KP_FI void emit_each(const BLK& B, const SelCtx& x, const CS& cs, RepFn rep, boo
 // `targets`, the binding's spec.Clusters entries that are candidates with
 // trep(rank) > 0 (0 for those the list already holds).
 template <class BLK, class RepFn, class TRepFn>
-KP_FI void emit_lists(const BLK& B, const SelCtx& x, const uint64_t* pl, int np, RepFn rep, bool targets,
-                      TRepFn trep) {
+KP_FI void emit_lists(const BLK& B, const SelCtx& x, uint64_t* pl, int np, RepFn rep, bool targets, TRepFn trep) {
   const BindHdr& h = *x.h;
   const int nt = targets ? h.tgt_cnt : 0;
   auto trank = [&](int j) { return (uint32_t)x.bv->ipool[h.tgt_off + 2 * j]; };
   int32_t mine = 0;
-  for (int i = B.tid(); i < np; i += B.nth())
-    if (rep((uint32_t)(pl[i] >> 32), (int64_t)(uint32_t)pl[i]) > 0) mine++;
+  for (int i = B.tid(); i < np; i += B.nth()) {  // replicas replace the votes (same thread, both passes)
+    const int32_t r = rep((uint32_t)(pl[i] >> 32), (int64_t)(uint32_t)pl[i]);
+    pl[i] = (pl[i] & ~0xffffffffull) | (uint64_t)(uint32_t)r;
+    if (r > 0) mine++;
+  }
   for (int j = B.tid(); j < nt; j += B.nth())
     if (mask_test(x.frow, (int)trank(j)) && trep(trank(j)) > 0) mine++;
   int32_t tot;
@@ -184,7 +186,7 @@ KP_FI void emit_lists(const BLK& B, const SelCtx& x, const uint64_t* pl, int np,
   uint64_t o = base + (uint64_t)off;
   for (int i = B.tid(); i < np; i += B.nth()) {
     const uint32_t rk = (uint32_t)(pl[i] >> 32);
-    const int32_t r = rep(rk, (int64_t)(uint32_t)pl[i]);
+    const int32_t r = (int32_t)(uint32_t)pl[i];
     if (r > 0) {
       x.sink.out_idx[o] = x.s->perm[rk];
       x.sink.out_rep[o] = r;
@@ -518,7 +520,7 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
       return member(rk, v, v0) && v >= w.Lb;
     };
     emit_lists(
-        B, x, w.pl, w.np,
+        B, x, const_cast<uint64_t*>(w.pl), w.np,
         [&](uint32_t rk, int64_t v) {
           int32_t r = web_seats(w, v, rk);
           if (merge && tgt(rk)) r = add32(r, sched_rep_of(x, rk));
