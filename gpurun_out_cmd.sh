@@ -1,4 +1,3 @@
-rm -f gpurun_out/bench_config*.log
-for c in 1 2 6 7; do timeout -k 10 300 python bench.py --config $c --steps 100 --warmup 2 --no-cpu --check 300 > gpurun_out/bench_config$c.log 2>&1 || exit $?; done
-timeout -k 10 300 python bench.py --config 4 --steps 30 --warmup 2 --no-cpu --check 300 > gpurun_out/bench_config4.log 2>&1 || exit $?
-timeout -k 10 300 python bench.py --config 5 --bindings 125000 --steps 12 --warmup 2 --no-cpu --check 300 > gpurun_out/bench_config5.log 2>&1 || exit $?
+rm -rf gpurun_out/prof_kt4
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit $?
+cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_kt4 -o kt -- python3 $GRAFT_REPO_ROOT/bench.py --config 4 --steps 5 --warmup 1 --no-cpu --inflight 1 --e2e-reps 0 --check 0 > $GRAFT_REPO_ROOT/gpurun_out/prof_kt4.log 2>&1

@@ -34,6 +34,30 @@ KP_HD inline Item item_from_key(const SelCtx& x, uint64_t k) {
   it.pad = 0;
   return it;
 }
+// #{j < m : keys[j] < k}: four independent chains so the LDS reads (the same
+// address in every lane) overlap instead of waiting one by one.
+KP_FI int count_less(const uint64_t* keys, int m, uint64_t k) {
+  int p0 = 0, p1 = 0, p2 = 0, p3 = 0, j = 0;
+  for (; j + 4 <= m; j += 4) {
+    p0 += keys[j] < k ? 1 : 0;
+    p1 += keys[j + 1] < k ? 1 : 0;
+    p2 += keys[j + 2] < k ? 1 : 0;
+    p3 += keys[j + 3] < k ? 1 : 0;
+  }
+  for (; j < m; j++) p0 += keys[j] < k ? 1 : 0;
+  return p0 + p1 + p2 + p3;
+}
+// Distinct keys[0..m) (the rank sits in the low bits) as items in ascending key
+// order: each key's position is the count of smaller keys (block-parallel; the
+// list is at most 2 * kSmallMax long).
+template <class BLK>
+KP_FI void place_sorted(const BLK& B, const SelCtx& x, const uint64_t* keys, int m, Item* dst) {
+  for (int i = B.tid(); i < m; i += B.nth()) {
+    const uint64_t k = keys[i];
+    dst[count_less(keys, m, k)] = item_from_key(x, k);
+  }
+  B.sync();
+}
 
 // scheduledClusters helpers: spec.Clusters entries whose cluster is a candidate
 // (assignment.go:125-142). Targets are unique here (BF_DUP_TARGETS goes slow).
@@ -645,19 +669,7 @@ KP_FI bool sel_cluster_fast(const BLK& B, const SelCtx& x, const Cands& cd, uint
     n += tot;
   }
   B.sync();
-  if (B.tid() == 0) {  // sorted order (sortClusters)
-    for (int i = 1; i < n; i++) {
-      uint64_t k0 = keys[i];
-      int j = i - 1;
-      while (j >= 0 && keys[j] > k0) {
-        keys[j + 1] = keys[j];
-        j--;
-      }
-      keys[j + 1] = k0;
-    }
-    for (int i = 0; i < n; i++) items[i] = item_from_key(x, keys[i]);
-  }
-  B.sync();
+  place_sorted(B, x, keys, n, items);  // sorted order (sortClusters)
   if (need != -1) {
     int64_t tot = 0;
     for (int i = 0; i < n; i++) tot += items[i].avail;
@@ -983,6 +995,7 @@ KP_FI void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L,
     if (L.cnt[r] == 0 || (monotone && L.sumAvail[r] < target)) L.done[r] = 1;  // never breaks: totals
   }
   B.sync();
+  KP_COUNT(x, 21, 1);
   for (;;) {
     bool any = false;
     for (int r = B.tid(); r < R; r += B.nth()) {
@@ -990,6 +1003,7 @@ KP_FI void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L,
       L.minkey[r] = ~0ull;
     }
     if (!B.any(any)) break;
+    KP_COUNT(x, 25, 1);
     for (int i = B.tid(); i < cd.F; i += B.nth()) {
       int r = cd.g[i];
       if (r < 0 || L.done[r]) continue;
@@ -1082,10 +1096,8 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
     if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, -1);
     return;
   }
-  int n = 0;
-  if (B.tid() == 0)
-    for (int j = 0; j < nsel; j++) items[n++] = item_from_key(x, heads[sel[j]]);
-  n = nsel;
+  for (int j = B.tid(); j < nsel; j += B.nth()) items[j] = item_from_key(x, heads[sel[j]]);
+  int n = nsel;
   B.sync();
   if (restCnt > 0 && total <= kc) {
     // the restCnt smallest non-head keys, ascending: heads drop out of the list
@@ -1097,13 +1109,13 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
     for (int i = B.tid(); i < (int)total; i += B.nth()) {
       const uint64_t k = keys[i];
       if (k == ~0ull) continue;
-      int64_t pos = 0;
-      for (int j = 0; j < (int)total; j++) pos += keys[j] < k ? 1 : 0;
+      const int64_t pos = count_less(keys, (int)total, k);
       if (pos < restCnt) items[nsel + pos] = item_from_key(x, k);
     }
     n = nsel + (int)restCnt;
     B.sync();
   } else if (restCnt > 0) {
+    KP_COUNT(x, 31, 1);
     auto incand = [&](int i) {
       int r = cd.g[i];
       return r >= 0 && rsel[r] >= 0 && cand_key(x, cd, i, cd.v[i]) != heads[r];
@@ -1125,20 +1137,8 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
       m += tt;
     }
     B.sync();
-    if (B.tid() == 0) {
-      for (int i = 1; i < m; i++) {
-        uint64_t k0 = keys[i];
-        int j = i - 1;
-        while (j >= 0 && keys[j] > k0) {
-          keys[j + 1] = keys[j];
-          j--;
-        }
-        keys[j + 1] = k0;
-      }
-      for (int i = 0; i < m; i++) items[nsel + i] = item_from_key(x, keys[i]);
-    }
+    place_sorted(B, x, keys, m, items + nsel);
     n = nsel + m;
-    B.sync();
   }
   KP_STAMP(x, 19);
   assign_small(B, x, items, n, scratch, cap, area_bytes);

@@ -101,6 +101,10 @@ KP_HD inline int32_t est_at(const SelCtx& x, int c) { return est_merge(x, x.erow
       kp_t0 = t;                                                         \
     }                                                                    \
   } while (0)
+#define KP_COUNT(ctx_, i, v)                                             \
+  do {                                                                   \
+    if (threadIdx.x == 0 && (ctx_).dbg) atomicAdd(&(ctx_).dbg[i], (unsigned long long)(v)); \
+  } while (0)
 #define KP_STAMPD(dbg, i)                                                \
   do {                                                                   \
     if (threadIdx.x == 0 && (dbg)) {                                     \
@@ -115,6 +119,9 @@ KP_HD inline int32_t est_at(const SelCtx& x, int c) { return est_merge(x, x.erow
   do {                 \
   } while (0)
 #define KP_STAMPD(dbg, i) \
+  do {                    \
+  } while (0)
+#define KP_COUNT(x, i, v) \
   do {                    \
   } while (0)
 #endif
