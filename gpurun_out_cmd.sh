@@ -1,1 +1,2 @@
-timeout -k 10 300 python bench.py --config 4 --lib karmada_amd/libkp_stamps.so --steps 2 --warmup 1 --no-cpu --check 0 --inflight 1 --e2e-reps 0 > gpurun_out/st4.log 2>&1 || exit $?
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --steps 100 --warmup 2 --no-cpu --check 300 > gpurun_out/final_q.log 2>&1
