@@ -126,10 +126,11 @@ def cpu_baseline(u, opts, budget_s):
     }
 
 
-def parity_check(u, res, opts, n_check, seed):
+def parity_check(u, results, opts, n_check, seed):
     """Oracle (FAST mode) on n_check bindings sampled from the timed batch, compared
-    with the engine's results of the last timed step (status, error, multiset of
-    targets). Test infrastructure, after the timed region."""
+    with each given result list (status, error, multiset of targets): the serial
+    run and every in-flight lane's last step. Test infrastructure, after the timed
+    region. Returns (bindings checked, mismatches summed over the lists)."""
     import random
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
@@ -140,8 +141,38 @@ def parity_check(u, res, opts, n_check, seed):
     idx = sorted(random.Random(seed).sample(range(u.n_bindings), n))
     arr = (api.kp_binding * n)(*[u.bindings[i] for i in idx])
     want = O.schedule_c(u.clusters, u.n_clusters, arr, n, opts, O.FAST, min(16, cpu_threads()))
-    bad = sum(1 for k, i in enumerate(idx) if res[i] != want[k])
+    bad = sum(1 for res in results for k, i in enumerate(idx) if res[i] != want[k])
     return n, bad
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without WORLD_SIZE: start N rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torch.distributed.run sets them,
+    rendezvous on 127.0.0.1) and exit with the first failing rank's code. This parent
+    never touches the GPU: each rank selects its own device (LOCAL_RANK)."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        time.sleep(0.2)
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in procs:  # a rank failed: the others would wait at a collective
+                    q.terminate()
+    return rc
 
 
 def main():
@@ -164,15 +195,23 @@ def main():
                          "so one batch's result copy-back and host steps overlap another's kernels")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+
     from karmada_amd import api, synth
     from karmada_amd.dist import Csr
     from karmada_amd.engine import Batch, Engine, Snapshot
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    # KP_DIST_FORCE=1 runs the collective path (snapshot broadcast, CSR all-gather)
+    # even at world size 1, so RCCL is exercised on a one-GPU box
+    if world > 1 or os.environ.get("KP_DIST_FORCE"):
         import torch
         import torch.distributed as dist
         # one rank per GPU over RCCL ("nccl"); KP_DIST_BACKEND=gloo rehearses the
@@ -182,8 +221,11 @@ def main():
             torch.cuda.set_device(local)
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
         else:
+            # gloo: host tensors; ranks may share a GPU, or run the CPU build (--lib
+            # karmada_amd/libkp_cpusim.so) with no GPU at all
             local = local % max(1, torch.cuda.device_count())
-            torch.cuda.set_device(local)
+            if torch.cuda.device_count() > 0:
+                torch.cuda.set_device(local)
             dist.init_process_group(backend=backend)
         tdev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
 
@@ -192,10 +234,18 @@ def main():
     C_ = args.clusters or C_def
     B = args.bindings or B_def
     seed = args.seed if args.seed is not None else cfg
-    lo, hi = rank * B, (rank + 1) * B
-
+    total = B * world  # B bindings per GPU on average (weak scaling)
     t0 = time.perf_counter()
+    if world > 1:
+        # cost-balanced contiguous shards of the whole universe (SURVEY §8(e) cost
+        # model C + Rep_b * log2 F_b, F_b bounded by C before filtering)
+        from karmada_amd.dist import binding_costs, shard_range_weighted
+        costs = binding_costs(synth.replicas(cfg, seed, C_, 0, total), C_)
+        lo, hi = shard_range_weighted(costs, world, rank)
+    else:
+        lo, hi = 0, B
     u = synth.Universe(cfg, seed, C_, lo, hi)
+    B_rank = hi - lo
     gen_s = time.perf_counter() - t0
     opts = api.options()
     eng = Engine(local, lib_path=os.path.join(ROOT, args.lib)) if args.lib else Engine(local)
@@ -216,7 +266,8 @@ def main():
         if dist is not None:
             import torch
             dist.barrier()
-            torch.cuda.synchronize()
+            if torch.cuda.device_count() > 0:
+                torch.cuda.synchronize()
 
     # in-flight batches: engine k schedules the same packed bindings (its own snapshot
     # replica and batch); steps are split over them, each step = one whole batch
@@ -253,7 +304,10 @@ def main():
             x.join()
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    r = results[0]
+    rank_ms = 1e3 * elapsed / args.steps
+    # every lane's last result (engine-owned until that engine's next call), copied
+    # now: the in-flight lanes are parity-checked too, not only the serial run below
+    lane_csr = [Csr.from_results(x) for x in results if x is not None]
     # one batch at a time (no overlap), for reference: a short serial run on engine 0
     serial_ms = None
     if len(lanes) > 1:
@@ -273,21 +327,31 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             serial_ms = float(t.item())
     # ---- after the timed region ----
+    if len(lanes) == 1:
+        r = results[0]
     csr = Csr.from_results(r)
     res = csr.to_python()
     n_ok = int((csr.status == 0).sum())
     n_targets_rank = n_targets = csr.n_targets
+    per_rank_ms = [round(rank_ms, 3)]
     if dist is not None:
         import torch
         from karmada_amd.dist import gather_csr
         t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        pr = [torch.zeros(1, dtype=torch.float64, device=tdev) for _ in range(dist.get_world_size())]
+        dist.all_gather(pr, torch.tensor([rank_ms], dtype=torch.float64, device=tdev))
+        per_rank_ms = [round(float(x.item()), 3) for x in pr]
         whole = gather_csr(csr)  # two-phase CSR all-gather (counts, then padded arrays)
         n_ok = int((whole.status == 0).sum())
         n_targets = whole.n_targets
 
-    n_chk, n_bad = parity_check(u, res, opts, args.check, 1000 + rank) if args.check > 0 else (0, 0)
+    # the oracle re-checks a sample of the serial run and of every in-flight lane's
+    # last batch (lanes run concurrently on separate engines and streams)
+    results_checked = [res] + [c.to_python() for c in lane_csr]
+    n_chk, n_bad = parity_check(u, results_checked, opts, args.check, 1000 + rank) if args.check > 0 else (0, 0)
+    n_lanes_chk = len(results_checked) if args.check > 0 else 0
     if dist is not None:
         t = torch.tensor([n_chk, n_bad], dtype=torch.int64, device=tdev)
         dist.all_reduce(t)
@@ -339,12 +403,12 @@ def main():
     def avg(k):
         return sum(x[k] for x in st_all) / len(st_all)
     ms_per_step = 1e3 * elapsed / args.steps
-    value = (B * world) / (elapsed / args.steps)
+    value = total / (elapsed / args.steps)  # every rank's bindings over the max-over-ranks time
     last = st_all[-1]
     pair_ms, sel_ms = avg("pair_kernel_ms"), avg("select_kernel_ms")
     sel_all_ms, filter_ms = avg("sel_all_kernel_ms"), avg("filter_kernel_ms")
     bits = last["bits"] == 1
-    pair_b, sel_b = compulsory_bytes(B, int(last["n_sel_all"]), C_, n_targets_rank, snap_bytes,
+    pair_b, sel_b = compulsory_bytes(B_rank, int(last["n_sel_all"]), C_, n_targets_rank, snap_bytes,
                                      int(last["n_classes"]) if bits else 0)
     stage = "k_est_class+k_filter" if bits else PAIR_KERNELS.get(last["pair_kind"], "k_pair")
     cands = [(stage, pair_ms, pair_b), ("k_select_all", sel_all_ms, sel_b)]
@@ -374,7 +438,7 @@ def main():
         "inflight": len(lanes),
         # one batch at a time on one engine (nothing overlapped): ms per batch and the rate
         "serial_ms_per_step": round(serial_ms, 3) if serial_ms else round(ms_per_step, 3),
-        "serial_value": round(B * world / (serial_ms * 1e-3), 1) if serial_ms else round(value, 1),
+        "serial_value": round(total / (serial_ms * 1e-3), 1) if serial_ms else round(value, 1),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -383,7 +447,9 @@ def main():
         "config": {"workload": f"config{cfg}: {B} bindings/GPU x {C_} clusters, seed {seed}, "
                                "resource-model grades, DynamicWeight/Aggregated" if cfg == 3 else
                    f"config{cfg}: {B} bindings/GPU x {C_} clusters, seed {seed}",
-                   "bindings_per_gpu": B, "clusters": C_, "parallelism": f"binding-shard x{world}"},
+                   "bindings_per_gpu": B, "bindings_total": total, "clusters": C_,
+                   "parallelism": f"binding-shard x{world}" + (" (cost-balanced, RCCL snapshot broadcast + "
+                                                               "CSR all-gather)" if world > 1 else "")},
         "roofline": roof,
         # compulsory bytes of the whole step (every kernel) over the whole step's time
         "step_roofline": {"achieved": round(step_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -397,16 +463,18 @@ def main():
         "estimator_classes": int(last["n_classes"]) if bits else None,
         # bindings/s including host packing + upload: pipelined over two engines (the
         # value), and one batch at a time (end_to_end_serial_ms per batch)
-        "end_to_end_value": round(B * world / e2e_pipe, 1) if e2e_pipe else None,
+        "end_to_end_value": round(total / e2e_pipe, 1) if e2e_pipe else None,
         "end_to_end_ms": round(1e3 * e2e_pipe, 2) if e2e_pipe else None,
         "end_to_end_serial_ms": round(1e3 * e2e, 2) if e2e else None,
         "setup_s": {"generate": round(gen_s, 2), "snapshot_pack_upload": round(snap_s, 3),
                     "binding_pack_upload": round(pack_s, 3)},
+        "per_rank_ms": per_rank_ms,
         "scheduled_ok": n_ok,
         "result_targets": n_targets,
         "slow_path_bindings": int(last["n_slow"]),
         # bindings of the timed batch (sampled over all ranks) re-checked against the oracle
         "parity_checked": n_chk,
+        "parity_lanes": n_lanes_chk,  # result lists checked per rank: the serial run + each in-flight lane
         "parity_bad": n_bad,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 9
+#define KP_ABI_VERSION 10
 
 /* ------------------------------------------------------------------------- */
 /* Object model                                                              */
@@ -145,6 +145,18 @@ typedef struct kp_target_cluster {
   int32_t replicas;
 } kp_target_cluster;
 
+/* workv1alpha2.Component (pkg/apis/work/v1alpha2/binding_types.go): one pod template
+ * of a multi-template workload; ReplicaRequirements.ResourceRequest only (the
+ * NodeClaim never filters the estimator's model nodes, which carry no Node object,
+ * scheduling_simulator_components.go:149-153). */
+typedef struct kp_component {
+  kp_str name;
+  int32_t replicas;
+  uint8_t has_replica_requirements;
+  const kp_resource* resource_request;
+  uint32_t n_resource_request;
+} kp_component;
+
 /* ResourceBindingSpec + the status fields Schedule reads. */
 typedef struct kp_binding {
   kp_str uid; /* spec.Resource.UID: FNV tie-break (pkg/util/helper/binding.go:117-144) */
@@ -161,6 +173,10 @@ typedef struct kp_binding {
   const kp_resource* resource_request;
   uint32_t n_resource_request;
   uint32_t n_components; /* len(spec.Components) */
+  const kp_component* components; /* spec.Components (binding_types.go:89-98): read only with the
+                                     MultiplePodTemplatesScheduling gate on, for bindings
+                                     isMultiTemplateSchedulingApplicable accepts
+                                     (core/estimation.go:43-65); NULL there -> KP_EINVAL */
   const kp_target_cluster* clusters; /* spec.Clusters (previous result) */
   uint32_t n_clusters;
   const kp_str* eviction_from; /* spec.GracefulEvictionTasks[].FromCluster */
@@ -240,17 +256,6 @@ typedef struct kp_cluster {
   uint32_t n_allocatable_modelings;
 } kp_cluster;
 
-/* workv1alpha2.Component (pkg/apis/work/v1alpha2/binding_types.go): one pod template
- * of a multi-template workload; ReplicaRequirements.ResourceRequest only (the
- * NodeClaim never filters the estimator's model nodes, which carry no Node object,
- * scheduling_simulator_components.go:149-153). */
-typedef struct kp_component {
-  kp_str name;
-  int32_t replicas;
-  uint8_t has_replica_requirements;
-  const kp_resource* resource_request;
-  uint32_t n_resource_request;
-} kp_component;
 
 /* In-tree plugin names (pkg/scheduler/framework/plugins/registry.go:33-50). */
 enum {
@@ -299,7 +304,10 @@ enum {
   KP_ERR_FRESH_NOT_ENOUGH = 10,      /* assignment.go:218-221 wrapping division_algorithm.go:76-78; arg = available */
   KP_ERR_SCALE_DOWN_NOT_ENOUGH = 11, /* assignment.go:228-231; arg = available */
   KP_ERR_SCALE_UP_NOT_ENOUGH = 12,   /* assignment.go:236-239; arg = available */
-  KP_ERR_UNDEFINED_STRATEGY = 13     /* division_algorithm.go:97-99 */
+  KP_ERR_UNDEFINED_STRATEGY = 13,    /* division_algorithm.go:97-99 */
+  KP_ERR_RESULT_CAPACITY = 14        /* engine limit, no reference site: a serial result list
+                                        outgrew the batch's result pool (arg = its length);
+                                        never expected, reported instead of written */
 };
 
 /* Per-batch results, engine-owned, valid until the next call on the engine.

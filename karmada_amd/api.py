@@ -68,13 +68,18 @@ class kp_target_cluster(C.Structure):
     _fields_ = [("name", kp_str), ("replicas", i32)]
 
 
+class kp_component(C.Structure):
+    _fields_ = [("name", kp_str), ("replicas", i32), ("has_replica_requirements", u8),
+                ("resource_request", C.POINTER(kp_resource)), ("n_resource_request", u32)]
+
+
 class kp_binding(C.Structure):
     _fields_ = [
         ("uid", kp_str), ("api_version", kp_str), ("kind", kp_str), ("namespace_", kp_str), ("name", kp_str),
         ("replicas", i32),
         ("has_replica_requirements", u8), ("has_node_claim", u8),
         ("resource_request", C.POINTER(kp_resource)), ("n_resource_request", u32),
-        ("n_components", u32),
+        ("n_components", u32), ("components", C.POINTER(kp_component)),
         ("clusters", C.POINTER(kp_target_cluster)), ("n_clusters", u32),
         ("eviction_from", C.POINTER(kp_str)), ("n_eviction_from", u32),
         ("has_reschedule_triggered_at", u8), ("has_last_scheduled_time", u8),
@@ -136,11 +141,6 @@ class kp_cluster(C.Structure):
         ("allocating", C.POINTER(kp_resource)), ("n_allocating", u32),
         ("allocatable_modelings", C.POINTER(kp_allocatable_modeling)), ("n_allocatable_modelings", u32),
     ]
-
-
-class kp_component(C.Structure):
-    _fields_ = [("name", kp_str), ("replicas", i32), ("has_replica_requirements", u8),
-                ("resource_request", C.POINTER(kp_resource)), ("n_resource_request", u32)]
 
 
 class kp_options(C.Structure):
@@ -227,7 +227,7 @@ ERR_NAMES = {
     0: "none", 1: "fit", 2: "region_min_groups", 3: "region_cluster_min", 4: "cluster_min_groups",
     5: "cluster_resource", 6: "spread_unsupported", 7: "no_clusters", 8: "unsupported_strategy",
     9: "overflow_not_enough", 10: "fresh_not_enough", 11: "scale_down_not_enough",
-    12: "scale_up_not_enough", 13: "undefined_strategy",
+    12: "scale_up_not_enough", 13: "undefined_strategy", 14: "result_capacity",
 }
 
 
@@ -395,7 +395,10 @@ class World:
             b.resource_request, b.n_resource_request = self.resources(rr.get("resourceRequest"))
             b.has_node_claim = int(rr.get("nodeClaim") is not None)
         comps = d.get("components")
-        b.n_components = len(comps) if isinstance(comps, list) else int(comps or 0)
+        if isinstance(comps, list):
+            b.components, b.n_components = self.components(comps)
+        else:
+            b.n_components = int(comps or 0)
         b.clusters, b.n_clusters = self.arr(kp_target_cluster, [
             kp_target_cluster(self.s(t["name"]), int(t.get("replicas", 0))) for t in d.get("clusters") or []])
         b.eviction_from, b.n_eviction_from = self.strs([t["fromCluster"] for t in d.get("gracefulEvictionTasks") or []])

@@ -180,6 +180,20 @@ int component_sets(stream_t, const SnapView& s, const SetsArgs* A, const int32_t
   return 0;
 }
 
+int sets_rows(stream_t, const SnapView& s, const SetsArgs* A, const int64_t* off, int64_t* scratch, int32_t* row,
+              uint32_t* ovf) {
+  for (int r = 0; r < s.C; r++) body_sets_row(s, *A, off, r, scratch, row, ovf);
+  return 0;
+}
+
+int rows_from_class(stream_t, const SnapView& s, const BatchView& bv, const int32_t* list, int n, const int32_t* bcls,
+                    const int32_t* cls_rows, const uint64_t* fmask, int32_t* est) {
+  grid(n, 0, [&](int blk, unsigned char* sm) {
+    body_rows_from_class(CpuBlk{(int64_t*)sm}, blk, s, bv, list, bcls, cls_rows, fmask, est);
+  });
+  return 0;
+}
+
 int grades(stream_t, const GradesArgs& A) {
   for (uint64_t i = 0; i < A.n; i++) body_grades(A, i);
   return 0;
@@ -244,6 +258,31 @@ int kpsim_webster(const int32_t* votes, const uint32_t* ranks, int n, int32_t N,
   WebRes w = webster_par(B, parties, N, desc != 0, ss);
   for (int i = 0; i < n; i++) out[i] = web_seats(w, v[i], r[i]);
   return w.mode;
+}
+
+// webster_serial (k_slow's exact AllocateWebsterSeats) over n parties with int64
+// votes of any sign and ranks (name order); seats per party into out.
+void kpsim_webster_serial(const int64_t* votes, const uint32_t* ranks, int n, int32_t N, int desc, int32_t* out) {
+  std::vector<int32_t> heap(n > 0 ? n : 1);
+  kp::webster_serial(ranks, votes, out, heap.data(), n, N, desc != 0);
+}
+
+// MergeTargetClusters (pkg/util/binding.go:91-115) as SerialAssign::merge does it:
+// old = (on, orr)[0, no), new = (nn, nr)[0, nw); result into (out_n, out_r), returns
+// its length (<= no + nw).
+int kpsim_merge_targets(const uint32_t* on, const int32_t* orr, int no, const uint32_t* nn, const int32_t* nr, int nw,
+                        uint32_t* out_n, int32_t* out_r) {
+  using namespace kp;
+  const int cap = no + nw + 1;
+  std::vector<unsigned char> mem(serial_scratch_bytes(cap));
+  SerialScratch sc = serial_scratch_carve(mem.data(), cap);
+  for (int i = 0; i < no; i++) sc.sn[i] = on[i], sc.sr[i] = orr[i];
+  for (int i = 0; i < nw; i++) sc.tn[i] = nn[i], sc.tr[i] = nr[i];
+  SelCtx x{};
+  SerialAssign sa{x, sc, false};
+  const int k = sa.merge(no, nw);
+  for (int i = 0; i < k; i++) out_n[i] = sc.tn[i], out_r[i] = sc.tr[i];
+  return k;
 }
 
 // wsel_max over values (>= 0): largest v* with sum{v_i >= v*} >= target.

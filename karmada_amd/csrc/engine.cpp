@@ -172,6 +172,15 @@ struct kp_batch {
   // a representative binding per class; their raw GeneralEstimator rows [n][Cp]
   std::vector<int32_t> bcls, crep;
   int32_t *d_bcls = nullptr, *d_crep = nullptr, *cls_rows = nullptr;
+  // component-set classes (BF_SETS): class id and resolved component list of each;
+  // their rows are MaxAvailableComponentSets per cluster (k_sets_rows), and in the
+  // pair-row mode the BF_SETS bindings' rows are rebuilt from them (k_rows_from_class)
+  std::vector<int32_t> sets_cls, l_sets;
+  std::vector<SetsArgs> sets_args;
+  SetsArgs* d_sets_args = nullptr;
+  int64_t *d_sets_off = nullptr, *d_sets_scratch = nullptr;
+  int32_t* d_sets_list = nullptr;
+  std::string err;  // packing error text
   int32_t *d_all = nullptr, *d_cluster = nullptr, *d_region = nullptr, *d_slowlist = nullptr, *d_cs = nullptr;
   int32_t *status = nullptr, *errc = nullptr, *slow = nullptr;
   int64_t* arg = nullptr;
@@ -180,7 +189,7 @@ struct kp_batch {
   unsigned long long* counter = nullptr;
   uint32_t* stats = nullptr;
   unsigned long long* dbg = nullptr;
-  uint32_t h_stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t h_stats[16] = {};  // [0..7] slow-path counts, [8] component-set simulation overflow
   uint32_t* out_idx = nullptr;
   int32_t* out_rep = nullptr;
   uint64_t* offsets_d = nullptr;
@@ -211,6 +220,8 @@ struct kp_batch {
   }
   std::vector<RegionOut> h_rout;
 };
+
+int build_sets_args(const kp_snapshot* s, const kp_component* comps, uint32_t K, SetsArgs* A, std::string* err);
 
 // ============================================================================
 // Snapshot packing (cache.Snapshot, cache.go:124-139, packed once)
@@ -1131,6 +1142,21 @@ struct Packer {
     else if (hasCluster) h.sel = SEL_CLUSTER;
     else h.sel = SEL_ERR_UNSUPPORTED;
     h.need_replicas = (!b.has_replica_scheduling || S(b.replica_scheduling_type) == "Duplicated") ? -1 : b.replicas;
+    // runReplicaEstimator / SelectClusters with the MultiplePodTemplatesScheduling gate:
+    // isMultiTemplateSchedulingApplicable (core/estimation.go:43-65) = components and a
+    // cluster spread constraint with MinGroups == MaxGroups == 1. Such a binding's
+    // estimator row is MaxAvailableComponentSets (core/util.go:113-118) and it needs one
+    // available replica (one set) in SelectBestClusters (common.go:42-46).
+    if (o.multiple_pod_templates_scheduling && b.n_components > 0) {
+      bool one = false;
+      for (uint32_t i = 0; i < b.n_spread_constraints; i++)
+        one = one || (S(b.spread_constraints[i].spread_by_field) == "cluster" &&
+                      b.spread_constraints[i].min_groups == 1 && b.spread_constraints[i].max_groups == 1);
+      if (one) {
+        f |= BF_SETS;
+        if (h.need_replicas != -1) h.need_replicas = 1;
+      }
+    }
     if (rst == "Duplicated") f |= BF_GROUP_DUP;
     // strategy (assignment.go:95-123)
     if (rst == "Duplicated") h.strategy = ST_DUPLICATED;
@@ -1785,17 +1811,36 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
   // estimator classes: thread-local ids (bt->bcls) and keys, unified below
   bt->bcls.assign(n, 0);
   std::vector<std::vector<std::string>> tkeys(T);
+  std::vector<std::string> terr(T);
   auto run = [&](int t) {
     Packer pk{s, &pl[t]};
     std::unordered_map<std::string, int32_t> ids;
     std::string key;
+    SetsArgs A;
     for (int i = lo[t]; i < lo[t + 1]; i++) {
       pk.pack(bindings[i], bt->hdr[i]);
       if (bt->hdr[i].flags & BF_NONWORKLOAD_EST) {
         bt->bcls[i] = -1;
         continue;
       }
-      est_key(bt->hdr[i], pl[t], &key);
+      if (bt->hdr[i].flags & BF_SETS) {
+        // a component-set class: key 'S' + the resolved SetsArgs (est_key's keys
+        // start with the 0/1 ReplicaRequirements word, never 'S')
+        std::string err;
+        const int rc = build_sets_args(s, bindings[i].components, bindings[i].n_components, &A, &err);
+        if (rc == KP_EINVAL) {
+          bt->hdr[i].flags = (bt->hdr[i].flags & ~(uint32_t)BF_SETS) | BF_BAD;  // status ERROR, as a bad request
+        } else if (rc != KP_OK) {
+          if (terr[t].empty()) terr[t] = err;
+          bt->hdr[i].flags &= ~(uint32_t)BF_SETS;
+        }
+      }
+      if (bt->hdr[i].flags & BF_SETS) {
+        key.assign(1, 'S');
+        key.append((const char*)&A, sizeof(A));
+      } else {
+        est_key(bt->hdr[i], pl[t], &key);
+      }
       auto it = ids.find(key);
       if (it == ids.end()) {
         it = ids.emplace(key, (int32_t)tkeys[t].size()).first;
@@ -1811,6 +1856,11 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
     for (int t = 0; t < T; t++) th.emplace_back(run, t);
     for (auto& x : th) x.join();
   }
+  for (auto& x : terr)
+    if (!x.empty()) {
+      bt->err = x;
+      return false;
+    }
   size_t ni = 0, nl = 0, nt = 0, np = 0, nn = 0;
   for (auto& q : pl) ni += q.ipool.size(), nl += q.lpool.size(), nt += q.tols.size(), np += q.progs.size(),
                      nn += q.instrs.size();
@@ -1862,7 +1912,16 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
     for (size_t j = 0; j < tkeys[t].size(); j++) {
       auto it = gid.emplace(tkeys[t][j], (int32_t)gid.size() + 1).first;
       remap[j] = it->second;
-      if ((size_t)it->second == bt->crep.size()) bt->crep.push_back(-1);
+      if ((size_t)it->second == bt->crep.size()) {
+        bt->crep.push_back(-1);
+        const std::string& k = tkeys[t][j];
+        if (!k.empty() && k[0] == 'S') {  // component-set class: its rows come from k_sets_rows
+          SetsArgs A;
+          memcpy(&A, k.data() + 1, sizeof(A));
+          bt->sets_cls.push_back(it->second);
+          bt->sets_args.push_back(A);
+        }
+      }
     }
     for (int i = lo[t]; i < lo[t + 1]; i++) {
       const int32_t g = bt->bcls[i] < 0 ? 0 : remap[bt->bcls[i]];
@@ -1884,8 +1943,15 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   bt->B = (int)n;
   bt->hdr.resize(n);
   const auto tp0 = std::chrono::steady_clock::now();
+  if (s->opts.multiple_pod_templates_scheduling)
+    for (uint64_t i = 0; i < n; i++)
+      if (bindings[i].n_components > 0 && !bindings[i].components) {
+        e->err = "kp_batch_create: binding " + std::to_string(i) +
+                 " has n_components > 0 but no components (the MultiplePodTemplatesScheduling gate reads them)";
+        return KP_EINVAL;
+      }
   if (!pack_parallel(s, bindings, (int)n, bt)) {
-    e->err = "batch pools exceed 2^31 entries";
+    e->err = bt->err.empty() ? "batch pools exceed 2^31 entries" : bt->err;
     return KP_ENOTSUP;
   }
   for (uint64_t i = 0; i < n; i++) {
@@ -1977,7 +2043,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->start, B);
   a.add(&bt->count, B);
   a.add(&bt->counter, 1);
-  a.add(&bt->stats, 8);
+  a.add(&bt->stats, 16);
 #ifdef KP_STAMPS
   a.add(&bt->dbg, 32);
 #endif
@@ -1994,6 +2060,23 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->rnsel, std::max(1, nr));
   a.add(&bt->nhost, 1);
   a.add(&bt->slow_scratch, bt->slow_slot * bt->slow_grid);
+  // component-set classes: per cluster rank its node-run scratch (one run per model
+  // node at most, capped at kSetsRunsMax) for k_sets_rows, reused class after class
+  std::vector<int64_t> sets_off;
+  if (!bt->sets_cls.empty()) {
+    for (uint64_t i = 0; i < n; i++)
+      if (bt->hdr[i].flags & BF_SETS) bt->l_sets.push_back((int32_t)i);
+    sets_off.assign((size_t)s->C + 1, 0);
+    for (int r = 0; r < s->C; r++) {
+      int64_t nodes = 0;
+      for (int g = s->mgrp_off[r]; g < s->mgrp_off[r + 1]; g++) nodes += s->mgrp_cnt[g];
+      sets_off[r + 1] = sets_off[r] + std::max<int64_t>(1, std::min<int64_t>(nodes, kSetsRunsMax));
+    }
+    a.add(&bt->d_sets_args, bt->sets_args.size());
+    a.add(&bt->d_sets_off, sets_off.size());
+    a.add(&bt->d_sets_scratch, (size_t)sets_off.back() * (1 + kSetsSlots));
+    a.add(&bt->d_sets_list, bt->l_sets.size());
+  }
   const auto tp1 = std::chrono::steady_clock::now();
   HIPCHK(a.alloc());
   const auto tp2 = std::chrono::steady_clock::now();
@@ -2007,7 +2090,16 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   HIPCHK(up(d_progs, bt->progs.data(), sizeof(Prog) * bt->progs.size()));
   HIPCHK(up(d_instrs, bt->instrs.data(), sizeof(Instr) * bt->instrs.size()));
   HIPCHK(up(bt->d_bcls, bt->bcls.data(), 4 * bt->bcls.size()));
-  HIPCHK(up(bt->d_crep, bt->crep.data(), 4 * bt->crep.size()));
+  {  // representatives of the k_est_class rows; -1 for the component-set classes (k_sets_rows)
+    std::vector<int32_t> rep = bt->crep;
+    for (int32_t g : bt->sets_cls) rep[g] = -1;
+    HIPCHK(up(bt->d_crep, rep.data(), 4 * rep.size()));
+  }
+  if (!bt->sets_cls.empty()) {
+    HIPCHK(up(bt->d_sets_args, bt->sets_args.data(), sizeof(SetsArgs) * bt->sets_args.size()));
+    HIPCHK(up(bt->d_sets_off, sets_off.data(), 8 * sets_off.size()));
+    HIPCHK(up(bt->d_sets_list, bt->l_sets.data(), 4 * bt->l_sets.size()));
+  }
   HIPCHK(up(bt->d_all, bt->l_all.data(), 4 * bt->l_all.size()));
   HIPCHK(up(bt->d_cluster, bt->l_cluster.data(), 4 * bt->l_cluster.size()));
   HIPCHK(up(bt->d_region, bt->l_region.data(), 4 * bt->l_region.size()));
@@ -2067,7 +2159,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   }
   if (batch_lds_check(e, s, bt)) return KP_ENOTSUP;
   HIPCHK(dev::h2d(bt->counter, &bt->out_cap, sizeof(unsigned long long), st));  // the shared area's start
-  HIPCHK(dev::fill(bt->stats, 0, 8 * sizeof(uint32_t), st));
+  HIPCHK(dev::fill(bt->stats, 0, sizeof(bt->h_stats), st));
   KArgs ka;
   ka.s = s->view;
   ka.bv = bt->view;
@@ -2081,6 +2173,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   ka.sink.arg = bt->arg;
   ka.sink.start = bt->start;
   ka.sink.count = bt->count;
+  ka.sink.cap_end = std::max<uint64_t>(1, 2 * bt->out_cap);
   ka.slow = bt->slow;
   ka.stats = bt->stats;
   ka.slow_ids = bt->d_slowlist;
@@ -2121,6 +2214,14 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     HIPCHK(dev::pair(sp, s->view, bt->view, nullptr, 0, B, bt->fmask, bt->est, nullptr, 0, md_cap, smem_pair(s, md_cap),
                      fast));
   }
+  // component-set classes (BF_SETS bindings): their class rows, and in the pair-row
+  // mode those bindings' own rows rebuilt from them (feasible clusters only)
+  for (size_t j = 0; j < bt->sets_cls.size(); j++)
+    HIPCHK(dev::sets_rows(sp, s->view, bt->d_sets_args + j, bt->d_sets_off, bt->d_sets_scratch,
+                          bt->cls_rows + (size_t)bt->sets_cls[j] * s->Cp, bt->stats + 8));
+  if (!bits && !bt->l_sets.empty())
+    HIPCHK(dev::rows_from_class(sp, s->view, bt->view, bt->d_sets_list, (int)bt->l_sets.size(), bt->d_bcls,
+                                bt->cls_rows, bt->fmask, bt->est));
   HIPCHK(dev::event_record(e->ev[4], sp));
   HIPCHK(dev::stream_wait(st, e->ev[4]));  // every pair row precedes the rest
   HIPCHK(dev::event_record(e->ev[1], st));
@@ -2251,6 +2352,11 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   HIPCHK(dev::d2h(bt->h_offsets.data(), bt->offsets_d, 8 * (size_t)(B + 1), st));
   HIPCHK(dev::d2h(bt->h_stats, bt->stats, sizeof(bt->h_stats), st));
   HIPCHK(dev::sync(st));
+  if (bt->h_stats[8]) {
+    e->err = "kp_schedule_batch: a MaxAvailableComponentSets simulation needs more than " +
+             std::to_string(kSetsRunsMax) + " node runs in one cluster";
+    return KP_ENOTSUP;
+  }
   double tc0 = now_ms();
   const uint64_t tot = bt->h_offsets[B];
   if (tot > bt->h_res_cap || !bt->h_cidx) {
@@ -2376,33 +2482,30 @@ int kp_filter_reasons(kp_engine* e, kp_batch* bt, uint32_t* out_reasons) {
   return KP_OK;
 }
 
-int kp_max_available_component_sets(kp_engine* e, const kp_snapshot* sc, const kp_component* comps, uint32_t K,
-                                    const uint32_t* cluster_idx, uint64_t n, int32_t* out) {
-  if (!e || !sc || (K && !comps) || (n && (!cluster_idx || !out))) return KP_EINVAL;
-  (void)dev::set_device(e->device);
-  kp_snapshot* s = const_cast<kp_snapshot*>(sc);
-  if (!s->opts.multiple_pod_templates_scheduling) {
-    e->err = "MaxAvailableComponentSets: the MultiplePodTemplatesScheduling gate is off";
-    return KP_ENOTSUP;
-  }
+}  // extern "C"
+
+// One component list resolved against the snapshot's resource dictionary (SetsArgs,
+// kp_sets.h): podsInSet, perSetRequirement (general.go:371-401, wrapping int64) and
+// each component's util.NewResource request (resource.go:46-75). KP_EINVAL for an
+// unparsable quantity, KP_ENOTSUP beyond the device limits.
+int build_sets_args(const kp_snapshot* s, const kp_component* comps, uint32_t K, SetsArgs* A, std::string* err) {
   if (K > (uint32_t)kSetsComp) {
-    e->err = "MaxAvailableComponentSets: more than 16 components";
+    *err = "MaxAvailableComponentSets: more than 16 components";
     return KP_ENOTSUP;
   }
-  SetsArgs A;
-  memset(&A, 0, sizeof(A));
-  A.K = (int32_t)K;
+  memset(A, 0, sizeof(*A));
+  A->K = (int32_t)K;
   std::map<std::string, int64_t> per;       // perSetRequirement (general.go:389-401), wrapping int64
   std::vector<std::map<std::string, int64_t>> nr(K);  // util.NewResource of each request
   std::vector<std::string> slots;
   int64_t pps = 0;
   for (uint32_t k = 0; k < K; k++) {
-    A.replicas[k] = comps[k].replicas;
+    A->replicas[k] = comps[k].replicas;
     pps += comps[k].replicas;  // podsInSet
     if (!comps[k].has_replica_requirements) continue;
     QtyMap rq;
     if (!qmap(comps[k].resource_request, comps[k].n_resource_request, &rq)) {
-      e->err = "MaxAvailableComponentSets: unparsable quantity";
+      *err = "MaxAvailableComponentSets: unparsable quantity";
       return KP_EINVAL;
     }
     for (auto& kv : rq) {
@@ -2418,29 +2521,45 @@ int kp_max_available_component_sets(kp_engine* e, const kp_snapshot* sc, const k
     }
   }
   if (slots.size() + 1 > (size_t)kSetsSlots || per.size() > (size_t)kSetsPer) {
-    e->err = "MaxAvailableComponentSets: too many distinct resources";
+    *err = "MaxAvailableComponentSets: too many distinct resources";
     return KP_ENOTSUP;
   }
-  A.NS = (int32_t)slots.size() + 1;
-  for (size_t j = 0; j < slots.size(); j++) A.slot_rid[j] = s->res.get(slots[j]);
-  A.slot_rid[slots.size()] = -2;  // pods
+  A->NS = (int32_t)slots.size() + 1;
+  for (size_t j = 0; j < slots.size(); j++) A->slot_rid[j] = s->res.get(slots[j]);
+  A->slot_rid[slots.size()] = -2;  // pods
   for (uint32_t k = 0; k < K; k++) {
     for (size_t j = 0; j < slots.size(); j++) {
       auto it = nr[k].find(slots[j]);
       const int64_t v = it == nr[k].end() ? 0 : it->second;
-      A.req[k][j] = v;
-      A.pos[k][j] = v > 0 ? v : 0;
+      A->req[k][j] = v;
+      A->pos[k][j] = v > 0 ? v : 0;
     }
-    A.req[k][slots.size()] = 1;
-    A.pos[k][slots.size()] = 1;
+    A->req[k][slots.size()] = 1;
+    A->pos[k][slots.size()] = 1;
   }
-  A.pods_per_set = pps;
+  A->pods_per_set = pps;
   for (auto& kv : per) {
-    A.per_rid[A.nper] = s->res.get(kv.first);
-    A.per_req[A.nper] = kv.second;
-    A.per_nonzero |= kv.second != 0 ? 1 : 0;
-    A.nper++;
+    A->per_rid[A->nper] = s->res.get(kv.first);
+    A->per_req[A->nper] = kv.second;
+    A->per_nonzero |= kv.second != 0 ? 1 : 0;
+    A->nper++;
   }
+  return KP_OK;
+}
+
+extern "C" {
+
+int kp_max_available_component_sets(kp_engine* e, const kp_snapshot* sc, const kp_component* comps, uint32_t K,
+                                    const uint32_t* cluster_idx, uint64_t n, int32_t* out) {
+  if (!e || !sc || (K && !comps) || (n && (!cluster_idx || !out))) return KP_EINVAL;
+  (void)dev::set_device(e->device);
+  kp_snapshot* s = const_cast<kp_snapshot*>(sc);
+  if (!s->opts.multiple_pod_templates_scheduling) {
+    e->err = "MaxAvailableComponentSets: the MultiplePodTemplatesScheduling gate is off";
+    return KP_ENOTSUP;
+  }
+  SetsArgs A;
+  if (int rc = build_sets_args(s, comps, K, &A, &e->err)) return rc;
   std::vector<int32_t> ranks(n);
   std::vector<int64_t> off(n + 1, 0);  // runs per cluster: its model node count (a run holds >= 1 node)
   for (uint64_t i = 0; i < n; i++) {

@@ -135,6 +135,16 @@ extern "C" __global__ void __launch_bounds__(64) k_sets(SnapView s, const SetsAr
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) body_sets(s, A, ranks, off, i, scratch, out);
 }
+extern "C" __global__ void __launch_bounds__(64) k_sets_rows(SnapView s, const SetsArgs* A, const int64_t* off,
+                                                            int64_t* scratch, int32_t* row, uint32_t* ovf) {
+  const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (r < s.C) body_sets_row(s, *A, off, r, scratch, row, ovf);
+}
+extern "C" __global__ void __launch_bounds__(256) k_rows_from_class(SnapView s, BatchView bv, const int32_t* list,
+                                                                  const int32_t* bcls, const int32_t* cls_rows,
+                                                                  const uint64_t* fmask, int32_t* est) {
+  body_rows_from_class(GpuBlk{nullptr}, (int)blockIdx.x, s, bv, list, bcls, cls_rows, fmask, est);
+}
 extern "C" __global__ void __launch_bounds__(256) k_grades(GradesArgs A) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < A.n) body_grades(A, i);
@@ -338,6 +348,22 @@ int component_sets(stream_t st, const SnapView& s, const SetsArgs* A, const int3
                    uint64_t n, int64_t* scratch, int32_t* out) {
   if (n == 0) return 0;
   hipLaunchKernelGGL(k_sets, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)st, s, A, ranks, off, n, scratch, out);
+  return chk(hipGetLastError());
+}
+
+int sets_rows(stream_t st, const SnapView& s, const SetsArgs* A, const int64_t* off, int64_t* scratch, int32_t* row,
+              uint32_t* ovf) {
+  if (s.C <= 0) return 0;
+  hipLaunchKernelGGL(k_sets_rows, dim3((unsigned)((s.C + 63) / 64)), dim3(64), 0, (hipStream_t)st, s, A, off, scratch,
+                     row, ovf);
+  return chk(hipGetLastError());
+}
+
+int rows_from_class(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* list, int n,
+                    const int32_t* bcls, const int32_t* cls_rows, const uint64_t* fmask, int32_t* est) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_rows_from_class, dim3(n), dim3(256), 0, (hipStream_t)st, s, bv, list, bcls, cls_rows, fmask,
+                     est);
   return chk(hipGetLastError());
 }
 

@@ -829,6 +829,7 @@ struct Sink {
   int64_t* arg;
   uint64_t* start;
   uint32_t* count;
+  uint64_t cap_end;  // entries of out_idx/out_rep: the slots [0, out_cap) + the shared area
 };
 
 // ============================================================================
@@ -1060,7 +1061,10 @@ KP_HD inline void sort_tcl(uint32_t* name, int32_t* rep, int n) {
 // ============================================================================
 // Webster / Sainte-Lague priorities (webstermethod.go:57-85)
 // ============================================================================
-// float64(Votes) / float64(2*Seats+1) with Seats < 2^30 (no int32 wrap).
+// float64(Votes) / float64(2*Seats+1) with Seats < 2^30 (no int32 wrap). From 2^30
+// seats on, 2*Seats+1 wraps negative in Go's int32: the block-parallel paths hand
+// targets of 2^30 seats or more to the serial emulation (webster_serial).
+constexpr int64_t kSeatWrap = (int64_t)1 << 30;
 KP_HD inline double w_prio(int64_t v, int64_t k) { return (double)v / (double)(2 * k + 1); }
 
 // #{k >= 0 : prio(v,k) >= t} (ge) or > t, for v >= 0, t > 0, saturating at cap.
@@ -1131,25 +1135,90 @@ KP_HD inline void webster_serial(const uint32_t* name, const int64_t* votes, int
                                  int32_t N, bool desc) {
   for (int i = 0; i < n; i++) seats[i] = 0;
   if (n == 0 || N <= 0) return;
-  bool neg = false;
+  int npos = 0, nzero = 0, ipos = -1;
   int64_t V = 0;
   for (int i = 0; i < n; i++) {
-    if (votes[i] < 0) neg = true;
-    V += votes[i];
+    V += votes[i] > 0 ? votes[i] : 0;
+    if (votes[i] > 0) npos++, ipos = i;
+    if (votes[i] == 0) nzero++;
+  }
+  auto before = [&](int j, int i) { return desc ? name[j] > name[i] : name[j] < name[i]; };  // name tie-break
+  // Party i's k-th seat has priority v_i / int32(2k+1) (webstermethod.go:60-61): for
+  // v > 0 positive and falling while k < 2^30, then negative (2k+1 wraps) and
+  // falling; for v = 0 always 0; for v < 0 negative and RISING. Every positive
+  // element comes first, so while npos * 2^30 >= N the seats are the top N of the
+  // positive parties' elements (below); otherwise the positive parties take 2^30
+  // each and the rest R goes, in heap order, to: the zero-vote parties (priority 0
+  // beats every negative one; ties by seats then name: a round robin in name
+  // order); else to the positive party's wrapped seats while they stay above the
+  // best negative head v_j (a tie goes to the fewer seats, j), and then to j, whose
+  // priority only rises once it has a seat.
+  if (npos <= 1 && (int64_t)N > (int64_t)npos * kSeatWrap) {
+    if (ipos >= 0) seats[ipos] = (int32_t)kSeatWrap;
+    int64_t R = (int64_t)N - (int64_t)npos * kSeatWrap;
+    if (nzero > 0) {
+      const int64_t q = R / nzero, rem = R % nzero;
+      for (int i = 0; i < n; i++) {
+        if (votes[i] != 0) continue;
+        int64_t ahead = 0;
+        for (int j = 0; j < n; j++) ahead += (votes[j] == 0 && before(j, i)) ? 1 : 0;
+        seats[i] = (int32_t)(q + (ahead < rem ? 1 : 0));
+      }
+      return;
+    }
+    int jn = -1;  // the best negative head: largest v, then the name order
+    for (int j = 0; j < n; j++)
+      if (votes[j] < 0 && (jn < 0 || votes[j] > votes[jn] || (votes[j] == votes[jn] && before(j, jn)))) jn = j;
+    if (ipos >= 0) {
+      // wrapped seats of the positive party: k = 2^30 + m, priority v / (2k+1 - 2^32), falling in m
+      const double vj = jn >= 0 ? (double)votes[jn] : 0.0;
+      auto above = [&](int64_t m) {
+        const int64_t k = kSeatWrap + m;
+        return jn < 0 || (double)votes[ipos] / (double)(int32_t)(uint32_t)(2 * k + 1) > vj;
+      };
+      int64_t lo = 0, hi = R;  // m seats taken: the first m with !above(m), or R
+      while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (above(mid)) lo = mid + 1;
+        else hi = mid;
+      }
+      seats[ipos] = (int32_t)((int64_t)seats[ipos] + lo);
+      R -= lo;
+    }
+    if (R > 0 && jn >= 0) seats[jn] = (int32_t)R;
+    return;
   }
   int32_t done = 0;
-  if (!neg && V > 0) {
-    double t0 = N > n ? (double)V / (2.0 * (double)(N - n)) : (double)V;
-    for (int iter = 0; iter < 80; iter++) {
+  if (npos > 0) {
+    // Count threshold t over the positive parties: every element with priority > t
+    // is in the top N when the count is <= N. Bisected while the heap's share
+    // would be large, so the heap below orders about the tie group at the N-th
+    // priority. A party's count stops at 2^30 (its later priorities are negative).
+    const int64_t cap = (int64_t)N + 1 < kSeatWrap ? (int64_t)N + 1 : kSeatWrap;
+    auto total = [&](double t) {
       int64_t S = 0;
-      for (int i = 0; i < n; i++) S += w_count(votes[i], t0, (int64_t)N + 1, false);
-      if (S <= N) break;
-      t0 *= 2.0;
+      for (int i = 0; i < n; i++) S += votes[i] > 0 ? w_count(votes[i], t, cap, false) : 0;
+      return S;
+    };
+    double hi = (double)V / (2.0 * (double)N), lo = 0;
+    int64_t S = total(hi);
+    for (int it = 0; it < 200 && S > (int64_t)N; it++) {
+      lo = hi;
+      hi *= 2.0;
+      S = total(hi);
     }
-    for (int i = 0; i < n; i++) {
-      seats[i] = (int32_t)w_count(votes[i], t0, (int64_t)N + 1, false);
-      done += seats[i];
+    for (int it = 0; it < 64 && S <= (int64_t)N && (int64_t)N - S > 4 * (int64_t)n + 64; it++) {
+      const double mid = lo + (hi - lo) * 0.5;
+      if (!(mid > lo && mid < hi)) break;
+      const int64_t Sm = total(mid);
+      if (Sm <= (int64_t)N) hi = mid, S = Sm;
+      else lo = mid;
     }
+    if (S <= (int64_t)N)
+      for (int i = 0; i < n; i++) {
+        seats[i] = votes[i] > 0 ? (int32_t)w_count(votes[i], hi, cap, false) : 0;
+        done += seats[i];
+      }
   }
   WHeap w{name, votes, seats, heap, desc};
   for (int i = 0; i < n; i++) heap[i] = i;

@@ -64,6 +64,14 @@ int region_groups(stream_t st, const RegionOut* rout, const int32_t* rstat, cons
 // (A, ranks and off in device memory; cluster i's runs at scratch[off[i], off[i+1])).
 int component_sets(stream_t st, const SnapView& s, const SetsArgs* A, const int32_t* ranks, const int64_t* off,
                    uint64_t n, int64_t* scratch, int32_t* out);
+// Component-set class row: row[r] = sets_one for every cluster rank r < C (cluster r's
+// runs at scratch[off[r], off[r+1])); *ovf = 1 when a simulation outgrew its runs.
+int sets_rows(stream_t st, const SnapView& s, const SetsArgs* A, const int64_t* off, int64_t* scratch, int32_t* row,
+              uint32_t* ovf);
+// Pair-row mode: est[b][c] of the n bindings list[i] rebuilt from their class rows
+// (cal_merge_bf with spec.Replicas on feasible clusters, 0 elsewhere, as pair_eval writes).
+int rows_from_class(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* list, int n,
+                    const int32_t* bcls, const int32_t* cls_rows, const uint64_t* fmask, int32_t* est);
 // kp_model_grades: A.counts[grade] += 1 per node (body_grades); A's arrays in device memory.
 int grades(stream_t st, const GradesArgs& A);
 // kp_node_max_replicas: *A.sum += int32 sum of node_replicas over the nodes (wrapping).

@@ -266,6 +266,7 @@ KP_FI void body_est_class(const BLK& B, int k, unsigned char* smem, const SnapVi
     for (int c = B.tid(); c < s.Cp; c += B.nth()) row[c] = kInt32Max;
     return;
   }
+  if (rep[k] < 0) return;  // a component-set class (k_sets_rows writes it)
   const BindHdr h = bv.hdr[rep[k]];
   int32_t* md = (int32_t*)(smem + kRedBytes);  // MaxDivided per template, zero past n_tmpl
   const bool rr = (h.flags & BF_HAS_RR) != 0;
@@ -274,6 +275,20 @@ KP_FI void body_est_class(const BLK& B, int k, unsigned char* smem, const SnapVi
   const MdTab mdt = md_regs(md);
   for (int c = B.tid(); c < s.Cp; c += B.nth())
     row[c] = est_compute_bf<Fast>(s, bv, h, c, mdt.v, est_load<Fast>(s, bv, h, c, ldcol(s.flags, c)));
+}
+
+// Pair-row mode, BF_SETS binding list[blk]: its calAvailableReplicas row from its
+// component-set class row (core/util.go:57-110 over MaxAvailableComponentSets), as
+// pair_eval writes it: cal_merge_bf on feasible clusters, 0 elsewhere.
+template <class BLK>
+KP_FI void body_rows_from_class(const BLK& B, int blk, const SnapView& s, const BatchView& bv, const int32_t* list,
+                                const int32_t* bcls, const int32_t* cls_rows, const uint64_t* fmask, int32_t* est) {
+  const int b = list[blk];
+  const int32_t rep = bv.hdr[b].replicas;
+  const int32_t* cr = cls_rows + (size_t)bcls[b] * s.Cp;
+  const uint64_t* fr = fmask + (size_t)b * s.W;
+  int32_t* row = est + (size_t)b * s.Cp;
+  for (int c = B.tid(); c < s.C; c += B.nth()) row[c] = mask_test(fr, c) ? cal_merge_bf(rep, cr[c]) : 0;
 }
 
 // Pair stage for binding list[b0 + blk] (b0 + blk without a list): each wave evaluates 64 consecutive clusters

@@ -81,7 +81,8 @@ enum : uint32_t {
   BF_HAS_RR = 1u << 0,          // ReplicaRequirements != nil
   BF_NONWORKLOAD_EST = 1u << 1, // Replicas==0 && no components: estimator skipped (util.go:69-73)
   BF_WORKLOAD_ASSIGN = 1u << 2, // (Replicas>0 || RR!=nil) && components<=1 (common.go:68)
-  // bit 3 unused
+  BF_SETS = 1u << 3,            // MultiplePodTemplatesScheduling gate + isMultiTemplateSchedulingApplicable:
+                                // the estimator row is MaxAvailableComponentSets (core/util.go:113-118)
   BF_FRESH = 1u << 4,           // RescheduleRequired (assignment.go:118-120)
   BF_UID_DESC = 1u << 5,        // FNV-1a(uid) odd -> name-descending tie-break
   BF_OVERFLOW = 1u << 6,        // enableOverflow (common.go:156-170)

@@ -307,6 +307,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
     });
     B.maxsum(wmax, wsum);
     if (wmax >= kInt32Max) return SLOW_WEIGHT;
+    if ((int64_t)h.replicas >= kSeatWrap) return SLOW_WRAP;  // seats past 2^30 (w_prio)
     const bool all1 = wsum == 0;  // getStaticWeightInfoList: every candidate weight 1
     auto parties = [&](auto fn) {
       cs.each([&](uint32_t rk, int32_t w) {
@@ -431,7 +432,8 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
     B.reduce2(vmin, [](int64_t p, int64_t q) { return p < q ? p : q; }, (int64_t)0, nparty,
               [](int64_t p, int64_t q) { return p + q; }, (int64_t)0);
   }
-  if (vmin < 0 || sabs >= (int64_t)kInt32Max) return SLOW_WRAP;  // int32 wrap hazard
+  // int32 wrap hazards: vote sums, and seats past 2^30 (w_prio)
+  if (vmin < 0 || sabs >= (int64_t)kInt32Max || (int64_t)target >= kSeatWrap) return SLOW_WRAP;
   KP_STAMP(x, 2);
   if ((int32_t)vtot < target) {
     if (B.tid() == 0) sink_error(x, KP_STATUS_UNSCHEDULABLE, not_enough, vtot);

@@ -518,10 +518,22 @@ KP_HD inline void sink_serial(const SelCtx& x, const SerialScratch& sc, const Se
     k.count[b] = 0;
     return;
   }
-  // the binding's own slot when the list fits it; else (overflow tiers can append the
-  // spec.Clusters entries once per tier) the shared area past every slot
+  // The binding's own slot when the list fits it (out_cap = min(C, Replicas) +
+  // len(spec.Clusters) bounds every AssignReplicas result: the positive new entries
+  // of all overflow tiers hold at most Replicas seats on distinct candidates, and
+  // MergeTargetClusters adds only scheduled clusters, each in one tier); else the
+  // shared area past every slot, checked against its end so a wrong bound reports
+  // an error instead of writing past the allocation.
   unsigned long long base = (uint64_t)o.n <= x.h->out_cap ? (unsigned long long)x.h->out_off
                                                           : kp_atomic_add(k.counter, (unsigned long long)o.n);
+  if (base + (uint64_t)o.n > k.cap_end) {
+    k.status[b] = KP_STATUS_ERROR;
+    k.err[b] = KP_ERR_RESULT_CAPACITY;
+    k.arg[b] = o.n;
+    k.start[b] = 0;
+    k.count[b] = 0;
+    return;
+  }
   k.start[b] = base;
   k.count[b] = (uint32_t)o.n;
   for (int i = 0; i < o.n; i++) {

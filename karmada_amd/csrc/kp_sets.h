@@ -180,4 +180,18 @@ KP_HD inline void body_sets(const SnapView& s, const SetsArgs* A, const int32_t*
   out[i] = sets_one(s, *A, ranks[i], scratch + (size_t)off[i] * (1 + kSetsSlots), (int)(off[i + 1] - off[i]));
 }
 
+// Component-set class row (kp_schedule_batch, BF_SETS bindings): cluster rank r's
+// answer; a simulation that outgrew its runs raises *ovf (the batch then fails with
+// KP_ENOTSUP) instead of leaving kSetsOverflow in the row.
+KP_HD inline void body_sets_row(const SnapView& s, const SetsArgs& A, const int64_t* off, int r, int64_t* scratch,
+                                int32_t* row, uint32_t* ovf) {
+  const int32_t v = sets_one(s, A, r, scratch + (size_t)off[r] * (1 + kSetsSlots), (int)(off[r + 1] - off[r]));
+  if (v == kSetsOverflow) {
+    *ovf = 1u;
+    row[r] = 0;
+  } else {
+    row[r] = v;
+  }
+}
+
 }  // namespace kp

@@ -16,6 +16,15 @@
 //   7  "ties": clusters in three identical capacity classes, mostly Aggregated,
 //      so equal AvailableReplicas straddle the Aggregated cut (sort.Sort's
 //      permutation of equal keys decides; SURVEY hazard H2), parity only.
+//   8  "wrap": clusters whose estimates approach MaxInt32 (pods ~1-2.1e9, huge
+//      resources, model-grade counts near 2^31), so the int32 sums of
+//      GetSumOfReplicas, dynamicDivideReplicas and the Aggregated prefix wrap
+//      (SURVEY hazard H5), StaticWeight weights >= 2^31, spec.Clusters replicas
+//      near 2^31 and seat counts up to MaxInt32; parity only.
+//   9  "templates": multi-template workloads (spec.Components) for the
+//      MultiplePodTemplatesScheduling gate: most carry a cluster spread constraint
+//      with MinGroups = MaxGroups = 1 (isMultiTemplateSchedulingApplicable), over
+//      config-3 clusters with resource models; parity only.
 #include <stdint.h>
 
 #include <cmath>
@@ -182,7 +191,7 @@ void gen_cluster(kps_world& w, uint32_t i, kp_cluster& c) {
   c.n_api_enablements = na;
   // resource summary
   c.has_resource_summary = 1;
-  const bool gpu = cfg == 3 || cfg == 5 || cfg == 6;
+  const bool gpu = cfg == 3 || cfg == 5 || cfg == 6 || cfg == 9;
   int nres = gpu ? 5 : 4;
   kp_resource* al = w.a.alloc<kp_resource>(nres);
   kp_resource* ad = w.a.alloc<kp_resource>(nres);
@@ -196,6 +205,13 @@ void gen_cluster(kps_world& w, uint32_t i, kp_cluster& c) {
     pods = 11000;
     eph = 100;
     f = 0;
+  }
+  if (cfg == 8) {  // estimates near MaxInt32: the pod count binds (getAllowedPodNumber)
+    cpu = 100000000;
+    memg = (int64_t)1 << 30;
+    pods = r.range(1000000000, 2147483000);
+    eph = 1000000;
+    f = r.p(0.5) ? 0 : 0.001 * r.unit();
   }
   al[0] = {w.s("cpu"), w.s(std::to_string(cpu))};
   al[1] = {w.s("memory"), w.s(std::to_string(memg) + "Gi")};
@@ -216,7 +232,7 @@ void gen_cluster(kps_world& w, uint32_t i, kp_cluster& c) {
   if (cfg == 6 && r.p(0.05)) c.has_resource_summary = 0;
   if (cfg == 6 && r.p(0.03)) c.deleting = 1;
   // resource models: 8 grades over (cpu, memory) with monotone mins
-  if (cfg == 3 || cfg == 5 || (cfg == 6 && r.p(0.5))) {
+  if (cfg == 3 || cfg == 5 || cfg == 9 || (cfg == 6 && r.p(0.5)) || (cfg == 8 && r.p(0.3))) {
     const int K = 8;
     kp_resource_model* rm = w.a.alloc<kp_resource_model>(K);
     kp_allocatable_modeling* am = w.a.alloc<kp_allocatable_modeling>(K);
@@ -226,7 +242,7 @@ void gen_cluster(kps_world& w, uint32_t i, kp_cluster& c) {
       rg[0] = {w.s("cpu"), w.s(std::to_string(c0)), w.s(std::to_string(c1))};
       rg[1] = {w.s("memory"), w.s(std::to_string(4 * c0) + "Gi"), w.s(std::to_string(4 * c1) + "Gi")};
       rm[g] = {(uint32_t)g, rg, 2};
-      am[g] = {(uint32_t)g, r.range(0, 64)};
+      am[g] = {(uint32_t)g, cfg == 8 ? r.range((int64_t)1 << 29, 2147483647) : r.range(0, 64)};
     }
     c.resource_models = rm;
     c.n_resource_models = K;
@@ -249,6 +265,37 @@ kp_cluster_affinity label_in(kps_world& w, Rng& r, int nvals) {
   a.match_expressions = rq;
   a.n_match_expressions = 1;
   return a;
+}
+
+// 1..kmax components (workv1alpha2.Component) with small replica counts and requests.
+void gen_components(kps_world& w, Rng& r, kp_binding& b, int kmax) {
+  const int K = 1 + (int)r.below(kmax);
+  kp_component* cs = w.a.alloc<kp_component>(K);
+  for (int k = 0; k < K; k++) {
+    cs[k].name = w.s("comp-" + std::to_string(k));
+    cs[k].replicas = (int32_t)r.range(r.p(0.05) ? 0 : 1, 4);
+    cs[k].has_replica_requirements = r.p(0.9);
+    if (cs[k].has_replica_requirements) {
+      const int nq = r.p(0.15) ? 3 : 2;
+      kp_resource* rq = w.a.alloc<kp_resource>(nq);
+      rq[0] = {w.s("cpu"), w.s(kCpu[r.below(6)])};
+      rq[1] = {w.s("memory"), w.s(kMem[r.below(7)])};
+      if (nq == 3) rq[2] = {w.s("nvidia.com/gpu"), w.s("1")};
+      cs[k].resource_request = rq;
+      cs[k].n_resource_request = nq;
+    }
+  }
+  b.components = cs;
+  b.n_components = K;
+}
+// a cluster spread constraint MinGroups = MaxGroups = 1 (+ sometimes a region one)
+void one_cluster_spread(kps_world& w, Rng& r, kp_binding& b) {
+  kp_spread_constraint* sc = w.a.alloc<kp_spread_constraint>(2);
+  int n = 0;
+  if (r.p(0.15)) sc[n++] = {w.s("region"), {}, 2, 1};
+  sc[n++] = {w.s("cluster"), {}, 1, 1};
+  b.spread_constraints = sc;
+  b.n_spread_constraints = n;
 }
 
 void gen_binding(kps_world& w, uint64_t i, kp_binding& b) {
@@ -356,6 +403,78 @@ void gen_binding(kps_world& w, uint64_t i, kp_binding& b) {
     b.eviction_from = ev;
     b.n_eviction_from = 1;
   }
+  if (cfg == 8) {
+    double x = r.unit();
+    b.has_cluster_affinity = r.p(0.5) ? b.has_cluster_affinity : 0;
+    if (x < 0.35) {
+      // DynamicWeight
+    } else if (x < 0.7) {
+      b.replica_division_preference = w.s("Aggregated");
+      b.has_weight_preference = 0;
+      b.dynamic_weight = kp_str{nullptr, 0};
+    } else if (x < 0.88) {  // StaticWeight, weights around and beyond 2^31
+      b.dynamic_weight = kp_str{nullptr, 0};
+      const int64_t kW[] = {1, 5, 2147483647, 2147483648ll, 3000000000ll, (int64_t)1 << 40};
+      const int n = 1 + (int)r.below(3);
+      kp_static_weight* sw = w.a.alloc<kp_static_weight>(n);
+      for (int k = 0; k < n; k++) sw[k] = kp_static_weight{label_in(w, r, 2 + (int)r.below(5)), kW[r.below(6)]};
+      b.static_weights = sw;
+      b.n_static_weights = n;
+    } else {
+      b.replica_scheduling_type = w.s("Duplicated");
+    }
+    const double y = r.unit();
+    b.replicas = y < 0.6 ? (int32_t)r.range(1, 1000000) : (y < 0.9 ? (int32_t)r.range(100000000, 2147483647)
+                                                                      : (int32_t)r.range(1, 20));
+    if (r.p(0.4) && C > 0) {  // previous placement: sums of spec.Clusters wrap
+      int n = 1 + (int)r.below(std::min<uint32_t>(4, C));
+      kp_target_cluster* tc = w.a.alloc<kp_target_cluster>(n);
+      uint32_t c0 = (uint32_t)r.below(C);
+      for (int k = 0; k < n; k++)
+        tc[k] = {w.s(w.cname((c0 + 5 * k) % C)), (int32_t)(r.p(0.6) ? r.range(600000000, 2147483647) : r.range(0, 1000))};
+      b.clusters = tc;
+      b.n_clusters = n;
+    } else {
+      b.clusters = nullptr;
+      b.n_clusters = 0;
+    }
+    if (r.p(0.1)) {
+      b.has_reschedule_triggered_at = 1;
+      b.has_last_scheduled_time = 1;
+      b.reschedule_triggered_at_ns = 2000;
+      b.last_scheduled_time_ns = 1000;
+    }
+    b.n_resource_request = 2;
+    kp_resource* rq = w.a.alloc<kp_resource>(2);
+    rq[0] = {w.s("cpu"), w.s(r.p(0.8) ? "1m" : "2")};
+    rq[1] = {w.s("memory"), w.s(r.p(0.8) ? "1Ki" : "1Gi")};
+    b.resource_request = rq;
+    return;
+  }
+  if (cfg == 9) {
+    gen_components(w, r, b, 4);
+    const double x = r.unit();
+    if (x < 0.7) one_cluster_spread(w, r, b);
+    else if (x < 0.85) {
+      kp_spread_constraint* sc = w.a.alloc<kp_spread_constraint>(1);
+      sc[0] = {w.s("cluster"), {}, 3, 1};
+      b.spread_constraints = sc;
+      b.n_spread_constraints = 1;
+    }
+    const double y = r.unit();
+    if (y < 0.25) {
+      b.replica_scheduling_type = w.s("Duplicated");
+    } else if (y < 0.55) {
+      b.replica_division_preference = w.s("Aggregated");
+      b.has_weight_preference = 0;
+      b.dynamic_weight = kp_str{nullptr, 0};
+    } else if (y < 0.6) {
+      b.has_replica_scheduling = 0;
+    }
+    if (r.p(0.3)) b.replicas = 0;  // spec.Replicas is not set for most multi-template kinds
+    if (r.p(0.2)) b.has_replica_requirements = 0;
+    return;
+  }
   if (cfg == 7) {
     b.replica_division_preference = w.s(r.p(0.8) ? "Aggregated" : "Weighted");
     if (r.p(0.7)) b.has_cluster_affinity = 0;  // keep most clusters feasible
@@ -379,8 +498,8 @@ void gen_binding(kps_world& w, uint64_t i, kp_binding& b) {
     b.has_replica_requirements = r.p(0.5);
   } else if (x < 0.10) {
     b.replicas = (int32_t)r.range(0, 3);
-  } else if (x < 0.12) {
-    b.n_components = 2;
+  } else if (x < 0.14) {
+    gen_components(w, r, b, 3);
   }
   double y = r.unit();
   if (y < 0.15) {
@@ -452,7 +571,9 @@ void gen_binding(kps_world& w, uint64_t i, kp_binding& b) {
     b.cluster_affinity = a;
     b.n_cluster_affinities = 0;
   }
-  if (r.p(0.25)) {  // spread constraints
+  if (b.n_components > 0 && r.p(0.6)) {
+    one_cluster_spread(w, r, b);
+  } else if (r.p(0.25)) {  // spread constraints
     double z = r.unit();
     kp_spread_constraint* sc = w.a.alloc<kp_spread_constraint>(2);
     if (z < 0.4) {
@@ -512,6 +633,24 @@ const kp_cluster* kps_clusters(const kps_world* w, uint64_t* n) {
 const kp_binding* kps_bindings(const kps_world* w, uint64_t* n) {
   *n = w->bindings.size();
   return w->bindings.data();
+}
+
+// spec.Replicas of bindings [b_lo, b_hi) (the §8(e) shard cost model), without
+// keeping them: each binding is generated into a scratch world and dropped.
+int kps_replicas(int config, uint64_t seed, uint32_t n_clusters, uint64_t b_lo, uint64_t b_hi, int32_t* out) {
+  if (!out || b_hi < b_lo) return -1;
+  kps_world w;
+  w.config = config;
+  w.seed = seed;
+  w.C = n_clusters;
+  for (uint64_t i = b_lo; i < b_hi; i++) {
+    if (((i - b_lo) & 4095) == 0) w.a = Arena();  // release the previous chunk's strings
+    kp_binding b;
+    memset(&b, 0, sizeof(b));
+    gen_binding(w, i, b);
+    out[i - b_lo] = b.replicas;
+  }
+  return 0;
 }
 
 }  // extern "C"

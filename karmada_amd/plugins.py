@@ -1,0 +1,236 @@
+"""The reference's plugin and estimator interfaces over the engine, as the Go shim in
+INTEGRATION.md implements them (the Python mirror the tests drive):
+
+  Result / Registry / Framework   framework.Result (framework/interface.go:103-211),
+                                  runtime.Registry (runtime/registry.go:31-100) and the
+                                  RunFilterPlugins / RunScorePlugins loops
+                                  (runtime/framework.go:93-170)
+  KpFilter                        framework.FilterPlugin (interface.go:85-89): answers
+                                  Filter(binding, cluster) from a batch's feasibility and
+                                  reason words (kp_filter_batch / kp_filter_reasons)
+  KpScore                         framework.ScorePlugin (interface.go:215-223): the summed
+                                  in-tree score per pair (kp_score_batch), no normalizer
+  KpEstimator                     estimatorclient.ReplicaEstimator (estimator/client/
+                                  interface.go:39-44): MaxAvailableReplicas through
+                                  kp_max_available_replicas (clusters in request order),
+                                  MaxAvailableComponentSets through
+                                  kp_max_available_component_sets
+  enabled_plugins_mask            `--plugins` (options.go:163) filtered over the in-tree
+                                  registry (plugins/registry.go:33-50) as kp_options'
+                                  enabled_plugins bitmask
+
+A batch is keyed by binding slot: the shim computes the device arrays once per batch
+and every per-pair call is a lookup. The product path is the C-ABI; nothing here
+computes a filter, score or estimate itself.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+from karmada_amd import api
+from karmada_amd.engine import Batch, Snapshot
+
+SUCCESS, UNSCHEDULABLE, ERROR = 0, 1, 2  # framework.Code (interface.go:124-133)
+
+# in-tree plugin names (plugins/registry.go:33-50) -> kp_options.enabled_plugins bits
+IN_TREE = {
+    "APIEnablement": api.PLUGIN_API_ENABLEMENT,
+    "TaintToleration": api.PLUGIN_TAINT_TOLERATION,
+    "ClusterAffinity": api.PLUGIN_CLUSTER_AFFINITY,
+    "SpreadConstraint": api.PLUGIN_SPREAD_CONSTRAINT,
+    "ClusterLocality": api.PLUGIN_CLUSTER_LOCALITY,
+    "ClusterEviction": api.PLUGIN_CLUSTER_EVICTION,
+}
+
+
+class Result:
+    """framework.Result: a code and reasons; None stands for Success (interface.go:175-177)."""
+
+    def __init__(self, code: int = SUCCESS, *reasons: str):
+        self.code = code
+        self.reasons = list(reasons)
+
+    def is_success(self) -> bool:
+        return self.code == SUCCESS
+
+    def __repr__(self):
+        return f"Result({self.code}, {self.reasons})"
+
+
+def is_success(r: Optional[Result]) -> bool:
+    return r is None or r.is_success()
+
+
+class Registry(dict):
+    """runtime.Registry: plugin name -> factory (registry.go:31-100)."""
+
+    def register(self, name: str, factory: Callable):
+        if name in self:
+            raise ValueError(f"a plugin named {name} already exists")
+        self[name] = factory
+
+    def unregister(self, name: str):
+        if name not in self:
+            raise ValueError(f"no plugin named {name} exists")
+        del self[name]
+
+    def merge(self, other: "Registry"):
+        for k, f in other.items():
+            self.register(k, f)
+
+    def factory_names(self) -> List[str]:
+        return sorted(self)
+
+    def filter(self, names: Sequence[str]) -> "Registry":
+        """--plugins: '*' enables every plugin, 'foo' enables foo, '-foo' disables it
+        (registry.go:74-100; a '-foo' before any plugin is enabled has no effect)."""
+        out = Registry()
+        if "*" in names:
+            out.update(self)
+        for n in names:
+            if n in self:
+                out[n] = self[n]
+                continue
+            if n.startswith("-") and len(out) > 0:
+                out.pop(n.lstrip("-"), None)
+        return out
+
+
+def enabled_plugins_mask(names: Sequence[str]) -> int:
+    """kp_options.enabled_plugins for a `--plugins` flag value over the in-tree registry."""
+    reg = Registry({k: None for k in IN_TREE})
+    m = 0
+    for k in reg.filter(names):
+        m |= IN_TREE[k]
+    return m
+
+
+class Framework:
+    """frameworkImpl (runtime/framework.go:64-184): the filter plugins run in order with
+    a short circuit on the first non-success Result; the score plugins' scores are
+    collected per plugin, with NormalizeScore when a plugin has ScoreExtensions."""
+
+    def __init__(self, registry: Registry):
+        self.filter_plugins, self.score_plugins = [], []
+        for name in registry.factory_names():
+            p = registry[name]()
+            if hasattr(p, "filter"):
+                self.filter_plugins.append(p)
+            if hasattr(p, "score"):
+                self.score_plugins.append(p)
+
+    def run_filter_plugins(self, ctx) -> Optional[Result]:
+        for p in self.filter_plugins:
+            r = p.filter(ctx)
+            if not is_success(r):
+                return r
+        return Result(SUCCESS)
+
+    def run_score_plugins(self, spec, clusters) -> Tuple[Optional[Dict[str, List[Tuple[object, int]]]], Optional[Result]]:
+        """(PluginToClusterScores, nil) or (nil, an Error Result); weights are all 1
+        (scorePluginsWeightMap is never populated, framework.go:41,156)."""
+        out = {}
+        for p in self.score_plugins:
+            scores = []
+            for c in clusters:
+                s, r = p.score(spec, c)
+                if not is_success(r):
+                    return None, Result(ERROR, f"plugin {p.name()!r} failed with: {r.reasons}")
+                scores.append((c, s))
+            ext = p.score_extensions() if hasattr(p, "score_extensions") else None
+            if ext is not None:
+                r = ext.normalize_score(scores)
+                if not is_success(r):
+                    return None, Result(ERROR, f"plugin {p.name()!r} normalizeScore failed with: {r.reasons}")
+            out[p.name()] = scores
+        return out, None
+
+
+class BatchView:
+    """One batch's device answers, fetched once and looked up per (binding slot, cluster).
+    `clusters` are the snapshot's cluster dicts in caller order (for taint reasons)."""
+
+    def __init__(self, snap: Snapshot, batch: Batch, clusters: Optional[Sequence[dict]] = None):
+        self.snap, self.batch, self.clusters = snap, batch, clusters
+        eng = snap.engine
+        self.C = len(snap.names)
+        self.index = {n: i for i, n in enumerate(snap.names)}
+        nb = batch.n
+        self.reasons = (C.c_uint32 * max(1, nb * self.C))()
+        eng._check(eng.L.kp_filter_reasons(eng.h, batch.h, self.reasons), "kp_filter_reasons")
+        self.scores = (C.c_int64 * max(1, nb * self.C))()
+        eng._check(eng.L.kp_score_batch(eng.h, batch.h, self.scores), "kp_score_batch")
+
+    def reason(self, slot: int, cluster: str) -> int:
+        return int(self.reasons[slot * self.C + self.index[cluster]])
+
+    def score(self, slot: int, cluster: str) -> int:
+        return int(self.scores[slot * self.C + self.index[cluster]])
+
+
+class KpFilter:
+    """FilterPlugin answering every in-tree filter at once from the batch (register it
+    with the in-tree filters disabled: --plugins=*,-APIEnablement,...). ctx = (slot,
+    cluster name). A deleting cluster is skipped by findClustersThatFit before any
+    plugin runs (generic_scheduler.go:138-142); here it reads as Success."""
+
+    def __init__(self, view: BatchView):
+        self.view = view
+
+    def name(self) -> str:
+        return "KpFilter"
+
+    def filter(self, ctx) -> Optional[Result]:
+        slot, cluster = ctx
+        w = self.view.reason(slot, cluster)
+        code = w & 0xFF
+        if code in (api.REASON_FIT, api.REASON_DELETING):
+            return None
+        cl = self.view.clusters[self.view.index[cluster]] if self.view.clusters is not None else {"taints": []}
+        return Result(UNSCHEDULABLE, api.reason_text(w, cl))
+
+
+class KpScore:
+    """ScorePlugin: the summed in-tree score (ClusterLocality + ClusterAffinity's 0)."""
+
+    def __init__(self, view: BatchView):
+        self.view = view
+
+    def name(self) -> str:
+        return "KpScore"
+
+    def score(self, spec, cluster) -> Tuple[int, Optional[Result]]:
+        return self.view.score(spec, cluster), None
+
+    def score_extensions(self):
+        return None
+
+
+class KpEstimator:
+    """ReplicaEstimator for the GeneralEstimator's place in GetReplicaEstimators()."""
+
+    def __init__(self, snap: Snapshot, batch: Batch):
+        self.snap, self.batch = snap, batch
+
+    def max_available_replicas(self, slot: int, clusters: Sequence[str]) -> List[Tuple[str, int]]:
+        """[]TargetCluster in the request's cluster order (general.go:57-64)."""
+        eng = self.snap.engine
+        idx = {n: i for i, n in enumerate(self.snap.names)}
+        ci = (C.c_uint32 * max(1, len(clusters)))(*[idx[n] for n in clusters])
+        out = (C.c_int32 * max(1, len(clusters)))()
+        eng._check(eng.L.kp_max_available_replicas(eng.h, self.batch.h, slot, ci, len(clusters), out),
+                   "kp_max_available_replicas")
+        return [(n, int(out[i])) for i, n in enumerate(clusters)]
+
+    def max_available_component_sets(self, components: Sequence[dict], clusters: Sequence[str]) -> List[Tuple[str, int]]:
+        """[]ComponentSetEstimationResponse in request order (general.go:154-162)."""
+        eng = self.snap.engine
+        w = api.World()
+        ca, nc = w.components(components)
+        idx = {n: i for i, n in enumerate(self.snap.names)}
+        ci = (C.c_uint32 * max(1, len(clusters)))(*[idx[n] for n in clusters])
+        out = (C.c_int32 * max(1, len(clusters)))()
+        eng._check(eng.L.kp_max_available_component_sets(eng.h, self.snap.h, ca, nc, ci, len(clusters), out),
+                   "kp_max_available_component_sets")
+        return [(n, int(out[i])) for i, n in enumerate(clusters)]

@@ -19,6 +19,8 @@ CONFIGS = {
     5: (10_000, 1_000_000),
     6: (300, 5_000),   # edge workload (every branch), parity only
     7: (2_000, 5_000),  # Aggregated tie straddles (sort.Sort permutation), parity only
+    8: (64, 2_000),     # int32 wrap of replica sums, weights >= 2^31, parity only
+    9: (2_000, 5_000),  # multi-template workloads (MultiplePodTemplatesScheduling), parity only
 }
 
 
@@ -34,8 +36,19 @@ def lib():
         L.kps_clusters.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.kps_bindings.restype = C.POINTER(api.kp_binding)
         L.kps_bindings.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+        L.kps_replicas.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.POINTER(C.c_int32)]
         _LIB = L
     return _LIB
+
+
+def replicas(config: int, seed: int, n_clusters: int, lo: int, hi: int):
+    """spec.Replicas of bindings [lo, hi) of the universe (numpy int32), for shard costs."""
+    import numpy as np
+    out = np.zeros(max(0, hi - lo), dtype=np.int32)
+    if len(out) and lib().kps_replicas(config, seed, n_clusters, lo, hi,
+                                        out.ctypes.data_as(C.POINTER(C.c_int32))) != 0:
+        raise RuntimeError("kps_replicas failed")
+    return out
 
 
 class Universe:

@@ -385,12 +385,20 @@ struct Cluster {
   ResourceList allocatable, allocated, allocating;
   vector<AllocModel> modelings;
 };
+struct Component {
+  i32 replicas = 0;
+  bool has_rr = false;
+  ResourceList request;
+};
+// workv1alpha2.Component (binding_types.go:89-98): one pod template of a
+// multi-template workload (Replicas + ReplicaRequirements.ResourceRequest).
 struct Binding {
   string uid, api_version, kind, ns, name;
   i32 replicas = 0;
   bool has_rr = false, has_node_claim = false;
   ResourceList request;
   uint32_t n_components = 0;
+  vector<Component> comps;  // spec.Components (empty when the caller passed counts only)
   vector<TargetCluster> clusters;
   vector<string> eviction;
   bool has_rta = false, has_lst = false;
@@ -411,6 +419,7 @@ struct Binding {
 struct Options {
   bool empty_workload_propagation = false;
   bool models_gate = true;
+  bool multi_templates = false;  // MultiplePodTemplatesScheduling (features.go, alpha, default off)
   uint32_t plugins = KP_PLUGIN_ALL;
 };
 
@@ -491,6 +500,14 @@ Binding convBinding(const kp_binding& b) {
   o.has_node_claim = b.has_node_claim;
   if (!parseList(b.resource_request, b.n_resource_request, &o.request)) o.bad = true;
   o.n_components = b.n_components;
+  if (b.components)
+    for (uint32_t i = 0; i < b.n_components; i++) {
+      Component k;
+      k.replicas = b.components[i].replicas;
+      k.has_rr = b.components[i].has_replica_requirements != 0;
+      if (!parseList(b.components[i].resource_request, b.components[i].n_resource_request, &k.request)) o.bad = true;
+      o.comps.push_back(k);
+    }
   for (uint32_t i = 0; i < b.n_clusters; i++) o.clusters.push_back({S(b.clusters[i].name), b.clusters[i].replicas});
   for (uint32_t i = 0; i < b.n_eviction_from; i++) o.eviction.push_back(S(b.eviction_from[i]));
   o.has_rta = b.has_reschedule_triggered_at;
@@ -528,6 +545,7 @@ Options convOptions(const kp_options* o) {
   if (o) {
     r.empty_workload_propagation = o->enable_empty_workload_propagation;
     r.models_gate = o->customized_cluster_resource_modeling;
+    r.multi_templates = o->multiple_pod_templates_scheduling;
     r.plugins = o->enabled_plugins;
   }
   return r;
@@ -1101,11 +1119,6 @@ i32 maxAvailableReplicas(const Cluster& c, const Binding& b, const Options& o, i
 // GeneralEstimator.MaxAvailableComponentSets (general.go:154-292), assumed
 // workloads empty (SchedulingOvercommitProtection off).
 // ===========================================================================
-struct Component {
-  i32 replicas = 0;
-  bool has_rr = false;
-  ResourceList request;
-};
 
 // quantityAsInt64 (general.go:417-427): DecimalSI / DecimalExponent -> MilliValue,
 // BinarySI -> Value.
@@ -1292,6 +1305,16 @@ i32 maxAvailableComponentSets(const Cluster& c, const vector<Component>& comps, 
   return num < maxSets ? num : maxSets;
 }
 
+// isMultiTemplateSchedulingApplicable (core/estimation.go:43-65): components present and a
+// cluster spread constraint with MinGroups == MaxGroups == 1.
+bool multiTemplateApplicable(const Binding& b) {
+  if (b.n_components == 0) return false;
+  for (auto& sc : b.spreads)
+    if (sc.field == "cluster" && sc.min == 1 && sc.max == 1) return true;
+  return false;
+}
+bool useComponentSets(const Binding& b, const Options& o) { return o.multi_templates && multiTemplateApplicable(b); }
+
 // calAvailableReplicas (pkg/scheduler/core/util.go:57-110) with the general estimator only.
 vector<TargetCluster> calAvailableReplicas(const vector<const Cluster*>& clusters, const Binding& b, const Options& o,
                                            int mode) {
@@ -1301,8 +1324,13 @@ vector<TargetCluster> calAvailableReplicas(const vector<const Cluster*>& cluster
     out[i].replicas = INT32_MAX;
   }
   if (b.replicas == 0 && b.n_components == 0) return out;
+  // runReplicaEstimator (util.go:113-118): with the MultiplePodTemplatesScheduling gate
+  // and isMultiTemplateSchedulingApplicable, MaxAvailableComponentSets answers
+  // (calculateMultiTemplateAvailableSets, estimation.go:77-113; the general estimator
+  // answers every cluster, never UnauthenticReplica).
+  const bool sets = useComponentSets(b, o);
   for (size_t i = 0; i < clusters.size(); i++) {
-    i32 r = maxAvailableReplicas(*clusters[i], b, o, mode);
+    i32 r = sets ? maxAvailableComponentSets(*clusters[i], b.comps, o, mode) : maxAvailableReplicas(*clusters[i], b, o, mode);
     if (r != -1 && out[i].replicas > r) out[i].replicas = r;  // mergeReplicaResults (util.go:157-170)
   }
   for (auto& t : out)
@@ -1603,6 +1631,97 @@ struct WebsterPQ {
     up((int)P.size() - 1);
   }
 };
+// FAST mode only (g_webster_fast, set by kpo_schedule's workers for KPO_FAST): seats
+// the first S heap pops at once. The heap pops a strict total order of the elements
+// (party i, seat k) keyed by (v_i/(2k+1) desc, k asc, name), a party's elements in k
+// order, so for any t >= 0 the elements with priority > t are
+// exactly the first S pops when their count S <= newSeats; the heap then runs the
+// remaining newSeats - S pops from there. Elements with k >= 2^30 (2*Seats+1 wraps
+// in int32, webstermethod.go:60-61) are left to the heap. Only for fresh parties
+// (no initial seats) with non-negative votes; tests/test_oracle_synth.py checks it
+// against the literal loop.
+thread_local bool g_webster_fast = false;
+i32 websterPreseat(vector<Party>& P, i32 N, int tie_mode) {
+  if (N <= 64) return 0;
+  i64 V = 0;
+  int npos = 0, nzero = 0, ipos = -1;
+  for (size_t i = 0; i < P.size(); i++) {
+    if (P[i].seats != 0) return 0;
+    V += P[i].votes > 0 ? P[i].votes : 0;
+    if (P[i].votes > 0) npos++, ipos = (int)i;
+    nzero += P[i].votes == 0;
+  }
+  const i64 kCap = (i64)1 << 30;
+  auto ahead = [&](int a, int b) { return tie_mode == 2 ? P[a].name > P[b].name : P[a].name < P[b].name; };
+  if (npos <= 1 && (i64)N > (i64)npos * kCap) {
+    // Every positive party's first 2^30 elements have positive priority; after them
+    // its denominator 2*Seats+1 wraps negative in int32. The rest R goes, in heap
+    // order, to the zero-vote parties (priority 0; ties by seats then name: a round
+    // robin in name order), else to the positive party's wrapped seats while they
+    // stay above the best negative head v_j (a tie goes to fewer seats: j), then to
+    // j, whose priority only rises once it holds a seat.
+    if (ipos >= 0) P[ipos].seats = (i32)kCap;
+    i64 R = (i64)N - (i64)npos * kCap;
+    if (nzero) {
+      vector<int> z;
+      for (size_t i = 0; i < P.size(); i++)
+        if (P[i].votes == 0) z.push_back((int)i);
+      std::sort(z.begin(), z.end(), ahead);
+      for (size_t j = 0; j < z.size(); j++) P[z[j]].seats = (i32)(R / nzero + ((i64)j < R % nzero ? 1 : 0));
+      return N;
+    }
+    int jn = -1;
+    for (size_t j = 0; j < P.size(); j++)
+      if (P[j].votes < 0 && (jn < 0 || P[j].votes > P[jn].votes || (P[j].votes == P[jn].votes && ahead((int)j, jn))))
+        jn = (int)j;
+    if (ipos >= 0) {
+      i64 m = 0;  // wrapped seats k = 2^30 + m while WebsterPQ::prio stays above v_j (literal, one by one)
+      for (; m < R; m++) {
+        Party q = P[ipos];
+        q.seats = (i32)(kCap + m);
+        if (jn >= 0 && !(WebsterPQ::prio(q) > (double)P[jn].votes)) break;
+      }
+      P[ipos].seats = (i32)(kCap + m);
+      R -= m;
+    }
+    if (R > 0 && jn >= 0) P[jn].seats = (i32)R;
+    return N;
+  }
+  if (npos == 0) return 0;
+  auto count = [&](i64 v, double t) -> i64 {  // #{k < 2^30 : fl(v/(2k+1)) > t}
+    if (v <= 0 || !((double)v > t)) return 0;
+    double q = ((double)v / t - 1.0) / 2.0;
+    i64 k = q >= (double)(kCap - 1) ? kCap - 1 : (q < 0 ? 0 : (i64)q);
+    while (k > 0 && !((double)v / (double)(2 * k + 1) > t)) k--;
+    while (k + 1 < kCap && (double)v / (double)(2 * (k + 1) + 1) > t) k++;
+    return k + 1;
+  };
+  auto total = [&](double t) {
+    i64 S = 0;
+    for (auto& p : P) S += p.votes > 0 ? count(p.votes, t) : 0;
+    return S;
+  };
+  // t_hi: count <= N; t_lo: count > N (or 0); bisect so that the heap's share is
+  // about the tie group at the N-th priority
+  double hi = (double)V / (2.0 * (double)N), lo = 0;
+  for (int it = 0; it < 200 && total(hi) > (i64)N; it++) {
+    lo = hi;
+    hi *= 1.5;
+  }
+  if (total(hi) > (i64)N) return 0;
+  for (int it = 0; it < 64 && lo < hi && (i64)N - total(hi) > 4 * (i64)P.size() + 64; it++) {
+    const double mid = lo + (hi - lo) / 2;
+    if (mid <= lo || mid >= hi) break;
+    if (total(mid) <= (i64)N) hi = mid;
+    else lo = mid;
+  }
+  i64 S = 0;
+  for (auto& p : P) {
+    p.seats = p.votes > 0 ? (i32)count(p.votes, hi) : 0;
+    S += p.seats;
+  }
+  return (i32)S;
+}
 int tieModeForUID(const string& uid) {
   if (uid.empty()) return 1;
   return (fnv32a(uid) & 1) ? 2 : 1;
@@ -1622,8 +1741,9 @@ vector<Party> AllocateWebsterSeats(i32 newSeats, const vector<std::pair<string, 
   pq.tie_mode = tie_mode;
   for (auto& kv : parties) pq.P.push_back(kv.second);
   if (pq.P.empty()) return {};
+  i32 preseated = g_webster_fast ? websterPreseat(pq.P, newSeats, tie_mode) : 0;
   pq.init();
-  for (i32 remaining = newSeats; remaining > 0; remaining--) {
+  for (i32 remaining = newSeats - preseated; remaining > 0; remaining--) {
     Party p = pq.pop();
     p.seats = add32(p.seats, 1);
     pq.push(p);
@@ -2235,7 +2355,9 @@ ScheduleOut Schedule(const World& w, const Binding& b, int mode) {
   for (auto* c : feasible) scored.push_back({c, ScoreCluster(b, *c, w.opts)});
   // selectClusters -> SelectClusters (common.go:34-48)
   GroupInfoAll info = GroupClustersWithScore(scored, b, nullptr, w.opts, mode);
-  SelectResult sel = SelectBestClusters(b, info, b.replicas);
+  // SelectClusters (common.go:34-48): a multi-template workload is placed as one set,
+  // so it needs 1 available replica (:42-46)
+  SelectResult sel = SelectBestClusters(b, info, useComponentSets(b, w.opts) ? 1 : b.replicas);
   if (sel.err != KP_ERR_NONE) {
     out.status = KP_STATUS_ERROR;
     out.err = sel.err;
@@ -2392,7 +2514,10 @@ extern "C" {
 
 int kpo_schedule(kpo_world* k, const kp_binding* b, uint64_t n, int mode, int n_threads, kpo_results** outp) {
   vector<ScheduleOut> res(n);
-  ParallelFor(n, n_threads, [&](uint64_t i) { res[i] = Schedule(k->w, convBinding(b[i]), mode); });
+  ParallelFor(n, n_threads, [&](uint64_t i) {
+    g_webster_fast = mode == KPO_FAST;
+    res[i] = Schedule(k->w, convBinding(b[i]), mode);
+  });
   *outp = PackResults(res);
   return 0;
 }
@@ -2401,6 +2526,7 @@ int kpo_schedule_affinities(kpo_world* k, const kp_binding* b, uint64_t n, int m
                             kpo_results** outp, int32_t* affinity_index, int32_t* attempts) {
   vector<ScheduleOut> res(n);
   ParallelFor(n, n_threads, [&](uint64_t i) {
+    g_webster_fast = mode == KPO_FAST;
     res[i] = ScheduleWithAffinities(k->w, b[i], mode, &affinity_index[i], &attempts[i]);
   });
   *outp = PackResults(res);
@@ -2522,6 +2648,30 @@ int kpo_estimator_part(const kp_cluster* c, const kp_binding* b, const kp_option
   return -1;
 }
 
+void kpo_set_webster_fast(int on) { g_webster_fast = on != 0; }
+static vector<TargetCluster> convTargets(const kp_target_cluster* t, uint32_t n) {
+  vector<TargetCluster> v;
+  for (uint32_t i = 0; i < n; i++) v.push_back({S(t[i].name), t[i].replicas});
+  return v;
+}
+int32_t kpo_sum_replicas(const kp_target_cluster* t, uint32_t n) { return GetSumOfReplicas(convTargets(t, n)); }
+int kpo_merge_target_clusters(const kp_target_cluster* old_t, uint32_t n_old, const kp_target_cluster* new_t,
+                              uint32_t n_new, const kp_target_cluster* names, uint32_t n_names, int32_t* out_idx,
+                              int32_t* out_rep, uint32_t out_cap) {
+  auto r = MergeTargetClusters(convTargets(old_t, n_old), convTargets(new_t, n_new));
+  uint32_t k = 0;
+  for (auto& t : r) {
+    if (k >= out_cap) break;
+    int32_t idx = -1;
+    for (uint32_t j = 0; j < n_names; j++)
+      if (S(names[j].name) == t.name) idx = (int32_t)j;
+    out_idx[k] = idx;
+    out_rep[k] = t.replicas;
+    k++;
+  }
+  return (int)r.size();
+}
+int kpo_reschedule_required(const kp_binding* b) { return RescheduleRequired(convBinding(*b)) ? 1 : 0; }
 int kpo_allocate_webster(int32_t new_seats, const kp_str* vote_names, const int64_t* votes, uint32_t n_votes,
                          const kp_str* init_names, const int32_t* init_seats, uint32_t n_init, int tie_mode,
                          kp_str uid, int32_t* out_seats, uint32_t out_cap) {

@@ -103,6 +103,18 @@ int kpo_allocate_webster(int32_t new_seats, const kp_str* vote_names, const int6
                          uint32_t n_votes, const kp_str* init_names, const int32_t* init_seats,
                          uint32_t n_init, int tie_mode, kp_str uid, int32_t* out_seats,
                          uint32_t out_cap);
+/* The calling thread's AllocateWebsterSeats: 0 = the literal heap loop (default), 1 = the
+ * FAST form (threshold-preseated, then the heap; kpo_schedule's KPO_FAST workers use it). */
+void kpo_set_webster_fast(int on);
+/* util.GetSumOfReplicas (pkg/util/binding.go:72-78, int32 wrapping). */
+int32_t kpo_sum_replicas(const kp_target_cluster* t, uint32_t n);
+/* util.MergeTargetClusters (binding.go:91-115): result entries as indices into `names`
+ * (-1 if absent) + replicas; returns the result length. */
+int kpo_merge_target_clusters(const kp_target_cluster* old_t, uint32_t n_old, const kp_target_cluster* new_t,
+                              uint32_t n_new, const kp_target_cluster* names, uint32_t n_names, int32_t* out_idx,
+                              int32_t* out_rep, uint32_t out_cap);
+/* util.RescheduleRequired (binding.go:117-127) of the binding's two timestamps. */
+int kpo_reschedule_required(const kp_binding* b);
 /* helper.SpreadReplicasByTargetClusters / Dispenser.AllocateByWeight;
  * returns #targets written (name order), names as indices into `tcs`. */
 int kpo_spread_replicas(int32_t num, const kp_target_cluster* tcs, uint32_t n,

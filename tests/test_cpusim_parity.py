@@ -56,6 +56,7 @@ def compare(got, want, label):
     (1, 1, 10, 1000), (2, 2, 300, 400), (3, 3, 200, 300), (4, 4, 400, 500),
     (6, 6, 120, 1500), (6, 7, 40, 1500), (6, 8, 1, 200), (6, 9, 257, 600),
     (7, 17, 300, 400), (7, 18, 13, 300), (5, 5, 500, 600),
+    (8, 4, 64, 300), (8, 7, 24, 200),
 ])
 def test_cpusim_schedule_parity(engine, config, seed, n_clusters, n_bindings, rows):
     u = synth.Universe(config, seed, n_clusters, 0, n_bindings)
@@ -111,3 +112,17 @@ def test_cpusim_parallel_packing(engine):
     assert many == one
     ba, n = u.binding_slice(0, u.n_bindings)
     compare(many, O.schedule_c(u.clusters, u.n_clusters, ba, n, opts, O.FAST, 8), "parallel packing")
+
+
+@pytest.mark.parametrize("rows", [False, True], ids=["bits", "rows"])
+@pytest.mark.parametrize("config,seed,n_clusters,n_bindings,multi", [
+    (9, 1, 300, 600, True), (9, 2, 120, 300, False), (6, 3, 120, 1500, True),
+])
+def test_cpusim_multi_templates(engine, config, seed, n_clusters, n_bindings, multi, rows):
+    """MultiplePodTemplatesScheduling on: MaxAvailableComponentSets class rows
+    (k_sets_rows) and SelectBestClusters' one-set need (common.go:42-46)."""
+    u = synth.Universe(config, seed, n_clusters, 0, n_bindings)
+    opts = api.options(multi_templates=multi)
+    ba, n = u.binding_slice(0, n_bindings)
+    want = O.schedule_c(u.clusters, u.n_clusters, ba, n, opts, O.FAST, 8)
+    compare(run(engine, u, opts, rows=rows), want, f"multi {multi} config {config} seed {seed}")

@@ -72,9 +72,16 @@ CASES = [
     # overflow tiers with ~5k-entry serial lists in many concurrent k_slow workgroups
     # (the serial scratch sizing fix)
     (6, 13, 5000, 4000),
-    # C > ~8.6k: k_select_all's LDS leaves one workgroup per CU -> k_select_all_wide
+    # C > ~8.6k: gathered candidates would leave one workgroup per CU, so in the
+    # bitset mode the SEL_ALL bindings take k_select_all_stream (the pair-row test
+    # below runs the gathered k_select_all_wide at this size)
     (6, 21, 9000, 1000),
     (7, 22, 9000, 600),
+    # int32 wrap of replica sums, StaticWeight weights >= 2^31 and seat counts past
+    # 2^30 (SURVEY hazard H5): k_slow's serial route (SLOW_WRAP / SLOW_WEIGHT)
+    (8, 4, 64, 2000),
+    (8, 5, 16, 600),
+    (8, 6, 300, 1500),
     # BASELINE configs at the cluster counts they are quoted on (binding slices of
     # the bench universes: same seeds as bench.py)
     (3, 3, 5000, 2000),
@@ -93,6 +100,8 @@ def test_schedule_parity(engine, config, seed, n_clusters, n_bindings):
 
 @pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
     (3, 3, 500, 1000), (2, 2, 1000, 1000), (5, 5, 3000, 1200), (7, 17, 2000, 1000), (3, 3, 5000, 1000),
+    # C >= 9000: the gathered SEL_ALL kernel needs more than 80 KB of LDS -> k_select_all_wide
+    (6, 21, 9000, 600), (7, 22, 9000, 400), (3, 23, 10000, 300),
 ])
 def test_schedule_parity_pair_rows(engine, config, seed, n_clusters, n_bindings):
     """The per-binding pair-row route (KP_PAIR_ROWS=1: k_pair_fast_* writes every
@@ -109,6 +118,28 @@ def test_schedule_parity_pair_rows(engine, config, seed, n_clusters, n_bindings)
         os.environ.pop("KP_PAIR_ROWS", None)
     compare(got, oracle_schedule(u, opts), f"pair rows config {config} seed {seed}")
     assert bits == 0
+
+
+@pytest.mark.parametrize("rows", [False, True], ids=["bits", "rows"])
+@pytest.mark.parametrize("config,seed,n_clusters,n_bindings,multi", [
+    (9, 31, 2000, 2000, True), (9, 32, 500, 1500, False), (6, 33, 300, 2000, True), (9, 34, 5000, 800, True),
+])
+def test_schedule_parity_multi_templates(engine, config, seed, n_clusters, n_bindings, multi, rows):
+    """MultiplePodTemplatesScheduling: bindings that isMultiTemplateSchedulingApplicable
+    accepts take MaxAvailableComponentSets as their estimator row (k_sets_rows; core/
+    util.go:113-118, estimation.go:77-113) and need one replica in SelectBestClusters
+    (common.go:42-46); with the gate off the same bindings take the single-template
+    route."""
+    import os
+    u = synth.Universe(config, seed, n_clusters, 0, n_bindings)
+    opts = api.options(multi_templates=multi)
+    if rows:
+        os.environ["KP_PAIR_ROWS"] = "1"
+    try:
+        got = gpu_schedule(engine, u, opts)
+    finally:
+        os.environ.pop("KP_PAIR_ROWS", None)
+    compare(got, oracle_schedule(u, opts), f"multi-templates {multi} config {config} seed {seed}")
 
 
 @pytest.mark.parametrize("prop,plugins,gate", [

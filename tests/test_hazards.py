@@ -1,0 +1,210 @@
+"""Parity hazards of SURVEY.md §8 on the CPU: the int32 sums and seat counts of
+hazard H5, the pkg/util/binding_test.go tables (GetSumOfReplicas, MergeTargetClusters,
+RescheduleRequired), and a one-binding batch whose serial result list is checked
+against the batch's result pool (sink_serial). The engine side runs through
+libkp_cpusim.so (engine.cpp + the kernel bodies on the host); the GPU build of the
+same universes is checked in tests/test_gpu_parity.py."""
+import ctypes as C
+import json
+import os
+
+import pytest
+
+from karmada_amd import api
+from karmada_amd.engine import PKG, Batch, Snapshot
+import oracle_lib as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+SIM = C.CDLL(os.path.join(PKG, "libkp_cpusim.so"))
+SIM.kpsim_webster_serial.argtypes = [C.POINTER(C.c_int64), C.POINTER(C.c_uint32), C.c_int, C.c_int32, C.c_int,
+                                     C.POINTER(C.c_int32)]
+SIM.kpsim_merge_targets.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.c_int, C.POINTER(C.c_uint32),
+                                    C.POINTER(C.c_int32), C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_int32)]
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def olib():
+    L = O.lib()
+    L.kpo_set_webster_fast.argtypes = [C.c_int]
+    L.kpo_sum_replicas.restype = C.c_int32
+    L.kpo_sum_replicas.argtypes = [C.POINTER(api.kp_target_cluster), C.c_uint32]
+    L.kpo_merge_target_clusters.argtypes = [C.POINTER(api.kp_target_cluster), C.c_uint32,
+                                            C.POINTER(api.kp_target_cluster), C.c_uint32,
+                                            C.POINTER(api.kp_target_cluster), C.c_uint32, C.POINTER(C.c_int32),
+                                            C.POINTER(C.c_int32), C.c_uint32]
+    L.kpo_reschedule_required.argtypes = [C.POINTER(api.kp_binding)]
+    return L
+
+
+# ---- pkg/util/binding_test.go ---------------------------------------------------------
+def targets(w, ts):
+    a, n = w.arr(api.kp_target_cluster, [api.kp_target_cluster(w.s(t["name"]), t["replicas"]) for t in ts])
+    return a, n
+
+
+@pytest.mark.parametrize("case", load("util_binding.json")["sum"], ids=lambda c: c["name"])
+def test_get_sum_of_replicas(case):
+    w = api.World()
+    a, n = targets(w, case["clusters"])
+    assert olib().kpo_sum_replicas(a, n) == case["expected"]
+
+
+def test_get_sum_of_replicas_wraps():
+    """GetSumOfReplicas adds int32 (binding.go:72-78): 2^31-1 + 2 wraps to -2^31+1."""
+    w = api.World()
+    a, n = targets(w, [{"name": "a", "replicas": 2**31 - 1}, {"name": "b", "replicas": 2}])
+    assert olib().kpo_sum_replicas(a, n) == -2**31 + 1
+
+
+@pytest.mark.parametrize("case", load("util_binding.json")["merge"], ids=lambda c: c["name"])
+def test_merge_target_clusters(case):
+    names = sorted({t["name"] for t in case["old"] + case["new"] + case["expected"]})
+    want = sorted((names.index(t["name"]), t["replicas"]) for t in case["expected"])
+    # oracle
+    w = api.World()
+    oa, no = targets(w, case["old"])
+    na, nn = targets(w, case["new"])
+    ka, kn = targets(w, [{"name": x, "replicas": 0} for x in names])
+    cap = no + nn + 1
+    oi, orp = (C.c_int32 * cap)(), (C.c_int32 * cap)()
+    k = olib().kpo_merge_target_clusters(oa, no, na, nn, ka, kn, oi, orp, cap)
+    assert sorted((oi[i], orp[i]) for i in range(k)) == want
+    # engine (SerialAssign::merge, names as ranks)
+    on = (C.c_uint32 * cap)(*[names.index(t["name"]) for t in case["old"]])
+    orr = (C.c_int32 * cap)(*[t["replicas"] for t in case["old"]])
+    nw = (C.c_uint32 * cap)(*[names.index(t["name"]) for t in case["new"]])
+    nr = (C.c_int32 * cap)(*[t["replicas"] for t in case["new"]])
+    xn, xr = (C.c_uint32 * cap)(), (C.c_int32 * cap)()
+    k = SIM.kpsim_merge_targets(on, orr, len(case["old"]), nw, nr, len(case["new"]), xn, xr)
+    assert sorted((int(xn[i]), xr[i]) for i in range(k)) == want
+
+
+APPS = [{"groupVersion": "apps/v1", "resources": [{"kind": "Deployment"}]}]
+
+
+def reschedule_binding(w, rta, lst):
+    d = {"uid": "u", "replicas": 4, "replicaRequirements": {"resourceRequest": {"cpu": "1"}},
+         "clusters": [{"name": "member1", "replicas": 4}],
+         "placement": {"replicaScheduling": {"replicaSchedulingType": "Divided",
+                                             "replicaDivisionPreference": "Weighted",
+                                             "weightPreference": {"dynamicWeight": "AvailableReplicas"}}}}
+    if rta is not None:
+        d["rescheduleTriggeredAt"] = rta
+    if lst is not None:
+        d["lastScheduledTime"] = lst
+    return d
+
+
+@pytest.mark.parametrize("case", load("util_binding.json")["reschedule"], ids=lambda c: c["name"])
+def test_reschedule_required(case, cpusim_engine):
+    """The oracle hook against the table, and the engine's packer (BF_FRESH) through the
+    placement it causes: RescheduleRequired re-divides every replica (dynamicFreshScale),
+    otherwise the unchanged previous placement {member1: 4} stays."""
+    w = api.World()
+    d = reschedule_binding(w, case["rescheduleTriggeredAt"], case["lastScheduledTime"])
+    bs, n = w.bindings([d])
+    assert bool(olib().kpo_reschedule_required(bs)) == case["want"]
+    cl = [{"name": f"member{i}", "apiEnablements": APPS, "resourceSummary": {"allocatable": {"cpu": "8", "pods": "110"}}}
+          for i in (1, 2)]
+    ca, nc = w.clusters(cl)
+    opts = api.options()
+    snap = Snapshot.from_structs(cpusim_engine, ca, nc, [c["name"] for c in cl], opts)
+    b = Batch(snap, structs=(bs, n))
+    got = b.schedule()
+    b.close()
+    snap.close()
+    want = O.schedule_c(ca, nc, bs, n, opts, O.FAST, 1)
+    assert got == want
+    fresh_targets = [(0, 2), (1, 2)]
+    assert (got[0]["targets"] == fresh_targets) == case["want"]
+
+
+# ---- Webster past 2^30 seats and with zero / negative votes ----------------------------
+WRAP = load("webster_wrap.json")["cases"] if os.path.exists(os.path.join(GOLDEN, "webster_wrap.json")) else []
+
+
+@pytest.mark.parametrize("case", WRAP, ids=lambda c: "%s-%d" % (c["votes"], c["seats"]))
+def test_webster_wrap(case):
+    """AllocateWebsterSeats where int32 2*Seats+1 wraps or votes are <= 0, against the
+    oracle's literal heap loop (tests/golden/make_webster_wrap.py): the oracle's FAST
+    form and the engine's serial emulation (k_slow's webster_serial)."""
+    votes, N, tie = case["votes"], case["seats"], case["tie_mode"]
+    n = len(votes)
+    L = olib()
+    L.kpo_set_webster_fast(1)
+    try:
+        w = api.World()
+        names, _ = w.arr(api.kp_str, [w.s(x) for x in case["names"]])
+        out = (C.c_int32 * n)()
+        L.kpo_allocate_webster(N, names, (C.c_int64 * n)(*votes), n, None, None, 0, tie, api.kp_str(None, 0), out, n)
+        assert list(out) == case["want"]
+    finally:
+        L.kpo_set_webster_fast(0)
+    got = (C.c_int32 * n)()
+    SIM.kpsim_webster_serial((C.c_int64 * n)(*votes), (C.c_uint32 * n)(*range(n)), n, N, 1 if tie == 2 else 0, got)
+    assert list(got) == case["want"]
+
+
+def test_webster_serial_matches_literal_small():
+    """webster_serial (threshold + heap) against the oracle's literal heap on seeded
+    vote lists of every sign mix at small seat counts."""
+    import random
+    rng = random.Random(5)
+    L = olib()
+    for _ in range(300):
+        n = rng.choice([1, 2, 3, 5, 9, 40])
+        votes = [rng.choice([0, 0, -3, 1, 7, rng.randint(-50, 1000), rng.randint(1, 2**31 - 1)]) for _ in range(n)]
+        N = rng.choice([1, 2, 10, 65, 500, 3000])
+        tie = rng.choice([1, 2])
+        w = api.World()
+        names, _ = w.arr(api.kp_str, [w.s("m%03d" % i) for i in range(n)])
+        want = (C.c_int32 * n)()
+        L.kpo_allocate_webster(N, names, (C.c_int64 * n)(*votes), n, None, None, 0, tie, api.kp_str(None, 0), want, n)
+        if sum(votes) == 0:
+            continue  # Dispenser returns before Webster (binding.go:98-101)
+        got = (C.c_int32 * n)()
+        SIM.kpsim_webster_serial((C.c_int64 * n)(*votes), (C.c_uint32 * n)(*range(n)), n, N, 1 if tie == 2 else 0,
+                                 got)
+        assert list(got) == list(want), (votes, N, tie)
+
+
+# ---- sink_serial: one binding, overflow tiers + spec.Clusters -------------------------
+def test_single_binding_overflow_tiers_result_pool(cpusim_engine):
+    """A one-binding batch whose AssignReplicas runs the overflow tiers over spec.Clusters
+    entries spread across the tiers (common.go:97-139): the serial result must fit the
+    batch's result pool (out_cap, kp_select.h sink_serial) and match the oracle."""
+    w = api.World()
+    cl = [{"name": f"m{i}", "labels": {"tier": str(i % 3)}, "apiEnablements": APPS,
+           "resourceSummary": {"allocatable": {"cpu": str(2 + i), "pods": "110"}}} for i in range(9)]
+    ca, nc = w.clusters(cl)
+
+    def aff(v):
+        return {"labelSelector": {"matchLabels": {"tier": v}}}
+    bindings = []
+    for rep in (1, 3, 7, 30, 200):
+        for strat in ("Aggregated", "Weighted"):
+            rs = {"replicaSchedulingType": "Divided", "replicaDivisionPreference": strat}
+            if strat == "Weighted":
+                rs["weightPreference"] = {"dynamicWeight": "AvailableReplicas"}
+            bindings.append({
+                "uid": "odd-%d" % rep, "replicas": rep, "replicaRequirements": {"resourceRequest": {"cpu": "1"}},
+                "clusters": [{"name": "m%d" % i, "replicas": 1 + i % 2} for i in (0, 1, 2, 4, 5, 7, 8)],
+                "schedulerObservedAffinityName": "t",
+                "placement": {"clusterAffinities": [dict(aff("0"), affinityName="t",
+                                                         overflowAffinities=[aff("1"), aff("2")])],
+                              "replicaScheduling": rs}})
+    opts = api.options()
+    snap = Snapshot.from_structs(cpusim_engine, ca, nc, [c["name"] for c in cl], opts)
+    for d in bindings:
+        bs, n = w.bindings([d])
+        b = Batch(snap, structs=(bs, n))
+        got = b.schedule()
+        b.close()
+        want = O.schedule_c(ca, nc, bs, n, opts, O.FAST, 1)
+        assert got[0]["err"] != 14, got  # KP_ERR_RESULT_CAPACITY
+        assert got == want, (d["replicas"], got, want)
+    snap.close()
