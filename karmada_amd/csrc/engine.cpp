@@ -2236,10 +2236,9 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     // Candidates gathered into LDS (k_select_all), or, in bits mode, streamed from
     // the feasibility and class rows (k_select_all_stream): for the StaticWeight
     // bindings (votes from per-rule bitsets), and for all when the gathered
-    // candidates would leave one workgroup per CU (C ~ 8.6k+). KP_SEL_GATHER=1 /
-    // KP_SEL_STREAM=1 force one kernel for all.
-    const bool stream_all = bits && (getenv("KP_SEL_STREAM") || smem_all(s) > 80 * 1024) && !getenv("KP_SEL_GATHER");
-    const bool stream_w = bits && !getenv("KP_SEL_GATHER");
+    // candidates would leave one workgroup per CU (C ~ 8.6k+).
+    const bool stream_all = bits && smem_all(s) > 80 * 1024;
+    const bool stream_w = bits;
     const int na = stream_all ? 0 : (stream_w ? bt->n_all_dyn : k.n);
     if (na > 0) {
       KArgs g = k;

@@ -48,28 +48,47 @@ def main():
     for r in rows:
         out["reschedule"].append({"name": cv.ev(r.get("name")), "rescheduleTriggeredAt": t(r.get("rescheduleTriggeredAt")),
                                   "lastScheduledTime": t(r.get("lastScheduledTime")), "want": cv.ev(r.get("want"))})
-    # runtime.Registry (pkg/scheduler/framework/runtime/registry_test.go)
+    # runtime.Registry (pkg/scheduler/framework/runtime/registry_test.go): its rows hold
+    # only names and string lists, read field by field (the Registry-typed field `r`
+    # is the table's fixed registry of `plugins`)
+    import re
     rpath = "pkg/scheduler/framework/runtime/registry_test.go"
     with open(os.path.join(REF, rpath), encoding="utf-8") as f:
         rsrc = f.read()
-    import re
-    m = re.search(r"plugins := \[\]string\{([^}]*)\}", rsrc)
-    registered = [x.strip().strip('"') for x in m.group(1).split(",")]
+    registered = re.findall(r'"([^"]*)"', re.search(r"plugins := \[\]string\{([^}]*)\}", rsrc).group(1))
+
+    def rows_of(func):
+        body_start = rsrc.index("func %s(" % func)
+        body = rsrc[body_start:rsrc.index("\nfunc ", body_start + 1)]
+        line = rsrc[:body_start].count("\n") + 1
+        out_rows = []
+        for blk in re.split(r"\n\t\t\{\n", body)[1:]:
+            row = {}
+            for k, v in re.findall(r"(\w+):\s+(\[\]string\{[^}]*\}|nil|\"[^\"]*\"|true|false|r),", blk):
+                if v.startswith("[]string"):
+                    row[k] = re.findall(r'"([^"]*)"', v)
+                elif v == "nil":
+                    row[k] = []
+                elif v in ("true", "false"):
+                    row[k] = v == "true"
+                elif v.startswith('"'):
+                    row[k] = v[1:-1]
+            if "name" in row:
+                out_rows.append(row)
+        return out_rows, line
     reg = {"source": [], "filter": [], "register": [], "unregister": []}
-    rows, line = table(rsrc, "TestRegistry_Filter")
+    rows, line = rows_of("TestRegistry_Filter")
     reg["source"].append("%s:%d (TestRegistry_Filter)" % (rpath, line))
     for r in rows:
-        reg["filter"].append({"name": cv.ev(r.get("name")), "registered": registered,
-                              "curPlugins": cv.strs(r.get("curPlugins")),
-                              "expectedPlugins": cv.strs(r.get("expectedPlugins"))})
+        reg["filter"].append({"name": r["name"], "registered": registered, "curPlugins": r["curPlugins"],
+                              "expectedPlugins": r["expectedPlugins"]})
     for fn, key, arg in (("TestRegistry_Register", "register", "registeringPlugin"),
                          ("TestRegistry_Unregister", "unregister", "removingPlugin")):
-        rows, line = table(rsrc, fn)
+        rows, line = rows_of(fn)
         reg["source"].append("%s:%d (%s)" % (rpath, line, fn))
         for r in rows:
-            reg[key].append({"name": cv.ev(r.get("name")), "initialPlugins": cv.strs(r.get("initialPlugins")),
-                             "plugin": cv.ev(r.get(arg)), "wantErr": cv.ev(r.get("wantErr")),
-                             "expectedPlugins": cv.strs(r.get("expectedPlugins"))})
+            reg[key].append({"name": r["name"], "initialPlugins": r.get("initialPlugins", []), "plugin": r[arg],
+                             "wantErr": r["wantErr"], "expectedPlugins": r["expectedPlugins"]})
     out["registry"] = reg
     with open(os.path.join(OUT, "util_binding.json"), "w") as f:
         json.dump(out, f, indent=1)

@@ -126,3 +126,18 @@ def test_cpusim_multi_templates(engine, config, seed, n_clusters, n_bindings, mu
     ba, n = u.binding_slice(0, n_bindings)
     want = O.schedule_c(u.clusters, u.n_clusters, ba, n, opts, O.FAST, 8)
     compare(run(engine, u, opts, rows=rows), want, f"multi {multi} config {config} seed {seed}")
+
+
+def test_cpusim_region_host_dfs(engine):
+    """selectGroups on the host (KP_REGION_HOST=1: the route of snapshots with more
+    regions than the device DFS arrays, and of bindings past its node budget) gives
+    the device DFS's results: config 4's region spread against the oracle."""
+    u = synth.Universe(4, 44, 400, 0, 400)
+    opts = api.options()
+    want = O.schedule_c(u.clusters, u.n_clusters, u.bindings, u.n_bindings, opts, O.FAST, 8)
+    os.environ["KP_REGION_HOST"] = "1"
+    try:
+        got = run(engine, u, opts)
+    finally:
+        os.environ.pop("KP_REGION_HOST", None)
+    compare(got, want, "region host DFS")
