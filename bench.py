@@ -472,6 +472,9 @@ def main():
         "scheduled_ok": n_ok,
         "result_targets": n_targets,
         "slow_path_bindings": int(last["n_slow"]),
+        # SEL_ALL DynamicWeight/Aggregated bindings scheduled over their deciding candidates
+        # (k_select_top) and the ones it handed to the full-candidate kernel
+        "select_top": {"bindings": int(last["n_top"]), "fallback": int(last["n_top_fallback"])},
         # bindings of the timed batch (sampled over all ranks) re-checked against the oracle
         "parity_checked": n_chk,
         "parity_lanes": n_lanes_chk,  # result lists checked per rank: the serial run + each in-flight lane

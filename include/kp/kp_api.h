@@ -359,6 +359,8 @@ typedef struct kp_stage_times {
   float sel_all_kernel_ms; /* the two-kernel path's SEL_ALL select kernel alone (HIP events) */
   uint32_t n_sel_all;      /* bindings of the SEL_ALL select kernel (SelectBestClusters selects all) */
   uint32_t n_classes;      /* estimator-class rows computed (bits == 1; row 0 = non-workload) */
+  uint32_t n_top;          /* SEL_ALL bindings given to k_select_top (deciding-candidate subsets) */
+  uint32_t n_top_fallback; /* of those, the ones it handed to the full-candidate kernel */
 } kp_stage_times;
 
 /* ------------------------------------------------------------------------- */

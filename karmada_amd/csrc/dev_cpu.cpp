@@ -15,6 +15,7 @@
 #include "kp_dev.h"
 #include "kp_sets.h"
 #include "kp_kernels.h"
+#include "kp_top.h"
 
 namespace kp {
 namespace dev {
@@ -131,14 +132,16 @@ int filter(stream_t, const SnapView& s, const BatchView& bv, uint64_t* fmask) {
 int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x) {
   switch (which) {
     case SEL_LAUNCH_ALL: {
+      const int n = a.n_dev ? (int)*a.n_dev : a.n;
       const size_t need = kRedBytes + 4 * (size_t)((((a.s.Cp + 31) >> 5) + 3) & ~3) + 8 * (size_t)a.s.Cp + 3072 +
                           8 * (size_t)sel_all_ecap(a.s.Cp) + 64;
-      grid(a.n, need > smem ? need : smem,
+      grid(n, need > smem ? need : smem,
            [&](int blk, unsigned char* sm) { body_select_all(CpuBlk{(int64_t*)sm}, blk, sm, a); });
       break;
     }
     case SEL_LAUNCH_ALL_STREAM:
-      grid(a.n, smem, [&](int blk, unsigned char* sm) { body_select_all_stream(CpuBlk{(int64_t*)sm}, blk, sm, a); });
+      grid(a.n_dev ? (int)*a.n_dev : a.n, smem,
+           [&](int blk, unsigned char* sm) { body_select_all_stream(CpuBlk{(int64_t*)sm}, blk, sm, a); });
       break;
     case SEL_LAUNCH_CLUSTER:
       grid(a.n, smem,
@@ -161,6 +164,21 @@ int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const Sele
     default:
       return -1;
   }
+  return 0;
+}
+
+int class_order(stream_t, const SnapView& s, const int32_t* rows, int n_rows, uint64_t* ord, int64_t* tot,
+                int32_t* ok) {
+  int P = 1;
+  while (P < s.C) P <<= 1;
+  grid(n_rows, 8 * (size_t)P, [&](int k, unsigned char* sm) {
+    body_class_order(CpuBlk{(int64_t*)sm}, k, (uint64_t*)(sm + kRedBytes), P, s, rows, ord, tot, ok);
+  });
+  return 0;
+}
+
+int select_top(stream_t, const KArgs& a, const TopArgs& t, size_t slice) {
+  grid(a.n, slice, [&](int blk, unsigned char* sm) { body_select_top(CpuBlk{(int64_t*)sm}, blk, sm, a, t); });
   return 0;
 }
 

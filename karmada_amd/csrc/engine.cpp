@@ -27,6 +27,7 @@
 #include "kp_pdq.h"
 #include "kp_sets.h"
 #include "kp_nodes.h"
+#include "kp_top.h"
 
 using namespace kp;
 
@@ -125,6 +126,10 @@ struct kp_engine {
   } aff;
   int n_threads = 8;
   size_t max_lds = 65536;
+  // k_select_top (kp_top.h): on, and its subset capacity per binding (LDS entries);
+  // KP_TOP=0 / KP_TOP_CAP=<n> at engine creation (tests, tuning)
+  bool top_on = true;
+  int top_cap = 512;
 };
 
 struct kp_snapshot {
@@ -175,6 +180,10 @@ struct kp_batch {
   // component-set classes (BF_SETS): class id and resolved component list of each;
   // their rows are MaxAvailableComponentSets per cluster (k_sets_rows), and in the
   // pair-row mode the BF_SETS bindings' rows are rebuilt from them (k_rows_from_class)
+  // k_select_top: per-class candidate orders, row sums and walkability; its fallback list
+  uint64_t* d_ord = nullptr;
+  int64_t* d_ctot = nullptr;
+  int32_t *d_cok = nullptr, *d_fb = nullptr;
   std::vector<int32_t> sets_cls, l_sets;
   std::vector<SetsArgs> sets_args;
   SetsArgs* d_sets_args = nullptr;
@@ -1518,6 +1527,8 @@ int kp_engine_create(int device, kp_engine** out) {
   }
   for (auto& ev : e->ev) (void)dev::event_create(&ev);
   e->max_lds = dev::max_lds_per_block(device);
+  if (const char* v = getenv("KP_TOP")) e->top_on = atoi(v) != 0;
+  if (const char* v = getenv("KP_TOP_CAP")) e->top_cap = std::max(64, std::min(1024, atoi(v) & ~63));
   unsigned hc = std::thread::hardware_concurrency();
   e->n_threads = (int)std::max(1u, std::min(16u, hc));
   *out = e;
@@ -2060,6 +2071,12 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->rnsel, std::max(1, nr));
   a.add(&bt->nhost, 1);
   a.add(&bt->slow_scratch, bt->slow_slot * bt->slow_grid);
+  if (s->C <= 16384 && !bt->crep.empty()) {  // k_select_top (bits mode): class orders, fallback list
+    a.add(&bt->d_ord, bt->crep.size() * (size_t)s->Cp);
+    a.add(&bt->d_ctot, bt->crep.size());
+    a.add(&bt->d_cok, bt->crep.size());
+    a.add(&bt->d_fb, std::max(1, bt->n_all_dyn));
+  }
   // component-set classes: per cluster rank its node-run scratch (one run per model
   // node at most, capped at kSetsRunsMax) for k_sets_rows, reused class after class
   std::vector<int64_t> sets_off;
@@ -2222,6 +2239,11 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   if (!bits && !bt->l_sets.empty())
     HIPCHK(dev::rows_from_class(sp, s->view, bt->view, bt->d_sets_list, (int)bt->l_sets.size(), bt->d_bcls,
                                 bt->cls_rows, bt->fmask, bt->est));
+  // SEL_ALL DynamicWeight / Aggregated over the deciding candidates (kp_top.h): the
+  // class rows' orders first
+  const bool top = bits && e->top_on && bt->d_ord != nullptr && bt->n_all_dyn > 0;
+  if (top)
+    HIPCHK(dev::class_order(sp, s->view, bt->cls_rows, (int)bt->crep.size(), bt->d_ord, bt->d_ctot, bt->d_cok));
   HIPCHK(dev::event_record(e->ev[4], sp));
   HIPCHK(dev::stream_wait(st, e->ev[4]));  // every pair row precedes the rest
   HIPCHK(dev::event_record(e->ev[1], st));
@@ -2240,12 +2262,31 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     const bool stream_all = bits && smem_all(s) > 80 * 1024;
     const bool stream_w = bits;
     const int na = stream_all ? 0 : (stream_w ? bt->n_all_dyn : k.n);
-    if (na > 0) {
+    if (top) {
+      // k_select_top over [0, n_all_dyn); the bindings it hands back (other strategies,
+      // subsets past capacity, ...) run with every candidate from its fallback list
+      KArgs g = k;
+      g.n = bt->n_all_dyn;
+      TopArgs ta{bt->d_ord, bt->d_ctot, bt->d_cok, bt->d_fb, bt->stats + 9, e->top_cap};
+      const size_t slice = (top_lds_bytes(s->Cp, e->top_cap) + 15) & ~(size_t)15;
+      HIPCHK(dev::select_top(sp, g, ta, slice));
+      KArgs f = k;
+      f.list = bt->d_fb;
+      f.n = bt->n_all_dyn;
+      f.n_dev = bt->stats + 9;
+      if (stream_all) HIPCHK(dev::select(sp, SEL_LAUNCH_ALL_STREAM, f, sel_stream_lds_bytes(s->Cp), cap, sx));
+      else HIPCHK(dev::select(sp, SEL_LAUNCH_ALL, f, smem_all(s), cap, sx));
+    } else if (na > 0) {
       KArgs g = k;
       g.n = na;
       HIPCHK(dev::select(sp, SEL_LAUNCH_ALL, g, smem_all(s), cap, sx));
     }
-    if (k.n - na > 0) {
+    if (top && k.n - bt->n_all_dyn > 0) {
+      KArgs g = k;
+      g.list = bt->d_all + bt->n_all_dyn;
+      g.n = k.n - bt->n_all_dyn;
+      HIPCHK(dev::select(sp, SEL_LAUNCH_ALL_STREAM, g, sel_stream_lds_bytes(s->Cp), cap, sx));
+    } else if (!top && k.n - na > 0) {
       KArgs g = k;
       g.list = bt->d_all + na;
       g.n = k.n - na;
@@ -2393,6 +2434,8 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   tm.bits = bits ? 1u : 0u;
   tm.n_classes = bits ? (uint32_t)bt->crep.size() : 0u;
   tm.n_slow = bt->h_stats[0];
+  tm.n_top = top ? (uint32_t)bt->n_all_dyn : 0u;
+  tm.n_top_fallback = top ? bt->h_stats[9] : 0u;
 #ifdef KP_STAMPS
   {
     unsigned long long h[32];

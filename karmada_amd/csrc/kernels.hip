@@ -17,6 +17,7 @@
 #include "kp_dev.h"
 #include "kp_kernels.h"
 #include "kp_sets.h"
+#include "kp_top.h"
 
 using namespace kp;
 
@@ -73,9 +74,34 @@ extern "C" __global__ void __launch_bounds__(64 * kFilterWaves) k_filter(SnapVie
   if (b >= bv.B) return;  // wave-uniform
   body_filter(GpuBlk{nullptr}, b, s, bv, fmask);
 }
+// A launch over a device-appended list (a.n_dev) runs a grid-stride loop; otherwise
+// one workgroup per list entry (one iteration).
+#define KP_LIST_LOOP(BODY)                                                       \
+  const int n_ = a.n_dev ? (int)*a.n_dev : a.n;                                  \
+  for (int blk = (int)blockIdx.x; blk < n_; blk += (int)gridDim.x) {             \
+    BODY;                                                                        \
+    __syncthreads();                                                             \
+  }
 extern "C" __global__ void __launch_bounds__(KP_SEL_MAX_THREADS, KP_SEL_MIN_WAVES) k_select_all(KArgs a) {
   KP_SMEM;
-  body_select_all(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a);
+  KP_LIST_LOOP(body_select_all(GpuBlk{(int64_t*)smem}, blk, smem, a))
+}
+// SEL_ALL DynamicWeight / Aggregated over the candidates that can matter (kp_top.h):
+// kTopWaves independent waves per workgroup, one binding each, no workgroup barrier.
+constexpr int kTopWaves = 2;  // small workgroups: LDS is granted per workgroup
+extern "C" __global__ void __launch_bounds__(64 * kTopWaves) k_select_top(KArgs a, TopArgs t, int slice) {
+  KP_SMEM;
+  const int w = (int)(threadIdx.x >> 6);
+  unsigned char* mine = smem + (size_t)w * (size_t)slice;
+  const int blk = (int)blockIdx.x * kTopWaves + w;
+  if (blk >= a.n) return;  // wave-uniform: the waves never synchronise with each other
+  body_select_top(WaveBlk{(int64_t*)mine}, blk, mine, a, t);
+}
+// Each estimator class's row in (estimate desc, rank asc) order: LDS bitonic sort.
+extern "C" __global__ void __launch_bounds__(1024) k_class_order(SnapView s, const int32_t* rows, int P, uint64_t* ord,
+                                                                int64_t* tot, int32_t* ok) {
+  KP_SMEM;
+  body_class_order(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, (uint64_t*)(smem + kRedBytes), P, s, rows, ord, tot, ok);
 }
 // SEL_ALL over streamed candidates: ~15 KB LDS at C = 5k, so LDS no longer bounds
 // the workgroups per CU; KP_STREAM_MIN_WAVES waves per SIMD bounds the VGPRs.
@@ -87,13 +113,13 @@ extern "C" __global__ void __launch_bounds__(KP_SEL_MAX_THREADS, KP_SEL_MIN_WAVE
 #endif
 extern "C" __global__ void __launch_bounds__(KP_STREAM_THREADS, KP_STREAM_MIN_WAVES) k_select_all_stream(KArgs a) {
   KP_SMEM;
-  body_select_all_stream(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a);
+  KP_LIST_LOOP(body_select_all_stream(GpuBlk{(int64_t*)smem}, blk, smem, a))
 }
 // Large snapshots (C ~ 10k): the candidate arrays alone take 8 B per cluster, so a
 // single workgroup fits a CU; 1024 threads then keep 16 waves in flight instead of 8.
 extern "C" __global__ void __launch_bounds__(1024) k_select_all_wide(KArgs a) {
   KP_SMEM;
-  body_select_all(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a);
+  KP_LIST_LOOP(body_select_all(GpuBlk{(int64_t*)smem}, blk, smem, a))
 }
 // Spread-constraint selection kernels: workgroup size (their LDS, ~8 B per cluster
 // of gathered candidates, bounds the workgroups per CU; wider ones hide latency).
@@ -296,14 +322,18 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
   if (a.n <= 0) return 0;
   hipStream_t h = (hipStream_t)st;
   switch (which) {
-    case SEL_LAUNCH_ALL:
-      if ((smem > kLdsPerCu / 2 && !getenv("KP_SEL_THREADS")) || getenv("KP_SEL_WIDE"))  // one workgroup per CU: go wide
-        hipLaunchKernelGGL(k_select_all_wide, dim3(a.n), dim3(1024), smem, h, a);
+    case SEL_LAUNCH_ALL: {
+      // a device-appended list: a persistent grid of a few workgroups per CU
+      const int g = a.n_dev ? std::min(a.n, 256 * 4) : a.n;
+      if (smem > kLdsPerCu / 2 && !getenv("KP_SEL_THREADS"))  // one workgroup per CU: go wide
+        hipLaunchKernelGGL(k_select_all_wide, dim3(g), dim3(1024), smem, h, a);
       else
-        hipLaunchKernelGGL(k_select_all, dim3(a.n), dim3(sel_threads()), smem, h, a);
+        hipLaunchKernelGGL(k_select_all, dim3(g), dim3(sel_threads()), smem, h, a);
       break;
+    }
     case SEL_LAUNCH_ALL_STREAM:
-      hipLaunchKernelGGL(k_select_all_stream, dim3(a.n), dim3(KP_STREAM_THREADS), smem, h, a);
+      hipLaunchKernelGGL(k_select_all_stream, dim3(a.n_dev ? std::min(a.n, 256 * 8) : a.n), dim3(KP_STREAM_THREADS),
+                         smem, h, a);
       break;
     case SEL_LAUNCH_CLUSTER:
       if (smem > kLdsPerCu / 2)
@@ -333,6 +363,30 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
     default:
       return chk(hipErrorInvalidValue);
   }
+  return chk(hipGetLastError());
+}
+
+int class_order(stream_t st, const SnapView& s, const int32_t* rows, int n_rows, uint64_t* ord, int64_t* tot,
+                int32_t* ok) {
+  if (n_rows <= 0 || s.C <= 0) return 0;
+  int P = 1;
+  while (P < s.C) P <<= 1;
+  const size_t smem = kRedBytes + 8 * (size_t)P;
+  if (smem > 65536 &&
+      chk(hipFuncSetAttribute((const void*)k_class_order, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)))
+    return -1;
+  hipLaunchKernelGGL(k_class_order, dim3(n_rows), dim3(1024), smem, (hipStream_t)st, s, rows, P, ord, tot, ok);
+  return chk(hipGetLastError());
+}
+
+int select_top(stream_t st, const KArgs& a, const TopArgs& t, size_t slice) {
+  if (a.n <= 0) return 0;
+  const size_t smem = slice * kTopWaves;
+  if (smem > 65536 &&
+      chk(hipFuncSetAttribute((const void*)k_select_top, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)))
+    return -1;
+  hipLaunchKernelGGL(k_select_top, dim3((a.n + kTopWaves - 1) / kTopWaves), dim3(64 * kTopWaves), smem,
+                     (hipStream_t)st, a, t, (int)slice);
   return chk(hipGetLastError());
 }
 

@@ -283,6 +283,157 @@ struct GpuBlk {
     return (T)a[0];
   }
 };
+
+// Block policy of ONE wave64 working alone (several such "blocks" share a
+// workgroup, each on its own binding and LDS slice): every reduction and scan is
+// DPP + readlane, and a sync is the wave's own barrier plus a fence, so no
+// workgroup barrier ever stalls the other waves. Same interface as GpuBlk.
+struct WaveBlk {
+  int64_t* red;  // >= 2 int64 of this wave's LDS (find_bin / bcast)
+  KP_INLINE int tid() const { return (int)(threadIdx.x & 63); }
+  KP_INLINE int nth() const { return 64; }
+  KP_INLINE int lane() const { return tid(); }
+  KP_INLINE int wid() const { return 0; }
+  KP_INLINE int nwaves() const { return 1; }
+  KP_INLINE void sync() const {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  template <class T, class Op>
+  KP_INLINE T wave_reduce(T v, Op op, T id) const {
+    v = op(v, kp_dpp<0xB1>(id, v));
+    v = op(v, kp_dpp<0x4E>(id, v));
+    v = op(v, kp_dpp<0x141>(id, v));
+    v = op(v, kp_dpp<0x140>(id, v));
+    return op(op(kp_readlane(v, 0), kp_readlane(v, 16)), op(kp_readlane(v, 32), kp_readlane(v, 48)));
+  }
+  template <class T>
+  KP_INLINE T wave_incl_scan(T x) const {
+    x += kp_dpp<0x111, 0xF, true>((T)0, x);
+    x += kp_dpp<0x112, 0xF, true>((T)0, x);
+    x += kp_dpp<0x114, 0xF, true>((T)0, x);
+    x += kp_dpp<0x118, 0xF, true>((T)0, x);
+    x += kp_dpp<0x142, 0xA>((T)0, x);
+    x += kp_dpp<0x143, 0xC>((T)0, x);
+    return x;
+  }
+  // The reductions also order the wave's earlier LDS writes before what follows,
+  // as GpuBlk's barrier does.
+  template <class T, class Op>
+  KP_INLINE T reduce(T v, Op op, T id) const {
+    sync();
+    return wave_reduce(v, op, id);
+  }
+  template <class OpA, class OpB>
+  KP_INLINE void reduce2(int64_t& x, OpA opa, int64_t ida, int64_t& y, OpB opb, int64_t idb) const {
+    sync();
+    x = wave_reduce(x, opa, ida);
+    y = wave_reduce(y, opb, idb);
+  }
+  template <class OpA, class OpB, class OpC, class OpD>
+  KP_INLINE void reduce4(int64_t& x, OpA opa, int64_t ida, int64_t& y, OpB opb, int64_t idb, int64_t& z, OpC opc,
+                         int64_t idc, int64_t& u, OpD opd, int64_t idd) const {
+    sync();
+    x = wave_reduce(x, opa, ida);
+    y = wave_reduce(y, opb, idb);
+    z = wave_reduce(z, opc, idc);
+    u = wave_reduce(u, opd, idd);
+  }
+  KP_INLINE int32_t wave_reserve(int32_t mine, uint32_t* ctr) const {
+    const int32_t incl = wave_incl_scan(mine);
+    const int32_t tot = kp_readlane(incl, 63);
+    int32_t base = 0;
+    if (lane() == 63 && tot > 0) base = (int32_t)atomicAdd(ctr, (uint32_t)tot);
+    base = kp_readlane(base, 63);
+    return base + incl - mine;
+  }
+  KP_INLINE int64_t sum64(int64_t v) const { return reduce(v, [](int64_t a, int64_t b) { return a + b; }, (int64_t)0); }
+  KP_INLINE uint64_t minu64(uint64_t v) const {
+    return reduce(v, [](uint64_t a, uint64_t b) { return a < b ? a : b; }, (uint64_t)~0ull);
+  }
+  KP_INLINE int64_t max64(int64_t v) const {
+    return reduce(v, [](int64_t a, int64_t b) { return a > b ? a : b; }, (int64_t)INT64_MIN);
+  }
+  KP_INLINE int64_t min64(int64_t v) const {
+    return reduce(v, [](int64_t a, int64_t b) { return a < b ? a : b; }, (int64_t)INT64_MAX);
+  }
+  KP_INLINE void sum2(int64_t& x, int64_t& y) const {
+    auto add = [](int64_t a, int64_t b) { return a + b; };
+    reduce2(x, add, 0, y, add, 0);
+  }
+  KP_INLINE void maxsum(int64_t& mx, int64_t& sm) const {
+    reduce2(mx, [](int64_t a, int64_t b) { return a > b ? a : b; }, INT64_MIN, sm,
+            [](int64_t a, int64_t b) { return a + b; }, 0);
+  }
+  KP_INLINE bool any(bool p) const {
+    sync();
+    return __ballot(p) != 0;
+  }
+  KP_INLINE int32_t excl_scan(int32_t v, int32_t* total) const {
+    sync();
+    const int32_t x = wave_incl_scan(v);
+    *total = kp_readlane(x, 63);
+    return x - v;
+  }
+  template <class T>
+  KP_INLINE int find_bin(const T* hist, int64_t k, int64_t* before, bool rev) const {
+    sync();
+    const int l = lane();
+    int64_t v[4], s = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int idx = rev ? 255 - (4 * l + q) : 4 * l + q;
+      v[q] = (int64_t)hist[idx];
+      s += v[q];
+    }
+    const int64_t incl = wave_incl_scan(s);
+    const uint64_t m = __ballot(incl >= k);
+    const int first = m ? (int)__builtin_ctzll(m) : 63;
+    int64_t c = incl - s;
+    int q = 0;
+    for (; q < 3; q++) {
+      if (c + v[q] >= k) break;
+      c += v[q];
+    }
+    *before = kp_readlane(c, first);
+    const int bin = rev ? 255 - (4 * l + q) : 4 * l + q;
+    return kp_readlane(bin, first);
+  }
+  KP_INLINE uint64_t and64(uint64_t v) const {
+    return reduce(v, [](uint64_t a, uint64_t b) { return a & b; }, (uint64_t)~0ull);
+  }
+  KP_INLINE uint64_t or64(uint64_t v) const {
+    return reduce(v, [](uint64_t a, uint64_t b) { return a | b; }, (uint64_t)0);
+  }
+  KP_INLINE void andor(uint64_t& an, uint64_t& on) const {
+    int64_t x = (int64_t)an, y = (int64_t)on;
+    reduce2(x, [](int64_t a, int64_t b) { return a & b; }, (int64_t)-1, y, [](int64_t a, int64_t b) { return a | b; },
+            (int64_t)0);
+    an = (uint64_t)x;
+    on = (uint64_t)y;
+  }
+  KP_INLINE void mask_store(uint64_t* row, int c, bool bit, int W) const {
+    const uint64_t m = __ballot(bit);
+    if (lane() == 0 && (c >> 6) < W) row[c >> 6] = m;
+  }
+  KP_INLINE int wwidth() const { return 64; }
+  KP_INLINE uint64_t wballot(bool p) const { return __ballot(p); }
+  KP_INLINE uint64_t wlt() const { return (1ull << lane()) - 1; }
+  KP_INLINE void wsync() const { sync(); }
+  // lane l's value to every lane; the wave's 32-bit sum (no barrier: registers only)
+  template <class T>
+  KP_INLINE T wread(T v, int l) const {
+    return kp_readlane(v, l);
+  }
+  KP_INLINE int32_t wsum32(int32_t v) const {
+    return wave_reduce(v, [](int32_t a, int32_t b) { return a + b; }, (int32_t)0);
+  }
+  template <class T>
+  KP_INLINE T bcast(T v) const {
+    sync();
+    return kp_readlane(v, 0);
+  }
+};
 #endif
 
 struct CpuBlk {
@@ -322,6 +473,11 @@ struct CpuBlk {
   uint64_t wballot(bool p) const { return p ? 1ull : 0ull; }
   uint64_t wlt() const { return 0; }
   void wsync() const {}
+  template <class T>
+  T wread(T v, int) const {
+    return v;
+  }
+  int32_t wsum32(int32_t v) const { return v; }
   template <class T>
   int find_bin(const T* hist, int64_t k, int64_t* before, bool rev) const {
     int64_t c = 0;

@@ -13,6 +13,7 @@
 
 namespace kp {
 struct SetsArgs;
+struct TopArgs;
 struct GradesArgs;
 struct NodeEstArgs;
 namespace dev {
@@ -56,6 +57,15 @@ int est_class(stream_t st, const SnapView& s, const BatchView& bv, const int32_t
 // requires s.n_bits > 0).
 int filter(stream_t st, const SnapView& s, const BatchView& bv, uint64_t* fmask);
 int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x);
+// Estimator-class orders for k_select_top: ord[k][i] = (estimate << 32 | rank) of
+// rows[k] sorted by estimate desc, rank asc; tot[k] its sum; ok[k] whether it can be
+// walked (body_class_order). C <= 16384.
+int class_order(stream_t st, const SnapView& s, const int32_t* rows, int n_rows, uint64_t* ord, int64_t* tot,
+                int32_t* ok);
+// SEL_ALL DynamicWeight / Aggregated bindings a.list[0, a.n) over their deciding
+// candidates (body_select_top), `slice` bytes of LDS per binding; the others are
+// appended to t.fb.
+int select_top(stream_t st, const KArgs& a, const TopArgs& t, size_t slice);
 // selectGroups for n region bindings (one thread each): rsel/rnsel as the host
 // step writes them; *nhost counts the bindings left to the host (kGroupsHost).
 int region_groups(stream_t st, const RegionOut* rout, const int32_t* rstat, const BindHdr* hdr, const int32_t* list,

@@ -24,6 +24,9 @@ struct KArgs {
   int32_t* slow_ids;      // bindings flagged for k_slow, [0, stats[0]) (append order)
   uint32_t* stats;        // [0]: bindings flagged for the serial path, [SLOW_*]: by reason
   unsigned long long* dbg;  // diagnostic build only: phase cycle sums (nullptr otherwise)
+  // set: the launch covers list[0, *n_dev) with a grid-stride loop (a list another
+  // kernel appended to, e.g. k_select_top's fallback list); n is its capacity
+  const uint32_t* n_dev = nullptr;
 };
 
 enum : int {

@@ -18,7 +18,8 @@ constexpr int kRegionMax = 256;
 
 // Reasons a binding leaves the fast paths for the exact serial path (stats[reason]).
 enum : int { SLOW_NONE = 0, SLOW_OVERFLOW_DUP = 1, SLOW_SCALE_DOWN = 2, SLOW_WRAP = 3, SLOW_TIE = 4, SLOW_WEIGHT = 5,
-             SLOW_CLUSTER = 6 };
+             SLOW_CLUSTER = 6,
+             SLOW_TOP_FULL = 100 };  // k_select_top only: the binding needs the full candidate set (not a k_slow reason)
 
 KP_HD inline uint64_t cand_key(const SelCtx& x, const Cands& cd, int i, int32_t est) {
   uint32_t rank = c_rank(cd, i);
@@ -272,6 +273,16 @@ struct DivSums {
   bool valid = false;
 };
 
+// sel_all_fast over a SUBSET of the candidates (k_select_top, kp_top.h): `cs` holds
+// every scheduled cluster among the candidates and the non-scheduled ones with the
+// largest votes (enough to decide the Webster top-N or the Aggregated cut exactly);
+// F is the full candidate count (sort.Sort's list length); complete: cs is every
+// candidate. A subset whose votes cannot cover the target returns SLOW_TOP_FULL.
+struct TopInfo {
+  int64_t F = 0;
+  bool complete = false;
+};
+
 // ----------------------------------------------------------------------------
 // SEL_ALL: every feasible cluster is selected (select_clusters.go:29-32) and
 // AssignReplicas runs block-parallel over the candidate set `cs` (F members).
@@ -279,7 +290,8 @@ struct DivSums {
 // binding needs the exact serial path (nothing written).
 // ----------------------------------------------------------------------------
 template <class BLK, class CS>
-KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScratch& ss) {
+KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScratch& ss,
+                       const TopInfo* top = nullptr) {
   KP_STAMP_INIT
   const BindHdr& h = *x.h;
   const bool desc = (h.flags & BF_UID_DESC) != 0;
@@ -376,6 +388,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
     ds.np = pn >> 32;
   }
   ds.valid = true;
+  if (top) ds.nparty = top->F;  // the whole TargetClustersList (SLOW_TIE's n > 12 test)
   const int32_t assigned = wrap32(asum);
   const bool anyPriorPos = apos != 0;
   int mode;  // 0 fresh, 1 scale up, 2 unchanged, 3 scale down
@@ -393,6 +406,8 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
     return SLOW_NONE;
   }
   const int32_t target = mode == 0 ? h.replicas : sub32(h.replicas, assigned);
+  // a subset that does not cover the target cannot report the availability error
+  if (top && !top->complete && (int32_t)ds.vtot < target) return SLOW_TOP_FULL;
   return divide_par(B, x, cs, target, mode == 0, mode == 1, anyPriorPos,
                     mode == 0 ? KP_ERR_FRESH_NOT_ENOUGH : KP_ERR_SCALE_UP_NOT_ENOUGH, ss, &ds);
 }

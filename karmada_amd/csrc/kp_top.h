@@ -1,0 +1,299 @@
+// kp_top.h — SEL_ALL DynamicWeight / Aggregated assignment over the candidates that
+// can matter (k_select_top), one wave64 per binding.
+//
+// The exact divisions (division_algorithm.go:75-101, webstermethod.go:112-161) only
+// look at a few candidates when the target is small against the candidate count:
+//   * Webster (DynamicWeight): a party whose vote is below the N-th largest party
+//     vote (N = seats) has N elements strictly above its first one, so it takes no
+//     seat; the parties with votes >= that N-th vote decide everything.
+//   * Aggregated: the cut (sort.Sort by Replicas desc, prior clusters first, prefix
+//     until the running sum reaches the target) keeps the prior clusters and the
+//     non-prior candidates whose votes are >= the cut value v*.
+// Each estimator class's row is sorted once per batch by (estimate desc, rank asc)
+// (k_class_order), so a binding walks its class's order, skipping infeasible
+// clusters (its k_filter row), and stops once the walked candidates cover the
+// target; it then takes the rest of the tie group at the last value. The scheduled
+// clusters (spec.Clusters among the candidates) are always in the subset: their
+// votes may include their replicas (fresh) and they lead the Aggregated order.
+// sel_all_fast then runs unchanged over that subset (kp_paths.h TopInfo), with the
+// full candidate count for sort.Sort's n > 12 test. Anything else — other
+// strategies, overflow tiers, a subset past its LDS capacity, a class whose
+// estimates could wrap int32 sums — goes to the fallback list, which the gathered
+// k_select_all then schedules with every candidate.
+#pragma once
+#include "kp_kernels.h"
+
+namespace kp {
+
+// ---- per-class candidate order ------------------------------------------------
+// ord[k][i], i < C: (estimate << 32) | rank of class k's row sorted by estimate
+// desc, rank asc; tot[k] = the row's sum over c < C; ok[k] = 0 when the row cannot
+// be walked (row 0 = non-workload MaxInt32, or an estimate at MaxInt32 whose merged
+// value is spec.Replicas and so differs per binding).
+template <class BLK>
+KP_FI void body_class_order(const BLK& B, int k, uint64_t* keys, int P, const SnapView& s, const int32_t* rows,
+                            uint64_t* ord, int64_t* tot, int32_t* ok) {
+  const int32_t* row = rows + (size_t)k * s.Cp;
+  int64_t sum = 0, bad = k == 0 ? 1 : 0;
+  for (int i = B.tid(); i < P; i += B.nth()) {
+    uint64_t key = ~0ull;
+    if (i < s.C) {
+      const int32_t e = row[i];
+      if (e < 0 || e == kInt32Max) bad = 1;
+      sum += e;
+      key = ((uint64_t)(uint32_t)(kInt32Max - (e < 0 ? 0 : e)) << 32) | (uint32_t)i;  // desc estimate, asc rank
+    }
+    keys[i] = key;
+  }
+  B.sync();
+  for (int len = 2; len <= P; len <<= 1)  // bitonic sort, ascending
+    for (int j = len >> 1; j > 0; j >>= 1) {
+      for (int i = B.tid(); i < P; i += B.nth()) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint64_t a = keys[i], b = keys[l];
+          const bool up = (i & len) == 0;
+          if ((a > b) == up) {
+            keys[i] = b;
+            keys[l] = a;
+          }
+        }
+      }
+      B.sync();
+    }
+  for (int i = B.tid(); i < s.C; i += B.nth()) {
+    const uint64_t key = keys[i];
+    const uint32_t e = (uint32_t)kInt32Max - (uint32_t)(key >> 32);
+    ord[(size_t)k * s.Cp + i] = ((uint64_t)e << 32) | (key & 0xffffffffull);
+  }
+  int64_t t = sum, b = bad;
+  B.reduce2(t, [](int64_t p, int64_t q) { return p + q; }, 0, b, [](int64_t p, int64_t q) { return p > q ? p : q; }, 0);
+  if (B.tid() == 0) {
+    tot[k] = t;
+    ok[k] = b ? 0 : 1;
+  }
+}
+
+// ---- per-binding subset selection ----------------------------------------------
+struct TopArgs {
+  const uint64_t* ord;  // [n_classes][Cp]
+  const int64_t* tot;   // [n_classes]
+  const int32_t* ok;    // [n_classes]
+  int32_t* fb;          // fallback list (bindings for the full-candidate kernel)
+  uint32_t* fb_n;       // its length
+  int cap;              // subset capacity (LDS entries per wave)
+};
+
+// Webster's party list / enumeration buffer of the subset path (u64 entries): larger
+// party sets take its uncompacted passes over the subset (exact, kp_select.h).
+constexpr int kTopEcap = 256;
+KP_HD inline int top_ecap(int cap) { return cap < kTopEcap ? cap : kTopEcap; }
+// LDS slice of one binding: [red 64 B | frow W u64 | tgt bits | S ranks cap | S votes cap | SelScratch]
+KP_HD inline size_t top_lds_bytes(int Cp, int cap) {
+  const int words = (Cp + 31) >> 5, W = Cp / 64;
+  return 64 + 8 * (size_t)W + 4 * (size_t)((words + 3) & ~3) + 8 * (size_t)cap + 3072 + 8 * (size_t)top_ecap(cap) +
+         64;
+}
+
+template <class BLK>
+KP_FI void top_fallback(const BLK& B, const KArgs& a, const TopArgs& t, int b) {
+  if (B.tid() == 0) t.fb[kp_atomic_add(t.fb_n, 1u)] = b;
+}
+
+template <class BLK>
+KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KArgs& a, const TopArgs& t) {
+  if (blk >= a.n) return;
+  KP_STAMP_INIT
+  const int b = a.list[blk];
+  const SnapView& s = a.s;
+  const BindHdr* h = &a.bv.hdr[b];
+  const int words = (s.Cp + 31) >> 5;
+  // eligibility: SEL_ALL Dynamic/Aggregated workloads the subset argument covers
+  const uint32_t fl = h->flags;
+  const int st = h->strategy;
+  const int32_t cls = a.bcls ? a.bcls[b] : 0;
+  bool elig = a.bcls != nullptr && h->sel == SEL_ALL && (st == ST_DYNAMIC || st == ST_AGGREGATED) &&
+              (fl & BF_WORKLOAD_ASSIGN) && !(fl & (BF_EMPTY_PROP | BF_BAD | BF_DUP_TARGETS | BF_OVERFLOW)) &&
+              h->ovf_mode == OVF_ZERO && h->replicas > 0 && t.ok[cls] != 0;
+  if (elig) {  // no int32 wrap anywhere: every vote sum stays below the class total + |scheduled replicas|
+    int64_t sch = 0;
+    for (int j = 0; j < h->tgt_cnt; j++) {
+      const int32_t r = kp_ldu(a.bv.ipool + h->tgt_off + 2 * j + 1);
+      sch += r < 0 ? -(int64_t)r : (int64_t)r;
+    }
+    elig = t.tot[cls] + sch < (int64_t)kInt32Max / 2;
+  }
+  if (!elig) {
+    top_fallback(B, a, t, b);
+    return;
+  }
+  // LDS carve
+  unsigned char* p = smem + 64;
+  uint64_t* frow = (uint64_t*)p;
+  p += 8 * (size_t)s.W;
+  uint32_t* tgt = (uint32_t*)p;
+  p += 4 * (size_t)((words + 3) & ~3);
+  Cands cd;
+  cd.r = (uint32_t*)p;
+  cd.v = (int32_t*)(cd.r + t.cap);
+  SelScratch ss = carve_sel_scratch((unsigned char*)(cd.v + t.cap), 2 * t.cap);
+  ss.cap = top_ecap(t.cap);
+  ss.dbg = a.dbg;
+  SelCtx x = make_ctx(a, b, tgt);
+  build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
+  int64_t F = 0;
+  for (int w = B.tid(); w < s.W; w += B.nth()) {
+    const uint64_t m = x.frow[w];
+    frow[w] = m;
+    F += popc64(m);
+  }
+  F = B.sum64(F);  // (also orders the frow copy before the walk)
+  x.frow = frow;   // every later feasibility test reads the LDS copy
+  KP_STAMP(x, 9);
+  KP_COUNT(x, 15, 1);
+  if (pre_checks(B, x, (int)F)) return;
+  // the scheduled clusters among the candidates (spec.Clusters ∩ feasible): always
+  // in the subset, with the votes the division gives them
+  const bool fresh = (fl & BF_FRESH) != 0;
+  const bool agg = st == ST_AGGREGATED;
+  uint32_t* ctr = (uint32_t*)smem;  // subset length
+  if (B.tid() == 0) *ctr = 0;
+  B.sync();
+  int64_t asum = 0, apos = 0, tsum = 0;
+  {
+    int32_t mine = 0;
+    for (int j = B.tid(); j < h->tgt_cnt; j += B.nth())
+      mine += mask_test(x.frow, (int)kp_ldu(a.bv.ipool + h->tgt_off + 2 * j)) ? 1 : 0;
+    int32_t pos = B.wave_reserve(mine, ctr);
+    for (int j = B.tid(); j < h->tgt_cnt; j += B.nth()) {
+      const uint32_t r = (uint32_t)kp_ldu(a.bv.ipool + h->tgt_off + 2 * j);
+      if (!mask_test(x.frow, (int)r)) continue;
+      const int32_t sr = kp_ldu(a.bv.ipool + h->tgt_off + 2 * j + 1);
+      const int32_t e = est_at(x, (int)r);  // the subset holds AllocatableReplicas (sel_all_fast adds
+      if (pos < t.cap) {                     // the scheduled replicas to a fresh vote itself)
+        cd.r[pos] = r;
+        cd.v[pos] = e;
+      }
+      pos++;
+      asum += sr;
+      apos += sr > 0 ? 1 : 0;
+      tsum += fresh ? add32(e, sr) : e;
+    }
+  }
+  B.sum2(asum, apos);
+  tsum = B.sum64(tsum);
+  int32_t n = (int32_t)*ctr;  // (the reductions ordered the reservation)
+  if (n > t.cap) {
+    top_fallback(B, a, t, b);
+    return;
+  }
+  const int32_t assigned = wrap32(asum);
+  bool complete = false;
+  KP_STAMP(x, 10);
+  if (fresh || assigned < h->replicas) {
+    // fresh / scale up: walk the class order for the non-scheduled candidates
+    const int32_t target = fresh ? h->replicas : sub32(h->replicas, assigned);
+    // Aggregated scale up with prior clusters: they lead the order (resortAvailableClusters,
+    // assignment.go:151-178); their votes count toward the cut before any walked one
+    int64_t psum = 0;
+    if (agg && !fresh && apos != 0) {
+      for (int i = B.tid(); i < n; i += B.nth())
+        if (h->tgt_cnt > 0 && sched_rep_of(x, cd.r[i]) > 0) psum += cd.v[i];
+      psum = B.sum64(psum);
+    }
+    const uint64_t* ord = t.ord + (size_t)cls * s.Cp;
+    const int lane = B.tid() % B.wwidth();
+    const int ww = B.wwidth();
+    uint64_t e_next = lane < s.C ? ord[lane] : 0;  // the next chunk's load, one iteration ahead
+    int64_t walked = 0, wsum = 0;
+    bool tie = false;
+    int32_t tie_v = 0;
+    // (Aggregated: the prior clusters alone may already reach the target; no walk)
+    const bool cov0 = agg && tsum >= (int64_t)target && psum >= (int64_t)target;
+    int i0_last = -B.wwidth();  // (the stamps build counts the walked chunks)
+    (void)i0_last;
+    for (int i0 = 0; !cov0; i0 += ww) {
+      i0_last = i0;
+      if (i0 >= s.C) {
+        complete = true;
+        break;
+      }
+      const int i = i0 + lane;
+      const uint64_t e = e_next;
+      if (i + ww < s.C) e_next = ord[i + ww];
+      bool in = false, past = false;
+      int32_t v = 0;
+      uint32_t r = 0;
+      if (i < s.C) {
+        r = (uint32_t)e;
+        v = (int32_t)(e >> 32);
+        in = ((frow[r >> 6] >> (r & 63)) & 1ull) && !(h->tgt_cnt > 0 && bit_test(tgt, (int)r));
+        if (tie) {
+          past = v < tie_v;
+          in = in && v == tie_v;
+        }
+      }
+      const uint64_t m = B.wballot(in);
+      const bool any_past = B.wballot(past) != 0;
+      const int cnt = popc64(m);
+      if (n + cnt > t.cap) {
+        n += cnt;
+        break;
+      }
+      if (in) {
+        const int pos = n + popc64(m & B.wlt());
+        cd.r[pos] = r;
+        cd.v[pos] = v;
+      }
+      n += cnt;
+      if (tie) {
+        if (any_past) break;
+        continue;
+      }
+      // the chunk's sum (int32: the class row's total is below 2^30) and its smallest
+      // walked vote: the last walked lane's, the order being votes desc
+      const int32_t add = B.wsum32(in ? v : 0);
+      const int32_t vmin = cnt > 0 ? B.wread(v, 63 - __builtin_clzll(m)) : 0;
+      walked += cnt;
+      wsum += add;
+      // covered: the subset's votes reach the target (the availability check passes on
+      // every candidate too) and the walked ones decide the division: the N-th largest
+      // party vote (DynamicWeight) or the cut value (Aggregated) is >= vmin
+      const bool cov = tsum + wsum >= (int64_t)target && (agg ? psum + wsum >= (int64_t)target : walked >= (int64_t)target);
+      if (cov) {  // then the rest of the tie group at the last (smallest) vote
+        tie = true;
+        tie_v = vmin;
+      }
+    }
+    KP_COUNT(x, 13, (i0_last + B.wwidth()) / B.wwidth());
+    if (n > t.cap) {
+      // Past capacity before covering the target: when every candidate's votes together
+      // stay below it, the answer is dynamicDivideReplicas' availability error
+      // (division_algorithm.go:75-78; the sum cannot wrap: the class total is below
+      // 2^30), which needs only that sum; otherwise the full-candidate kernel decides.
+      int64_t rest = 0;  // the votes of the feasible non-scheduled candidates
+      for (int c = B.tid(); c < s.C; c += B.nth())
+        if (((frow[c >> 6] >> (c & 63)) & 1ull) && !(h->tgt_cnt > 0 && bit_test(tgt, c))) rest += est_at(x, c);
+      rest = B.sum64(rest);
+      if ((int64_t)(int32_t)(tsum + rest) < (int64_t)target) {
+        if (B.tid() == 0)
+          sink_error(x, KP_STATUS_UNSCHEDULABLE, fresh ? KP_ERR_FRESH_NOT_ENOUGH : KP_ERR_SCALE_UP_NOT_ENOUGH,
+                     (int32_t)(tsum + rest));
+        return;
+      }
+      top_fallback(B, a, t, b);
+      return;
+    }
+  }
+  KP_STAMP(x, 11);
+  KP_COUNT(x, 14, n);
+  cd.F = n;
+  B.sync();
+  const TopInfo ti{F, complete};
+  const int why = sel_all_fast(B, x, LdsCands{&cd, B.tid(), B.nth()}, ss, &ti);
+  KP_STAMP(x, 12);
+  if (why == SLOW_TOP_FULL) top_fallback(B, a, t, b);
+  else if (why != SLOW_NONE && B.tid() == 0) flag_slow(a, b, why);
+}
+
+}  // namespace kp

@@ -141,3 +141,33 @@ def test_cpusim_region_host_dfs(engine):
     finally:
         os.environ.pop("KP_REGION_HOST", None)
     compare(got, want, "region host DFS")
+
+
+@pytest.mark.parametrize("top_env", [{"KP_TOP_CAP": "64"}, {"KP_TOP": "0"}], ids=["cap64", "off"])
+def test_cpusim_top_subsets(top_env):
+    """k_select_top (kp_top.h) at its smallest subset capacity (most bindings hand back
+    to the full-candidate kernel through the device fallback list) and switched off:
+    the same placements as the oracle either way."""
+    old = {k: os.environ.get(k) for k in top_env}
+    os.environ.update(top_env)
+    try:
+        e = Engine(0, lib_path=CPUSIM)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    try:
+        for config, seed, C_, B_ in [(3, 53, 400, 600), (7, 54, 300, 300), (6, 55, 150, 800)]:
+            u = synth.Universe(config, seed, C_, 0, B_)
+            opts = api.options()
+            want = O.schedule_c(u.clusters, u.n_clusters, u.bindings, u.n_bindings, opts, O.FAST, 8)
+            times = []
+            compare(run(e, u, opts, times=times), want, f"{top_env} config {config}")
+            if top_env.get("KP_TOP") == "0":
+                assert times[0]["n_top"] == 0
+            else:
+                assert times[0]["n_top_fallback"] > 0
+    finally:
+        e.close()

@@ -18,6 +18,9 @@ for s in "$@"; do
     bench_small) step bench_small 300 python bench.py --steps 3 --warmup 1 --bindings 5000 --no-cpu ;;
     bench) step bench 600 python bench.py ;;
     benchq) step benchq 300 python bench.py --steps 100 --warmup 2 --no-cpu --check 300 ;;
+    benchq_notop) KP_TOP=0 step benchq_notop 300 python bench.py --steps 100 --warmup 2 --no-cpu --check 300 --e2e-reps 0 ;;
+    cfg_*) c=${s#cfg_}; b=100000; [ "$c" = 5 ] && b=125000
+           step bench_cfg$c 300 python bench.py --config $c --bindings $b --steps 20 --warmup 2 --no-cpu --check 300 --e2e-reps 0 ;;
     bench_rows) KP_PAIR_ROWS=1 step bench_rows 300 python bench.py --steps 100 --warmup 2 --no-cpu --check 300 --e2e-reps 0 ;;
     sweep) for t in 256 512; do KP_SEL_THREADS=$t step sweep_$t 300 python bench.py --steps 3 --warmup 1 --no-cpu; done ;;
     chunks) for c in 4096 8192 16384 32768 200000; do KP_CHUNK=$c step chunk_$c 300 python bench.py --steps 5 --warmup 1 --no-cpu; done ;;
