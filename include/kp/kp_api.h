@@ -37,6 +37,7 @@
  *                                      (pkg/controllers/status/cluster_status_controller.go:642-677)
  *        kp_node_max_replicas       <- noderesource.nodeResourceEstimator.Estimate (estimator server,
  *                                      pkg/estimator/server/framework/plugins/noderesource)
+ *        kp_node_max_component_sets <- noderesource.nodeResourceEstimator.EstimateComponents
  *        kp_snapshot_create         <- cache.Cache.Snapshot (pkg/scheduler/cache/cache.go:124-139)
  *        kp_schedule_affinities     <- Scheduler.scheduleResourceBindingWithClusterAffinities
  *                                      (pkg/scheduler/scheduler.go:584-585,618-684)
@@ -54,7 +55,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 10
+#define KP_ABI_VERSION 11
 
 /* ------------------------------------------------------------------------- */
 /* Object model                                                              */
@@ -509,27 +510,76 @@ typedef struct kp_node {
 int kp_model_grades(kp_engine* e, const kp_resource_model* models, uint32_t n_models, const kp_node* nodes,
                     uint64_t n_nodes, int64_t* out_counts);
 
-/* pb.NodeClaim of the estimator request: nodeSelector and tolerations (required
- * node-affinity terms are not modeled: has_node_affinity != 0 -> KP_ENOTSUP). */
+/* corev1.NodeSelectorTerm of a required node affinity: MatchExpressions over node
+ * labels (In, NotIn, Exists, DoesNotExist, Gt, Lt) and MatchFields over the node's
+ * fields (metadata.name; In / NotIn with exactly one value). */
+typedef struct kp_node_selector_term {
+  const kp_requirement* match_expressions;
+  uint32_t n_match_expressions;
+  const kp_requirement* match_fields;
+  uint32_t n_match_fields;
+} kp_node_selector_term;
+
+/* pb.NodeClaim of the estimator request (pkg/estimator/pb): nodeSelector,
+ * tolerations and the required node affinity. has_node_affinity != 0 when
+ * NodeAffinityBytes decodes to a NodeSelector (pb/helpers.go:40-55); its terms are
+ * ORed (nodeaffinity.LazyErrorNodeSelector.Match), a term that fails to parse or is
+ * empty never matches, and a selector with no usable term matches no node. */
 typedef struct kp_node_claim {
   const kp_label* node_selector;
   uint32_t n_node_selector;
   const kp_toleration* tolerations;
   uint32_t n_tolerations;
   int32_t has_node_affinity;
+  const kp_node_selector_term* node_affinity_terms;
+  uint32_t n_node_affinity_terms;
 } kp_node_claim;
 
+/* pb.Component of an estimator server request: Replicas and ReplicaRequirements
+ * (ResourceRequest, NodeClaim). has_replica_requirements == 0: nil requirements
+ * (only the pod count is required, every node matches). */
+typedef struct kp_node_component {
+  int32_t replicas;
+  uint8_t has_replica_requirements;
+  const kp_resource* resource_request;
+  uint32_t n_resource_request;
+  const kp_node_claim* node_claim; /* NULL: no NodeClaim */
+} kp_node_component;
+
+/* pb.AssumedWorkload: a workload admitted but possibly not yet visible in node
+ * accounting, deducted first (one set, SimulateScheduling(components, 1)). */
+typedef struct kp_assumed_workload {
+  const kp_node_component* components;
+  uint32_t n_components;
+} kp_assumed_workload;
+
 /* The accurate estimator's per-node path: nodeResourceEstimator.Estimate
- * (estimator/server/framework/plugins/noderesource/noderesource.go:70-131) with no
- * assumed workloads: the sum over the nodes that MatchNode accepts (nodeSelector,
- * tolerations incl. the unschedulable taint, filter.go:38-90) of int32(MaxDivided)
- * of the node's available resources (allocatable - requested, clamped at 0; pods
- * = allocatable pods - n_pods, util/resource.go:96-115,221-248) for `request`.
- * claim may be NULL (no NodeClaim). *out = the int32 sum (Go's atomic int32 adds
- * wrap). Replaces AccurateSchedulerEstimatorServer.EstimateReplicas for one request
- * (estimate.go:33-76; 0 when there are no nodes). */
+ * (estimator/server/framework/plugins/noderesource/noderesource.go:70-131): the
+ * assumed workloads deducted in order (one first-fit set each), then the sum over
+ * the nodes that MatchNode accepts (nodeSelector, required node affinity,
+ * tolerations incl. the unschedulable taint; filter.go:38-99) of int32(MaxDivided)
+ * of the node's available resources (allocatable - requested, clamped at 0; pods =
+ * allocatable pods - n_pods, util/resource.go:96-115,221-248; noderesource.go:
+ * 135-144) for `request`. claim may be NULL (no NodeClaim). *out = the int32 sum
+ * (Go's atomic int32 adds wrap). Replaces AccurateSchedulerEstimatorServer.
+ * EstimateReplicas for one request (estimate.go:33-76; 0 when there are no nodes). */
 int kp_node_max_replicas(kp_engine* e, const kp_node* nodes, uint64_t n_nodes, const kp_resource* request,
-                         uint32_t n_request, const kp_node_claim* claim, int32_t* out);
+                         uint32_t n_request, const kp_node_claim* claim, const kp_assumed_workload* assumed,
+                         uint32_t n_assumed, int32_t* out);
+
+/* The accurate estimator's component-set path: nodeResourceEstimator.EstimateComponents
+ * (noderesource.go:146-190): the assumed workloads deducted as above, then the
+ * first-fit simulation (SchedulingSimulator.SimulateScheduling,
+ * scheduling_simulator_components.go:51-131) of complete component sets over the
+ * nodes' available resources, each component placed on the nodes that MatchNode
+ * accepts for its NodeClaim, up to MaxInt32 sets. n_components == 0 -> *out =
+ * MaxInt32 (noNodeConstraint, the reference's Noopperation result); otherwise *out
+ * = the set count (0 = the reference's Unschedulable "no enough resources").
+ * KP_ENOTSUP past 16 components per set, 64 in all, 16 assumed workloads or 7
+ * distinct requested resources. */
+int kp_node_max_component_sets(kp_engine* e, const kp_node* nodes, uint64_t n_nodes,
+                               const kp_node_component* components, uint32_t n_components,
+                               const kp_assumed_workload* assumed, uint32_t n_assumed, int32_t* out);
 
 /* Last schedule call's stage timings. */
 int kp_last_stage_times(const kp_engine* e, kp_stage_times* out);

@@ -116,10 +116,26 @@ class kp_node(C.Structure):
                 ("requested", C.POINTER(kp_resource)), ("n_requested", u32), ("n_pods", u32)]
 
 
+class kp_node_selector_term(C.Structure):
+    _fields_ = [("match_expressions", C.POINTER(kp_requirement)), ("n_match_expressions", u32),
+                ("match_fields", C.POINTER(kp_requirement)), ("n_match_fields", u32)]
+
+
 class kp_node_claim(C.Structure):
     _fields_ = [("node_selector", C.POINTER(kp_label)), ("n_node_selector", u32),
                 ("tolerations", C.POINTER(kp_toleration)), ("n_tolerations", u32),
-                ("has_node_affinity", i32)]
+                ("has_node_affinity", i32),
+                ("node_affinity_terms", C.POINTER(kp_node_selector_term)), ("n_node_affinity_terms", u32)]
+
+
+class kp_node_component(C.Structure):
+    _fields_ = [("replicas", i32), ("has_replica_requirements", u8),
+                ("resource_request", C.POINTER(kp_resource)), ("n_resource_request", u32),
+                ("node_claim", C.POINTER(kp_node_claim))]
+
+
+class kp_assumed_workload(C.Structure):
+    _fields_ = [("components", C.POINTER(kp_node_component)), ("n_components", u32)]
 
 
 class kp_allocatable_modeling(C.Structure):
@@ -330,7 +346,8 @@ class World:
         return a, len(ds)
 
     def node_claim(self, d: Optional[dict]):
-        """{nodeSelector: {k: v}, tolerations: [...], nodeAffinity: any} -> kp_node_claim or None."""
+        """{nodeSelector: {k: v}, tolerations: [...], nodeAffinity: {nodeSelectorTerms: [{matchExpressions,
+        matchFields}]}} -> kp_node_claim or None (nodeAffinity: the NodeSelector that NodeAffinityBytes holds)."""
         if d is None:
             return None
         c = kp_node_claim()
@@ -339,9 +356,35 @@ class World:
         c.tolerations, c.n_tolerations = self.arr(kp_toleration, [
             kp_toleration(self.s(t.get("key")), self.s(t.get("operator")), self.s(t.get("value")), self.s(t.get("effect")))
             for t in d.get("tolerations") or []])
-        c.has_node_affinity = int(d.get("nodeAffinity") is not None)
+        na = d.get("nodeAffinity")
+        c.has_node_affinity = int(na is not None)
+        terms = []
+        for t in (na or {}).get("nodeSelectorTerms") or []:
+            me, nme = self.requirements(t.get("matchExpressions"))
+            mf, nmf = self.requirements(t.get("matchFields"))
+            terms.append(kp_node_selector_term(me, nme, mf, nmf))
+        c.node_affinity_terms, c.n_node_affinity_terms = self.arr(kp_node_selector_term, terms)
         self._keep.append(c)
         return c
+
+    def node_components(self, comps):
+        """pb.Component dicts {replicas, replicaRequirements: {resourceRequest, nodeClaim}} -> kp_node_component[]."""
+        out = []
+        for c in comps or []:
+            rr = c.get("replicaRequirements")
+            ra, nr = self.resources((rr or {}).get("resourceRequest"))
+            nc = self.node_claim((rr or {}).get("nodeClaim"))
+            out.append(kp_node_component(int(c.get("replicas", 0)), 1 if rr is not None else 0, ra, nr,
+                                         C.pointer(nc) if nc is not None else None))
+        return self.arr(kp_node_component, out)
+
+    def assumed_workloads(self, ws):
+        """pb.AssumedWorkload dicts {components: [...]} -> kp_assumed_workload[]."""
+        out = []
+        for w in ws or []:
+            ca, nc = self.node_components(w.get("components"))
+            out.append(kp_assumed_workload(ca, nc))
+        return self.arr(kp_assumed_workload, out)
 
     # -- cluster ---------------------------------------------------------------------
     def cluster(self, d: dict) -> kp_cluster:

@@ -219,8 +219,20 @@ int grades(stream_t, const GradesArgs& A) {
 
 int node_est(stream_t, const NodeEstArgs& A) {
   uint32_t s = 0;
-  for (uint64_t i = 0; i < A.n; i++) s += (uint32_t)node_replicas(A, i);
+  for (uint64_t i = 0; i < A.v.n; i++) s += (uint32_t)node_replicas(A, i);
   *A.sum += s;
+  return 0;
+}
+
+int node_match(stream_t, const NodeView& v, const ClaimProg* P, int K, uint8_t* match) {
+  const uint64_t n = v.n * (uint64_t)K;
+  for (uint64_t i = 0; i < n; i++) body_node_match(v, P, i, match);
+  return 0;
+}
+
+int node_sets(stream_t, const NodeSetsArgs* A) {
+  int64_t red[2];
+  kp::node_sets(CpuBlk{red}, *A);
   return 0;
 }
 

@@ -2732,6 +2732,204 @@ bool node_available(const kp_node& nd, QtyMap* out) {
   *out = alloc;
   return true;
 }
+// A member cluster's nodes in one call's dictionary (NodeView's host arrays).
+struct HostNodes {
+  std::vector<uint32_t> flags;
+  std::vector<int32_t> name, lbl_off{0}, tnt_off{0}, tnt;
+  std::vector<int64_t> lbl, lbl_int;
+  std::vector<uint8_t> lbl_int_ok;
+};
+void pack_nodes(const kp_node* nodes, uint64_t n, Dict& d, HostNodes& h) {
+  for (uint64_t i = 0; i < n; i++) {
+    const kp_node& nd = nodes[i];
+    h.flags.push_back(nd.unschedulable ? 1u : 0u);
+    const std::string nm = S(nd.name);
+    h.name.push_back(nm.empty() ? -1 : d.add(nm));
+    std::map<std::string, std::string> lm;  // node.Labels is a map
+    for (uint32_t j = 0; j < nd.n_labels; j++) lm[S(nd.labels[j].key)] = S(nd.labels[j].value);
+    for (auto& kv : lm) {
+      h.lbl.push_back(((int64_t)d.add(kv.first) << 32) | (int64_t)(uint32_t)d.add(kv.second));
+      int64_t x = 0;
+      const bool ok = k8s::parse_int64(kv.second, &x);
+      h.lbl_int.push_back(ok ? x : 0);
+      h.lbl_int_ok.push_back(ok ? 1 : 0);
+    }
+    h.lbl_off.push_back((int32_t)h.lbl.size());
+    for (uint32_t j = 0; j < nd.n_taints; j++) {
+      const std::string ef = S(nd.taints[j].effect);
+      if (ef != "NoSchedule" && ef != "NoExecute") continue;  // DoNotScheduleTaintsFilterFunc
+      h.tnt.push_back(d.add(S(nd.taints[j].key)));
+      h.tnt.push_back(d.add(S(nd.taints[j].value)));
+      h.tnt.push_back(ef == "NoSchedule" ? EFF_NOSCHEDULE : EFF_NOEXECUTE);
+    }
+    h.tnt_off.push_back((int32_t)(h.tnt.size() / 3));
+  }
+}
+// pb.NodeClaim -> ClaimProg's host arrays (offsets relative to this claim).
+struct HostClaim {
+  std::vector<int64_t> sel;
+  std::vector<Tol> tols;
+  int32_t tol_unsched = 0, has_aff = 0;
+  std::vector<int32_t> term_off{0};
+  std::vector<NodeReq> reqs;
+  std::vector<int32_t> vals;
+};
+void compile_claim(const kp_node_claim* c, Dict& d, HostClaim& h) {
+  if (!c) return;
+  std::map<std::string, std::string> sm;  // labels.SelectorFromSet: one requirement per key
+  for (uint32_t j = 0; j < c->n_node_selector; j++) sm[S(c->node_selector[j].key)] = S(c->node_selector[j].value);
+  for (auto& kv : sm) h.sel.push_back(((int64_t)d.add(kv.first) << 32) | (int64_t)(uint32_t)d.add(kv.second));
+  for (uint32_t j = 0; j < c->n_tolerations; j++) {
+    const kp_toleration& t = c->tolerations[j];
+    const std::string ef = S(t.effect), key = S(t.key), op = S(t.op), val = S(t.value);
+    // TolerationsTolerateTaint for {node.kubernetes.io/unschedulable, NoSchedule}
+    if ((ef.empty() || ef == "NoSchedule") && (key.empty() || key == "node.kubernetes.io/unschedulable") &&
+        (op == "Exists" || ((op.empty() || op == "Equal") && val.empty())))
+      h.tol_unsched = 1;
+    Tol x;
+    if (ef.empty()) x.eff = EFF_ANY;
+    else if (ef == "NoSchedule") x.eff = EFF_NOSCHEDULE;
+    else if (ef == "NoExecute") x.eff = EFF_NOEXECUTE;
+    else continue;
+    x.key = key.empty() ? -1 : d.add(key);
+    if (op.empty() || op == "Equal") {
+      x.op = TOL_EQUAL;
+      x.val = d.add(val);
+    } else if (op == "Exists") {
+      x.op = TOL_EXISTS;
+      x.val = -1;
+    } else {
+      continue;  // Lt/Gt disabled, unknown operators never tolerate
+    }
+    h.tols.push_back(x);
+  }
+  // nodeaffinity.NewLazyErrorNodeSelector (nodeaffinity.go:50-67, 155-263): empty
+  // terms select nothing and are dropped; a term with a parse error never matches.
+  h.has_aff = c->has_node_affinity ? 1 : 0;
+  if (!h.has_aff) return;
+  for (uint32_t t = 0; t < c->n_node_affinity_terms; t++) {
+    const kp_node_selector_term& term = c->node_affinity_terms[t];
+    if (term.n_match_expressions == 0 && term.n_match_fields == 0) continue;
+    std::vector<NodeReq> rq;
+    std::vector<int32_t> vl;
+    bool ok = true;
+    for (uint32_t q = 0; q < term.n_match_expressions && ok; q++) {  // nodeSelectorRequirementsAsSelector
+      const kp_requirement& r = term.match_expressions[q];
+      const std::string key = S(r.key), op = S(r.op);
+      if (!(op == "In" || op == "NotIn" || op == "Exists" || op == "DoesNotExist" || op == "Gt" || op == "Lt") ||
+          !Packer::valid_req(key, op, r.values, r.n_values)) {
+        ok = false;
+        break;
+      }
+      NodeReq x{};
+      x.key = d.add(key);
+      if (op == "In" || op == "NotIn") {
+        x.op = op == "In" ? NA_IN : NA_NOTIN;
+        x.voff = (int32_t)(h.vals.size() + vl.size());
+        for (uint32_t j = 0; j < r.n_values; j++) vl.push_back(d.add(S(r.values[j])));
+        x.nv = (int32_t)r.n_values;
+      } else if (op == "Exists" || op == "DoesNotExist") {
+        x.op = op == "Exists" ? NA_EXISTS : NA_DNE;
+      } else {
+        x.op = op == "Gt" ? NA_GT : NA_LT;
+        k8s::parse_int64(S(r.values[0]), &x.x);
+      }
+      rq.push_back(x);
+    }
+    for (uint32_t q = 0; q < term.n_match_fields && ok; q++) {  // nodeSelectorRequirementsAsFieldSelector
+      const kp_requirement& r = term.match_fields[q];
+      const std::string key = S(r.key), op = S(r.op);
+      if (!(op == "In" || op == "NotIn") || r.n_values != 1) {
+        ok = false;
+        break;
+      }
+      const std::string v = S(r.values[0]);
+      NodeReq x{};
+      if (key == "metadata.name") {  // extractNodeFields: the only field a node carries
+        x.op = op == "In" ? NA_NAME_IN : NA_NAME_NOTIN;
+        x.voff = d.add(v);
+      } else {  // fields.Set.Get of an absent field is ""
+        x.op = ((op == "In") == v.empty()) ? NA_FIELD_TRUE : NA_FIELD_FALSE;
+      }
+      rq.push_back(x);
+    }
+    if (!ok) continue;
+    h.reqs.insert(h.reqs.end(), rq.begin(), rq.end());
+    h.vals.insert(h.vals.end(), vl.begin(), vl.end());
+    h.term_off.push_back((int32_t)h.reqs.size());
+  }
+}
+// Device copies of HostNodes and of several claims (one ClaimProg each).
+struct DevNodes {
+  NodeView v{};
+  std::vector<ClaimProg> progs;
+  uint32_t *d_flags = nullptr;
+  int32_t *d_name = nullptr, *d_loff = nullptr, *d_toff = nullptr, *d_tnt = nullptr, *d_toffs = nullptr,
+          *d_vals = nullptr;
+  int64_t *d_lbl = nullptr, *d_lint = nullptr, *d_sel = nullptr;
+  uint8_t* d_lok = nullptr;
+  Tol* d_tols = nullptr;
+  NodeReq* d_reqs = nullptr;
+  std::vector<int64_t> sel;
+  std::vector<Tol> tols;
+  std::vector<int32_t> toffs, vals;
+  std::vector<NodeReq> reqs;
+  std::vector<size_t> o_sel, o_tol, o_toff, o_req, o_val;
+  void plan(Arena& ar, const HostNodes& h, const std::vector<HostClaim>& cl) {
+    for (auto& c : cl) {
+      o_sel.push_back(sel.size());
+      o_tol.push_back(tols.size());
+      o_toff.push_back(toffs.size());
+      o_req.push_back(reqs.size());
+      o_val.push_back(vals.size());
+      sel.insert(sel.end(), c.sel.begin(), c.sel.end());
+      tols.insert(tols.end(), c.tols.begin(), c.tols.end());
+      toffs.insert(toffs.end(), c.term_off.begin(), c.term_off.end());
+      reqs.insert(reqs.end(), c.reqs.begin(), c.reqs.end());
+      vals.insert(vals.end(), c.vals.begin(), c.vals.end());
+    }
+    ar.add(&d_flags, std::max<size_t>(1, h.flags.size()));
+    ar.add(&d_name, std::max<size_t>(1, h.name.size()));
+    ar.add(&d_loff, h.lbl_off.size());
+    ar.add(&d_lbl, std::max<size_t>(1, h.lbl.size()));
+    ar.add(&d_lint, std::max<size_t>(1, h.lbl_int.size()));
+    ar.add(&d_lok, std::max<size_t>(1, h.lbl_int_ok.size()));
+    ar.add(&d_toff, h.tnt_off.size());
+    ar.add(&d_tnt, std::max<size_t>(1, h.tnt.size()));
+    ar.add(&d_sel, std::max<size_t>(1, sel.size()));
+    ar.add(&d_tols, std::max<size_t>(1, tols.size()));
+    ar.add(&d_toffs, std::max<size_t>(1, toffs.size()));
+    ar.add(&d_reqs, std::max<size_t>(1, reqs.size()));
+    ar.add(&d_vals, std::max<size_t>(1, vals.size()));
+  }
+  int upload(dev::stream_t st, const HostNodes& h, const std::vector<HostClaim>& cl, uint64_t n) {
+    auto up = [&](void* dd, const void* hp, size_t bytes) { return bytes ? dev::h2d(dd, hp, bytes, st) : 0; };
+    if (up(d_flags, h.flags.data(), 4 * h.flags.size()) || up(d_name, h.name.data(), 4 * h.name.size()) ||
+        up(d_loff, h.lbl_off.data(), 4 * h.lbl_off.size()) || up(d_lbl, h.lbl.data(), 8 * h.lbl.size()) ||
+        up(d_lint, h.lbl_int.data(), 8 * h.lbl_int.size()) || up(d_lok, h.lbl_int_ok.data(), h.lbl_int_ok.size()) ||
+        up(d_toff, h.tnt_off.data(), 4 * h.tnt_off.size()) || up(d_tnt, h.tnt.data(), 4 * h.tnt.size()) ||
+        up(d_sel, sel.data(), 8 * sel.size()) || up(d_tols, tols.data(), sizeof(Tol) * tols.size()) ||
+        up(d_toffs, toffs.data(), 4 * toffs.size()) || up(d_reqs, reqs.data(), sizeof(NodeReq) * reqs.size()) ||
+        up(d_vals, vals.data(), 4 * vals.size()))
+      return -1;
+    v = NodeView{n, d_flags, d_name, d_loff, d_lbl, d_lint, d_lok, d_toff, d_tnt};
+    for (size_t k = 0; k < cl.size(); k++) {
+      ClaimProg p{};
+      p.sel = d_sel + o_sel[k];
+      p.n_sel = (int32_t)cl[k].sel.size();
+      p.tols = d_tols + o_tol[k];
+      p.n_tols = (int32_t)cl[k].tols.size();
+      p.tol_unsched = cl[k].tol_unsched;
+      p.has_aff = cl[k].has_aff;
+      p.n_terms = (int32_t)cl[k].term_off.size() - 1;
+      p.term_off = d_toffs + o_toff[k];
+      p.reqs = d_reqs + o_req[k];
+      p.vals = d_vals + o_val[k];
+      progs.push_back(p);
+    }
+    return 0;
+  }
+};
 void split128(k8s::i128 v, int64_t* hi, uint64_t* lo) {
   *hi = (int64_t)(v >> 64);
   *lo = (uint64_t)v;
@@ -2817,162 +3015,244 @@ int kp_model_grades(kp_engine* e, const kp_resource_model* models, uint32_t n_mo
   return KP_OK;
 }
 
-int kp_node_max_replicas(kp_engine* e, const kp_node* nodes, uint64_t n_nodes, const kp_resource* request,
-                         uint32_t n_request, const kp_node_claim* claim, int32_t* out) {
-  if (!e || !out || (n_nodes && !nodes) || (n_request && !request)) return KP_EINVAL;
-  (void)dev::set_device(e->device);
-  *out = 0;
-  if (claim && claim->has_node_affinity) {
-    e->err = "kp_node_max_replicas: required node-affinity terms are not modeled";
+}  // extern "C"
+
+namespace {
+// One estimator-server call over a member cluster's nodes: the slots of every
+// resource the components (and the Estimate request) name, the nodes' available
+// resources in those slots, and a ClaimProg per component (+ the request's claim).
+struct NodeJob {
+  std::vector<std::string> slot{"pods"};
+  NodeSetsArgs A{};
+  std::vector<int64_t> avail;
+  std::vector<uint32_t> present;
+  Dict d;
+  HostNodes hn;
+  std::vector<HostClaim> cl;
+  std::string err;
+  int rc = KP_OK;
+  static bool divides(const std::string& nm) {
+    return nm == "cpu" || nm == "memory" || nm == "ephemeral-storage" || k8s::scalar_resource(nm);
+  }
+  static int64_t field(const NodeRes& r, const std::string& nm, bool* present) {
+    *present = true;
+    if (nm == "pods") return r.pods;
+    if (nm == "cpu") return r.cpu;
+    if (nm == "memory") return r.mem;
+    if (nm == "ephemeral-storage") return r.eph;
+    auto it = r.sc.find(nm);
+    *present = it != r.sc.end();
+    return *present ? it->second : 0;
+  }
+  int fail(int code, const char* m) {
+    rc = code;
+    err = m;
+    return code;
+  }
+  // phases: the assumed workloads (empty ones skipped), then `main` (may be empty).
+  int build(const kp_node* nodes, uint64_t n, const kp_assumed_workload* assumed, uint32_t n_assumed,
+            const kp_node_component* main, uint32_t K, const QtyMap* extra) {
+    std::vector<const kp_node_component*> comps;
+    A.n = n;
+    A.mono = 1;
+    A.n_phase = 0;
+    for (uint32_t w = 0; w < n_assumed; w++) {
+      if (assumed[w].n_components == 0) continue;  // noderesource.go:168-170
+      if (assumed[w].n_components > (uint32_t)kNodeComp || A.n_phase + 1 >= kNodePhase)
+        return fail(KP_ENOTSUP, "more than 16 assumed workloads or 16 components in one");
+      A.ph_k0[A.n_phase++] = (int32_t)comps.size();
+      for (uint32_t k = 0; k < assumed[w].n_components; k++) comps.push_back(&assumed[w].components[k]);
+    }
+    if (K) {
+      A.ph_k0[A.n_phase++] = (int32_t)comps.size();
+      for (uint32_t k = 0; k < K; k++) comps.push_back(&main[k]);
+    }
+    A.ph_k0[A.n_phase] = (int32_t)comps.size();
+    A.last_upper = K ? INT32_MAX : 1;
+    if (comps.size() > (size_t)kNodeCompAll) return fail(KP_ENOTSUP, "more than 64 components in all");
+    std::vector<NodeRes> creq(comps.size());
+    for (size_t k = 0; k < comps.size(); k++) {
+      const kp_node_component& c = *comps[k];
+      if (!c.has_replica_requirements) continue;
+      QtyMap q;
+      if (!qmap(c.resource_request, c.n_resource_request, &q)) return fail(KP_EINVAL, "unparsable resource request");
+      res_add(creq[k], q);
+      for (auto& kv : q)
+        if (divides(kv.first) && std::find(slot.begin(), slot.end(), kv.first) == slot.end()) slot.push_back(kv.first);
+    }
+    if (extra)
+      for (auto& kv : *extra)
+        if (divides(kv.first) && std::find(slot.begin(), slot.end(), kv.first) == slot.end()) slot.push_back(kv.first);
+    if (slot.size() > (size_t)kNodeRes) return fail(KP_ENOTSUP, "more than 7 distinct requested resources");
+    A.NU = (int32_t)slot.size();
+    for (size_t k = 0; k < comps.size(); k++) {
+      A.replicas[k] = comps[k]->replicas;
+      if (comps[k]->replicas < 0) A.mono = 0;
+      for (int u = 0; u < A.NU; u++) {
+        bool pr;
+        const int64_t v = u == 0 ? 1 : field(creq[k], slot[u], &pr);
+        A.req[k][u] = v;
+        A.pos[k][u] = v > 0 ? v : 0;
+        if (v < 0) A.mono = 0;
+      }
+    }
+    // getNodesAvailableResources / getNodeAvailableResource (noderesource.go:135-144,205-220)
+    avail.assign((size_t)n * A.NU, 0);
+    present.assign(n, 0);
+    for (uint64_t i = 0; i < n; i++) {
+      const kp_node& nd = nodes[i];
+      QtyMap al, rqd;
+      if (!qmap(nd.allocatable, nd.n_allocatable, &al) || !qmap(nd.requested, nd.n_requested, &rqd))
+        return fail(KP_EINVAL, "unparsable node quantity");
+      NodeRes a, r;
+      res_add(a, al);
+      res_add(r, rqd);
+      uint32_t pm = 0;
+      for (int u = 0; u < A.NU; u++) {
+        bool pa, prq;
+        const int64_t va = field(a, slot[u], &pa), vr = field(r, slot[u], &prq);
+        int64_t x = 0;
+        if (u == 0) x = std::max<int64_t>(std::max<int64_t>(va - vr, 0) - (int64_t)nd.n_pods, 0);
+        else if (pa) x = prq ? std::max<int64_t>(va - vr, 0) : va;  // SubResource: absent scalars stay absent
+        avail[(size_t)i * A.NU + u] = x;
+        if (pa) pm |= 1u << u;
+      }
+      present[i] = pm;
+    }
+    A.max_steps = A.mono ? 4 * (int64_t)comps.size() * ((int64_t)n + 2) + 64 : (int64_t)1 << 20;
+    pack_nodes(nodes, n, d, hn);
+    cl.resize(comps.size());
+    for (size_t k = 0; k < comps.size(); k++)
+      if (comps[k]->has_replica_requirements) compile_claim(comps[k]->node_claim, d, cl[k]);
+    return KP_OK;
+  }
+};
+}  // namespace
+
+extern "C" {
+
+// Runs the job's set phases on the device; *sets = the last phase's count. On
+// return the job's node state (d_avail) holds the deducted resources.
+static int node_job_run(kp_engine* e, NodeJob& J, const kp_node_claim* est_claim, NodeEstArgs* est, int32_t* sets) {
+  Arena ar;
+  DevNodes dn;
+  if (est) J.cl.emplace_back(), compile_claim(est_claim, J.d, J.cl.back());
+  dn.plan(ar, J.hn, J.cl);
+  const size_t NP = J.cl.size();
+  const int KS = J.A.ph_k0[J.A.n_phase];
+  ClaimProg* d_progs;
+  NodeSetsArgs* d_args;
+  int64_t* d_avail;
+  uint32_t *d_present, *d_ovf, *d_sum;
+  uint8_t* d_match;
+  int32_t* d_out;
+  ar.add(&d_progs, std::max<size_t>(1, NP));
+  ar.add(&d_args, 1);
+  ar.add(&d_avail, std::max<size_t>(1, J.avail.size()));
+  ar.add(&d_present, std::max<size_t>(1, J.present.size()));
+  ar.add(&d_match, std::max<size_t>(1, (size_t)KS * J.A.n));
+  ar.add(&d_out, 1);
+  ar.add(&d_ovf, 1);
+  ar.add(&d_sum, 1);
+  HIPCHK(ar.alloc());
+  dev::stream_t st = e->stream;
+  HIPCHK(dn.upload(st, J.hn, J.cl, J.A.n));
+  J.A.avail = d_avail;
+  J.A.present = d_present;
+  J.A.match = d_match;
+  J.A.out = d_out;
+  J.A.ovf = d_ovf;
+  if (NP) HIPCHK(dev::h2d(d_progs, dn.progs.data(), sizeof(ClaimProg) * NP, st));
+  HIPCHK(dev::h2d(d_args, &J.A, sizeof(J.A), st));
+  if (!J.avail.empty()) HIPCHK(dev::h2d(d_avail, J.avail.data(), 8 * J.avail.size(), st));
+  if (!J.present.empty()) HIPCHK(dev::h2d(d_present, J.present.data(), 4 * J.present.size(), st));
+  HIPCHK(dev::fill(d_out, 0, 4, st));
+  HIPCHK(dev::fill(d_ovf, 0, 4, st));
+  if (KS > 0 && J.A.n > 0) {
+    HIPCHK(dev::node_match(st, dn.v, d_progs, KS, d_match));
+    HIPCHK(dev::node_sets(st, d_args));
+  }
+  if (est) {
+    HIPCHK(dev::fill(d_sum, 0, 4, st));
+    est->v = dn.v;
+    est->p = dn.progs.back();
+    est->NU = J.A.NU;
+    est->avail = d_avail;
+    est->sum = d_sum;
+    HIPCHK(dev::node_est(st, *est));
+  }
+  int32_t res = 0;
+  uint32_t ovf = 0, sum = 0;
+  HIPCHK(dev::d2h(&res, d_out, 4, st));
+  HIPCHK(dev::d2h(&ovf, d_ovf, 4, st));
+  if (est) HIPCHK(dev::d2h(&sum, d_sum, 4, st));
+  HIPCHK(dev::sync(st));
+  if (ovf) {
+    e->err = "the first-fit simulation exceeded its step bound";
     return KP_ENOTSUP;
   }
+  *sets = est ? (int32_t)sum : res;
+  return KP_OK;
+}
+
+int kp_node_max_replicas(kp_engine* e, const kp_node* nodes, uint64_t n_nodes, const kp_resource* request,
+                         uint32_t n_request, const kp_node_claim* claim, const kp_assumed_workload* assumed,
+                         uint32_t n_assumed, int32_t* out) {
+  if (!e || !out || (n_nodes && !nodes) || (n_request && !request) || (n_assumed && !assumed)) return KP_EINVAL;
+  (void)dev::set_device(e->device);
+  *out = 0;
   QtyMap rq;
   if (!qmap(request, n_request, &rq)) {
     e->err = "kp_node_max_replicas: unparsable resource request";
     return KP_EINVAL;
   }
   if (n_nodes == 0) return KP_OK;  // estimate.go:43-45
+  NodeJob J;
+  if (J.build(nodes, n_nodes, assumed, n_assumed, nullptr, 0, &rq) != KP_OK) {
+    e->err = "kp_node_max_replicas: " + J.err;
+    return J.rc;
+  }
   // MaxDivided's dividing entries (resource.go:221-248): cpu milli, memory,
   // ephemeral-storage, scalar resources, each > 0
-  std::vector<std::string> qn;
-  std::vector<int64_t> qv;
+  NodeEstArgs E{};
   for (auto& kv : rq) {
     const std::string& nm = kv.first;
-    int64_t v = 0;
-    if (nm == "cpu") v = k8s::milli(kv.second);
-    else if (nm == "memory" || nm == "ephemeral-storage" || k8s::scalar_resource(nm)) v = k8s::value(kv.second);
-    else continue;
-    if (v > 0) {
-      qn.push_back(nm);
-      qv.push_back(v);
-    }
+    if (!NodeJob::divides(nm)) continue;
+    const int64_t v = nm == "cpu" ? k8s::milli(kv.second) : k8s::value(kv.second);
+    const int u = (int)(std::find(J.slot.begin(), J.slot.end(), nm) - J.slot.begin());
+    if (v > 0) E.q[u] = v;
   }
-  const int NQ = (int)qn.size();
-  Dict d;  // strings of this call
-  std::vector<int64_t> avail, pods, lbl, sel;
-  std::vector<uint32_t> flags;
-  std::vector<int32_t> lbl_off{0}, tnt_off{0}, tnt;
-  for (uint64_t i = 0; i < n_nodes; i++) {
-    const kp_node& nd = nodes[i];
-    QtyMap al, rqd;
-    if (!qmap(nd.allocatable, nd.n_allocatable, &al) || !qmap(nd.requested, nd.n_requested, &rqd)) {
-      e->err = "kp_node_max_replicas: unparsable node quantity";
-      return KP_EINVAL;
-    }
-    NodeRes a, r;  // getNodeAvailableResource (noderesource.go:135-144)
-    res_add(a, al);
-    res_add(r, rqd);
-    for (int j = 0; j < NQ; j++) {
-      int64_t x;
-      if (qn[j] == "cpu") x = std::max<int64_t>(a.cpu - r.cpu, 0);
-      else if (qn[j] == "memory") x = std::max<int64_t>(a.mem - r.mem, 0);
-      else if (qn[j] == "ephemeral-storage") x = std::max<int64_t>(a.eph - r.eph, 0);
-      else {
-        auto ia = a.sc.find(qn[j]);
-        auto ir = r.sc.find(qn[j]);
-        x = ia == a.sc.end() ? 0 : (ir == r.sc.end() ? ia->second : std::max<int64_t>(ia->second - ir->second, 0));
-      }
-      avail.push_back(x);
-    }
-    pods.push_back(std::max<int64_t>(std::max<int64_t>(a.pods - r.pods, 0) - (int64_t)nd.n_pods, 0));
-    flags.push_back(nd.unschedulable ? 1u : 0u);
-    std::map<std::string, std::string> lm;
-    for (uint32_t j = 0; j < nd.n_labels; j++) lm[S(nd.labels[j].key)] = S(nd.labels[j].value);
-    for (auto& kv : lm) lbl.push_back(((int64_t)d.add(kv.first) << 32) | (int64_t)(uint32_t)d.add(kv.second));
-    lbl_off.push_back((int32_t)lbl.size());
-    for (uint32_t j = 0; j < nd.n_taints; j++) {
-      const std::string ef = S(nd.taints[j].effect);
-      if (ef != "NoSchedule" && ef != "NoExecute") continue;  // DoNotScheduleTaintsFilterFunc
-      tnt.push_back(d.add(S(nd.taints[j].key)));
-      tnt.push_back(d.add(S(nd.taints[j].value)));
-      tnt.push_back(ef == "NoSchedule" ? EFF_NOSCHEDULE : EFF_NOEXECUTE);
-    }
-    tnt_off.push_back((int32_t)(tnt.size() / 3));
+  int32_t sum = 0;
+  const int rc = node_job_run(e, J, claim, &E, &sum);
+  if (rc != KP_OK) return rc;
+  *out = sum;
+  return KP_OK;
+}
+
+int kp_node_max_component_sets(kp_engine* e, const kp_node* nodes, uint64_t n_nodes,
+                               const kp_node_component* comps, uint32_t K, const kp_assumed_workload* assumed,
+                               uint32_t n_assumed, int32_t* out) {
+  if (!e || !out || (n_nodes && !nodes) || (K && !comps) || (n_assumed && !assumed)) return KP_EINVAL;
+  (void)dev::set_device(e->device);
+  *out = 0;
+  if (K == 0) {  // noNodeConstraint (noderesource.go:155-158)
+    *out = INT32_MAX;
+    return KP_OK;
   }
-  std::vector<Tol> tols;
-  int32_t tol_unsched = 0;
-  if (claim) {
-    std::map<std::string, std::string> sm;  // SelectorFromSet: one requirement per key
-    for (uint32_t j = 0; j < claim->n_node_selector; j++)
-      sm[S(claim->node_selector[j].key)] = S(claim->node_selector[j].value);
-    for (auto& kv : sm) sel.push_back(((int64_t)d.add(kv.first) << 32) | (int64_t)(uint32_t)d.add(kv.second));
-    for (uint32_t j = 0; j < claim->n_tolerations; j++) {
-      const kp_toleration& t = claim->tolerations[j];
-      const std::string ef = S(t.effect), key = S(t.key), op = S(t.op), val = S(t.value);
-      // TolerationsTolerateTaint for {node.kubernetes.io/unschedulable, NoSchedule}
-      if ((ef.empty() || ef == "NoSchedule") && (key.empty() || key == "node.kubernetes.io/unschedulable") &&
-          (op == "Exists" || ((op.empty() || op == "Equal") && val.empty())))
-        tol_unsched = 1;
-      Tol x;
-      if (ef.empty()) x.eff = EFF_ANY;
-      else if (ef == "NoSchedule") x.eff = EFF_NOSCHEDULE;
-      else if (ef == "NoExecute") x.eff = EFF_NOEXECUTE;
-      else continue;
-      x.key = key.empty() ? -1 : d.add(key);
-      if (op.empty() || op == "Equal") {
-        x.op = TOL_EQUAL;
-        x.val = d.add(val);
-      } else if (op == "Exists") {
-        x.op = TOL_EXISTS;
-        x.val = -1;
-      } else {
-        continue;  // Lt/Gt disabled, unknown operators never tolerate
-      }
-      tols.push_back(x);
-    }
+  if (K > (uint32_t)kNodeComp) {
+    e->err = "kp_node_max_component_sets: more than 16 components";
+    return KP_ENOTSUP;
   }
-  Arena ar;
-  int64_t *d_avail, *d_q, *d_pods, *d_lbl, *d_sel;
-  uint32_t *d_flags, *d_sum;
-  int32_t *d_loff, *d_toff, *d_tnt;
-  Tol* d_tols;
-  ar.add(&d_avail, std::max<size_t>(1, avail.size()));
-  ar.add(&d_q, std::max<size_t>(1, qv.size()));
-  ar.add(&d_pods, pods.size());
-  ar.add(&d_flags, flags.size());
-  ar.add(&d_loff, lbl_off.size());
-  ar.add(&d_lbl, std::max<size_t>(1, lbl.size()));
-  ar.add(&d_toff, tnt_off.size());
-  ar.add(&d_tnt, std::max<size_t>(1, tnt.size()));
-  ar.add(&d_sel, std::max<size_t>(1, sel.size()));
-  ar.add(&d_tols, std::max<size_t>(1, tols.size()));
-  ar.add(&d_sum, 1);
-  HIPCHK(ar.alloc());
-  dev::stream_t st = e->stream;
-  auto up = [&](void* dd, const void* h, size_t bytes) { return dev::h2d(dd, h, bytes, st); };
-  HIPCHK(up(d_avail, avail.data(), 8 * avail.size()));
-  HIPCHK(up(d_q, qv.data(), 8 * qv.size()));
-  HIPCHK(up(d_pods, pods.data(), 8 * pods.size()));
-  HIPCHK(up(d_flags, flags.data(), 4 * flags.size()));
-  HIPCHK(up(d_loff, lbl_off.data(), 4 * lbl_off.size()));
-  HIPCHK(up(d_lbl, lbl.data(), 8 * lbl.size()));
-  HIPCHK(up(d_toff, tnt_off.data(), 4 * tnt_off.size()));
-  HIPCHK(up(d_tnt, tnt.data(), 4 * tnt.size()));
-  HIPCHK(up(d_sel, sel.data(), 8 * sel.size()));
-  HIPCHK(up(d_tols, tols.data(), sizeof(Tol) * tols.size()));
-  HIPCHK(dev::fill(d_sum, 0, 4, st));
-  NodeEstArgs A;
-  A.n = n_nodes;
-  A.NQ = NQ;
-  A.avail = d_avail;
-  A.q = d_q;
-  A.pods = d_pods;
-  A.flags = d_flags;
-  A.lbl_off = d_loff;
-  A.lbl = d_lbl;
-  A.tnt_off = d_toff;
-  A.tnt = d_tnt;
-  A.sel = d_sel;
-  A.n_sel = (int32_t)sel.size();
-  A.tols = d_tols;
-  A.n_tols = (int32_t)tols.size();
-  A.tol_unsched = tol_unsched;
-  A.sum = d_sum;
-  HIPCHK(dev::node_est(st, A));
-  uint32_t sum = 0;
-  HIPCHK(dev::d2h(&sum, d_sum, 4, st));
-  HIPCHK(dev::sync(st));
-  *out = (int32_t)sum;
+  NodeJob J;
+  if (J.build(nodes, n_nodes, assumed, n_assumed, comps, K, nullptr) != KP_OK) {
+    e->err = "kp_node_max_component_sets: " + J.err;
+    return J.rc;
+  }
+  if (n_nodes == 0) return KP_OK;  // no node holds a set
+  int32_t sets = 0;
+  const int rc = node_job_run(e, J, nullptr, nullptr, &sets);
+  if (rc != KP_OK) return rc;
+  *out = sets;
   return KP_OK;
 }
 

@@ -179,8 +179,17 @@ extern "C" __global__ void __launch_bounds__(256) k_node_est(NodeEstArgs A) {
   __shared__ int64_t red[128];
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const GpuBlk B{red};
-  const int64_t s = B.sum64(i < A.n ? (int64_t)(uint32_t)node_replicas(A, i) : 0);
+  const int64_t s = B.sum64(i < A.v.n ? (int64_t)(uint32_t)node_replicas(A, i) : 0);
   if (threadIdx.x == 0) atomicAdd(A.sum, (uint32_t)(uint64_t)s);  // mod 2^32: Go's wrapping int32 adds
+}
+extern "C" __global__ void __launch_bounds__(256) k_node_match(NodeView v, const ClaimProg* P, uint64_t n,
+                                                               uint8_t* match) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) body_node_match(v, P, i, match);
+}
+extern "C" __global__ void __launch_bounds__(64) k_node_sets(const NodeSetsArgs* A) {
+  __shared__ int64_t red[2];
+  node_sets(WaveBlk{red}, *A);
 }
 extern "C" __global__ void __launch_bounds__(256) k_reasons(SnapView s, BatchView bv, uint64_t n, uint32_t* out) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
@@ -428,8 +437,20 @@ int grades(stream_t st, const GradesArgs& A) {
 }
 
 int node_est(stream_t st, const NodeEstArgs& A) {
-  if (A.n == 0) return 0;
-  hipLaunchKernelGGL(k_node_est, dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, (hipStream_t)st, A);
+  if (A.v.n == 0) return 0;
+  hipLaunchKernelGGL(k_node_est, dim3((unsigned)((A.v.n + 255) / 256)), dim3(256), 0, (hipStream_t)st, A);
+  return chk(hipGetLastError());
+}
+
+int node_match(stream_t st, const NodeView& v, const ClaimProg* P, int K, uint8_t* match) {
+  const uint64_t n = v.n * (uint64_t)K;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_node_match, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)st, v, P, n, match);
+  return chk(hipGetLastError());
+}
+
+int node_sets(stream_t st, const NodeSetsArgs* A) {
+  hipLaunchKernelGGL(k_node_sets, dim3(1), dim3(64), 0, (hipStream_t)st, A);
   return chk(hipGetLastError());
 }
 

@@ -16,6 +16,9 @@ struct SetsArgs;
 struct TopArgs;
 struct GradesArgs;
 struct NodeEstArgs;
+struct NodeView;
+struct ClaimProg;
+struct NodeSetsArgs;
 namespace dev {
 
 typedef void* stream_t;
@@ -86,6 +89,10 @@ int rows_from_class(stream_t st, const SnapView& s, const BatchView& bv, const i
 int grades(stream_t st, const GradesArgs& A);
 // kp_node_max_replicas: *A.sum += int32 sum of node_replicas over the nodes (wrapping).
 int node_est(stream_t st, const NodeEstArgs& A);
+// kp_node_max_component_sets: match[k * n + j] = MatchNode(node j, P[k]) (P in
+// device memory), then the first-fit set simulation by one wave (A in device memory).
+int node_match(stream_t st, const NodeView& v, const ClaimProg* P, int K, uint8_t* match);
+int node_sets(stream_t st, const NodeSetsArgs* A);
 // kp_filter_reasons: out[b * C + r] = pair_reason of binding b, cluster rank r.
 int reasons(stream_t st, const SnapView& s, const BatchView& bv, uint32_t* out);
 // CSR offsets[n + 1] of the per-binding results (counts of OK bindings), on the device;

@@ -25,7 +25,7 @@ from karmada_amd import api
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libkp.so")
-KP_ABI_VERSION = 10
+KP_ABI_VERSION = 11
 
 _LIBS = {}
 
@@ -35,7 +35,7 @@ EXPORTS = (
     "kp_snapshot_destroy", "kp_snapshot_export", "kp_snapshot_import", "kp_snapshot_update", "kp_batch_create",
     "kp_batch_destroy",
     "kp_schedule_batch", "kp_schedule_affinities", "kp_filter_batch", "kp_filter_reasons", "kp_score_batch", "kp_max_available_replicas", "kp_max_available_component_sets",
-    "kp_model_grades", "kp_node_max_replicas", "kp_last_stage_times",
+    "kp_model_grades", "kp_node_max_replicas", "kp_node_max_component_sets", "kp_last_stage_times",
 )
 
 KP_OK, KP_EINVAL, KP_ENOMEM, KP_EDEVICE, KP_ENOTSUP, KP_ESTATE = 0, -1, -2, -3, -4, -5
@@ -78,7 +78,11 @@ def load_library(path: str = LIB_PATH):
     L.kp_model_grades.argtypes = [vp, C.POINTER(api.kp_resource_model), C.c_uint32, C.POINTER(api.kp_node),
                                   C.c_uint64, C.POINTER(C.c_int64)]
     L.kp_node_max_replicas.argtypes = [vp, C.POINTER(api.kp_node), C.c_uint64, C.POINTER(api.kp_resource), C.c_uint32,
-                                       C.POINTER(api.kp_node_claim), C.POINTER(C.c_int32)]
+                                       C.POINTER(api.kp_node_claim), C.POINTER(api.kp_assumed_workload), C.c_uint32,
+                                       C.POINTER(C.c_int32)]
+    L.kp_node_max_component_sets.argtypes = [vp, C.POINTER(api.kp_node), C.c_uint64, C.POINTER(api.kp_node_component),
+                                             C.c_uint32, C.POINTER(api.kp_assumed_workload), C.c_uint32,
+                                             C.POINTER(C.c_int32)]
     L.kp_snapshot_export.argtypes = [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
     L.kp_snapshot_import.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(vp)]
     L.kp_snapshot_update.argtypes = [vp, vp, C.POINTER(api.kp_cluster), C.c_uint64, C.POINTER(C.c_int)]
@@ -148,16 +152,31 @@ class Engine:
         return [int(out[i]) for i in range(nm)]
 
     def node_max_replicas(self, nodes: Sequence[dict], request: Optional[Dict[str, str]],
-                          node_claim: Optional[dict] = None) -> int:
+                          node_claim: Optional[dict] = None, assumed: Optional[Sequence[dict]] = None) -> int:
         """The estimator server's per-node answer (kp_node_max_replicas;
-        noderesource.go:70-131) for one ReplicaRequirements."""
+        noderesource.go:70-131) for one ReplicaRequirements, after the assumed
+        workloads' deduction."""
         w = api.World()
         na, nn = w.nodes(nodes)
         ra, nr = w.resources(request)
         claim = w.node_claim(node_claim)
+        aa, namd = w.assumed_workloads(assumed)
         out = C.c_int32()
         self._check(self.L.kp_node_max_replicas(self.h, na, nn, ra, nr, C.byref(claim) if claim is not None else None,
-                                                C.byref(out)), "kp_node_max_replicas")
+                                                aa, namd, C.byref(out)), "kp_node_max_replicas")
+        return int(out.value)
+
+    def node_max_component_sets(self, nodes: Sequence[dict], components: Sequence[dict],
+                                assumed: Optional[Sequence[dict]] = None) -> int:
+        """The estimator server's component-set answer (kp_node_max_component_sets;
+        noderesource.go:146-190): complete sets of `components` the nodes hold."""
+        w = api.World()
+        na, nn = w.nodes(nodes)
+        ca, nc = w.node_components(components)
+        aa, namd = w.assumed_workloads(assumed)
+        out = C.c_int32()
+        self._check(self.L.kp_node_max_component_sets(self.h, na, nn, ca, nc, aa, namd, C.byref(out)),
+                    "kp_node_max_component_sets")
         return int(out.value)
 
     def stage_times(self) -> Dict[str, float]:

@@ -3024,58 +3024,247 @@ int kpo_model_grades(const kp_resource_model* models, uint32_t n_models, const k
   return 0;
 }
 
-// nodeResourceEstimator.Estimate (noderesource.go:70-131), no assumed workloads:
-// MatchNode (filter.go:60-90) then the int32 sum of MaxDivided over the nodes'
-// available resources (getNodeAvailableResource, :135-144).
+// ---- estimator server node matching (estimator/server/nodes/filter.go:38-99) ----
+// nodeaffinity.RequiredNodeAffinity (vendor/k8s.io/component-helpers/scheduling/
+// corev1/nodeaffinity/nodeaffinity.go:39-333): the nodeSelector as
+// labels.SelectorFromSet, and the required terms as a LazyErrorNodeSelector.
+struct NodeTerm {
+  bool parse_err = false;
+  bool has_labels = false, has_fields = false;
+  vector<Requirement> labels;
+  vector<std::pair<string, std::pair<bool, string>>> fields;  // key, (In?, value)
+};
+struct RequiredNodeAffinity {
+  bool has_selector = false;
+  LabelSet selector;
+  bool has_affinity = false;
+  vector<NodeTerm> terms;
+};
+// GetRequiredNodeAffinity (filter.go:38-57; nodeaffinity.go:306-319)
+RequiredNodeAffinity GetRequiredNodeAffinity(const kp_node_claim* c) {
+  RequiredNodeAffinity a;
+  if (!c) return a;
+  for (uint32_t j = 0; j < c->n_node_selector; j++) a.selector[S(c->node_selector[j].key)] = S(c->node_selector[j].value);
+  a.has_selector = !a.selector.empty();
+  if (!c->has_node_affinity) return a;  // UnmarshalNodeAffinity: no bytes -> nil
+  a.has_affinity = true;
+  for (uint32_t t = 0; t < c->n_node_affinity_terms; t++) {  // NewLazyErrorNodeSelector
+    const kp_node_selector_term& term = c->node_affinity_terms[t];
+    if (term.n_match_expressions == 0 && term.n_match_fields == 0) continue;  // isEmptyNodeSelectorTerm
+    NodeTerm nt;
+    if (term.n_match_expressions) {  // nodeSelectorRequirementsAsSelector (:213-250)
+      nt.has_labels = true;
+      vector<Req> rs;
+      for (uint32_t q = 0; q < term.n_match_expressions; q++) {
+        const kp_requirement& r = term.match_expressions[q];
+        Req x{S(r.key), S(r.op), {}};
+        for (uint32_t j = 0; j < r.n_values; j++) x.values.push_back(S(r.values[j]));
+        rs.push_back(x);
+      }
+      if (!NodeSelectorRequirementsAsSelector(rs, &nt.labels)) nt.parse_err = true;
+    }
+    if (term.n_match_fields) {  // nodeSelectorRequirementsAsFieldSelector (:257-289)
+      nt.has_fields = true;
+      for (uint32_t q = 0; q < term.n_match_fields; q++) {
+        const kp_requirement& r = term.match_fields[q];
+        const string op = S(r.op);
+        if ((op != "In" && op != "NotIn") || r.n_values != 1) {
+          nt.parse_err = true;
+          continue;
+        }
+        nt.fields.push_back({S(r.key), {op == "In", S(r.values[0])}});
+      }
+    }
+    a.terms.push_back(nt);
+  }
+  return a;
+}
+// RequiredNodeAffinity.Match (nodeaffinity.go:321-333) with errors ignored
+// (IsNodeAffinityMatched, filter.go:60-64).
+bool NodeAffinityMatches(const RequiredNodeAffinity& a, const kp_node& nd) {
+  LabelSet labels;
+  for (uint32_t j = 0; j < nd.n_labels; j++) labels[S(nd.labels[j].key)] = S(nd.labels[j].value);
+  if (a.has_selector)
+    for (auto& kv : a.selector) {
+      auto it = labels.find(kv.first);
+      if (it == labels.end() || it->second != kv.second) return false;
+    }
+  if (!a.has_affinity) return true;
+  std::map<string, string> fields;  // extractNodeFields
+  if (nd.name.len) fields["metadata.name"] = S(nd.name);
+  for (auto& t : a.terms) {  // LazyErrorNodeSelector.Match: any term
+    if (t.parse_err) continue;
+    bool ok = true;
+    if (t.has_labels)
+      for (auto& r : t.labels) ok = ok && ReqMatches(r, labels);
+    if (ok && t.has_fields && !fields.empty())
+      for (auto& f : t.fields) {
+        auto it = fields.find(f.first);
+        const string v = it == fields.end() ? string() : it->second;
+        ok = ok && ((v == f.second.second) == f.second.first);
+      }
+    if (ok) return true;
+  }
+  return false;
+}
+// IsTolerationMatched (filter.go:66-92)
+bool TolerationMatches(const kp_node& nd, const vector<Toleration>& tols) {
+  const Taint unsched{"node.kubernetes.io/unschedulable", "", "NoSchedule"};
+  bool tolUnsched = false;
+  for (auto& t : tols) tolUnsched = tolUnsched || ToleratesTaint(t, unsched);
+  if (nd.unschedulable && !tolUnsched) return false;
+  for (uint32_t j = 0; j < nd.n_taints; j++) {
+    const Taint taint{S(nd.taints[j].key), S(nd.taints[j].value), S(nd.taints[j].effect)};
+    if (!(taint.effect == "NoSchedule" || taint.effect == "NoExecute")) continue;
+    bool tol = false;
+    for (auto& t : tols) tol = tol || ToleratesTaint(t, taint);
+    if (!tol) return false;
+  }
+  return true;
+}
+vector<Toleration> TolerationsOf(const kp_node_claim* c) {
+  vector<Toleration> tols;
+  if (c)
+    for (uint32_t j = 0; j < c->n_tolerations; j++) {
+      const kp_toleration& t = c->tolerations[j];
+      tols.push_back(Toleration{S(t.key), S(t.op), S(t.value), S(t.effect)});
+    }
+  return tols;
+}
+// getNodeAvailableResource (noderesource.go:135-144)
+static bool NodeAvailable(const kp_node& nd, Resource* rest) {
+  bool ok = true;
+  Resource rq;
+  rest->Add(rl_of(nd.allocatable, nd.n_allocatable, &ok));
+  rq.Add(rl_of(nd.requested, nd.n_requested, &ok));
+  rest->Sub(rq);
+  rest->AllowedPodNumber = std::max<i64>(rest->AllowedPodNumber - (i64)nd.n_pods, 0);
+  return ok;
+}
+
+// SchedulingSimulator (scheduling_simulator_components.go:26-131) over the nodes'
+// available resources, literally: each set places every component first-fit from
+// the first node, one scan per component per set.
+struct NodeSimulator {
+  const kp_node* nodes;
+  uint64_t n;
+  vector<Resource> avail;  // node.Allocatable after getNodeAvailableResource
+  struct Comp {
+    Resource per;  // requiredPerReplica
+    RequiredNodeAffinity aff;
+    vector<Toleration> tols;
+    int32_t replicas;
+  };
+  bool init(const kp_node* ns, uint64_t nn) {
+    nodes = ns;
+    n = nn;
+    avail.assign(nn, Resource());
+    for (uint64_t i = 0; i < nn; i++)
+      if (!NodeAvailable(nodes[i], &avail[i])) return false;
+    return true;
+  }
+  static bool comps_of(const kp_node_component* comps, uint32_t K, vector<Comp>* out) {
+    out->assign(K, Comp());
+    for (uint32_t k = 0; k < K; k++) {
+      bool ok = true;
+      Comp& c = (*out)[k];
+      if (comps[k].has_replica_requirements) {
+        c.per.Add(rl_of(comps[k].resource_request, comps[k].n_resource_request, &ok));
+        if (!ok) return false;
+        c.aff = GetRequiredNodeAffinity(comps[k].node_claim);
+        c.tols = TolerationsOf(comps[k].node_claim);
+      }
+      c.per.AllowedPodNumber = 1;
+      c.replicas = comps[k].replicas;
+    }
+    return true;
+  }
+  static Resource multiply(Resource r, i64 f) {  // Resource.Multiply (resource.go:77-94), wrapping
+    auto m = [f](i64 v) { return (i64)((uint64_t)v * (uint64_t)f); };
+    r.MilliCPU = m(r.MilliCPU);
+    r.Memory = m(r.Memory);
+    r.EphemeralStorage = m(r.EphemeralStorage);
+    r.AllowedPodNumber = m(r.AllowedPodNumber);
+    for (auto& kv : r.Scalar) kv.second = m(kv.second);
+    return r;
+  }
+  bool scheduleComponent(const Comp& c) {  // (:95-131)
+    int32_t remaining = c.replicas;
+    for (uint64_t i = 0; i < n; i++) {
+      if (!(NodeAffinityMatches(c.aff, nodes[i]) && TolerationMatches(nodes[i], c.tols))) continue;
+      i64 allocatable = avail[i].MaxDivided(c.per);
+      if (allocatable == 0) continue;
+      if ((i64)remaining < allocatable) allocatable = remaining;
+      avail[i].Sub(multiply(c.per, allocatable));
+      remaining = (int32_t)(uint32_t)((uint32_t)remaining - (uint32_t)(int32_t)allocatable);
+      if (remaining == 0) return true;
+    }
+    return remaining == 0;
+  }
+  int32_t SimulateScheduling(const vector<Comp>& cs, int32_t upperBound) {  // (:51-77)
+    int32_t complete = 0;
+    while (complete < upperBound) {
+      bool ok = true;
+      for (size_t k = 0; k < cs.size() && ok; k++) ok = scheduleComponent(cs[k]);
+      if (!ok) break;
+      complete++;
+      bool any = false;  // a set of zero-replica components repeats to the bound unchanged
+      for (auto& c : cs) any = any || c.replicas != 0;
+      if (!any) return upperBound;
+    }
+    return complete;
+  }
+  // the assumed-workload deduction (noderesource.go:95-113,166-185)
+  bool deduct(const kp_assumed_workload* assumed, uint32_t n_assumed) {
+    for (uint32_t w = 0; w < n_assumed; w++) {
+      if (assumed[w].n_components == 0) continue;
+      vector<Comp> cs;
+      if (!comps_of(assumed[w].components, assumed[w].n_components, &cs)) return false;
+      SimulateScheduling(cs, 1);
+    }
+    return true;
+  }
+};
+
+// nodeResourceEstimator.Estimate (noderesource.go:70-131): the assumed workloads
+// deducted, then MatchNode (scheduling_simulator_components.go:149-156) and the
+// int32 sum of MaxDivided over the nodes' available resources.
 int kpo_node_max_replicas(const kp_node* nodes, uint64_t n_nodes, const kp_resource* request, uint32_t n_request,
-                          const kp_node_claim* claim, int32_t* out) {
+                          const kp_node_claim* claim, const kp_assumed_workload* assumed, uint32_t n_assumed,
+                          int32_t* out) {
   *out = 0;
-  if (claim && claim->has_node_affinity) return -2;
   bool ok = true;
   Resource req;
   req.Add(rl_of(request, n_request, &ok));
   if (!ok) return -1;
-  std::map<string, string> selector;
-  vector<Toleration> tols;
-  if (claim) {
-    for (uint32_t j = 0; j < claim->n_node_selector; j++)
-      selector[S(claim->node_selector[j].key)] = S(claim->node_selector[j].value);
-    for (uint32_t j = 0; j < claim->n_tolerations; j++) {
-      const kp_toleration& t = claim->tolerations[j];
-      tols.push_back(Toleration{S(t.key), S(t.op), S(t.value), S(t.effect)});
-    }
-  }
-  const Taint unsched{"node.kubernetes.io/unschedulable", "", "NoSchedule"};
-  bool tolUnsched = false;
-  for (auto& t : tols) tolUnsched = tolUnsched || ToleratesTaint(t, unsched);
+  NodeSimulator sim;
+  if (!sim.init(nodes, n_nodes) || !sim.deduct(assumed, n_assumed)) return -1;
+  const RequiredNodeAffinity aff = GetRequiredNodeAffinity(claim);
+  const vector<Toleration> tols = TolerationsOf(claim);
   uint32_t res = 0;  // atomic.AddInt32 wraps
   for (uint64_t k = 0; k < n_nodes; k++) {
-    const kp_node& nd = nodes[k];
-    std::map<string, string> labels;
-    for (uint32_t j = 0; j < nd.n_labels; j++) labels[S(nd.labels[j].key)] = S(nd.labels[j].value);
-    bool match = true;
-    for (auto& kv : selector) {  // labels.SelectorFromSet
-      auto it = labels.find(kv.first);
-      if (it == labels.end() || it->second != kv.second) match = false;
-    }
-    if (nd.unschedulable && !tolUnsched) match = false;
-    for (uint32_t j = 0; j < nd.n_taints && match; j++) {
-      const Taint taint{S(nd.taints[j].key), S(nd.taints[j].value), S(nd.taints[j].effect)};
-      if (!(taint.effect == "NoSchedule" || taint.effect == "NoExecute")) continue;
-      bool tol = false;
-      for (auto& t : tols) tol = tol || ToleratesTaint(t, taint);
-      if (!tol) match = false;
-    }
-    if (!match) continue;
-    Resource rest, rq;
-    rest.Add(rl_of(nd.allocatable, nd.n_allocatable, &ok));
-    rq.Add(rl_of(nd.requested, nd.n_requested, &ok));
-    if (!ok) return -1;
-    rest.Sub(rq);
-    rest.AllowedPodNumber = std::max<i64>(rest.AllowedPodNumber - (i64)nd.n_pods, 0);
-    res += (uint32_t)(int32_t)rest.MaxDivided(req);
+    if (!(NodeAffinityMatches(aff, nodes[k]) && TolerationMatches(nodes[k], tols))) continue;
+    res += (uint32_t)(int32_t)sim.avail[k].MaxDivided(req);
   }
   *out = (int32_t)res;
+  return 0;
+}
+
+// nodeResourceEstimator.EstimateComponents (noderesource.go:146-190):
+// SimulateScheduling(components, MaxInt32) after the deduction; MaxInt32 for an
+// empty component list.
+int kpo_node_max_component_sets(const kp_node* nodes, uint64_t n_nodes, const kp_node_component* comps, uint32_t K,
+                                const kp_assumed_workload* assumed, uint32_t n_assumed, int32_t* out) {
+  *out = 0;
+  if (K == 0) {
+    *out = INT32_MAX;
+    return 0;
+  }
+  NodeSimulator sim;
+  if (!sim.init(nodes, n_nodes) || !sim.deduct(assumed, n_assumed)) return -1;
+  vector<NodeSimulator::Comp> cs;
+  if (!NodeSimulator::comps_of(comps, K, &cs)) return -1;
+  *out = sim.SimulateScheduling(cs, INT32_MAX);
   return 0;
 }
 }  // extern "C"

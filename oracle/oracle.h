@@ -171,7 +171,10 @@ uint32_t kpo_fnv32a(const char* s, uint32_t len);
 int kpo_model_grades(const kp_resource_model* models, uint32_t n_models, const kp_node* nodes, uint64_t n_nodes,
                      int64_t* out);
 int kpo_node_max_replicas(const kp_node* nodes, uint64_t n_nodes, const kp_resource* request, uint32_t n_request,
-                          const kp_node_claim* claim, int32_t* out);
+                          const kp_node_claim* claim, const kp_assumed_workload* assumed, uint32_t n_assumed,
+                          int32_t* out);
+int kpo_node_max_component_sets(const kp_node* nodes, uint64_t n_nodes, const kp_node_component* comps, uint32_t K,
+                                const kp_assumed_workload* assumed, uint32_t n_assumed, int32_t* out);
 
 #ifdef __cplusplus
 }
