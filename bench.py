@@ -19,7 +19,7 @@ scheduler keeping two batches in flight); `serial_value` is one batch at a time.
 Roofline: the dominant kernel of the step (by its HIP-event time) against HBM
 peak with compulsory bytes, plus the counter-derived DRAM bytes
 (FETCH_SIZE x2 on gfx950 + WRITE_SIZE) and VALU issue fraction of the same
-kernel from the committed PMC summary (profiles/r02_pmc_config<N>.json).
+kernel from the committed PMC summary (profiles/r03_pmc_config<N>.json, else r02).
 """
 import argparse
 import json
@@ -66,11 +66,15 @@ def compulsory_bytes(n_bind, n_all, n_clusters, n_targets, snap_bytes, n_classes
 def load_pmc(config, kernel):
     """Per-launch PMC figures of `kernel` from the committed summary (same bench
     command, default sizes): {hbm_bytes (FETCH_SIZE*2 + WRITE_SIZE), valu_insts, ...}."""
-    try:
-        with open(os.path.join(ROOT, "profiles", f"r02_pmc_config{config}.json")) as f:
-            return json.load(f).get("kernels", {}).get(kernel)
-    except (OSError, ValueError):
-        return None
+    for rnd in ("r03", "r02"):  # the newest summary that holds the kernel
+        try:
+            with open(os.path.join(ROOT, "profiles", f"{rnd}_pmc_config{config}.json")) as f:
+                k = json.load(f).get("kernels", {}).get(kernel)
+        except (OSError, ValueError):
+            continue
+        if k:
+            return k
+    return None
 
 
 def cpu_threads():
@@ -411,7 +415,19 @@ def main():
     pair_b, sel_b = compulsory_bytes(B_rank, int(last["n_sel_all"]), C_, n_targets_rank, snap_bytes,
                                      int(last["n_classes"]) if bits else 0)
     stage = "k_est_class+k_filter" if bits else PAIR_KERNELS.get(last["pair_kind"], "k_pair")
-    cands = [(stage, pair_ms, pair_b), ("k_select_all", sel_all_ms, sel_b)]
+    top_ms = avg("top_kernel_ms")
+    n_top, n_fb, n_all = int(last["n_top"]), int(last["n_top_fallback"]), max(1, int(last["n_sel_all"]))
+    if top_ms > 0 and n_top > 0:
+        # k_select_top alone: its bindings' records and feasibility rows, each class
+        # row and its order (4 B + 4 B per cluster) once, the targets it writes
+        Cp = (C_ + 63) // 64 * 64
+        top_b = (n_top * (B_BIND + Cp / 8.0 + 28) + 8.0 * Cp * int(last["n_classes"])
+                 + 8.0 * n_targets_rank * (n_top - n_fb) / n_all)
+        cands = [(stage, pair_ms, pair_b), ("k_select_top", top_ms, top_b),
+                 ("SEL_ALL rest (k_class_order + k_select_all fallback + streamed)", sel_all_ms - top_ms,
+                  sel_b - top_b)]
+    else:
+        cands = [(stage, pair_ms, pair_b), ("k_select_all", sel_all_ms, sel_b)]
     kname, kms, kbytes = max(cands, key=lambda x: x[1])
     achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     profiled = (C_, B) == tuple(synth.CONFIGS[cfg])
@@ -457,6 +473,7 @@ def main():
         # filter stage: k_est_class + k_filter (bits mode) or the pair kernel
         "stages_ms": {"filter_stage": round(pair_ms, 3), "filter_kernel": round(filter_ms, 3),
                       "select_kernels": round(sel_ms, 3), "sel_all_kernel": round(sel_all_ms, 3),
+                      "select_top_kernel": round(top_ms, 3),
                       "host_region": round(avg("host_ms"), 3), "copy_back": round(avg("copy_ms"), 3),
                       "call_total": round(avg("total_ms"), 3)},
         "filter_mode": "bitset filter + estimator classes" if bits else "per-binding pair rows",

@@ -362,6 +362,7 @@ typedef struct kp_stage_times {
   uint32_t n_classes;      /* estimator-class rows computed (bits == 1; row 0 = non-workload) */
   uint32_t n_top;          /* SEL_ALL bindings given to k_select_top (deciding-candidate subsets) */
   uint32_t n_top_fallback; /* of those, the ones it handed to the full-candidate kernel */
+  float top_kernel_ms;     /* k_select_top alone (HIP events on its stream), 0 when it did not run */
 } kp_stage_times;
 
 /* ------------------------------------------------------------------------- */

@@ -114,7 +114,7 @@ struct kp_engine {
   dev::stream_t stream = nullptr;   // select kernels, copies (the batch's result order)
   dev::stream_t stream2 = nullptr;  // pair kernel, then the SEL_ALL select kernel
   dev::stream_t stream3 = nullptr;  // the cluster-spread select kernel, beside the other selects
-  dev::event_t ev[12] = {};
+  dev::event_t ev[14] = {};
   std::string err;
   kp_stage_times times{};
   struct {  // kp_schedule_affinities results
@@ -2269,7 +2269,9 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
       g.n = bt->n_all_dyn;
       TopArgs ta{bt->d_ord, bt->d_ctot, bt->d_cok, bt->d_fb, bt->stats + 9, e->top_cap};
       const size_t slice = (top_lds_bytes(s->Cp, e->top_cap) + 15) & ~(size_t)15;
+      HIPCHK(dev::event_record(e->ev[12], sp));
       HIPCHK(dev::select_top(sp, g, ta, slice));
+      HIPCHK(dev::event_record(e->ev[13], sp));
       KArgs f = k;
       f.list = bt->d_fb;
       f.n = bt->n_all_dyn;
@@ -2436,6 +2438,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   tm.n_slow = bt->h_stats[0];
   tm.n_top = top ? (uint32_t)bt->n_all_dyn : 0u;
   tm.n_top_fallback = top ? bt->h_stats[9] : 0u;
+  tm.top_kernel_ms = top ? dev::event_ms(e->ev[12], e->ev[13]) : 0.f;
 #ifdef KP_STAMPS
   {
     unsigned long long h[32];

@@ -1066,6 +1066,17 @@ KP_HD inline void sort_tcl(uint32_t* name, int32_t* rep, int n) {
 // targets of 2^30 seats or more to the serial emulation (webster_serial).
 constexpr int64_t kSeatWrap = (int64_t)1 << 30;
 KP_HD inline double w_prio(int64_t v, int64_t k) { return (double)v / (double)(2 * k + 1); }
+// Bit pattern of a double and back (positive doubles order as their patterns do).
+KP_HD inline uint64_t kp_dbits(double d) {
+  uint64_t u;
+  __builtin_memcpy(&u, &d, 8);
+  return u;
+}
+KP_HD inline double kp_bitsd(uint64_t u) {
+  double d;
+  __builtin_memcpy(&d, &u, 8);
+  return d;
+}
 
 // #{k >= 0 : prio(v,k) >= t} (ge) or > t, for v >= 0, t > 0, saturating at cap.
 KP_HD inline int64_t w_count(int64_t v, double t, int64_t cap, bool ge) {

@@ -398,6 +398,243 @@ struct StreamCands {
   KP_FI uint64_t okey(const SelCtx& xx, uint32_t rk, int32_t v0) const { return cand_order_key(xx, rk, v0); }
   static constexpr bool kExact = false;
 };
+// StaticWeight SEL_ALL at class level (assignByStaticWeightStrategy, assignment.go:
+// 193-211; getStaticWeightInfoList, division_algorithm.go:38-72; AllocateWebsterSeats,
+// webstermethod.go:112-161). A candidate's vote is the largest weight among the
+// rules whose cluster bitset holds it, so the candidates fall into at most
+// kSwRules + 1 vote classes, counted from the feasibility row by word popcounts.
+// Parties of one class receive the same seats except at the tie priority t*, where
+// the heap orders the tied parties by (seats asc, name): t* (the N-th largest
+// priority, counted with class multiplicities) is found by a W-ary search over the
+// double's bit pattern, each class's seats above t* follow from w_count, the tied
+// classes (distinct seat counts: two integer votes below 2^31 over one divisor
+// never round to the same double) take their extra seat in seat order, and in the
+// one class split by the remaining seats the first k members by name (the last k
+// for a descending UID tie-breaker) take it. Returns false (nothing written) when
+// the general path must run: overflow/duplicate targets, saturated weights, seat
+// counts past 2^30.
+struct SwClass {
+  int64_t v[kSwRules + 1];    // vote of class j (0: not a party)
+  int64_t n[kSwRules + 1];    // members
+  int64_t sgt[kSwRules + 1];  // seats above t*
+  int32_t order[kSwRules];    // rules by weight desc
+  int32_t lend[kSwRules];     // class j = rules order[lend[j-1] .. lend[j]) (equal weights: one class)
+  int32_t bonus[kSwRules + 1];  // 1: every member takes a tie seat
+  int32_t split, k, nc, nl;   // class split by the tie seats, members of it that take one; classes; rule classes
+  int32_t ok;
+};
+template <class BLK>
+KP_FI bool static_class_fast(const BLK& B, const SelCtx& x, const uint64_t* swb, int nsw, int F, SwClass* sh) {
+  KP_STAMP_INIT
+  const BindHdr& h = *x.h;
+  const SnapView& s = *x.s;
+  if (!(h.flags & BF_WORKLOAD_ASSIGN) || (h.flags & (BF_OVERFLOW | BF_DUP_TARGETS))) return false;
+  if ((int64_t)h.replicas >= kSeatWrap) return false;
+  const bool wp = (h.flags & BF_HAS_WP) != 0;
+  const int nr = wp ? nsw : 0;
+  if (B.tid() == 0) {
+    // rules by weight desc: a candidate's vote is its first matching rule's
+    // weight; rules of equal weight form one class
+    int64_t wt[kSwRules];
+    for (int j = 0; j < nr; j++) {
+      wt[j] = kp_ldu(x.bv->lpool + h.sw_w_off + j);
+      int m = j;
+      while (m > 0 && wt[sh->order[m - 1]] < wt[j]) {
+        sh->order[m] = sh->order[m - 1];
+        m--;
+      }
+      sh->order[m] = j;
+    }
+    int nl = 0;
+    for (int j = 0; j < nr; j++) {
+      if (j > 0 && wt[sh->order[j]] == wt[sh->order[j - 1]]) {
+        sh->lend[nl - 1] = j + 1;
+        continue;
+      }
+      sh->v[nl] = wt[sh->order[j]];
+      sh->lend[nl] = j + 1;
+      nl++;
+    }
+    sh->nl = nl;
+    sh->v[nl] = 0;
+  }
+  B.sync();
+  const int nl = sh->nl;
+  // members of rule class j in word w (j == nl: matching no rule)
+  auto rule_mask = [&](int w, int j) {
+    uint64_t rest = x.frow[w];
+    int q = 0;
+    for (int l = 0; l < nl; l++) {
+      uint64_t u = 0;
+      for (; q < sh->lend[l]; q++) u |= swb[(size_t)sh->order[q] * s.W + w];
+      const uint64_t m = rest & u;
+      if (l == j) return m;
+      rest &= ~m;
+    }
+    return rest;
+  };
+  int64_t cnt[kSwRules + 1];
+  for (int j = 0; j <= kSwRules; j++) cnt[j] = 0;
+  for (int w = B.tid(); w < s.W; w += B.nth())
+    for (int j = 0; j <= nl; j++) cnt[j] += popc64(rule_mask(w, j));
+  for (int j = 0; j <= nl; j++) cnt[j] = B.sum64(cnt[j]);
+  if (B.tid() == 0) {
+    SwClass& c = *sh;
+    c.ok = 1;
+    int64_t wsum = 0;
+    for (int j = 0; j < nl; j++) {
+      c.n[j] = cnt[j];
+      if (c.v[j] > 0 && c.n[j] > 0) {
+        if (c.v[j] >= kInt32Max) c.ok = 0;  // SLOW_WEIGHT
+        wsum += c.v[j];
+      }
+    }
+    c.n[nl] = cnt[nl];
+    if (!wp || wsum == 0) {  // every candidate weight 1 (getStaticWeightInfoList): one class
+      c.nc = 1;
+      c.v[0] = 1;
+      c.n[0] = F;
+    } else {
+      c.nc = nl + 1;
+    }
+    for (int j = 0; j < c.nc; j++) {
+      c.sgt[j] = 0;
+      c.bonus[j] = 0;
+    }
+    c.split = -1;
+    c.k = 0;
+  }
+  B.sync();
+  if (!sh->ok) return false;
+  KP_STAMP(x, 2);
+  // class of a candidate: its rule class, or 0 for all of them when weights are all 1
+  const bool one = sh->nc == 1;
+  auto cls_mask = [&](int w, int j) { return one ? x.frow[w] : rule_mask(w, j); };
+  const int32_t N = h.replicas;
+  const int nc = sh->nc;
+  if (N > 0) {
+    // t* = the largest double t with #{priorities >= t} >= N (bit patterns of
+    // positive doubles order as the values do)
+    auto cnt_ge = [&](double t) {
+      int64_t tot = 0;
+      for (int j = 0; j < nc; j++)
+        if (sh->v[j] > 0 && sh->n[j] > 0) tot += sh->n[j] * w_count(sh->v[j], t, (int64_t)N + 1, true);
+      return tot;
+    };
+    int64_t vmax = 0;
+    for (int j = 0; j < nc; j++)
+      if (sh->n[j] > 0 && sh->v[j] > vmax) vmax = sh->v[j];
+    uint64_t lo = 1, hi = kp_dbits((double)vmax);  // cnt_ge(lo) >= N; answer in [lo, hi]
+    const int W = B.wwidth();
+    while (lo < hi) {
+      const uint64_t span = hi - lo;
+      const uint64_t step = span / (uint64_t)(W + 1) + 1;
+      const uint64_t probe = lo + step * (uint64_t)(B.lane() + 1);
+      const bool good = probe <= hi && cnt_ge(kp_bitsd(probe)) >= N;
+      const uint64_t bal = B.wballot(good);
+      // good probes form a prefix (cnt_ge is non-increasing in t)
+      const int ng = bal ? 64 - __builtin_clzll(bal) : 0;
+      const uint64_t nlo = lo + step * (uint64_t)ng;
+      uint64_t nhi = lo + step * (uint64_t)(ng + 1) - 1;
+      lo = nlo;
+      hi = nhi < hi ? nhi : hi;
+    }
+    if (B.tid() == 0) {
+      const double t = kp_bitsd(lo);
+      int64_t G = N;
+      for (int j = 0; j < nc; j++) {
+        if (sh->v[j] <= 0 || sh->n[j] <= 0) continue;
+        sh->sgt[j] = w_count(sh->v[j], t, (int64_t)N + 1, false);
+        G -= sh->n[j] * sh->sgt[j];
+      }
+      // tied classes in seat order take the remaining G seats
+      for (;;) {
+        int best = -1;
+        for (int j = 0; j < nc; j++) {
+          if (sh->v[j] <= 0 || sh->n[j] <= 0 || sh->bonus[j] || j == sh->split) continue;
+          if (w_prio(sh->v[j], sh->sgt[j]) != t) continue;
+          if (best < 0 || sh->sgt[j] < sh->sgt[best]) best = j;
+        }
+        if (best < 0 || G <= 0) break;
+        if (G >= sh->n[best]) {
+          sh->bonus[best] = 1;
+          G -= sh->n[best];
+        } else {
+          sh->split = best;
+          sh->k = (int32_t)G;
+          G = 0;
+        }
+      }
+    }
+    B.sync();
+  }
+  KP_STAMP(x, 3);
+  // emit: each thread owns a contiguous run of words (rank order); a member of the
+  // split class knows its index in the class from the run prefix
+  const bool prop = (h.flags & BF_EMPTY_PROP) != 0;
+  const bool desc = (h.flags & BF_UID_DESC) != 0;
+  const int per = (s.W + B.nth() - 1) / B.nth();
+  const int w0 = B.tid() * per, w1 = w0 + per < s.W ? w0 + per : s.W;
+  auto seats = [&](int j) { return sh->v[j] > 0 ? (int32_t)(sh->sgt[j] + sh->bonus[j]) : (int32_t)0; };
+  int32_t mine = 0, msplit = 0;
+  for (int w = w0; w < w1; w++) {
+    for (int j = 0; j < nc; j++) {
+      const int c = popc64(cls_mask(w, j));
+      if (j == sh->split) msplit += c;
+      if (prop || seats(j) > 0 || j == sh->split) mine += c;  // split members: counted below
+    }
+  }
+  int32_t tsplit;
+  const int32_t before = B.excl_scan(msplit, &tsplit);
+  // members of the split class with a tie seat: names [0, k) ascending, the last k descending
+  const int64_t lo_i = desc ? (int64_t)tsplit - sh->k : 0, hi_i = desc ? (int64_t)tsplit : (int64_t)sh->k;
+  if (sh->split >= 0 && !prop && seats(sh->split) == 0) {  // split members without a seat are not emitted
+    int64_t a0 = before, a1 = (int64_t)before + msplit;
+    const int64_t in = (a1 < hi_i ? a1 : hi_i) - (a0 > lo_i ? a0 : lo_i);
+    mine -= msplit - (int32_t)(in > 0 ? in : 0);
+  }
+  int32_t tot;
+  const int32_t off = B.excl_scan(mine, &tot);
+  const uint64_t base = h.out_off;
+  if (B.tid() == 0) {
+    x.sink.status[x.b] = KP_STATUS_OK;
+    x.sink.err[x.b] = KP_ERR_NONE;
+    x.sink.arg[x.b] = 0;
+    x.sink.start[x.b] = base;
+    x.sink.count[x.b] = (uint32_t)tot;
+  }
+  uint64_t o = base + (uint64_t)off;
+  int64_t si = before;  // index of the next split-class member
+  for (int w = w0; w < w1; w++) {
+    const uint64_t fw = x.frow[w];
+    if (!fw) continue;
+    uint64_t cm[kSwRules + 1];
+    for (int j = 0; j < nc; j++) cm[j] = cls_mask(w, j);
+    uint64_t m = fw;
+    while (m) {
+      const int bit = __builtin_ctzll(m);
+      m &= m - 1;
+      const uint64_t b1 = 1ull << bit;
+      int j = 0;
+      while (j < nc - 1 && !(cm[j] & b1)) j++;
+      int32_t r = seats(j);
+      if (j == sh->split) {
+        if (si >= lo_i && si < hi_i) r++;
+        si++;
+      }
+      if (prop || r > 0) {
+        const uint32_t rk = (uint32_t)(w * 64 + bit);
+        x.sink.out_idx[o] = s.perm[rk];
+        x.sink.out_rep[o] = r;
+        o++;
+      }
+    }
+  }
+  KP_STAMP(x, 4);
+  (void)F;
+  return true;
+}
+
 template <class BLK>
 KP_FI void body_select_all_stream(const BLK& B, int blk, unsigned char* smem, const KArgs& a) {
   if (blk >= a.n) return;
@@ -422,6 +659,9 @@ KP_FI void body_select_all_stream(const BLK& B, int blk, unsigned char* smem, co
   for (int w = B.tid(); w < s.W; w += B.nth()) F += popc64(x.frow[w]);
   F = B.sum64(F);  // (its barrier also publishes tgt and swb)
   KP_STAMP(x, 1);
+  if (weights && (rules || !(h->flags & BF_HAS_WP)) && F > 0 && !(h->flags & BF_BAD)) {
+    if (static_class_fast(B, x, swb, rules ? h->sw_cnt : 0, (int)F, (SwClass*)ss.hist)) return;
+  }
   const StreamCands cs{&x, s.C, B.tid(), B.nth(), weights, rules ? swb : nullptr, rules ? h->sw_cnt : 0};
   select_all_common(B, a, x, cs, (int)F, ss);
 }

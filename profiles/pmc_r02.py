@@ -1,7 +1,7 @@
 """Per-kernel, per-launch PMC summary (the JSON bench.py reads for its roofline) from
 the rocprofv3 passes of prof_pmc.sh: gpurun_out/pmc_<tag>/p*/.
 
-usage: python profiles/pmc_r02.py gpurun_out/pmc_<tag> profiles/r02_pmc_config<N>.json "<bench command>"
+usage: python profiles/pmc_r02.py gpurun_out/pmc_<tag> profiles/r0N_pmc_config<N>.json "<bench command>"
 
 hbm_bytes = FETCH_SIZE*2 + WRITE_SIZE per launch, in bytes: rocprofv3 reports both in
 KiB, and on gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads

@@ -80,3 +80,46 @@ def test_filter_score_gpu(gpu_engine):
     bad = [c["name"] for c in PLUG["filters"] if engine_filter(gpu_engine, c) != c["fit"]]
     bad += [c["name"] for c in PLUG["scores"] if engine_score(gpu_engine, c) != c["score"]]
     assert not bad, bad
+
+
+# Test_extractClusterFields (pkg/util/selector_test.go:927-986): the field set a
+# cluster exposes to FieldSelector requirements (selector.go:187-199) is {provider,
+# region} for the non-empty ones. extractClusterFields is internal, so each table
+# row is observed through ClusterAffinity field selectors: Exists on a field
+# passes exactly when the row's want set holds it, and In [value] on each held
+# field passes.
+EXTRACT_FIELDS = [
+    ("empty", {}, {}),
+    ("provider is set", {"provider": "foo"}, {"provider": "foo"}),
+    ("region is set", {"region": "foo"}, {"region": "foo"}),
+    ("all are set", {"provider": "foo", "region": "bar"}, {"provider": "foo", "region": "bar"}),
+]
+
+
+def field_cases():
+    out = []
+    for name, spec, want in EXTRACT_FIELDS:
+        cluster = {"name": "member1", "labels": {}, **spec}
+        probes = [([{"key": f, "operator": "Exists", "values": []}], f in want) for f in ("provider", "region")]
+        probes += [([{"key": f, "operator": "In", "values": [v]}], True) for f, v in want.items()]
+        probes += [([{"key": f, "operator": "DoesNotExist", "values": []}], f not in want) for f in ("provider", "region")]
+        for exprs, fit in probes:
+            binding = {"placement": {"clusterAffinity": {"fieldSelector": {"matchExpressions": exprs}}}}
+            out.append({"name": f"{name}: {exprs[0]['key']} {exprs[0]['operator']}", "plugin": "ClusterAffinity",
+                        "binding": binding, "cluster": cluster, "fit": fit})
+    return out
+
+
+FIELD_CASES = field_cases()
+
+
+@pytest.mark.parametrize("case", FIELD_CASES, ids=[c["name"] for c in FIELD_CASES])
+def test_extract_cluster_fields(cpusim_engine, case):
+    assert oracle_filter(case) == case["fit"]
+    assert engine_filter(cpusim_engine, case) == case["fit"]
+
+
+@pytest.mark.gpu
+def test_extract_cluster_fields_gpu(gpu_engine):
+    bad = [c["name"] for c in FIELD_CASES if engine_filter(gpu_engine, c) != c["fit"]]
+    assert not bad, bad

@@ -26,6 +26,8 @@ for s in "$@"; do
     chunks) for c in 4096 8192 16384 32768 200000; do KP_CHUNK=$c step chunk_$c 300 python bench.py --steps 5 --warmup 1 --no-cpu; done ;;
     configs) for c in 2 4 6; do step bench_config$c 300 python bench.py --config $c --steps 3 --warmup 1 --no-cpu; done
              step bench_config5 300 python bench.py --config 5 --bindings 125000 --steps 3 --warmup 1 --no-cpu ;;
+    stampsc_*) c=${s#stampsc_}; b=100000; [ "$c" = 5 ] && b=125000
+           step stamps_cfg$c 300 python bench.py --lib karmada_amd/libkp_stamps.so --config $c --bindings $b --steps 2 --warmup 1 --no-cpu --check 0 --inflight 1 --e2e-reps 0 ;;
     stamps) step stamps 300 python bench.py --lib karmada_amd/libkp_stamps.so --steps 2 --warmup 1 --no-cpu --check 0 ;;
     lib_*) n=${s#lib_}; step bench_$n 300 python bench.py --lib karmada_amd/libkp_$n.so --steps 50 --warmup 2 --no-cpu --check 200 ;;
     libst_*) n=${s#libst_}; step stamps_$n 300 python bench.py --lib karmada_amd/libkp_$n.so --steps 2 --warmup 1 --no-cpu --check 0 ;;
@@ -35,6 +37,8 @@ for s in "$@"; do
     prof_write) step prof_write 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --pmc WRITE_SIZE --output-format csv -d $ROOT/gpurun_out/prof_write -o w -- python3 $ROOT/bench.py --steps 2 --warmup 0 --no-cpu" ;;
     dist2) KP_DIST_BACKEND=gloo step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --bindings 20000 ;;
     prof_kt45) for c in 4 5; do step prof_kt$c 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/prof_kt$c -o kt -- python3 $ROOT/bench.py --config $c --bindings 100000 --steps 3 --warmup 1 --no-cpu"; done ;;
+    pmc_*) c=${s#pmc_}; b=100000; [ "$c" = 5 ] && b=125000
+           step pmc_cfg$c 900 bash tools/gpu/prof_pmc.sh cfg$c --config $c --bindings $b ;;
     prof_l2) step prof_l2 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $ROOT/gpurun_out/prof_l2 -o l -- python3 $ROOT/bench.py --steps 2 --warmup 0 --no-cpu" ;;
   esac
 done
