@@ -224,6 +224,11 @@ int node_est(stream_t, const NodeEstArgs& A) {
   return 0;
 }
 
+int select_static(stream_t, const KArgs& a, size_t slice) {
+  grid(a.n, slice, [&](int blk, unsigned char* sm) { body_select_static(CpuBlk{(int64_t*)sm}, blk, sm, a); });
+  return 0;
+}
+
 int node_match(stream_t, const NodeView& v, const ClaimProg* P, int K, uint8_t* match) {
   const uint64_t n = v.n * (uint64_t)K;
   for (uint64_t i = 0; i < n; i++) body_node_match(v, P, i, match);

@@ -167,6 +167,7 @@ struct kp_batch {
   std::vector<Instr> instrs;
   std::vector<int32_t> l_all, l_cluster, l_region, l_slow, l_cs;  // l_cs: cluster + region bindings
   int n_all_dyn = 0;  // l_all = [other strategies | StaticWeight]: the first n_all_dyn are not StaticWeight
+  int n_static = 0;   // of the StaticWeight ones, the first n_static take k_select_static (static_ok)
   uint64_t out_cap = 0;
   Arena dev;
   BatchView view{};
@@ -1977,6 +1978,24 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   bt->n_all_dyn = (int)(std::stable_partition(bt->l_all.begin(), bt->l_all.end(),
                                               [&](int32_t i) { return bt->hdr[i].strategy != ST_STATIC; }) -
                         bt->l_all.begin());
+  // StaticWeight bindings the class-level kernel covers first (bits mode only)
+  {
+    const kp_snapshot* sn = bt->snap;
+    auto static_ok = [&](int32_t i) {
+      const BindHdr& h = bt->hdr[i];
+      if (h.sel != SEL_ALL || h.strategy != ST_STATIC || h.replicas < 0 || (int64_t)h.replicas >= kSeatWrap) return false;
+      if (!(h.flags & BF_WORKLOAD_ASSIGN) || (h.flags & (BF_OVERFLOW | BF_DUP_TARGETS | BF_BAD))) return false;
+      if (sn->view.C >= 65536) return false;  // packed class counts
+      if (h.flags & BF_HAS_WP) {
+        if (h.sw_cnt > kSwRules || sn->view.n_bits <= 0) return false;
+        for (int j = 0; j < h.sw_cnt; j++)
+          if (bt->lpool[h.sw_w_off + j] >= (int64_t)kInt32Max) return false;  // saturated votes: SLOW_WEIGHT
+      }
+      return true;
+    };
+    bt->n_static = (int)(std::stable_partition(bt->l_all.begin() + bt->n_all_dyn, bt->l_all.end(), static_ok) -
+                         (bt->l_all.begin() + bt->n_all_dyn));
+  }
   bt->l_slow = bt->l_all;
   bt->l_slow.insert(bt->l_slow.end(), bt->l_cluster.begin(), bt->l_cluster.end());
   bt->l_cs = bt->l_cluster;
@@ -2283,15 +2302,20 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
       g.n = na;
       HIPCHK(dev::select(sp, SEL_LAUNCH_ALL, g, smem_all(s), cap, sx));
     }
-    if (top && k.n - bt->n_all_dyn > 0) {
+    // the rest: StaticWeight at class level (k_select_static) where it applies, then
+    // the streamed kernel
+    int rest0 = top ? bt->n_all_dyn : na;
+    if (bits && rest0 == bt->n_all_dyn && bt->n_static > 0) {
       KArgs g = k;
-      g.list = bt->d_all + bt->n_all_dyn;
-      g.n = k.n - bt->n_all_dyn;
-      HIPCHK(dev::select(sp, SEL_LAUNCH_ALL_STREAM, g, sel_stream_lds_bytes(s->Cp), cap, sx));
-    } else if (!top && k.n - na > 0) {
+      g.list = bt->d_all + rest0;
+      g.n = bt->n_static;
+      HIPCHK(dev::select_static(sp, g, (static_lds_bytes(s->view.W) + 15) & ~(size_t)15));
+      rest0 += bt->n_static;
+    }
+    if (k.n - rest0 > 0) {
       KArgs g = k;
-      g.list = bt->d_all + na;
-      g.n = k.n - na;
+      g.list = bt->d_all + rest0;
+      g.n = k.n - rest0;
       HIPCHK(dev::select(sp, SEL_LAUNCH_ALL_STREAM, g, sel_stream_lds_bytes(s->Cp), cap, sx));
     }
   }

@@ -97,6 +97,17 @@ extern "C" __global__ void __launch_bounds__(64 * kTopWaves) k_select_top(KArgs 
   if (blk >= a.n) return;  // wave-uniform: the waves never synchronise with each other
   body_select_top(WaveBlk{(int64_t*)mine}, blk, mine, a, t);
 }
+// StaticWeight SEL_ALL at class level (kp_kernels.h body_select_static): one wave per
+// binding, kStaticWaves independent waves per workgroup.
+constexpr int kStaticWaves = 4;
+extern "C" __global__ void __launch_bounds__(64 * kStaticWaves) k_select_static(KArgs a, int slice) {
+  KP_SMEM;
+  const int w = (int)(threadIdx.x >> 6);
+  unsigned char* mine = smem + (size_t)w * (size_t)slice;
+  const int blk = (int)blockIdx.x * kStaticWaves + w;
+  if (blk >= a.n) return;  // wave-uniform: the waves never synchronise with each other
+  body_select_static(WaveBlk{(int64_t*)mine}, blk, mine, a);
+}
 // Each estimator class's row in (estimate desc, rank asc) order: LDS bitonic sort.
 extern "C" __global__ void __launch_bounds__(1024) k_class_order(SnapView s, const int32_t* rows, int P, uint64_t* ord,
                                                                 int64_t* tot, int32_t* ok) {
@@ -396,6 +407,17 @@ int select_top(stream_t st, const KArgs& a, const TopArgs& t, size_t slice) {
     return -1;
   hipLaunchKernelGGL(k_select_top, dim3((a.n + kTopWaves - 1) / kTopWaves), dim3(64 * kTopWaves), smem,
                      (hipStream_t)st, a, t, (int)slice);
+  return chk(hipGetLastError());
+}
+
+int select_static(stream_t st, const KArgs& a, size_t slice) {
+  if (a.n <= 0) return 0;
+  const size_t smem = slice * kStaticWaves;
+  if (smem > 65536 &&
+      chk(hipFuncSetAttribute((const void*)k_select_static, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)))
+    return -1;
+  hipLaunchKernelGGL(k_select_static, dim3((a.n + kStaticWaves - 1) / kStaticWaves), dim3(64 * kStaticWaves), smem,
+                     (hipStream_t)st, a, (int)slice);
   return chk(hipGetLastError());
 }
 

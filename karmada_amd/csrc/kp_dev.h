@@ -89,6 +89,9 @@ int rows_from_class(stream_t st, const SnapView& s, const BatchView& bv, const i
 int grades(stream_t st, const GradesArgs& A);
 // kp_node_max_replicas: *A.sum += int32 sum of node_replicas over the nodes (wrapping).
 int node_est(stream_t st, const NodeEstArgs& A);
+// StaticWeight SEL_ALL bindings a.list[0, a.n) at class level (body_select_static),
+// one wave each with `slice` bytes of LDS.
+int select_static(stream_t st, const KArgs& a, size_t slice);
 // kp_node_max_component_sets: match[k * n + j] = MatchNode(node j, P[k]) (P in
 // device memory), then the first-fit set simulation by one wave (A in device memory).
 int node_match(stream_t st, const NodeView& v, const ClaimProg* P, int K, uint8_t* match);

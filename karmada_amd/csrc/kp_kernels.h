@@ -398,21 +398,22 @@ struct StreamCands {
   KP_FI uint64_t okey(const SelCtx& xx, uint32_t rk, int32_t v0) const { return cand_order_key(xx, rk, v0); }
   static constexpr bool kExact = false;
 };
-// StaticWeight SEL_ALL at class level (assignByStaticWeightStrategy, assignment.go:
-// 193-211; getStaticWeightInfoList, division_algorithm.go:38-72; AllocateWebsterSeats,
-// webstermethod.go:112-161). A candidate's vote is the largest weight among the
-// rules whose cluster bitset holds it, so the candidates fall into at most
-// kSwRules + 1 vote classes, counted from the feasibility row by word popcounts.
+// StaticWeight SEL_ALL at class level (k_select_static, one wave per binding):
+// assignByStaticWeightStrategy (assignment.go:193-211) over getStaticWeightInfoList
+// (division_algorithm.go:38-72) and AllocateWebsterSeats (webstermethod.go:112-161).
+// A candidate's vote is the largest weight among the rules whose cluster bitset
+// holds it, so the candidates fall into at most kSwRules + 1 vote classes (rules
+// of equal weight form one), counted from the feasibility row by word popcounts.
 // Parties of one class receive the same seats except at the tie priority t*, where
 // the heap orders the tied parties by (seats asc, name): t* (the N-th largest
 // priority, counted with class multiplicities) is found by a W-ary search over the
-// double's bit pattern, each class's seats above t* follow from w_count, the tied
-// classes (distinct seat counts: two integer votes below 2^31 over one divisor
-// never round to the same double) take their extra seat in seat order, and in the
-// one class split by the remaining seats the first k members by name (the last k
-// for a descending UID tie-breaker) take it. Returns false (nothing written) when
-// the general path must run: overflow/duplicate targets, saturated weights, seat
-// counts past 2^30.
+// double's bit pattern inside the divisor-method bracket, each class's seats above
+// t* follow from w_count, the tied classes (distinct seat counts: two integer
+// votes below 2^31 over one divisor never round to the same double) take their
+// extra seat in seat order, and in the one class split by the remaining seats the
+// first k members by name (the last k for a descending UID tie-breaker) take it.
+// The host routes here only bindings this covers (select_static_ok); the rest keep
+// the streamed kernel.
 struct SwClass {
   int64_t v[kSwRules + 1];    // vote of class j (0: not a party)
   int64_t n[kSwRules + 1];    // members
@@ -421,17 +422,38 @@ struct SwClass {
   int32_t lend[kSwRules];     // class j = rules order[lend[j-1] .. lend[j]) (equal weights: one class)
   int32_t bonus[kSwRules + 1];  // 1: every member takes a tie seat
   int32_t split, k, nc, nl;   // class split by the tie seats, members of it that take one; classes; rule classes
-  int32_t ok;
+  int32_t ok, pad;
+  uint64_t tbits;             // t*
 };
+// Per-binding LDS of k_select_static: [red 64 | SwClass | rule bits kSwRules x W |
+// emitted W u64 | split members W u64 | split offsets W u32 | emit offsets W u32]
+KP_HD inline size_t static_lds_bytes(int W) {
+  return 64 + ((sizeof(SwClass) + 15) & ~(size_t)15) + 8 * (size_t)kSwRules * W + 16 * (size_t)W + 8 * (size_t)W;
+}
 template <class BLK>
-KP_FI bool static_class_fast(const BLK& B, const SelCtx& x, const uint64_t* swb, int nsw, int F, SwClass* sh) {
+KP_FI void body_select_static(const BLK& B, int blk, unsigned char* smem, const KArgs& a) {
+  if (blk >= a.n) return;
   KP_STAMP_INIT
-  const BindHdr& h = *x.h;
-  const SnapView& s = *x.s;
-  if (!(h.flags & BF_WORKLOAD_ASSIGN) || (h.flags & (BF_OVERFLOW | BF_DUP_TARGETS))) return false;
-  if ((int64_t)h.replicas >= kSeatWrap) return false;
+  const int b = a.list[blk];
+  const SnapView& s = a.s;
+  const int W = s.W;
+  SwClass* sh = (SwClass*)(smem + 64);
+  uint64_t* swb = (uint64_t*)(smem + 64 + ((sizeof(SwClass) + 15) & ~(size_t)15));
+  uint64_t* em = swb + (size_t)kSwRules * W;
+  uint64_t* cms = em + W;
+  uint32_t* spo = (uint32_t*)(cms + W);
+  uint32_t* eo = spo + W;
+  const BindHdr& h = a.bv.hdr[b];
+  SelCtx x = make_ctx(a, b, nullptr);
   const bool wp = (h.flags & BF_HAS_WP) != 0;
-  const int nr = wp ? nsw : 0;
+  const int nr = wp ? h.sw_cnt : 0;
+  // per-thread contiguous word runs (word order = rank order = name order)
+  const int per = (W + B.nth() - 1) / B.nth();
+  const int w0 = B.tid() * per < W ? B.tid() * per : W, w1 = w0 + per < W ? w0 + per : W;
+  int64_t F = 0;
+  for (int w = w0; w < w1; w++) F += popc64(x.frow[w]);
+  for (int i = B.tid(); i < nr * W; i += B.nth())  // getStaticWeightInfoList's ClusterMatches per rule
+    swb[i] = prog_word(s, a.bv, kp_ldu(a.bv.ipool + h.sw_off + i / W), i % W);
   if (B.tid() == 0) {
     // rules by weight desc: a candidate's vote is its first matching rule's
     // weight; rules of equal weight form one class
@@ -458,7 +480,8 @@ KP_FI bool static_class_fast(const BLK& B, const SelCtx& x, const uint64_t* swb,
     sh->nl = nl;
     sh->v[nl] = 0;
   }
-  B.sync();
+  F = B.sum64(F);  // (its barrier also publishes swb and the rule order)
+  if (pre_checks(B, x, (int)F)) return;
   const int nl = sh->nl;
   // members of rule class j in word w (j == nl: matching no rule)
   auto rule_mask = [&](int w, int j) {
@@ -466,28 +489,39 @@ KP_FI bool static_class_fast(const BLK& B, const SelCtx& x, const uint64_t* swb,
     int q = 0;
     for (int l = 0; l < nl; l++) {
       uint64_t u = 0;
-      for (; q < sh->lend[l]; q++) u |= swb[(size_t)sh->order[q] * s.W + w];
+      for (; q < sh->lend[l]; q++) u |= swb[(size_t)sh->order[q] * W + w];
       const uint64_t m = rest & u;
       if (l == j) return m;
       rest &= ~m;
     }
     return rest;
   };
-  int64_t cnt[kSwRules + 1];
-  for (int j = 0; j <= kSwRules; j++) cnt[j] = 0;
-  for (int w = B.tid(); w < s.W; w += B.nth())
-    for (int j = 0; j <= nl; j++) cnt[j] += popc64(rule_mask(w, j));
-  for (int j = 0; j <= nl; j++) cnt[j] = B.sum64(cnt[j]);
+  // class counts: 16-bit fields packed four to an int64 (C < 2^16), one reduction
+  int64_t c03 = 0, c4 = 0;
+  for (int w = w0; w < w1; w++) {
+    uint64_t rest = x.frow[w];
+    int q = 0;
+    for (int l = 0; l < nl; l++) {
+      uint64_t u = 0;
+      for (; q < sh->lend[l]; q++) u |= swb[(size_t)sh->order[q] * W + w];
+      const uint64_t m = rest & u;
+      if (l < 4) c03 += (int64_t)popc64(m) << (16 * l);
+      else c4 += popc64(m);
+      rest &= ~m;
+    }
+    if (nl < 4) c03 += (int64_t)popc64(rest) << (16 * nl);
+    else c4 += popc64(rest);
+  }
+  B.sum2(c03, c4);
+  KP_STAMP(x, 2);
   if (B.tid() == 0) {
     SwClass& c = *sh;
-    c.ok = 1;
+    int64_t cnt[kSwRules + 1];
+    for (int j = 0; j <= nl; j++) cnt[j] = j < 4 ? (c03 >> (16 * j)) & 0xffff : c4;
     int64_t wsum = 0;
     for (int j = 0; j < nl; j++) {
       c.n[j] = cnt[j];
-      if (c.v[j] > 0 && c.n[j] > 0) {
-        if (c.v[j] >= kInt32Max) c.ok = 0;  // SLOW_WEIGHT
-        wsum += c.v[j];
-      }
+      if (c.v[j] > 0 && c.n[j] > 0) wsum += c.v[j];
     }
     c.n[nl] = cnt[nl];
     if (!wp || wsum == 0) {  // every candidate weight 1 (getStaticWeightInfoList): one class
@@ -505,38 +539,47 @@ KP_FI bool static_class_fast(const BLK& B, const SelCtx& x, const uint64_t* swb,
     c.k = 0;
   }
   B.sync();
-  if (!sh->ok) return false;
-  KP_STAMP(x, 2);
-  // class of a candidate: its rule class, or 0 for all of them when weights are all 1
-  const bool one = sh->nc == 1;
-  auto cls_mask = [&](int w, int j) { return one ? x.frow[w] : rule_mask(w, j); };
   const int32_t N = h.replicas;
   const int nc = sh->nc;
+  const bool one = nc == 1;
+  auto cls_mask = [&](int w, int j) { return one ? x.frow[w] : rule_mask(w, j); };
   if (N > 0) {
-    // t* = the largest double t with #{priorities >= t} >= N (bit patterns of
-    // positive doubles order as the values do)
+    // t* = the largest double t with #{priorities >= t} >= N, searched over the bit
+    // patterns of positive doubles (they order as the values) inside the bracket
+    // V/(2N+P) <= t* < V/(2N-P-1) (V: the votes' sum, P: the parties)
     auto cnt_ge = [&](double t) {
       int64_t tot = 0;
       for (int j = 0; j < nc; j++)
         if (sh->v[j] > 0 && sh->n[j] > 0) tot += sh->n[j] * w_count(sh->v[j], t, (int64_t)N + 1, true);
       return tot;
     };
-    int64_t vmax = 0;
+    int64_t vmax = 0, V = 0, P = 0;
     for (int j = 0; j < nc; j++)
-      if (sh->n[j] > 0 && sh->v[j] > vmax) vmax = sh->v[j];
-    uint64_t lo = 1, hi = kp_dbits((double)vmax);  // cnt_ge(lo) >= N; answer in [lo, hi]
-    const int W = B.wwidth();
+      if (sh->n[j] > 0 && sh->v[j] > 0) {
+        vmax = sh->v[j] > vmax ? sh->v[j] : vmax;
+        V += sh->v[j] * sh->n[j];
+        P += sh->n[j];
+      }
+    uint64_t lo = kp_dbits((double)V / (double)(2 * (int64_t)N + P));
+    lo = lo > 8 ? lo - 8 : 1;
+    uint64_t hi = kp_dbits((double)vmax);
+    if (2 * (int64_t)N - P - 1 > 0) {
+      const uint64_t u = kp_dbits((double)V / (double)(2 * (int64_t)N - P - 1)) + 8;
+      hi = u < hi ? u : hi;
+    }
+    if (hi < lo || !(cnt_ge(kp_bitsd(lo)) >= N)) {  // (rounding at the bracket's ends)
+      lo = 1;
+      hi = kp_dbits((double)vmax);
+    }
+    const int ww = B.wwidth();
     while (lo < hi) {
-      const uint64_t span = hi - lo;
-      const uint64_t step = span / (uint64_t)(W + 1) + 1;
+      const uint64_t step = (hi - lo) / (uint64_t)(ww + 1) + 1;
       const uint64_t probe = lo + step * (uint64_t)(B.lane() + 1);
       const bool good = probe <= hi && cnt_ge(kp_bitsd(probe)) >= N;
-      const uint64_t bal = B.wballot(good);
-      // good probes form a prefix (cnt_ge is non-increasing in t)
+      const uint64_t bal = B.wballot(good);  // good probes form a prefix (cnt_ge is non-increasing)
       const int ng = bal ? 64 - __builtin_clzll(bal) : 0;
-      const uint64_t nlo = lo + step * (uint64_t)ng;
-      uint64_t nhi = lo + step * (uint64_t)(ng + 1) - 1;
-      lo = nlo;
+      const uint64_t nhi = lo + step * (uint64_t)(ng + 1) - 1;
+      lo = lo + step * (uint64_t)ng;
       hi = nhi < hi ? nhi : hi;
     }
     if (B.tid() == 0) {
@@ -547,8 +590,7 @@ KP_FI bool static_class_fast(const BLK& B, const SelCtx& x, const uint64_t* swb,
         sh->sgt[j] = w_count(sh->v[j], t, (int64_t)N + 1, false);
         G -= sh->n[j] * sh->sgt[j];
       }
-      // tied classes in seat order take the remaining G seats
-      for (;;) {
+      for (;;) {  // tied classes in seat order take the remaining G seats
         int best = -1;
         for (int j = 0; j < nc; j++) {
           if (sh->v[j] <= 0 || sh->n[j] <= 0 || sh->bonus[j] || j == sh->split) continue;
@@ -569,32 +611,55 @@ KP_FI bool static_class_fast(const BLK& B, const SelCtx& x, const uint64_t* swb,
     B.sync();
   }
   KP_STAMP(x, 3);
-  // emit: each thread owns a contiguous run of words (rank order); a member of the
-  // split class knows its index in the class from the run prefix
+  // emit (removeZeroReplicasCluster unless EnableEmptyWorkloadPropagation), in rank
+  // order: per-word emitted masks and offsets, then one thread per cluster
   const bool prop = (h.flags & BF_EMPTY_PROP) != 0;
   const bool desc = (h.flags & BF_UID_DESC) != 0;
-  const int per = (s.W + B.nth() - 1) / B.nth();
-  const int w0 = B.tid() * per, w1 = w0 + per < s.W ? w0 + per : s.W;
+  const int split = sh->split;
   auto seats = [&](int j) { return sh->v[j] > 0 ? (int32_t)(sh->sgt[j] + sh->bonus[j]) : (int32_t)0; };
-  int32_t mine = 0, msplit = 0;
+  int32_t msplit = 0;
   for (int w = w0; w < w1; w++) {
+    uint64_t e = 0, sp = 0;
     for (int j = 0; j < nc; j++) {
-      const int c = popc64(cls_mask(w, j));
-      if (j == sh->split) msplit += c;
-      if (prop || seats(j) > 0 || j == sh->split) mine += c;  // split members: counted below
+      const uint64_t m = cls_mask(w, j);
+      if (j == split) sp = m;
+      if (prop || seats(j) > 0) e |= m;
     }
+    em[w] = e;
+    cms[w] = sp;
+    msplit += popc64(sp);
   }
   int32_t tsplit;
-  const int32_t before = B.excl_scan(msplit, &tsplit);
-  // members of the split class with a tie seat: names [0, k) ascending, the last k descending
+  int32_t run = B.excl_scan(msplit, &tsplit);
+  // the split class's members with a tie seat: names [0, k) ascending, the last k descending
   const int64_t lo_i = desc ? (int64_t)tsplit - sh->k : 0, hi_i = desc ? (int64_t)tsplit : (int64_t)sh->k;
-  if (sh->split >= 0 && !prop && seats(sh->split) == 0) {  // split members without a seat are not emitted
-    int64_t a0 = before, a1 = (int64_t)before + msplit;
-    const int64_t in = (a1 < hi_i ? a1 : hi_i) - (a0 > lo_i ? a0 : lo_i);
-    mine -= msplit - (int32_t)(in > 0 ? in : 0);
+  int32_t mine = 0;
+  for (int w = w0; w < w1; w++) {
+    spo[w] = (uint32_t)run;
+    uint64_t sp = cms[w];
+    const int c = popc64(sp);
+    if (split >= 0 && c > 0) {
+      if (run >= lo_i && run + c <= hi_i) {
+        em[w] |= sp;
+      } else if (run < hi_i && run + c > lo_i) {
+        int64_t idx = run;
+        while (sp) {
+          const uint64_t bit = sp & (~sp + 1);
+          if (idx >= lo_i && idx < hi_i) em[w] |= bit;
+          sp ^= bit;
+          idx++;
+        }
+      }
+    }
+    run += c;
+    mine += popc64(em[w]);
   }
   int32_t tot;
-  const int32_t off = B.excl_scan(mine, &tot);
+  int32_t off = B.excl_scan(mine, &tot);
+  for (int w = w0; w < w1; w++) {
+    eo[w] = (uint32_t)off;
+    off += popc64(em[w]);
+  }
   const uint64_t base = h.out_off;
   if (B.tid() == 0) {
     x.sink.status[x.b] = KP_STATUS_OK;
@@ -603,36 +668,30 @@ KP_FI bool static_class_fast(const BLK& B, const SelCtx& x, const uint64_t* swb,
     x.sink.start[x.b] = base;
     x.sink.count[x.b] = (uint32_t)tot;
   }
-  uint64_t o = base + (uint64_t)off;
-  int64_t si = before;  // index of the next split-class member
-  for (int w = w0; w < w1; w++) {
-    const uint64_t fw = x.frow[w];
-    if (!fw) continue;
-    uint64_t cm[kSwRules + 1];
-    for (int j = 0; j < nc; j++) cm[j] = cls_mask(w, j);
-    uint64_t m = fw;
-    while (m) {
-      const int bit = __builtin_ctzll(m);
-      m &= m - 1;
-      const uint64_t b1 = 1ull << bit;
-      int j = 0;
-      while (j < nc - 1 && !(cm[j] & b1)) j++;
-      int32_t r = seats(j);
-      if (j == sh->split) {
-        if (si >= lo_i && si < hi_i) r++;
-        si++;
-      }
-      if (prop || r > 0) {
-        const uint32_t rk = (uint32_t)(w * 64 + bit);
-        x.sink.out_idx[o] = s.perm[rk];
-        x.sink.out_rep[o] = r;
-        o++;
+  B.sync();
+  for (int c = B.tid(); c < s.C; c += B.nth()) {
+    const int w = c >> 6;
+    const uint64_t bit = 1ull << (c & 63), below = bit - 1;
+    if (!(em[w] & bit)) continue;
+    int j = 0;
+    if (!one) {  // the first rule class (weight desc) whose bitset holds c
+      int q = 0;
+      for (; j < nl; j++) {
+        bool in = false;
+        for (; q < sh->lend[j]; q++) in = in || ((swb[(size_t)sh->order[q] * W + w] & bit) != 0);
+        if (in) break;
       }
     }
+    int32_t r = seats(j);
+    if (j == split) {
+      const int64_t idx = (int64_t)spo[w] + popc64(cms[w] & below);
+      if (idx >= lo_i && idx < hi_i) r++;
+    }
+    const uint64_t o = base + eo[w] + (uint64_t)popc64(em[w] & below);
+    x.sink.out_idx[o] = s.perm[c];
+    x.sink.out_rep[o] = r;
   }
   KP_STAMP(x, 4);
-  (void)F;
-  return true;
 }
 
 template <class BLK>
@@ -659,9 +718,6 @@ KP_FI void body_select_all_stream(const BLK& B, int blk, unsigned char* smem, co
   for (int w = B.tid(); w < s.W; w += B.nth()) F += popc64(x.frow[w]);
   F = B.sum64(F);  // (its barrier also publishes tgt and swb)
   KP_STAMP(x, 1);
-  if (weights && (rules || !(h->flags & BF_HAS_WP)) && F > 0 && !(h->flags & BF_BAD)) {
-    if (static_class_fast(B, x, swb, rules ? h->sw_cnt : 0, (int)F, (SwClass*)ss.hist)) return;
-  }
   const StreamCands cs{&x, s.C, B.tid(), B.nth(), weights, rules ? swb : nullptr, rules ? h->sw_cnt : 0};
   select_all_common(B, a, x, cs, (int)F, ss);
 }
