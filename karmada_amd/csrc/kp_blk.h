@@ -268,6 +268,9 @@ struct GpuBlk {
   KP_INLINE int wwidth() const { return 64; }
   KP_INLINE uint64_t wballot(bool p) const { return __ballot(p); }
   KP_INLINE uint64_t wlt() const { return (1ull << lane()) - 1; }  // lanes below this one
+  KP_INLINE uint64_t wminu64(uint64_t v) const {  // the wave's minimum (no workgroup barrier)
+    return wave_reduce(v, [](uint64_t a, uint64_t b) { return a < b ? a : b; }, (uint64_t)~0ull);
+  }
   // Orders this wave's LDS/global accesses: writes made by one lane before it
   // are visible to every lane of the wave after it.
   KP_INLINE void wsync() const {
@@ -419,6 +422,9 @@ struct WaveBlk {
   KP_INLINE int wwidth() const { return 64; }
   KP_INLINE uint64_t wballot(bool p) const { return __ballot(p); }
   KP_INLINE uint64_t wlt() const { return (1ull << lane()) - 1; }
+  KP_INLINE uint64_t wminu64(uint64_t v) const {
+    return wave_reduce(v, [](uint64_t a, uint64_t b) { return a < b ? a : b; }, (uint64_t)~0ull);
+  }
   KP_INLINE void wsync() const { sync(); }
   // lane l's value to every lane; the wave's 32-bit sum (no barrier: registers only)
   template <class T>
@@ -472,6 +478,7 @@ struct CpuBlk {
   int wwidth() const { return 1; }
   uint64_t wballot(bool p) const { return p ? 1ull : 0ull; }
   uint64_t wlt() const { return 0; }
+  uint64_t wminu64(uint64_t v) const { return v; }
   void wsync() const {}
   template <class T>
   T wread(T v, int) const {

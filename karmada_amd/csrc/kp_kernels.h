@@ -807,7 +807,7 @@ KP_FI void body_region_a(const BLK& B, int blk, unsigned char* smem, const KArgs
     if (B.tid() == 0) rstat[blk] = -1;
     return;
   }
-  region_a(B, x, cd, L, rout + (size_t)blk * R);
+  if (!region_a_fast(B, x, cd, L, rout + (size_t)blk * R)) region_a(B, x, cd, L, rout + (size_t)blk * R);
   KP_STAMP(x, 24);
   if (B.tid() == 0) rstat[blk] = 0;
 }

@@ -12,6 +12,11 @@
 #pragma once
 #include "kp_select.h"
 
+#include <type_traits>
+#if !defined(__HIP_DEVICE_COMPILE__)
+#include <vector>
+#endif
+
 namespace kp {
 
 constexpr int kRegionMax = 256;
@@ -25,6 +30,13 @@ KP_HD inline uint64_t cand_key(const SelCtx& x, const Cands& cd, int i, int32_t 
   uint32_t rank = c_rank(cd, i);
   int64_t avail = (int64_t)est + (int64_t)assigned_of(*x.bv, *x.h, x.tgt_bits, rank);
   return sort_key(c_ovf(cd, i), locality_score(*x.h, x.tgt_bits, rank), avail, rank);
+}
+// A candidate's sortClusters key kept in place of its (rank, estimate) pair (the
+// spread kernels compute it once after the gather).
+KP_HD inline uint64_t ckey(const Cands& cd, int i) { return ((uint64_t)cd.r[i] << 32) | (uint64_t)(uint32_t)cd.v[i]; }
+KP_HD inline void put_ckey(const Cands& cd, int i, uint64_t k) {
+  cd.r[i] = (uint32_t)(k >> 32);
+  cd.v[i] = (int32_t)(uint32_t)k;
 }
 KP_HD inline Item item_from_key(const SelCtx& x, uint64_t k) {
   Item it;
@@ -628,10 +640,34 @@ KP_FI void assign_small(const BLK& B, const SelCtx& x, const Item* items, int n,
     y.frow = selb;
     const SelScratch ss = carve_sel_scratch((unsigned char*)(selb + W), x.s->Cp);
     const bool weights = x.h->strategy == ST_STATIC;
-    const int why = sel_all_fast(B, y, ItemCands{items, n, B.tid(), B.nth(), &y, weights}, ss);
-    B.sync();
-    if (why == SLOW_NONE) return;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (std::is_same<BLK, GpuBlk>::value) {
+      // a list of at most 64: one wave runs the division, so its passes meet at
+      // wave barriers instead of the workgroup's; the other waves wait below
+      if (n <= 64 && B.nwaves() > 1) {
+        int32_t* whyp = (int32_t*)(B.red + 126);
+        if (B.wid() == 0) {
+          const WaveBlk wb{B.red};
+          const int w = sel_all_fast(wb, y, ItemCands{items, n, wb.tid(), 64, &y, weights}, ss);
+          if (wb.tid() == 0) *whyp = w;
+        }
+        B.sync();
+        const int why = *whyp;
+        B.sync();
+        if (why == SLOW_NONE) return;
+        goto serial;
+      }
+    }
+#endif
+    {
+      const int why = sel_all_fast(B, y, ItemCands{items, n, B.tid(), B.nth(), &y, weights}, ss);
+      B.sync();
+      if (why == SLOW_NONE) return;
+    }
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+serial:
+#endif
   if (B.tid() == 0) {
     SerialScratch sc = serial_scratch_carve(scratch, cap);
     SerialAssign sa{x, sc, (x.h->flags & BF_UID_DESC) != 0};
@@ -666,7 +702,10 @@ KP_FI bool sel_cluster_fast(const BLK& B, const SelCtx& x, const Cands& cd, uint
     return true;
   }
   KP_STAMP_INIT
-  auto key = [&](int i) { return cand_key(x, cd, i, cd.v[i]); };
+  // every candidate's sortClusters key once, in place of its (rank, estimate) pair
+  for (int i = B.tid(); i < F; i += B.nth()) put_ckey(cd, i, cand_key(x, cd, i, cd.v[i]));
+  B.sync();
+  auto key = [&](int i) { return ckey(cd, i); };
   auto all = [&](int) { return true; };
   uint64_t kth = radix_select(B, hist, F, all, key, needCnt);
   KP_STAMP(x, 28);
@@ -960,6 +999,139 @@ KP_HD inline int64_t go_ceil_div_i64(int32_t a, int64_t b) {
   if (q != q || q >= 9223372036854775808.0 || q < -9223372036854775808.0) return INT64_MIN;  // amd64 CVTTSD2SQ
   return (int64_t)q;
 }
+// region_a with the candidates bucketed by region (the same answers): every
+// candidate's sortClusters key is computed once and kept in place of its (rank,
+// estimate) pair (high word in cd.r, low word in cd.v), the region index array
+// cd.g becomes a permutation that lists each region's candidates contiguously,
+// and each wave walks whole regions (calcGroupScore's prefix in key order) by
+// repeated wave minima: no block barrier and no LDS atomic per walk step.
+// Returns false (nothing changed) when the candidates exceed the staging the
+// permutation needs (kRegionStage per thread); the caller then runs region_a.
+constexpr int kRegionStage = 32;
+
+template <class BLK>
+KP_FI bool region_a_fast(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L, RegionOut* out) {
+  const int F = cd.F;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (F > kRegionStage * B.nth()) return false;
+#endif
+  const BindHdr& h = *x.h;
+  const int R = x.s->n_regions;
+  int32_t* off = (int32_t*)L.minkey;  // [R + 1] region segment offsets
+  int32_t* cur = (int32_t*)L.last;    // [R] fill cursors
+  uint16_t* idx = (uint16_t*)cd.g;    // the permutation, in place of the region indices
+  for (int r = B.tid(); r < R; r += B.nth()) {
+    L.cnt[r] = 0;
+    L.dvalid[r] = 0;
+    L.sumAvail[r] = 0;
+    L.sumScore[r] = 0;
+    L.dscore[r] = 0;
+    L.amin[r] = 0;
+  }
+  B.sync();
+  const bool dup = (h.flags & BF_GROUP_DUP) != 0;
+  for (int i = B.tid(); i < F; i += B.nth()) {
+    const uint64_t k = cand_key(x, cd, i, cd.v[i]);
+    put_ckey(cd, i, k);
+    const int r = cd.g[i];
+    if (r < 0) continue;
+    const int64_t av = key_avail(k), sc = key_score(k);
+    kp_atomic_add(&L.cnt[r], 1);
+    kp_atomic_add((unsigned long long*)&L.sumAvail[r], (unsigned long long)av);
+    if (sc) kp_atomic_add((unsigned long long*)&L.sumScore[r], (unsigned long long)sc);
+    if (av < 0) kp_atomic_add((unsigned long long*)&L.amin[r], 1ull);  // negative count
+    if (dup && av >= (int64_t)h.replicas) {
+      kp_atomic_add(&L.dvalid[r], 1);
+      if (sc) kp_atomic_add((unsigned long long*)&L.dscore[r], (unsigned long long)sc);
+    }
+  }
+  B.sync();
+  if (dup) {  // calcGroupScoreForDuplicate
+    for (int r = B.tid(); r < R; r += B.nth()) {
+      const int64_t v = L.dvalid[r];
+      out[r].count = L.cnt[r];
+      out[r].score = v == 0 ? 0 : add64(mul64(v, 1000), L.dscore[r] / v);
+    }
+    B.sync();
+    return true;
+  }
+  if (B.tid() == 0) {
+    int32_t o = 0;
+    for (int r = 0; r < R; r++) {
+      off[r] = o;
+      cur[r] = o;
+      o += L.cnt[r];
+    }
+    off[R] = o;
+  }
+  B.sync();
+  // the permutation: region r's candidates at [off[r], off[r + 1])
+#if defined(__HIP_DEVICE_COMPILE__)
+  int16_t gg[kRegionStage];
+#pragma unroll
+  for (int j = 0; j < kRegionStage; j++) {
+    const int i = B.tid() + j * B.nth();
+    gg[j] = i < F ? cd.g[i] : (int16_t)-1;
+  }
+  B.sync();
+#pragma unroll
+  for (int j = 0; j < kRegionStage; j++) {
+    const int i = B.tid() + j * B.nth();
+    if (i < F && gg[j] >= 0) idx[kp_atomic_add(&cur[gg[j]], 1)] = (uint16_t)i;
+  }
+#else
+  {
+    std::vector<int16_t> gg(cd.g, cd.g + F);
+    for (int i = 0; i < F; i++)
+      if (gg[i] >= 0) idx[cur[gg[i]]++] = (uint16_t)i;
+  }
+#endif
+  B.sync();
+  // calcGroupScore (divided): each region's clusters in sortClusters order until
+  // validClusters >= max(clusterMinGroups, minGroups) and the sum reaches the target
+  const int64_t target = go_ceil_div_i64(h.replicas, h.region_min);
+  int64_t m = h.cluster_min;
+  if (m < h.region_min) m = h.region_min;
+  const int ww = B.wwidth(), lane = B.lane();
+  auto key = [&](int j) { return ckey(cd, j); };
+  for (int r = B.wid(); r < R; r += B.nwaves()) {
+    const int64_t cnt = L.cnt[r];
+    int64_t sa = L.sumAvail[r], ss = L.sumScore[r], valid = cnt;
+    if (cnt > 0 && !(L.amin[r] == 0 && sa < target)) {  // a monotone region short of the target never breaks
+      uint64_t last = 0;
+      int64_t wcnt = 0, wsum = 0, wscore = 0;
+      for (;;) {
+        uint64_t mn = ~0ull;
+        for (int j = off[r] + lane; j < off[r + 1]; j += ww) {
+          const uint64_t k = key(idx[j]);
+          if ((wcnt == 0 || k > last) && k < mn) mn = k;
+        }
+        mn = B.wminu64(mn);
+        if (mn == ~0ull) break;  // walked the whole region: the totals
+        last = mn;
+        wcnt++;
+        wsum = add64(wsum, key_avail(mn));
+        wscore = add64(wscore, key_score(mn));
+        if (wcnt >= m && wsum >= target) {
+          sa = wsum;
+          ss = wscore;
+          valid = wcnt;
+          break;
+        }
+      }
+      KP_COUNT(x, 25, wcnt);
+    }
+    if (lane == 0) {
+      out[r].count = (int32_t)cnt;
+      if (cnt == 0) out[r].score = 0;
+      else if (sa < target) out[r].score = add64(mul64(sa, 1000), ss / cnt);
+      else out[r].score = add64(mul64(target, 1000), ss / valid);
+    }
+  }
+  B.sync();
+  return true;
+}
+
 template <class BLK>
 KP_FI void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L, RegionOut* out) {
   const BindHdr& h = *x.h;
@@ -1077,6 +1249,8 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
   KP_STAMP_INIT
   const BindHdr& h = *x.h;
   const int R = x.s->n_regions;
+  // every candidate's sortClusters key once, in place of its (rank, estimate) pair
+  for (int i = B.tid(); i < cd.F; i += B.nth()) put_ckey(cd, i, cand_key(x, cd, i, cd.v[i]));
   for (int r = B.tid(); r < R; r += B.nth()) {
     heads[r] = ~0ull;
     rsel[r] = -1;
@@ -1099,7 +1273,7 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
   int32_t pos = B.wave_reserve(mine, ctr);
   for (int i = B.tid(); i < cd.F; i += B.nth()) {
     if (!in_sel(i)) continue;
-    const uint64_t k = cand_key(x, cd, i, cd.v[i]);
+    const uint64_t k = ckey(cd, i);
     kp_atomic_min_u64(&heads[cd.g[i]], k);
     if (pos < kc) keys[pos] = k;
     pos++;
@@ -1135,9 +1309,9 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
     KP_COUNT(x, 31, 1);
     auto incand = [&](int i) {
       int r = cd.g[i];
-      return r >= 0 && rsel[r] >= 0 && cand_key(x, cd, i, cd.v[i]) != heads[r];
+      return r >= 0 && rsel[r] >= 0 && ckey(cd, i) != heads[r];
     };
-    auto key = [&](int i) { return cand_key(x, cd, i, cd.v[i]); };
+    auto key = [&](int i) { return ckey(cd, i); };
     uint64_t kth = radix_select(B, hist, cd.F, incand, key, restCnt);
     int m = 0;
     for (int t0 = 0; t0 < cd.F; t0 += B.nth()) {
