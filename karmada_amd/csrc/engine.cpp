@@ -780,6 +780,39 @@ struct Pools {
 struct Packer {
   kp_snapshot* s;
   Pools* bt;  // this packer's pools (one per packing thread, merged by kp_batch_create)
+  // per-packer caches: the last (apiVersion, kind) and its GVK id, parsed quantity
+  // strings, and scratch lists reused across bindings (no per-binding allocation)
+  std::string gvkey;
+  SvMap<std::pair<bool, k8s::Qty>> qcache;
+  SvMap<int32_t> gvk_cache;  // apiVersion + '\0' + kind -> GVK id
+  SvMap<bool> scalar_cache;  // resource name -> IsScalarResourceName
+  std::vector<int32_t> tmp_t, tmp_rk, tmp_sr, tmp_mr;
+  std::vector<int64_t> tmp_sq, tmp_mq;
+  std::vector<std::pair<std::string_view, k8s::Qty>> tmp_rq;
+  std::vector<Instr> tmp_out;
+  std::vector<int32_t> tmp_vals;
+  std::vector<std::pair<std::string_view, std::string_view>> tmp_ml;
+
+  bool scalar(std::string_view nm) {
+    auto it = scalar_cache.find(nm);
+    if (it != scalar_cache.end()) return it->second;
+    const bool v = k8s::scalar_resource(std::string(nm));
+    if (scalar_cache.size() < 4096) scalar_cache.emplace(std::string(nm), v);
+    return v;
+  }
+
+  bool qty(std::string_view str, k8s::Qty* q) {
+    auto it = qcache.find(str);
+    if (it != qcache.end()) {
+      *q = it->second.second;
+      return it->second.first;
+    }
+    k8s::Qty v;
+    const bool ok = k8s::parse_quantity(str, &v);
+    if (qcache.size() < 4096) qcache.emplace(std::string(str), std::make_pair(ok, v));
+    *q = v;
+    return ok;
+  }
 
   int32_t list(const std::vector<int32_t>& v) {
     int32_t off = (int32_t)bt->ipool.size();
@@ -794,8 +827,10 @@ struct Packer {
     }
     return r;
   }
-  std::vector<int32_t> vals(const kp_str* v, uint32_t n) {
-    std::vector<int32_t> r;
+  // (the list lives until the next call: callers hand it to list() at once)
+  const std::vector<int32_t>& vals(const kp_str* v, uint32_t n) {
+    std::vector<int32_t>& r = tmp_vals;
+    r.clear();
     for (uint32_t i = 0; i < n; i++) {
       int32_t id = s->str.get(SV(v[i]));
       if (id >= 0) r.push_back(id);
@@ -812,7 +847,7 @@ struct Packer {
     out.push_back(i);
   }
   // labels.NewRequirement validation (labels/selector.go:150-230)
-  static bool valid_req(const std::string& key, const std::string& op, const kp_str* v, uint32_t n) {
+  static bool valid_req(std::string_view key, std::string_view op, const kp_str* v, uint32_t n) {
     bool ok = k8s::label_key(key);
     if (op == "In" || op == "NotIn") ok = ok && n > 0;
     else if (op == "=") ok = ok && n == 1;
@@ -821,40 +856,53 @@ struct Packer {
       ok = ok && n == 1;
       for (uint32_t i = 0; i < n; i++) {
         int64_t x;
-        if (!k8s::parse_int64(S(v[i]), &x)) ok = false;
+        if (!k8s::parse_int64(SV(v[i]), &x)) ok = false;
       }
     } else {
       ok = false;
     }
     for (uint32_t i = 0; i < n; i++)
-      if (!k8s::label_value(S(v[i]))) ok = false;
+      if (!k8s::label_value(SV(v[i]))) ok = false;
     return ok;
   }
   // util.ClusterMatches compiled to a conjunction program (selector.go:97-155)
   int32_t compile(const kp_cluster_affinity& a) {
-    std::vector<Instr> out;
+    std::vector<Instr>& out = tmp_out;
+    out.clear();
     bool never = false;
     if (a.n_exclude_clusters) {
       auto r = ranks(a.exclude_clusters, a.n_exclude_clusters);
       if (!r.empty()) ins(out, OP_EXCLUDE, list(r), (int32_t)r.size());
     }
     if (a.has_label_selector) {  // metav1.LabelSelectorAsSelector (helpers.go:36-74)
-      std::map<std::string, std::string> ml;
-      for (uint32_t i = 0; i < a.n_match_labels; i++) ml[S(a.match_labels[i].key)] = S(a.match_labels[i].value);
+      // matchLabels as a map: key order, a repeated key's last value
+      auto& ml = tmp_ml;
+      ml.clear();
+      for (uint32_t i = 0; i < a.n_match_labels; i++) {
+        const std::string_view k = SV(a.match_labels[i].key), v = SV(a.match_labels[i].value);
+        bool dup = false;
+        for (auto& kv : ml)
+          if (kv.first == k) {
+            kv.second = v;
+            dup = true;
+          }
+        if (!dup) ml.push_back({k, v});
+      }
+      std::sort(ml.begin(), ml.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
       for (auto& kv : ml) {
-        kp_str v{kv.second.c_str(), (uint32_t)kv.second.size()};
+        kp_str v{kv.second.data(), (uint32_t)kv.second.size()};
         if (!valid_req(kv.first, "=", &v, 1)) never = true;
         int32_t slot = s->keys.get(kv.first);
         int32_t id = s->str.get(kv.second);
         if (slot < 0 || id < 0) never = never || true;
         else {
-          std::vector<int32_t> one{id};
-          ins(out, OP_LBL_IN, slot, list(one), 1);
+          tmp_vals.assign(1, id);
+          ins(out, OP_LBL_IN, slot, list(tmp_vals), 1);
         }
       }
       for (uint32_t i = 0; i < a.n_match_expressions; i++) {
         const kp_requirement& r = a.match_expressions[i];
-        std::string key = S(r.key), op = S(r.op);
+        const std::string_view key = SV(r.key), op = SV(r.op);
         if (!(op == "In" || op == "NotIn" || op == "Exists" || op == "DoesNotExist") ||
             !valid_req(key, op, r.values, r.n_values)) {
           never = true;
@@ -862,11 +910,11 @@ struct Packer {
         }
         int32_t slot = s->keys.get(key);
         if (op == "In") {
-          auto v = vals(r.values, r.n_values);
+          const auto& v = vals(r.values, r.n_values);
           if (slot < 0 || v.empty()) never = true;
           else ins(out, OP_LBL_IN, slot, list(v), (int32_t)v.size());
         } else if (op == "NotIn") {
-          auto v = vals(r.values, r.n_values);
+          const auto& v = vals(r.values, r.n_values);
           if (slot >= 0) ins(out, OP_LBL_NOTIN, slot, list(v), (int32_t)v.size());
         } else if (op == "Exists") {
           if (slot < 0) never = true;
@@ -881,9 +929,9 @@ struct Packer {
       bool others_ok = true;
       for (uint32_t i = 0; i < a.n_field_expressions; i++) {
         const kp_requirement& r = a.field_expressions[i];
-        std::string key = S(r.key), op = S(r.op);
+        const std::string_view key = SV(r.key), op = SV(r.op);
         if (key == "zone") {  // matchZones (selector.go:208-235)
-          auto v = vals(r.values, r.n_values);
+          const auto& v = vals(r.values, r.n_values);
           if (op == "In") ins(out, OP_ZONE_IN, 0, list(v), (int32_t)v.size());
           else if (op == "NotIn") ins(out, OP_ZONE_NOTIN, 0, list(v), (int32_t)v.size());
           else if (op == "Exists") ins(out, OP_ZONE_EXISTS);
@@ -900,11 +948,11 @@ struct Packer {
         }
         int field = key == "provider" ? 0 : (key == "region" ? 1 : 2);  // extractClusterFields
         if (op == "In") {
-          auto v = vals(r.values, r.n_values);
+          const auto& v = vals(r.values, r.n_values);
           if (field == 2 || v.empty()) never = true;
           else ins(out, OP_FLD_IN, field, list(v), (int32_t)v.size());
         } else if (op == "NotIn") {
-          auto v = vals(r.values, r.n_values);
+          const auto& v = vals(r.values, r.n_values);
           if (field != 2) ins(out, OP_FLD_NOTIN, field, list(v), (int32_t)v.size());
         } else if (op == "Exists") {
           if (field == 2) never = true;
@@ -957,22 +1005,34 @@ struct Packer {
     if (b.has_weight_preference) f |= BF_HAS_WP;
     // APIEnablement GVK (group_version.go:211-226,300-305)
     {
-      std::string av = S(b.api_version), g, ver;
-      size_t slashes = std::count(av.begin(), av.end(), '/');
-      if (!(av.empty() || av == "/")) {
-        if (slashes == 0) ver = av;
-        else if (slashes == 1) {
-          g = av.substr(0, av.find('/'));
-          ver = av.substr(av.find('/') + 1);
+      gvkey.assign(SV(b.api_version));
+      gvkey.push_back('\0');
+      gvkey.append(SV(b.kind));
+      auto it = gvk_cache.find(std::string_view(gvkey));
+      if (it != gvk_cache.end()) {
+        h.gvk = it->second;  // (a batch repeats a few kinds)
+      } else {
+        std::string av = S(b.api_version), g, ver;
+        size_t slashes = std::count(av.begin(), av.end(), '/');
+        if (!(av.empty() || av == "/")) {
+          if (slashes == 0) ver = av;
+          else if (slashes == 1) {
+            g = av.substr(0, av.find('/'));
+            ver = av.substr(av.find('/') + 1);
+          }
         }
+        std::string gv = g.empty() ? ver : g + "/" + ver;
+        h.gvk = s->gvk.get(gv + '\0' + S(b.kind));
+        if (gvk_cache.size() < 4096) gvk_cache.emplace(gvkey, h.gvk);
       }
-      std::string gv = g.empty() ? ver : g + "/" + ver;
-      h.gvk = s->gvk.get(gv + '\0' + S(b.kind));
     }
     // spec.Clusters
     h.n_targets_all = (int32_t)b.n_clusters;
     {
-      std::vector<int32_t> t, rk;
+      std::vector<int32_t>& t = tmp_t;
+      std::vector<int32_t>& rk = tmp_rk;
+      t.clear();
+      rk.clear();
       for (uint32_t i = 0; i < b.n_clusters; i++) {
         auto it = s->rank_of.find(SV(b.clusters[i].name));
         if (it == s->rank_of.end()) continue;
@@ -995,7 +1055,7 @@ struct Packer {
     h.tol_off = (int32_t)bt->tols.size();
     for (uint32_t i = 0; i < b.n_tolerations; i++) {
       const kp_toleration& t = b.tolerations[i];
-      std::string eff = S(t.effect), key = S(t.key), op = S(t.op);
+      const std::string_view eff = SV(t.effect), key = SV(t.key), op = SV(t.op);
       Tol x;
       if (eff.empty()) x.eff = EFF_ANY;
       else if (eff == "NoSchedule") x.eff = EFF_NOSCHEDULE;
@@ -1071,10 +1131,11 @@ struct Packer {
     {
       // the ResourceList as (name, quantity) in name order, a repeated name's last
       // entry winning (the map the reference decodes), without per-entry allocation
-      std::vector<std::pair<std::string_view, k8s::Qty>> rq;
+      auto& rq = tmp_rq;
+      rq.clear();
       for (uint32_t i = 0; i < b.n_resource_request; i++) {
         k8s::Qty q;
-        if (!k8s::parse_quantity(SV(b.resource_request[i].quantity), &q)) f |= BF_BAD;
+        if (!qty(SV(b.resource_request[i].quantity), &q)) f |= BF_BAD;
         const std::string_view nm = SV(b.resource_request[i].name);
         bool dup = false;
         for (auto& kv : rq)
@@ -1085,8 +1146,9 @@ struct Packer {
         if (!dup) rq.push_back({nm, q});
       }
       std::sort(rq.begin(), rq.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-      std::vector<int32_t> sr, mr;
-      std::vector<int64_t> sq, mq;
+      auto &sr = tmp_sr, &mr = tmp_mr;
+      auto &sq = tmp_sq, &mq = tmp_mq;
+      sr.clear(), mr.clear(), sq.clear(), mq.clear();
       for (auto& kv : rq) {
         const std::string_view nm = kv.first;
         const bool cpu = nm == "cpu", mem = nm == "memory";
@@ -1103,7 +1165,7 @@ struct Packer {
             mr.push_back(rid);
             mq.push_back(m);
           }
-        } else if (mem || nm == "ephemeral-storage" || (nm != "pods" && k8s::scalar_resource(std::string(nm)))) {
+        } else if (mem || nm == "ephemeral-storage" || (nm != "pods" && scalar(nm))) {
           if (v > 0) {
             mr.push_back(rid);
             mq.push_back(v);
@@ -1120,13 +1182,13 @@ struct Packer {
       bt->lpool.insert(bt->lpool.end(), mq.begin(), mq.end());
     }
     // spread constraints: filter presence + selection kind (select_clusters.go:28-80)
-    std::string rst = b.has_replica_scheduling ? S(b.replica_scheduling_type) : std::string("Duplicated");
-    std::string div = S(b.replica_division_preference);
+    const std::string_view rst = b.has_replica_scheduling ? SV(b.replica_scheduling_type) : std::string_view("Duplicated");
+    const std::string_view div = SV(b.replica_division_preference);
     bool hasRegion = false, hasCluster = false;
     int n_order = 0;
     for (uint32_t i = 0; i < b.n_spread_constraints; i++) {
       const kp_spread_constraint& sc = b.spread_constraints[i];
-      std::string fld = S(sc.spread_by_field);
+      const std::string_view fld = SV(sc.spread_by_field);
       const int code = fld == "provider" ? 1 : fld == "region" ? 2 : fld == "zone" ? 3 : 0;
       bool seen = false;
       for (int k = 0; k < n_order; k++) seen = seen || ((h.spread_order >> (2 * k)) & 3) == code;
@@ -1145,13 +1207,13 @@ struct Packer {
         h.cluster_max = sc.max_groups;
       }
     }
-    bool ignoreSpread = b.has_replica_scheduling && S(b.replica_scheduling_type) == "Divided" && div == "Weighted" &&
+    bool ignoreSpread = b.has_replica_scheduling && SV(b.replica_scheduling_type) == "Divided" && div == "Weighted" &&
                         (!b.has_weight_preference || (b.n_static_weights != 0 && b.dynamic_weight.len == 0));
     if (b.n_spread_constraints == 0 || ignoreSpread) h.sel = SEL_ALL;
     else if (hasRegion) h.sel = SEL_REGION;
     else if (hasCluster) h.sel = SEL_CLUSTER;
     else h.sel = SEL_ERR_UNSUPPORTED;
-    h.need_replicas = (!b.has_replica_scheduling || S(b.replica_scheduling_type) == "Duplicated") ? -1 : b.replicas;
+    h.need_replicas = (!b.has_replica_scheduling || SV(b.replica_scheduling_type) == "Duplicated") ? -1 : b.replicas;
     // runReplicaEstimator / SelectClusters with the MultiplePodTemplatesScheduling gate:
     // isMultiTemplateSchedulingApplicable (core/estimation.go:43-65) = components and a
     // cluster spread constraint with MinGroups == MaxGroups == 1. Such a binding's
@@ -1160,7 +1222,7 @@ struct Packer {
     if (o.multiple_pod_templates_scheduling && b.n_components > 0) {
       bool one = false;
       for (uint32_t i = 0; i < b.n_spread_constraints; i++)
-        one = one || (S(b.spread_constraints[i].spread_by_field) == "cluster" &&
+        one = one || (SV(b.spread_constraints[i].spread_by_field) == "cluster" &&
                       b.spread_constraints[i].min_groups == 1 && b.spread_constraints[i].max_groups == 1);
       if (one) {
         f |= BF_SETS;
@@ -1861,6 +1923,7 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       bt->bcls[i] = it->second;
     }
   };
+  const auto tq0 = std::chrono::steady_clock::now();
   if (T == 1) {
     run(0);
   } else {
@@ -1868,6 +1931,7 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
     for (int t = 0; t < T; t++) th.emplace_back(run, t);
     for (auto& x : th) x.join();
   }
+  const auto tq1 = std::chrono::steady_clock::now();
   for (auto& x : terr)
     if (!x.empty()) {
       bt->err = x;
@@ -1940,6 +2004,11 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       bt->bcls[i] = g;
       if (g && bt->crep[g] < 0) bt->crep[g] = i;
     }
+  }
+  if (getenv("KP_PACK_TIMING")) {
+    auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+    fprintf(stderr, "pack_parallel: %d threads, pack %.1f ms, merge+classes %.1f ms\n", T, ms(tq0, tq1),
+            ms(tq1, std::chrono::steady_clock::now()));
   }
   return true;
 }

@@ -147,42 +147,42 @@ inline bool parse_quantity(std::string_view str, Qty* out) {
 
 inline bool alnum(char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9'); }
 inline bool lower_alnum(char c) { return (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9'); }
-inline bool label_fmt(const std::string& s) {
+inline bool label_fmt(std::string_view s) {
   if (s.empty() || !alnum(s.front()) || !alnum(s.back())) return false;
   for (char c : s)
     if (!(alnum(c) || c == '-' || c == '_' || c == '.')) return false;
   return true;
 }
-inline bool dns1123_subdomain(const std::string& s) {
+inline bool dns1123_subdomain(std::string_view s) {
   if (s.empty() || s.size() > 253) return false;
   size_t st = 0;
   for (;;) {
     size_t d = s.find('.', st);
-    std::string l = s.substr(st, d == std::string::npos ? std::string::npos : d - st);
+    std::string_view l = s.substr(st, d == std::string_view::npos ? std::string_view::npos : d - st);
     if (l.empty() || !lower_alnum(l.front()) || !lower_alnum(l.back())) return false;
     for (char c : l)
       if (!(lower_alnum(c) || c == '-')) return false;
-    if (d == std::string::npos) return true;
+    if (d == std::string_view::npos) return true;
     st = d + 1;
   }
 }
-inline bool label_key(const std::string& v) {  // content.IsLabelKey
+inline bool label_key(std::string_view v) {  // content.IsLabelKey
   size_t sl = v.find('/');
-  std::string name = v;
-  if (sl != std::string::npos) {
-    if (v.find('/', sl + 1) != std::string::npos) return false;
-    std::string pre = v.substr(0, sl);
+  std::string_view name = v;
+  if (sl != std::string_view::npos) {
+    if (v.find('/', sl + 1) != std::string_view::npos) return false;
+    std::string_view pre = v.substr(0, sl);
     name = v.substr(sl + 1);
     if (pre.empty() || !dns1123_subdomain(pre)) return false;
   }
   if (name.empty() || name.size() > 63) return false;
   return label_fmt(name);
 }
-inline bool label_value(const std::string& v) {  // content.IsLabelValue
+inline bool label_value(std::string_view v) {  // content.IsLabelValue
   if (v.size() > 63) return false;
   return v.empty() || label_fmt(v);
 }
-inline bool parse_int64(const std::string& s, int64_t* out) {  // strconv.ParseInt(s, 10, 64)
+inline bool parse_int64(std::string_view s, int64_t* out) {  // strconv.ParseInt(s, 10, 64)
   if (s.empty()) return false;
   size_t i = 0;
   bool neg = false;
@@ -204,7 +204,7 @@ inline bool parse_int64(const std::string& s, int64_t* out) {  // strconv.ParseI
 // lifted.IsScalarResourceName (pkg/util/lifted/resourcename.go:31-34, corev1helpers.go:39-82)
 inline bool scalar_resource(const std::string& n) {
   bool native = n.find('/') == std::string::npos || n.find("kubernetes.io/") != std::string::npos;
-  bool extended = !native && n.rfind("requests.", 0) != 0 && label_key("requests." + n);
+  bool extended = !native && n.rfind("requests.", 0) != 0 && label_key(std::string("requests.") + n);
   return extended || n.rfind("hugepages-", 0) == 0 || n.find("kubernetes.io/") != std::string::npos ||
          n.rfind("attachable-volumes-", 0) == 0;
 }

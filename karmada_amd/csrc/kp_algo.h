@@ -1107,6 +1107,25 @@ KP_HD inline int64_t w_count(int64_t v, double t, int64_t cap, bool ge) {
   return k;
 }
 
+// w_count with r = v * rt, rt = fl(1/t) computed once per pass (no division per
+// party): r's relative error stays below 2^-52 (two roundings), so y's error
+// stays below r*2^-52, far inside the same tol band, and every count the fast
+// path returns is the exact one; the band itself takes the exact divisions.
+KP_HD inline int64_t w_count_r(int64_t v, double t, double rt, int64_t cap, bool ge) {
+  if (v <= 0) return 0;
+  const double r = (double)v * rt;
+  const double y = (r - 1.0) * 0.5;
+  if (r >= 1.0) {
+    const double fy = kp_floor(y);
+    const double fr = y - fy, tol = r * 0x1p-44;
+    if (fr > tol && fr < 1.0 - tol) {
+      const double kf = fy + 1.0;
+      return kf > (double)cap ? cap : (int64_t)kf;
+    }
+  }
+  return w_count(v, t, cap, ge);
+}
+
 // Serial exact AllocateWebsterSeats for parties with unique names and votes >= 0
 // (dispenser with nil init): result seats[] per party. Names order: rank asc,
 // `desc` flips the name tie-break (tieBreakerByUID, binding.go:117-144).

@@ -643,6 +643,7 @@ KP_FI int gather(const BLK& B, const SelCtx& x, Cands cd, bool weights) {
 struct WebRes {
   int mode;       // 0 no parties, 1 all zero seats, 2 normal
   double t;       // t*
+  double rt = 0;  // fl(1 / t*) (w_count_r)
   uint64_t tie;   // tie-key threshold (inclusive)
   int32_t N;
   bool desc;
@@ -658,7 +659,7 @@ KP_HD inline uint64_t tie_key(int64_t base, uint32_t rank, bool desc) {
 }
 KP_HD inline int32_t web_seats(const WebRes& w, int64_t v, uint32_t rank) {
   if (w.mode != 2 || (double)v < w.t) return 0;  // every priority of v is below t*
-  int64_t base = w_count(v, w.t, (int64_t)w.N + 1, false);
+  int64_t base = w_count_r(v, w.t, w.rt, (int64_t)w.N + 1, false);
   if (base < w.N && w_prio(v, base) == w.t && tie_key(base, rank, w.desc) <= w.tie) base++;
   return (int32_t)base;
 }
@@ -867,9 +868,10 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   const int64_t capN = (int64_t)N;
   auto cnt2 = [&](double ta, double tb, int64_t* ca, int64_t* cb) {
     int64_t a = 0, b = 0;
+    const double ra = 1.0 / ta, rb = 1.0 / tb;
     parties([&](uint32_t, int64_t v) {
-      a += w_count(v, ta, capN, true);
-      b += w_count(v, tb, capN, true);
+      a += w_count_r(v, ta, ra, capN, true);
+      b += w_count_r(v, tb, rb, capN, true);
     });
     B.sum2(a, b);
     *ca = a;
@@ -877,7 +879,8 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   };
   auto cnt1 = [&](double t) {
     int64_t c = 0;
-    parties([&](uint32_t, int64_t v) { c += w_count(v, t, capN, true); });
+    const double rt = 1.0 / t;
+    parties([&](uint32_t, int64_t v) { c += w_count_r(v, t, rt, capN, true); });
     return B.sum64(c);
   };
   // invariant: cnt_ge(lo) >= N > cnt_ge(hi), lo < hi (as bit patterns)
@@ -939,6 +942,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     tstar = bitsd(rank_select(B, sc.buf, E, (int64_t)N - chi, true, (uint64_t*)sc.whist));
   }
   r.t = tstar;
+  r.rt = 1.0 / tstar;
   r.compact = compact;
   r.np = np;
   r.Lb = Lb;
@@ -946,8 +950,9 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   KP_STAMPD(sc.dbg, 12);
   // seats strictly above t*, then the tie group at t* ordered by (k asc, name)
   int64_t S = 0, T = 0;
+  const double rts = 1.0 / tstar;
   parties([&](uint32_t, int64_t v) {
-    int64_t base = w_count(v, tstar, (int64_t)N + 1, false);
+    int64_t base = w_count_r(v, tstar, rts, (int64_t)N + 1, false);
     S += base;
     if (w_prio(v, base) == tstar) T++;
   });
@@ -959,13 +964,13 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   } else if (T <= (int64_t)ecap) {
     int32_t mine = 0;
     parties([&](uint32_t, int64_t v) {
-      int64_t base = w_count(v, tstar, (int64_t)N + 1, false);
+      int64_t base = w_count_r(v, tstar, rts, (int64_t)N + 1, false);
       if (w_prio(v, base) == tstar) mine++;
     });
     int32_t n;
     int32_t pos = B.excl_scan(mine, &n);
     parties([&](uint32_t rk, int64_t v) {
-      int64_t base = w_count(v, tstar, (int64_t)N + 1, false);
+      int64_t base = w_count_r(v, tstar, rts, (int64_t)N + 1, false);
       if (w_prio(v, base) == tstar) sc.buf[pos++] = tie_key(base, rk, desc);
     });
     B.sync();
@@ -976,7 +981,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
       uint64_t mid = tlo + (thi - tlo) / 2;
       int64_t c = 0;
       parties([&](uint32_t rk, int64_t v) {
-        int64_t base = w_count(v, tstar, (int64_t)N + 1, false);
+        int64_t base = w_count_r(v, tstar, rts, (int64_t)N + 1, false);
         if (w_prio(v, base) == tstar && tie_key(base, rk, desc) <= mid) c++;
       });
       c = B.sum64(c);
