@@ -13,6 +13,8 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <tuple>
 #include <string>
 #include <string_view>
 #include <thread>
@@ -64,11 +66,66 @@ struct Dict {
   }
 };
 
-// One device allocation carved into aligned sub-buffers.
+// Process-wide pools of freed batch buffers: a batch's device arena (per device)
+// and its page-locked result buffers go back here on kp_batch_destroy and the next
+// batch of a fitting size takes them, so a stream of batches pays hipMalloc /
+// hipHostMalloc (and the frees) once. A block is reused for requests of at least
+// half its size; each pool keeps at most kPoolKeep blocks.
+struct BufPool {
+  static constexpr size_t kPoolKeep = 8;
+  std::mutex mu;
+  std::vector<std::tuple<int, void*, size_t>> free;  // (device or -1 for host, pointer, bytes)
+  void* get(int dev_id, size_t bytes, size_t* got) {
+    std::lock_guard<std::mutex> g(mu);
+    size_t best = (size_t)-1;
+    for (size_t i = 0; i < free.size(); i++) {
+      auto& [d, p, n] = free[i];
+      if (d == dev_id && n >= bytes && n <= 2 * bytes + (1u << 20) && (best == (size_t)-1 || n < std::get<2>(free[best])))
+        best = i;
+    }
+    if (best == (size_t)-1) return nullptr;
+    void* p = std::get<1>(free[best]);
+    *got = std::get<2>(free[best]);
+    free.erase(free.begin() + (long)best);
+    return p;
+  }
+  void put(int dev_id, void* p, size_t bytes) {
+    if (!p) return;
+    std::tuple<int, void*, size_t> drop{-2, nullptr, 0};
+    {
+      std::lock_guard<std::mutex> g(mu);
+      free.emplace_back(dev_id, p, bytes);
+      if (free.size() > kPoolKeep) {  // the oldest goes
+        drop = free.front();
+        free.erase(free.begin());
+      }
+    }
+    if (std::get<1>(drop)) {
+      if (std::get<0>(drop) < 0) dev::host_release(std::get<1>(drop));
+      else dev::release(std::get<1>(drop));
+    }
+  }
+};
+BufPool& buf_pool() {
+  static BufPool* p = new BufPool();  // never destroyed: buffers may return during exit
+  return *p;
+}
+void* pinned_get(size_t bytes, size_t* got) {
+  if (void* p = buf_pool().get(-1, bytes, got)) return p;
+  void* p = nullptr;
+  if (dev::host_alloc(&p, bytes)) return nullptr;
+  *got = bytes;
+  return p;
+}
+
+// One device allocation carved into aligned sub-buffers. pool_dev >= 0: the
+// allocation comes from (and returns to) the batch-buffer pool of that device.
 struct Arena {
   std::vector<std::pair<void**, size_t>> req;
   void* base = nullptr;
   size_t total = 0;
+  int pool_dev = -1;
+  size_t got = 0;
   template <class T>
   void add(T** p, size_t count) {
     req.push_back({(void**)p, count * sizeof(T)});
@@ -77,7 +134,11 @@ struct Arena {
     total = 0;
     for (auto& r : req) total += (r.second + 255) & ~(size_t)255;
     if (total == 0) total = 256;
-    if (dev::alloc(&base, total)) return -1;
+    if (pool_dev >= 0) base = buf_pool().get(pool_dev, total, &got);
+    if (!base) {
+      if (dev::alloc(&base, total)) return -1;
+      got = total;
+    }
     char* p = (char*)base;
     for (auto& r : req) {
       *r.first = p;
@@ -85,15 +146,18 @@ struct Arena {
     }
     return 0;
   }
-  void reset() {
-    if (base) dev::release(base);
+  void drop() {
+    if (!base) return;
+    if (pool_dev >= 0) buf_pool().put(pool_dev, base, got);
+    else dev::release(base);
     base = nullptr;
+  }
+  void reset() {
+    drop();
     req.clear();
     total = 0;
   }
-  ~Arena() {
-    if (base) dev::release(base);
-  }
+  ~Arena() { drop(); }
 };
 
 #define HIPCHK(x)                                                            \
@@ -223,9 +287,10 @@ struct kp_batch {
   uint32_t* h_cidx = nullptr;
   int32_t* h_crep = nullptr;
   uint64_t h_res_cap = 0;
+  size_t h_cidx_bytes = 0, h_crep_bytes = 0;  // their pooled block sizes
   ~kp_batch() {
-    dev::host_release(h_cidx);
-    dev::host_release(h_crep);
+    buf_pool().put(-1, h_cidx, h_cidx_bytes);
+    buf_pool().put(-1, h_crep, h_crep_bytes);
     if (est) dev::release(est);
   }
   std::vector<RegionOut> h_rout;
@@ -2114,6 +2179,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   bt->slow_grid = (int)std::max<size_t>(1, std::min<size_t>(256, bt->l_slow.size()));
   bt->fast_ok = batch_fast_ok(bt);
   Arena& a = bt->dev;
+  a.pool_dev = e->device;
   BindHdr* d_hdr;
   int32_t* d_ipool;
   int64_t* d_lpool;
@@ -2495,17 +2561,19 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   double tc0 = now_ms();
   const uint64_t tot = bt->h_offsets[B];
   if (tot > bt->h_res_cap || !bt->h_cidx) {
-    dev::host_release(bt->h_cidx);
-    dev::host_release(bt->h_crep);
+    buf_pool().put(-1, bt->h_cidx, bt->h_cidx_bytes);
+    buf_pool().put(-1, bt->h_crep, bt->h_crep_bytes);
     bt->h_cidx = nullptr;
     bt->h_crep = nullptr;
     bt->h_res_cap = 0;
     const uint64_t cap = std::max<uint64_t>(1, tot + tot / 4);  // headroom for repeated calls
-    if (dev::host_alloc((void**)&bt->h_cidx, 4 * cap) || dev::host_alloc((void**)&bt->h_crep, 4 * cap)) {
+    bt->h_cidx = (uint32_t*)pinned_get(4 * cap, &bt->h_cidx_bytes);
+    bt->h_crep = (int32_t*)pinned_get(4 * cap, &bt->h_crep_bytes);
+    if (!bt->h_cidx || !bt->h_crep) {
       e->err = "kp_schedule_batch: page-locked result buffers";
       return KP_ENOMEM;
     }
-    bt->h_res_cap = cap;
+    bt->h_res_cap = std::min(bt->h_cidx_bytes, bt->h_crep_bytes) / 4;
   }
   if (tot) {
     HIPCHK(dev::d2h(bt->h_cidx, bt->cidx_d, 4 * tot, st));
