@@ -2112,6 +2112,17 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   bt->n_all_dyn = (int)(std::stable_partition(bt->l_all.begin(), bt->l_all.end(),
                                               [&](int32_t i) { return bt->hdr[i].strategy != ST_STATIC; }) -
                         bt->l_all.begin());
+  // the non-StaticWeight SEL_ALL bindings grouped by estimator class (counting sort,
+  // stable): k_select_top hands each XCD a contiguous run of this list, so a
+  // class's order and row stay in few XCDs' L2
+  if (bt->n_all_dyn > 1 && !bt->crep.empty()) {
+    const size_t ncls = bt->crep.size();
+    std::vector<int32_t> cnt(ncls + 1, 0), out((size_t)bt->n_all_dyn);
+    for (int i = 0; i < bt->n_all_dyn; i++) cnt[(size_t)std::max(0, bt->bcls[bt->l_all[i]]) + 1]++;
+    for (size_t k = 1; k <= ncls; k++) cnt[k] += cnt[k - 1];
+    for (int i = 0; i < bt->n_all_dyn; i++) out[(size_t)cnt[(size_t)std::max(0, bt->bcls[bt->l_all[i]])]++] = bt->l_all[i];
+    std::copy(out.begin(), out.end(), bt->l_all.begin());
+  }
   // StaticWeight bindings the class-level kernel covers first (bits mode only)
   {
     const kp_snapshot* sn = bt->snap;

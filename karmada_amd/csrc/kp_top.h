@@ -204,7 +204,14 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     const uint64_t* ord = t.ord + (size_t)cls * s.Cp;
     const int lane = B.tid() % B.wwidth();
     const int ww = B.wwidth();
-    uint64_t e_next = lane < s.C ? ord[lane] : 0;  // the next chunk's load, one iteration ahead
+    // the walk's loads run kTopAhead chunks ahead (a register ring): the class
+    // order is read once, in order, and its L2 latency overlaps the chunk work
+    constexpr int kTopAhead = 4;
+    uint64_t ring[kTopAhead];
+#if defined(__clang__)
+#pragma unroll
+#endif
+    for (int q = 0; q < kTopAhead; q++) ring[q] = lane + q * ww < s.C ? ord[lane + q * ww] : 0;
     int64_t walked = 0, wsum = 0;
     bool tie = false;
     int32_t tie_v = 0;
@@ -219,8 +226,12 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
         break;
       }
       const int i = i0 + lane;
-      const uint64_t e = e_next;
-      if (i + ww < s.C) e_next = ord[i + ww];
+      const uint64_t e = ring[0];
+#if defined(__clang__)
+#pragma unroll
+#endif
+      for (int q = 0; q + 1 < kTopAhead; q++) ring[q] = ring[q + 1];
+      ring[kTopAhead - 1] = i + kTopAhead * ww < s.C ? ord[i + kTopAhead * ww] : 0;
       bool in = false, past = false;
       int32_t v = 0;
       uint32_t r = 0;
