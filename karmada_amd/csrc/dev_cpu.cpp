@@ -241,9 +241,9 @@ int node_sets(stream_t, const NodeSetsArgs* A) {
   return 0;
 }
 
-int reasons(stream_t, const SnapView& s, const BatchView& bv, uint32_t* out) {
-  const uint64_t n = (uint64_t)bv.B * (uint64_t)s.C;
-  for (uint64_t i = 0; i < n; i++) body_reasons(s, bv, i, out);
+int reasons(stream_t, const SnapView& s, const BatchView& bv, int b0, int nb, uint32_t* out) {
+  const uint64_t n = (uint64_t)nb * (uint64_t)s.C;
+  for (uint64_t i = 0; i < n; i++) body_reasons(s, bv, b0, i, out);
   return 0;
 }
 

@@ -2684,18 +2684,29 @@ int kp_filter_reasons(kp_engine* e, kp_batch* bt, uint32_t* out_reasons) {
   (void)dev::set_device(e->device);
   kp_snapshot* s = bt->snap;
   if (bt->B == 0 || s->C == 0) return KP_OK;
+  // bindings in chunks of at most kChunkPairs pairs through one reused device
+  // buffer (a 100k x 5k batch would otherwise take 2 GB on each side)
+  size_t chunk = (size_t)1 << 24;
+  if (const char* v = getenv("KP_REASONS_CHUNK")) chunk = std::max<size_t>(1, (size_t)atoll(v));  // (tests)
+  const int nb = (int)std::max<size_t>(1, std::min<size_t>((size_t)bt->B, chunk / (size_t)s->C));
+  const size_t pairs = (size_t)nb * s->C;
   uint32_t* d = nullptr;
-  const size_t n = (size_t)bt->B * s->C;
-  HIPCHK(dev::alloc((void**)&d, 4 * n));
-  std::vector<uint32_t> h(n);
-  int rc = (dev::reasons(e->stream, s->view, bt->view, d) || dev::d2h(h.data(), d, 4 * n, e->stream) ||
-            dev::sync(e->stream))
-               ? KP_EDEVICE
-               : KP_OK;
+  HIPCHK(dev::alloc((void**)&d, 4 * pairs));
+  std::vector<uint32_t> h(pairs);
+  int rc = KP_OK;
+  for (int b0 = 0; b0 < bt->B && rc == KP_OK; b0 += nb) {
+    const int m = std::min(nb, bt->B - b0);
+    if (dev::reasons(e->stream, s->view, bt->view, b0, m, d) || dev::d2h(h.data(), d, 4 * (size_t)m * s->C, e->stream) ||
+        dev::sync(e->stream)) {
+      e->err = std::string("kp_filter_reasons: ") + dev::last_error();
+      rc = KP_EDEVICE;
+      break;
+    }
+    for (int b = 0; b < m; b++)
+      for (int r = 0; r < s->C; r++) out_reasons[(size_t)(b0 + b) * s->C + s->perm[r]] = h[(size_t)b * s->C + r];
+  }
   dev::release(d);
   if (rc) return rc;
-  for (int b = 0; b < bt->B; b++)
-    for (int r = 0; r < s->C; r++) out_reasons[(size_t)b * s->C + s->perm[r]] = h[(size_t)b * s->C + r];
   return KP_OK;
 }
 

@@ -208,9 +208,9 @@ extern "C" __global__ void __launch_bounds__(64) k_node_sets(const NodeSetsArgs*
   __shared__ int64_t red[2];
   node_sets(WaveBlk{red}, *A);
 }
-extern "C" __global__ void __launch_bounds__(256) k_reasons(SnapView s, BatchView bv, uint64_t n, uint32_t* out) {
+extern "C" __global__ void __launch_bounds__(256) k_reasons(SnapView s, BatchView bv, int b0, uint64_t n, uint32_t* out) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    body_reasons(s, bv, i, out);
+    body_reasons(s, bv, b0, i, out);
 }
 extern "C" __global__ void __launch_bounds__(kOffThreads) k_offsets_a(const int32_t* status, const uint32_t* count, int n,
                                                                     uint64_t* offsets, uint64_t* part) {
@@ -482,11 +482,11 @@ int node_sets(stream_t st, const NodeSetsArgs* A) {
   return chk(hipGetLastError());
 }
 
-int reasons(stream_t st, const SnapView& s, const BatchView& bv, uint32_t* out) {
-  const uint64_t n = (uint64_t)bv.B * (uint64_t)s.C;
+int reasons(stream_t st, const SnapView& s, const BatchView& bv, int b0, int nb, uint32_t* out) {
+  const uint64_t n = (uint64_t)nb * (uint64_t)s.C;
   if (n == 0) return 0;
   const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_reasons, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)st, s, bv, n, out);
+  hipLaunchKernelGGL(k_reasons, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)st, s, bv, b0, n, out);
   return chk(hipGetLastError());
 }
 

@@ -96,8 +96,8 @@ int select_static(stream_t st, const KArgs& a, size_t slice);
 // device memory), then the first-fit set simulation by one wave (A in device memory).
 int node_match(stream_t st, const NodeView& v, const ClaimProg* P, int K, uint8_t* match);
 int node_sets(stream_t st, const NodeSetsArgs* A);
-// kp_filter_reasons: out[b * C + r] = pair_reason of binding b, cluster rank r.
-int reasons(stream_t st, const SnapView& s, const BatchView& bv, uint32_t* out);
+// kp_filter_reasons: out[(b - b0) * C + r] = pair_reason of binding b in [b0, b0 + nb), cluster rank r.
+int reasons(stream_t st, const SnapView& s, const BatchView& bv, int b0, int nb, uint32_t* out);
 // CSR offsets[n + 1] of the per-binding results (counts of OK bindings), on the device;
 // part: ceil(n / kOffChunk) u64 of scratch.
 int offsets(stream_t st, const int32_t* status, const uint32_t* count, int n, uint64_t* off, uint64_t* part);

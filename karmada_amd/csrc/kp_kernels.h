@@ -1061,9 +1061,10 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
 
 // kp_filter_reasons: one thread per (binding, cluster) pair, grid-strided;
 // out[b * C + r] for cluster rank r < C.
-KP_HD inline void body_reasons(const SnapView& s, const BatchView& bv, uint64_t i, uint32_t* out) {
+// out[i] for pair i of bindings [b0, b0 + n / C): binding b0 + i / C, cluster rank i % C.
+KP_HD inline void body_reasons(const SnapView& s, const BatchView& bv, int b0, uint64_t i, uint32_t* out) {
   const uint64_t C = (uint64_t)s.C;
-  const int b = (int)(i / C), r = (int)(i % C);
+  const int b = b0 + (int)(i / C), r = (int)(i % C);
   out[i] = pair_reason(s, bv, bv.hdr[b], r);
 }
 

@@ -177,7 +177,12 @@ def gather_csr(local: Csr) -> Csr:
 
 
 def gather_results(local: List[dict], dst: int = 0) -> Optional[List[dict]]:
-    """Per-binding result dicts of every rank at `dst` via the CSR all-gather."""
+    """Per-binding result dicts of every rank at `dst` via the CSR all-gather.
+
+    The all-gather leaves the whole batch's CSR on every rank (the fixed-size RCCL
+    collective over xGMI is cheaper than a gather plus the padding handshake); only
+    `dst` converts it to dicts, the others return None. The result must be CSR-shaped
+    (status, err, arg, targets), as kp_schedule_batch's is."""
     t = sum(len(r["targets"]) for r in local)
     offs = np.zeros(len(local) + 1, np.int64)
     idx = np.zeros(t, np.int32)

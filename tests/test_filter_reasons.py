@@ -96,3 +96,15 @@ def test_reasons_gpu(gpu_engine):
     want = check(gpu_engine, 6, 31, 700, 300, api.options())
     check(gpu_engine, 4, 4, 5000, 20, api.options())
     assert len(want) == 700 * 300
+
+
+def test_reasons_cpusim_chunked(cpusim_engine, monkeypatch):
+    """The binding chunks of kp_filter_reasons (one reused device buffer) give the
+    same words as one pass: chunks of 3 bindings over 50 bindings x 37 clusters."""
+    u = synth.Universe(6, 71, 37, 0, 50)
+    opts = api.options()
+    want = oracle_reasons(u, opts, 50)
+    monkeypatch.setenv("KP_REASONS_CHUNK", str(3 * 37))
+    got = engine_reasons(cpusim_engine, u, opts, 50)
+    assert list(got) == want
+
