@@ -2113,8 +2113,10 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
                                               [&](int32_t i) { return bt->hdr[i].strategy != ST_STATIC; }) -
                         bt->l_all.begin());
   // the non-StaticWeight SEL_ALL bindings grouped by estimator class (counting sort,
-  // stable): k_select_top hands each XCD a contiguous run of this list, so a
-  // class's order and row stay in few XCDs' L2
+  // stable): the workgroups resident at any moment then cover a short run of the
+  // list, i.e. few classes, whose orders and rows stay in every XCD's L2
+  // (k_select_top 1.23 -> 1.10 ms at config 3; mapping each XCD to one contiguous
+  // run of the list instead was slower, 1.33 ms)
   if (bt->n_all_dyn > 1 && !bt->crep.empty()) {
     const size_t ncls = bt->crep.size();
     std::vector<int32_t> cnt(ncls + 1, 0), out((size_t)bt->n_all_dyn);

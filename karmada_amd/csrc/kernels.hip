@@ -89,17 +89,11 @@ extern "C" __global__ void __launch_bounds__(KP_SEL_MAX_THREADS, KP_SEL_MIN_WAVE
 // SEL_ALL DynamicWeight / Aggregated over the candidates that can matter (kp_top.h):
 // kTopWaves independent waves per workgroup, one binding each, no workgroup barrier.
 constexpr int kTopWaves = 2;  // small workgroups: LDS is granted per workgroup
-// Workgroup g runs on XCD g % 8 (round-robin dispatch); this maps the XCD's
-// workgroups onto one contiguous run of the list (the host groups it by class).
-__device__ __forceinline__ int xcd_chunk(int g, int n) {
-  const int x = g & 7, base = n >> 3, rem = n & 7;
-  return x * base + (x < rem ? x : rem) + (g >> 3);
-}
 extern "C" __global__ void __launch_bounds__(64 * kTopWaves) k_select_top(KArgs a, TopArgs t, int slice) {
   KP_SMEM;
   const int w = (int)(threadIdx.x >> 6);
   unsigned char* mine = smem + (size_t)w * (size_t)slice;
-  const int blk = xcd_chunk((int)blockIdx.x, (int)gridDim.x) * kTopWaves + w;
+  const int blk = (int)blockIdx.x * kTopWaves + w;
   if (blk >= a.n) return;  // wave-uniform: the waves never synchronise with each other
   body_select_top(WaveBlk{(int64_t*)mine}, blk, mine, a, t);
 }

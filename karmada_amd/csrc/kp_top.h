@@ -206,7 +206,10 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     const int ww = B.wwidth();
     // the walk's loads run kTopAhead chunks ahead (a register ring): the class
     // order is read once, in order, and its L2 latency overlaps the chunk work
-    constexpr int kTopAhead = 4;
+#ifndef KP_TOP_AHEAD
+#define KP_TOP_AHEAD 4
+#endif
+    constexpr int kTopAhead = KP_TOP_AHEAD;
     uint64_t ring[kTopAhead];
 #if defined(__clang__)
 #pragma unroll

@@ -22,6 +22,7 @@ for s in "$@"; do
     cfg_*) c=${s#cfg_}; b=100000; [ "$c" = 5 ] && b=125000
            step bench_cfg$c 300 python bench.py --config $c --bindings $b --steps 20 --warmup 2 --no-cpu --check 300 --e2e-reps 0 ;;
     bench_rows) KP_PAIR_ROWS=1 step bench_rows 300 python bench.py --steps 100 --warmup 2 --no-cpu --check 300 --e2e-reps 0 ;;
+    cpubase) step cpubase 900 python tools/cpu_baseline.py --budget 8 ;;
     capsweep) for c in 256 384 768 1024; do KP_TOP_CAP=$c step cap_$c 300 python bench.py --steps 50 --warmup 2 --no-cpu --check 100 --e2e-reps 0; done ;;
     sweep) for t in 256 512; do KP_SEL_THREADS=$t step sweep_$t 300 python bench.py --steps 3 --warmup 1 --no-cpu; done ;;
     chunks) for c in 4096 8192 16384 32768 200000; do KP_CHUNK=$c step chunk_$c 300 python bench.py --steps 5 --warmup 1 --no-cpu; done ;;
