@@ -1249,8 +1249,6 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
   KP_STAMP_INIT
   const BindHdr& h = *x.h;
   const int R = x.s->n_regions;
-  // every candidate's sortClusters key once, in place of its (rank, estimate) pair
-  for (int i = B.tid(); i < cd.F; i += B.nth()) put_ckey(cd, i, cand_key(x, cd, i, cd.v[i]));
   for (int r = B.tid(); r < R; r += B.nth()) {
     heads[r] = ~0ull;
     rsel[r] = -1;
@@ -1260,21 +1258,77 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
   if (B.tid() == 0) *ctr = 0;
   for (int j = B.tid(); j < nsel; j += B.nth()) rsel[sel[j]] = j;
   B.sync();
+  // Only the selected regions' candidates matter from here on: each one's
+  // sortClusters key is computed once and the list is compacted in place to them
+  // (key in place of the (rank, estimate) pair), so every later pass walks only
+  // the selected regions (staged through registers on the device; past the
+  // staging, every candidate keeps its key in place uncompacted).
+  Cands cd2 = cd;
+  {
+    auto keep_of = [&](int i) {
+      const int r = cd.g[i];
+      return r >= 0 && rsel[r] >= 0;
+    };
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (cd.F <= kRegionStage * B.nth()) {
+      uint64_t kk[kRegionStage];
+      int16_t gg[kRegionStage];
+      uint32_t keep = 0;
+      int32_t mine = 0;
+#pragma unroll
+      for (int j = 0; j < kRegionStage; j++) {
+        const int i = B.tid() + j * B.nth();
+        kk[j] = 0;
+        gg[j] = -1;
+        if (i < cd.F && keep_of(i)) {
+          kk[j] = cand_key(x, cd, i, cd.v[i]);
+          gg[j] = cd.g[i];
+          keep |= 1u << j;
+          mine++;
+        }
+      }
+      int32_t tot;
+      int32_t pos = B.excl_scan(mine, &tot);  // (its barrier: every read precedes every write)
+#pragma unroll
+      for (int j = 0; j < kRegionStage; j++)
+        if ((keep >> j) & 1u) {
+          put_ckey(cd, pos, kk[j]);
+          cd.g[pos] = gg[j];
+          pos++;
+        }
+      cd2.F = tot;
+    } else {
+      for (int i = B.tid(); i < cd.F; i += B.nth()) put_ckey(cd, i, cand_key(x, cd, i, cd.v[i]));
+    }
+#else
+    int pos = 0;
+    for (int i = 0; i < cd.F; i++)
+      if (keep_of(i)) {  // pos <= i: slot pos was read before
+        const uint64_t k = cand_key(x, cd, i, cd.v[i]);
+        const int16_t g = cd.g[i];
+        put_ckey(cd, pos, k);
+        cd.g[pos] = g;
+        pos++;
+      }
+    cd2.F = pos;
+#endif
+    B.sync();
+  }
   // One pass: each candidate of a selected region gets its sortClusters key
   // once; the region heads take the minimum and the keys are compacted into
   // `keys` (2*kSmallMax entries) when they fit.
   const int kc = 2 * kSmallMax;
   auto in_sel = [&](int i) {
-    const int r = cd.g[i];
+    const int r = cd2.g[i];
     return r >= 0 && rsel[r] >= 0;
   };
   int32_t mine = 0;
-  for (int i = B.tid(); i < cd.F; i += B.nth()) mine += in_sel(i) ? 1 : 0;
+  for (int i = B.tid(); i < cd2.F; i += B.nth()) mine += in_sel(i) ? 1 : 0;
   int32_t pos = B.wave_reserve(mine, ctr);
-  for (int i = B.tid(); i < cd.F; i += B.nth()) {
+  for (int i = B.tid(); i < cd2.F; i += B.nth()) {
     if (!in_sel(i)) continue;
-    const uint64_t k = ckey(cd, i);
-    kp_atomic_min_u64(&heads[cd.g[i]], k);
+    const uint64_t k = ckey(cd2, i);
+    kp_atomic_min_u64(&heads[cd2.g[i]], k);
     if (pos < kc) keys[pos] = k;
     pos++;
   }
@@ -1308,17 +1362,17 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
   } else if (restCnt > 0) {
     KP_COUNT(x, 31, 1);
     auto incand = [&](int i) {
-      int r = cd.g[i];
-      return r >= 0 && rsel[r] >= 0 && ckey(cd, i) != heads[r];
+      int r = cd2.g[i];
+      return r >= 0 && rsel[r] >= 0 && ckey(cd2, i) != heads[r];
     };
-    auto key = [&](int i) { return ckey(cd, i); };
-    uint64_t kth = radix_select(B, hist, cd.F, incand, key, restCnt);
+    auto key = [&](int i) { return ckey(cd2, i); };
+    uint64_t kth = radix_select(B, hist, cd2.F, incand, key, restCnt);
     int m = 0;
-    for (int t0 = 0; t0 < cd.F; t0 += B.nth()) {
+    for (int t0 = 0; t0 < cd2.F; t0 += B.nth()) {
       int i = t0 + B.tid();
       uint64_t k = 0;
       bool e = false;
-      if (i < cd.F && incand(i)) {
+      if (i < cd2.F && incand(i)) {
         k = key(i);
         e = k <= kth;
       }

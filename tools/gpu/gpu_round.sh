@@ -38,7 +38,7 @@ for s in "$@"; do
     prof_fetch) step prof_fetch 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --pmc FETCH_SIZE --output-format csv -d $ROOT/gpurun_out/prof_fetch -o f -- python3 $ROOT/bench.py --steps 2 --warmup 0 --no-cpu" ;;
     prof_write) step prof_write 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --pmc WRITE_SIZE --output-format csv -d $ROOT/gpurun_out/prof_write -o w -- python3 $ROOT/bench.py --steps 2 --warmup 0 --no-cpu" ;;
     dist2) KP_DIST_BACKEND=gloo step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --bindings 20000 ;;
-    prof_kt45) for c in 4 5; do step prof_kt$c 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/prof_kt$c -o kt -- python3 $ROOT/bench.py --config $c --bindings 100000 --steps 3 --warmup 1 --no-cpu"; done ;;
+    prof_kt45) for c in 4 5; do step prof_kt$c 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/gpurun_out/prof_kt$c -o kt -- python3 $ROOT/bench.py --config $c --bindings 100000 --steps 3 --warmup 1 --no-cpu --inflight 1 --e2e-reps 0 --check 0"; done ;;
     pmc_*) c=${s#pmc_}; b=100000; [ "$c" = 5 ] && b=125000
            step pmc_cfg$c 900 bash tools/gpu/prof_pmc.sh cfg$c --config $c --bindings $b ;;
     prof_l2) step prof_l2 600 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $ROOT/gpurun_out/prof_l2 -o l -- python3 $ROOT/bench.py --steps 2 --warmup 0 --no-cpu" ;;
