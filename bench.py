@@ -473,7 +473,7 @@ def main():
         # filter stage: k_est_class + k_filter (bits mode) or the pair kernel
         "stages_ms": {"filter_stage": round(pair_ms, 3), "filter_kernel": round(filter_ms, 3),
                       "select_kernels": round(sel_ms, 3), "sel_all_kernel": round(sel_all_ms, 3),
-                      "select_top_kernel": round(top_ms, 3),
+                      "select_top_kernel": round(top_ms, 3), "select_cluster_kernel": round(avg("cluster_kernel_ms"), 3),
                       "host_region": round(avg("host_ms"), 3), "copy_back": round(avg("copy_ms"), 3),
                       "call_total": round(avg("total_ms"), 3)},
         "filter_mode": "bitset filter + estimator classes" if bits else "per-binding pair rows",
@@ -492,6 +492,8 @@ def main():
         # SEL_ALL DynamicWeight/Aggregated bindings scheduled over their deciding candidates
         # (k_select_top) and the ones it handed to the full-candidate kernel
         "select_top": {"bindings": int(last["n_top"]), "fallback": int(last["n_top_fallback"])},
+        # cluster-spread bindings, and those selected over their estimator-class order
+        "select_cluster": {"bindings": int(last["n_cluster"]), "class_order": int(last["n_cluster_order"])},
         # bindings of the timed batch (sampled over all ranks) re-checked against the oracle
         "parity_checked": n_chk,
         "parity_lanes": n_lanes_chk,  # result lists checked per rank: the serial run + each in-flight lane

@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 11
+#define KP_ABI_VERSION 12
 
 /* ------------------------------------------------------------------------- */
 /* Object model                                                              */
@@ -363,6 +363,9 @@ typedef struct kp_stage_times {
   uint32_t n_top;          /* SEL_ALL bindings given to k_select_top (deciding-candidate subsets) */
   uint32_t n_top_fallback; /* of those, the ones it handed to the full-candidate kernel */
   float top_kernel_ms;     /* k_select_top alone (HIP events on its stream), 0 when it did not run */
+  uint32_t n_cluster;       /* cluster-spread bindings (selectBestClustersByCluster) */
+  uint32_t n_cluster_order; /* of those, the ones selected over their estimator-class order */
+  float cluster_kernel_ms;  /* the cluster-spread select kernel alone (HIP events on its stream) */
 } kp_stage_times;
 
 /* ------------------------------------------------------------------------- */

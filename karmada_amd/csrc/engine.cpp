@@ -178,7 +178,7 @@ struct kp_engine {
   dev::stream_t stream = nullptr;   // select kernels, copies (the batch's result order)
   dev::stream_t stream2 = nullptr;  // pair kernel, then the SEL_ALL select kernel
   dev::stream_t stream3 = nullptr;  // the cluster-spread select kernel, beside the other selects
-  dev::event_t ev[14] = {};
+  dev::event_t ev[16] = {};
   std::string err;
   kp_stage_times times{};
   struct {  // kp_schedule_affinities results
@@ -263,7 +263,8 @@ struct kp_batch {
   unsigned long long* counter = nullptr;
   uint32_t* stats = nullptr;
   unsigned long long* dbg = nullptr;
-  uint32_t h_stats[16] = {};  // [0..7] slow-path counts, [8] component-set simulation overflow
+  uint32_t h_stats[16] = {};  // [0..7] slow-path counts, [8] component-set simulation overflow, [9] k_select_top
+                              // fallbacks, [10] cluster-spread bindings selected over the class order
   uint32_t* out_idx = nullptr;
   int32_t* out_rep = nullptr;
   uint64_t* offsets_d = nullptr;
@@ -2409,7 +2410,9 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   // SEL_ALL DynamicWeight / Aggregated over the deciding candidates (kp_top.h): the
   // class rows' orders first
   const bool top = bits && e->top_on && bt->d_ord != nullptr && bt->n_all_dyn > 0;
-  if (top)
+  // class orders: k_select_top's walk, and the cluster-spread shortcut (cluster_by_order)
+  const bool orders = bits && e->top_on && bt->d_ord != nullptr && (bt->n_all_dyn > 0 || !bt->l_cluster.empty());
+  if (orders)
     HIPCHK(dev::class_order(sp, s->view, bt->cls_rows, (int)bt->crep.size(), bt->d_ord, bt->d_ctot, bt->d_cok));
   HIPCHK(dev::event_record(e->ev[4], sp));
   HIPCHK(dev::stream_wait(st, e->ev[4]));  // every pair row precedes the rest
@@ -2474,7 +2477,14 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     KArgs k = ka;
     k.list = bt->d_cluster;
     k.n = (int)bt->l_cluster.size();
+    if (orders) {
+      k.ord = bt->d_ord;
+      k.cok = bt->d_cok;
+      k.n_order = bt->stats + 10;
+    }
+    HIPCHK(dev::event_record(e->ev[14], s3));
     HIPCHK(dev::select(s3, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sx));
+    HIPCHK(dev::event_record(e->ev[15], s3));
   }
   HIPCHK(dev::event_record(e->ev[9], s3));
   double th0 = 0, th1 = 0;
@@ -2613,6 +2623,9 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   tm.n_top = top ? (uint32_t)bt->n_all_dyn : 0u;
   tm.n_top_fallback = top ? bt->h_stats[9] : 0u;
   tm.top_kernel_ms = top ? dev::event_ms(e->ev[12], e->ev[13]) : 0.f;
+  tm.n_cluster = (uint32_t)bt->l_cluster.size();
+  tm.n_cluster_order = orders ? bt->h_stats[10] : 0u;
+  tm.cluster_kernel_ms = bt->l_cluster.empty() ? 0.f : dev::event_ms(e->ev[14], e->ev[15]);
 #ifdef KP_STAMPS
   {
     unsigned long long h[32];

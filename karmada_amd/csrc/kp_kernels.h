@@ -725,6 +725,84 @@ KP_FI void body_select_all_stream(const BLK& B, int blk, unsigned char* smem, co
 // ---------------------------------------------------------------------------
 // Select stage: SEL_CLUSTER
 // ---------------------------------------------------------------------------
+// selectBestClustersByCluster (select_clusters_by_cluster.go:25-102) over the
+// binding's estimator-class order (k_class_order) instead of a gather and a radix
+// select. With no spec.Clusters (locality score 0, assigned replicas 0) and no
+// overflow tiers (order 0), the sortClusters key of every candidate reduces to
+// (estimate desc, name asc): the class order filtered by the feasibility row. The
+// first min(F, MaxGroups) feasible entries are then the selection, and the swap
+// step never fires (every rest cluster's AvailableReplicas is at most the last
+// selected one's, and it needs a strictly larger one), so only the resource check
+// remains. Returns false (nothing written) when the shortcut does not apply.
+template <class BLK>
+KP_FI bool cluster_by_order(const BLK& B, const KArgs& a, const SelCtx& x, uint32_t* hist, Item* items,
+                            unsigned char* scratch, int cap, size_t area_bytes) {
+  const BindHdr& h = *x.h;
+  if (!a.ord || !a.cok || !a.bcls) return false;
+  const int32_t cls = a.bcls[x.b];
+  if (cls <= 0 || !a.cok[cls] || h.tgt_cnt != 0 || h.ovf_mode != OVF_ZERO || (h.flags & BF_BAD)) return false;
+  const SnapView& s = *x.s;
+  int64_t F = 0;
+  for (int w = B.tid(); w < s.W; w += B.nth()) F += popc64(x.frow[w]);
+  F = B.sum64(F);
+  if (F == 0) {  // FitError (generic_scheduler.go:84-89)
+    if (B.tid() == 0) sink_error(x, KP_STATUS_FIT_ERROR, KP_ERR_FIT, s.C);
+    return true;
+  }
+  if (F < h.cluster_min) {
+    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_CLUSTER_MIN_GROUPS, 0);
+    return true;
+  }
+  int64_t needCnt = F < h.cluster_max ? F : h.cluster_max;
+  if (needCnt < 0) needCnt = 0;
+  const int32_t need = h.need_replicas;
+  if (needCnt == 0) {
+    if (B.tid() == 0) {
+      if (need == -1) sink_error(x, KP_STATUS_ERROR, KP_ERR_NO_CLUSTERS, 0);
+      else sink_error(x, KP_STATUS_ERROR, KP_ERR_CLUSTER_RESOURCE, 0);
+    }
+    return true;
+  }
+  if (needCnt > kSmallMax) return false;
+  // walk the class order, nth entries per step, keeping the feasible ones in order
+  const uint64_t* ord = a.ord + (size_t)cls * s.Cp;
+  int n = 0;
+  int64_t tot = 0;
+  for (int i0 = 0; i0 < s.C && n < needCnt; i0 += B.nth()) {
+    const int i = i0 + B.tid();
+    uint64_t e = 0;
+    bool in = false;
+    if (i < s.C) {
+      e = ord[i];
+      in = mask_test(x.frow, (int)(uint32_t)e);
+    }
+    int32_t cnt;
+    const int32_t pos = n + B.excl_scan(in ? 1 : 0, &cnt);
+    if (in && pos < needCnt) {
+      Item it;
+      it.rank = (uint32_t)e;
+      it.alloc = (int32_t)(e >> 32);  // est_at: the row holds no MaxInt32 (cok), so no merge
+      it.avail = (int64_t)(int32_t)(e >> 32);
+      it.ovf = 0;
+      it.pad = 0;
+      items[pos] = it;
+      tot += it.avail;
+    }
+    n += cnt;
+  }
+  B.sync();
+  if (n > needCnt) n = (int)needCnt;
+  tot = B.sum64(tot);
+  if (need != -1 && tot < (int64_t)need) {  // selectClustersByAvailableResource: no swap can help
+    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_CLUSTER_RESOURCE, needCnt);
+    return true;
+  }
+  (void)hist;
+  if (B.tid() == 0 && a.n_order) kp_atomic_add(a.n_order, 1u);
+  assign_small(B, x, items, n, scratch, cap, area_bytes);
+  return true;
+}
+
 template <class BLK>
 KP_FI void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const KArgs& a, int scratch_cap) {
   if (blk >= a.n) return;
@@ -743,11 +821,12 @@ KP_FI void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const
   build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
   SelCtx x = make_ctx(a, b, tgt);
   KP_STAMP(x, 26);
+  const size_t area_bytes = 8 * (size_t)a.s.Cp > serial_scratch_bytes(scratch_cap) ? 8 * (size_t)a.s.Cp
+                                                                                    : serial_scratch_bytes(scratch_cap);
+  if (cluster_by_order(B, a, x, hist, items, area, scratch_cap, area_bytes)) return;
   cd.F = gather(B, x, cd, false);
   KP_STAMP(x, 27);
   if (pre_checks(B, x, cd.F)) return;
-  const size_t area_bytes = 8 * (size_t)a.s.Cp > serial_scratch_bytes(scratch_cap) ? 8 * (size_t)a.s.Cp
-                                                                                    : serial_scratch_bytes(scratch_cap);
   if (!sel_cluster_fast(B, x, cd, hist, items, keys, area, scratch_cap, area_bytes)) {
     if (B.tid() == 0) flag_slow(a, b, SLOW_CLUSTER);
   }

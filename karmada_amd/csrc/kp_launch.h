@@ -27,6 +27,11 @@ struct KArgs {
   // set: the launch covers list[0, *n_dev) with a grid-stride loop (a list another
   // kernel appended to, e.g. k_select_top's fallback list); n is its capacity
   const uint32_t* n_dev = nullptr;
+  // k_class_order's per-class orders and walkability (bits mode; nullptr when the
+  // batch did not compute them): the spread kernels' class-order shortcut
+  const uint64_t* ord = nullptr;
+  const int32_t* cok = nullptr;
+  uint32_t* n_order = nullptr;  // count of the bindings that took it
 };
 
 enum : int {

@@ -25,7 +25,7 @@ from karmada_amd import api
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libkp.so")
-KP_ABI_VERSION = 11
+KP_ABI_VERSION = 12
 
 _LIBS = {}
 

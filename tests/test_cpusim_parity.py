@@ -67,6 +67,8 @@ def test_cpusim_schedule_parity(engine, config, seed, n_clusters, n_bindings, ro
     compare(run(engine, u, opts, rows=rows, times=times), want, f"config {config} seed {seed}")
     if config in (2, 3, 5, 7):  # fast estimator instances
         assert times[0]["bits"] == int(not rows)
+    if config in (4, 5) and not rows:  # cluster spread without spec.Clusters: the class-order selection
+        assert 0 < times[0]["n_cluster_order"] <= times[0]["n_cluster"]
 
 
 @pytest.mark.parametrize("prop,plugins,gate", [

@@ -96,6 +96,9 @@ def test_schedule_parity(engine, config, seed, n_clusters, n_bindings):
     u = synth.Universe(config, seed, n_clusters, 0, n_bindings)
     opts = api.options()
     compare(gpu_schedule(engine, u, opts), oracle_schedule(u, opts), f"config {config} seed {seed}")
+    if config in (4, 5):  # cluster spread without spec.Clusters: the class-order selection ran
+        t = engine.stage_times()
+        assert 0 < t["n_cluster_order"] <= t["n_cluster"]
 
 
 @pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
