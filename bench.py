@@ -494,6 +494,7 @@ def main():
         "select_top": {"bindings": int(last["n_top"]), "fallback": int(last["n_top_fallback"])},
         # cluster-spread bindings, and those selected over their estimator-class order
         "select_cluster": {"bindings": int(last["n_cluster"]), "class_order": int(last["n_cluster_order"])},
+        "select_region": {"bindings": int(last["n_region"]), "class_order": int(last["n_region_order"])},
         # bindings of the timed batch (sampled over all ranks) re-checked against the oracle
         "parity_checked": n_chk,
         "parity_lanes": n_lanes_chk,  # result lists checked per rank: the serial run + each in-flight lane

@@ -366,6 +366,8 @@ typedef struct kp_stage_times {
   uint32_t n_cluster;       /* cluster-spread bindings (selectBestClustersByCluster) */
   uint32_t n_cluster_order; /* of those, the ones selected over their estimator-class order */
   float cluster_kernel_ms;  /* the cluster-spread select kernel alone (HIP events on its stream) */
+  uint32_t n_region;        /* region-spread bindings (selectBestClustersByRegion) */
+  uint32_t n_region_order;  /* of those, the ones whose final selection walked their estimator-class order */
 } kp_stage_times;
 
 /* ------------------------------------------------------------------------- */

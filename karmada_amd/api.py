@@ -186,7 +186,7 @@ class kp_stage_times(C.Structure):
                 ("sel_all_kernel_ms", C.c_float), ("n_sel_all", C.c_uint32),
                 ("n_classes", C.c_uint32), ("n_top", C.c_uint32), ("n_top_fallback", C.c_uint32),
                 ("top_kernel_ms", C.c_float), ("n_cluster", C.c_uint32), ("n_cluster_order", C.c_uint32),
-                ("cluster_kernel_ms", C.c_float)]
+                ("cluster_kernel_ms", C.c_float), ("n_region", C.c_uint32), ("n_region_order", C.c_uint32)]
 
 
 PLUGIN_API_ENABLEMENT = 1 << 0

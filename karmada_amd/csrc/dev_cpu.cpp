@@ -153,7 +153,7 @@ int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const Sele
       break;
     case SEL_LAUNCH_REGION_B:
       grid(a.n, smem, [&](int blk, unsigned char* sm) {
-        body_region_b(CpuBlk{(int64_t*)sm}, blk, sm, a, x.rsel, x.rnsel, cap);
+        body_region_b(CpuBlk{(int64_t*)sm}, blk, sm, a, x.rsel, x.rnsel, x.rout, cap);
       });
       break;
     case SEL_LAUNCH_SLOW:

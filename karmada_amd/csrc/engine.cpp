@@ -264,7 +264,7 @@ struct kp_batch {
   uint32_t* stats = nullptr;
   unsigned long long* dbg = nullptr;
   uint32_t h_stats[16] = {};  // [0..7] slow-path counts, [8] component-set simulation overflow, [9] k_select_top
-                              // fallbacks, [10] cluster-spread bindings selected over the class order
+                              // fallbacks, [10] / [11] cluster- / region-spread bindings selected over the class order
   uint32_t* out_idx = nullptr;
   int32_t* out_rep = nullptr;
   uint64_t* offsets_d = nullptr;
@@ -2411,7 +2411,8 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   // class rows' orders first
   const bool top = bits && e->top_on && bt->d_ord != nullptr && bt->n_all_dyn > 0;
   // class orders: k_select_top's walk, and the cluster-spread shortcut (cluster_by_order)
-  const bool orders = bits && e->top_on && bt->d_ord != nullptr && (bt->n_all_dyn > 0 || !bt->l_cluster.empty());
+  const bool orders = bits && e->top_on && bt->d_ord != nullptr &&
+                      (bt->n_all_dyn > 0 || !bt->l_cluster.empty() || !bt->l_region.empty());
   if (orders)
     HIPCHK(dev::class_order(sp, s->view, bt->cls_rows, (int)bt->crep.size(), bt->d_ord, bt->d_ctot, bt->d_cok));
   HIPCHK(dev::event_record(e->ev[4], sp));
@@ -2493,6 +2494,11 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     KArgs k = ka;
     k.list = bt->d_region;
     k.n = nr;
+    if (orders) {  // region_b_by_order
+      k.ord = bt->d_ord;
+      k.cok = bt->d_cok;
+      k.n_order = bt->stats + 11;
+    }
     HIPCHK(dev::select(st, SEL_LAUNCH_REGION_A, k, smem_region_a(s), cap, sx));
     // selectGroups: on the device (one thread per binding) unless the snapshot
     // has more regions than its arrays hold; bindings whose DFS exceeds the node
@@ -2626,6 +2632,8 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   tm.n_cluster = (uint32_t)bt->l_cluster.size();
   tm.n_cluster_order = orders ? bt->h_stats[10] : 0u;
   tm.cluster_kernel_ms = bt->l_cluster.empty() ? 0.f : dev::event_ms(e->ev[14], e->ev[15]);
+  tm.n_region = (uint32_t)bt->l_region.size();
+  tm.n_region_order = orders ? bt->h_stats[11] : 0u;
 #ifdef KP_STAMPS
   {
     unsigned long long h[32];

@@ -147,9 +147,10 @@ extern "C" __global__ void __launch_bounds__(1024) k_select_all_wide(KArgs a) {
     body_region_a(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, rout, rstat);                              \
   }                                                                                                            \
   extern "C" __global__ void __launch_bounds__(T, MINW) k_region_b##SUF(KArgs a, const int32_t* rsel,           \
-                                                                      const int32_t* rnsel, int cap) {         \
+                                                                      const int32_t* rnsel,                    \
+                                                                      const RegionOut* rout, int cap) {        \
     KP_SMEM;                                                                                                   \
-    body_region_b(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, rsel, rnsel, cap);                         \
+    body_region_b(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, rsel, rnsel, rout, cap);                   \
   }
 KP_SPREAD_KERNELS(, 256, 3)
 KP_SPREAD_KERNELS(_wide, 512, 4)
@@ -369,9 +370,9 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
       break;
     case SEL_LAUNCH_REGION_B:
       if (smem > kLdsPerCu / 2)
-        hipLaunchKernelGGL(k_region_b_wide, dim3(a.n), dim3(512), smem, h, a, x.rsel, x.rnsel, cap);
+        hipLaunchKernelGGL(k_region_b_wide, dim3(a.n), dim3(512), smem, h, a, x.rsel, x.rnsel, x.rout, cap);
       else
-        hipLaunchKernelGGL(k_region_b, dim3(a.n), dim3(256), smem, h, a, x.rsel, x.rnsel, cap);
+        hipLaunchKernelGGL(k_region_b, dim3(a.n), dim3(256), smem, h, a, x.rsel, x.rnsel, x.rout, cap);
       break;
     case SEL_LAUNCH_SLOW:
       if (smem > 65536 &&

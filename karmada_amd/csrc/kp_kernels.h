@@ -891,11 +891,92 @@ KP_FI void body_region_a(const BLK& B, int blk, unsigned char* smem, const KArgs
   if (B.tid() == 0) rstat[blk] = 0;
 }
 
+// selectBestClustersByRegion (select_clusters_by_region.go:41-63) over the
+// binding's estimator-class order, for the bindings cluster_by_order covers (no
+// spec.Clusters, no overflow tiers: the sortClusters order is the class order
+// filtered by the feasibility row). Each selected region's head is its first entry
+// in that order, the rest are the next restCnt entries of the selected regions that
+// are not heads, and the candidate count comes from stage A's per-region counts, so
+// the walk stops once the heads and the rest are found instead of gathering every
+// candidate. hpos: [R] LDS. Returns false (nothing written) when it does not apply.
+template <class BLK>
+KP_FI bool region_b_by_order(const BLK& B, const KArgs& a, const SelCtx& x, const RegionOut* ro, const int32_t* sel,
+                             int nsel, unsigned long long* hpos, int32_t* rsel, Item* items, void* scratch, int cap,
+                             size_t area_bytes) {
+  const BindHdr& h = *x.h;
+  if (!a.ord || !a.cok || !a.bcls || !ro) return false;
+  const int32_t cls = a.bcls[x.b];
+  if (cls <= 0 || !a.cok[cls] || h.tgt_cnt != 0 || h.ovf_mode != OVF_ZERO || (h.flags & BF_BAD)) return false;
+  const SnapView& s = *x.s;
+  const int R = s.n_regions;
+  int64_t total = 0;
+  for (int j = 0; j < nsel; j++) total += ro[sel[j]].count;
+  int64_t needCnt = total < h.cluster_max ? total : h.cluster_max;
+  const int64_t restCnt = needCnt - nsel;
+  if (restCnt > kSmallMax - nsel) return false;  // the general path reports the engine limit
+  const int64_t want = restCnt > 0 ? restCnt : 0;
+  for (int r = B.tid(); r < R; r += B.nth()) {
+    hpos[r] = ~0ull;
+    rsel[r] = -1;
+  }
+  B.sync();
+  for (int j = B.tid(); j < nsel; j += B.nth()) rsel[sel[j]] = j;
+  B.sync();
+  const uint64_t* ord = a.ord + (size_t)cls * s.Cp;
+  int nh = 0, nr = 0;
+  for (int i0 = 0; i0 < s.C && (nh < nsel || nr < want); i0 += B.nth()) {
+    const int i = i0 + B.tid();
+    uint64_t e = 0;
+    int r = -1;
+    if (i < s.C) {
+      e = ord[i];
+      const int c = (int)(uint32_t)e;
+      if (mask_test(x.frow, c)) {
+        r = s.region_idx[c];
+        if (r >= 0 && rsel[r] < 0) r = -1;
+      }
+    }
+    // (a stale read is only larger: the minimum only falls)
+    if (r >= 0 && hpos[r] > (unsigned long long)i) kp_atomic_min_u64(&hpos[r], (unsigned long long)i);
+    B.sync();
+    const bool head = r >= 0 && hpos[r] == (unsigned long long)i;
+    const bool rest = r >= 0 && !head;
+    int32_t cnt;
+    const int32_t pk = B.excl_scan((rest ? 1 : 0) | (head ? 1 << 16 : 0), &cnt);
+    const int32_t pos = nr + (pk & 0xffff);
+    if (rest && pos < want) {
+      Item& it = items[nsel + pos];
+      it.rank = (uint32_t)e;
+      it.alloc = (int32_t)(e >> 32);  // est_at: the class row holds no MaxInt32 (cok)
+      it.avail = (int64_t)(int32_t)(e >> 32);
+      it.ovf = 0;
+      it.pad = 0;
+    }
+    nr += cnt & 0xffff;
+    nh += cnt >> 16;
+  }
+  B.sync();
+  if (nh < nsel || nr < want) return false;  // a selected region without a feasible cluster
+  for (int j = B.tid(); j < nsel; j += B.nth()) {
+    const uint64_t e = ord[hpos[sel[j]]];
+    Item& it = items[j];
+    it.rank = (uint32_t)e;
+    it.alloc = (int32_t)(e >> 32);
+    it.avail = (int64_t)(int32_t)(e >> 32);
+    it.ovf = 0;
+    it.pad = 0;
+  }
+  B.sync();
+  if (B.tid() == 0 && a.n_order) kp_atomic_add(a.n_order, 1u);
+  assign_small(B, x, items, nsel + (int)want, scratch, cap, area_bytes);
+  return true;
+}
+
 // Region stage B. rsel: [n][n_regions] selected region ids (path order); rnsel[n]:
 // count, -1000 when stage A already finalized, or -KP_ERR_* from the host step.
 template <class BLK>
 KP_FI void body_region_b(const BLK& B, int blk, unsigned char* smem, const KArgs& a, const int32_t* rsel,
-                         const int32_t* rnsel, int scratch_cap) {
+                         const int32_t* rnsel, const RegionOut* rout, int scratch_cap) {
   if (blk >= a.n) return;
   KP_STAMP_INIT
   const int b = a.list[blk];
@@ -932,11 +1013,14 @@ KP_FI void body_region_b(const BLK& B, int blk, unsigned char* smem, const KArgs
     return;
   }
   KP_STAMP(x, 16);
+  const size_t area_bytes = 8 * (size_t)a.s.Cp > serial_scratch_bytes(scratch_cap) ? 8 * (size_t)a.s.Cp
+                                                                                    : serial_scratch_bytes(scratch_cap);
+  if (region_b_by_order(B, a, x, rout ? rout + (size_t)blk * R : nullptr, rsel + (size_t)blk * R, nsel, heads, rs,
+                        items, p, scratch_cap, area_bytes))
+    return;
   cd.F = gather(B, x, cd, false);
   region_of_cands(B, a.s, cd);
   KP_STAMP(x, 17);
-  const size_t area_bytes = 8 * (size_t)a.s.Cp > serial_scratch_bytes(scratch_cap) ? 8 * (size_t)a.s.Cp
-                                                                                    : serial_scratch_bytes(scratch_cap);
   region_b(B, x, cd, rsel + (size_t)blk * R, nsel, hist, heads, rs, items, keys, p, scratch_cap, area_bytes);
 }
 

@@ -1009,6 +1009,22 @@ KP_HD inline int64_t go_ceil_div_i64(int32_t a, int64_t b) {
 // permutation needs (kRegionStage per thread); the caller then runs region_a.
 constexpr int kRegionStage = 32;
 
+// calcGroupScore's walk over a region (group_clusters.go:299-351) gives the same
+// score as its totals when the region is empty, or when every AvailableReplicas is
+// >= 0 (the prefix sums only grow) and either the whole region stays below the
+// target (the walk never breaks) or every cluster score is 0 (a break gives
+// target*1000 + 0, and so do totals at or above the target).
+KP_HD inline bool region_walk_free(int64_t cnt, int64_t negatives, int64_t sum_avail, int64_t sum_score,
+                                   int64_t target) {
+  return cnt == 0 || (negatives == 0 && (sum_avail < target || sum_score == 0));
+}
+// The score of a region whose walk is free: its totals.
+KP_HD inline int64_t region_score_totals(int64_t cnt, int64_t sum_avail, int64_t sum_score, int64_t target) {
+  if (cnt == 0) return 0;
+  if (sum_avail < target) return add64(mul64(sum_avail, 1000), sum_score / cnt);
+  return add64(mul64(target, 1000), sum_score / cnt);
+}
+
 template <class BLK>
 KP_FI bool region_a_fast(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L, RegionOut* out) {
   const int F = cd.F;
@@ -1055,6 +1071,20 @@ KP_FI bool region_a_fast(const BLK& B, const SelCtx& x, const Cands& cd, RegionL
     B.sync();
     return true;
   }
+  // calcGroupScore (divided) needs the walk only where it can stop early with a
+  // score that differs from the totals' (region_walk_free)
+  const int64_t target = go_ceil_div_i64(h.replicas, h.region_min);
+  bool walk = false;
+  for (int r = B.tid(); r < R; r += B.nth())
+    if (!region_walk_free(L.cnt[r], L.amin[r], L.sumAvail[r], L.sumScore[r], target)) walk = true;
+  if (!B.any(walk)) {
+    for (int r = B.tid(); r < R; r += B.nth()) {
+      out[r].count = L.cnt[r];
+      out[r].score = region_score_totals(L.cnt[r], L.sumAvail[r], L.sumScore[r], target);
+    }
+    B.sync();
+    return true;
+  }
   if (B.tid() == 0) {
     int32_t o = 0;
     for (int r = 0; r < R; r++) {
@@ -1089,7 +1119,6 @@ KP_FI bool region_a_fast(const BLK& B, const SelCtx& x, const Cands& cd, RegionL
   B.sync();
   // calcGroupScore (divided): each region's clusters in sortClusters order until
   // validClusters >= max(clusterMinGroups, minGroups) and the sum reaches the target
-  const int64_t target = go_ceil_div_i64(h.replicas, h.region_min);
   int64_t m = h.cluster_min;
   if (m < h.region_min) m = h.region_min;
   const int ww = B.wwidth(), lane = B.lane();
@@ -1097,7 +1126,7 @@ KP_FI bool region_a_fast(const BLK& B, const SelCtx& x, const Cands& cd, RegionL
   for (int r = B.wid(); r < R; r += B.nwaves()) {
     const int64_t cnt = L.cnt[r];
     int64_t sa = L.sumAvail[r], ss = L.sumScore[r], valid = cnt;
-    if (cnt > 0 && !(L.amin[r] == 0 && sa < target)) {  // a monotone region short of the target never breaks
+    if (!region_walk_free(cnt, L.amin[r], sa, ss, target)) {
       uint64_t last = 0;
       int64_t wcnt = 0, wsum = 0, wscore = 0;
       for (;;) {
@@ -1179,10 +1208,8 @@ KP_FI void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L,
   const int64_t target = go_ceil_div_i64(h.replicas, h.region_min);
   int64_t m = h.cluster_min;  // clusterMinGroups (last cluster constraint)
   if (m < h.region_min) m = h.region_min;
-  for (int r = B.tid(); r < R; r += B.nth()) {
-    bool monotone = L.amin[r] == 0;
-    if (L.cnt[r] == 0 || (monotone && L.sumAvail[r] < target)) L.done[r] = 1;  // never breaks: totals
-  }
+  for (int r = B.tid(); r < R; r += B.nth())
+    if (region_walk_free(L.cnt[r], L.amin[r], L.sumAvail[r], L.sumScore[r], target)) L.done[r] = 1;  // totals
   B.sync();
   KP_COUNT(x, 21, 1);
   for (;;) {

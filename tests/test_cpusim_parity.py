@@ -69,6 +69,8 @@ def test_cpusim_schedule_parity(engine, config, seed, n_clusters, n_bindings, ro
         assert times[0]["bits"] == int(not rows)
     if config in (4, 5) and not rows:  # cluster spread without spec.Clusters: the class-order selection
         assert 0 < times[0]["n_cluster_order"] <= times[0]["n_cluster"]
+    if config == 4 and not rows:
+        assert 0 < times[0]["n_region_order"] <= times[0]["n_region"]
 
 
 @pytest.mark.parametrize("prop,plugins,gate", [

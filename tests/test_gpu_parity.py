@@ -99,6 +99,8 @@ def test_schedule_parity(engine, config, seed, n_clusters, n_bindings):
     if config in (4, 5):  # cluster spread without spec.Clusters: the class-order selection ran
         t = engine.stage_times()
         assert 0 < t["n_cluster_order"] <= t["n_cluster"]
+        if config == 4:
+            assert 0 < t["n_region_order"] <= t["n_region"]
 
 
 @pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
