@@ -144,16 +144,17 @@ int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const Sele
            [&](int blk, unsigned char* sm) { body_select_all_stream(CpuBlk{(int64_t*)sm}, blk, sm, a); });
       break;
     case SEL_LAUNCH_CLUSTER:
-      grid(a.n, smem,
-           [&](int blk, unsigned char* sm) { body_select_cluster(CpuBlk{(int64_t*)sm}, blk, sm, a, cap); });
+      grid(a.n_dev ? (int)*a.n_dev : a.n, smem, [&](int j, unsigned char* sm) {
+        body_select_cluster(CpuBlk{(int64_t*)sm}, a.sub ? a.sub[j] : j, sm, a, cap);
+      });
       break;
     case SEL_LAUNCH_REGION_A:
       grid(a.n, smem,
            [&](int blk, unsigned char* sm) { body_region_a(CpuBlk{(int64_t*)sm}, blk, sm, a, x.rout, x.rstat); });
       break;
     case SEL_LAUNCH_REGION_B:
-      grid(a.n, smem, [&](int blk, unsigned char* sm) {
-        body_region_b(CpuBlk{(int64_t*)sm}, blk, sm, a, x.rsel, x.rnsel, x.rout, cap);
+      grid(a.n_dev ? (int)*a.n_dev : a.n, smem, [&](int j, unsigned char* sm) {
+        body_region_b(CpuBlk{(int64_t*)sm}, a.sub ? a.sub[j] : j, sm, a, x.rsel, x.rnsel, x.rout, cap);
       });
       break;
     case SEL_LAUNCH_SLOW:
@@ -221,6 +222,11 @@ int node_est(stream_t, const NodeEstArgs& A) {
   uint32_t s = 0;
   for (uint64_t i = 0; i < A.v.n; i++) s += (uint32_t)node_replicas(A, i);
   *A.sum += s;
+  return 0;
+}
+
+int spread_order(stream_t, const KArgs& a, const OrderArgs& o, size_t slice) {
+  grid(a.n, slice, [&](int blk, unsigned char* sm) { body_spread_order(CpuBlk{(int64_t*)sm}, blk, sm, a, o); });
   return 0;
 }
 

@@ -249,6 +249,7 @@ struct kp_batch {
   uint64_t* d_ord = nullptr;
   int64_t* d_ctot = nullptr;
   int32_t *d_cok = nullptr, *d_fb = nullptr;
+  int32_t *d_fbc = nullptr, *d_fbr = nullptr;  // k_spread_order's fallback lists (cluster / region positions)
   std::vector<int32_t> sets_cls, l_sets;
   std::vector<SetsArgs> sets_args;
   SetsArgs* d_sets_args = nullptr;
@@ -264,7 +265,8 @@ struct kp_batch {
   uint32_t* stats = nullptr;
   unsigned long long* dbg = nullptr;
   uint32_t h_stats[16] = {};  // [0..7] slow-path counts, [8] component-set simulation overflow, [9] k_select_top
-                              // fallbacks, [10] / [11] cluster- / region-spread bindings selected over the class order
+                              // fallbacks, [10] / [11] cluster- / region-spread bindings selected over the class order,
+                              // [12] / [13] k_spread_order's fallback list lengths
   uint32_t* out_idx = nullptr;
   int32_t* out_rep = nullptr;
   uint64_t* offsets_d = nullptr;
@@ -2224,7 +2226,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->counter, 1);
   a.add(&bt->stats, 16);
 #ifdef KP_STAMPS
-  a.add(&bt->dbg, 32);
+  a.add(&bt->dbg, 64);
 #endif
   // [0, out_cap): per-binding slots; [out_cap, 2 out_cap): serial results past their slot
   a.add(&bt->out_idx, std::max<uint64_t>(1, 2 * bt->out_cap));
@@ -2244,6 +2246,8 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
     a.add(&bt->d_ctot, bt->crep.size());
     a.add(&bt->d_cok, bt->crep.size());
     a.add(&bt->d_fb, std::max(1, bt->n_all_dyn));
+    a.add(&bt->d_fbc, std::max<size_t>(1, bt->l_cluster.size()));
+    a.add(&bt->d_fbr, std::max(1, nr));
   }
   // component-set classes: per cluster rank its node-run scratch (one run per model
   // node at most, capped at kSetsRunsMax) for k_sets_rows, reused class after class
@@ -2364,7 +2368,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   ka.slow_ids = bt->d_slowlist;
   ka.dbg = bt->dbg;
 #ifdef KP_STAMPS
-  HIPCHK(dev::fill(bt->dbg, 0, 32 * 8, st));
+  HIPCHK(dev::fill(bt->dbg, 0, 64 * 8, st));
 #endif
   dev::stream_t sp = e->stream2;
   HIPCHK(dev::event_record(e->ev[0], st));
@@ -2478,12 +2482,17 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
     KArgs k = ka;
     k.list = bt->d_cluster;
     k.n = (int)bt->l_cluster.size();
+    HIPCHK(dev::event_record(e->ev[14], s3));
     if (orders) {
+      // the class-order selection, one wave per binding; what it hands back runs below
       k.ord = bt->d_ord;
       k.cok = bt->d_cok;
       k.n_order = bt->stats + 10;
+      OrderArgs oa{nullptr, nullptr, nullptr, bt->d_fbc, bt->stats + 12, 0};
+      HIPCHK(dev::spread_order(s3, k, oa, (order_lds_bytes(s->view.W, s->view.n_regions) + 15) & ~(size_t)15));
+      k.sub = bt->d_fbc;
+      k.n_dev = bt->stats + 12;
     }
-    HIPCHK(dev::event_record(e->ev[14], s3));
     HIPCHK(dev::select(s3, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sx));
     HIPCHK(dev::event_record(e->ev[15], s3));
   }
@@ -2554,6 +2563,12 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
       th1 = now_ms();
       HIPCHK(dev::h2d(bt->rsel, bt->h_rsel.data(), 4 * bt->h_rsel.size(), st));
       HIPCHK(dev::h2d(bt->rnsel, bt->h_rnsel.data(), 4 * nr, st));
+    }
+    if (orders) {
+      OrderArgs oa{bt->rout, bt->rsel, bt->rnsel, bt->d_fbr, bt->stats + 13, 1};
+      HIPCHK(dev::spread_order(st, k, oa, (order_lds_bytes(s->view.W, R) + 15) & ~(size_t)15));
+      k.sub = bt->d_fbr;
+      k.n_dev = bt->stats + 13;
     }
     HIPCHK(dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sx));
   }
@@ -2636,20 +2651,21 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   tm.n_region_order = orders ? bt->h_stats[11] : 0u;
 #ifdef KP_STAMPS
   {
-    unsigned long long h[32];
+    unsigned long long h[64];
     HIPCHK(dev::d2h(h, bt->dbg, sizeof(h), st));
     HIPCHK(dev::sync(st));
     fprintf(stderr, "kp stamps (s_memtime ticks, summed over workgroups):");
-    for (int i = 0; i < 32; i++) fprintf(stderr, " [%d]=%llu", i, h[i]);
+    for (int i = 0; i < 64; i++)
+      if (h[i]) fprintf(stderr, " [%d]=%llu", i, h[i]);
     fprintf(stderr, "\n");
   }
 #endif
   if (getenv("KP_DEBUG_SLOW"))
     fprintf(stderr,
             "kp slow: total %u overflow/dup %u scale-down %u wrap %u tie %u weight %u cluster %u "
-            "(ties resolved block-parallel %u)\n",
+            "(ties resolved block-parallel %u); class-order spread fallbacks: cluster %u region %u\n",
             bt->h_stats[0], bt->h_stats[1], bt->h_stats[2], bt->h_stats[3], bt->h_stats[4], bt->h_stats[5],
-            bt->h_stats[6], bt->h_stats[7]);
+            bt->h_stats[6], bt->h_stats[7], bt->h_stats[12], bt->h_stats[13]);
   tm.pair_ms = ms_pair;
   tm.select_ms = ms_sel;
   tm.host_ms = th1 - th0;

@@ -108,6 +108,17 @@ extern "C" __global__ void __launch_bounds__(64 * kStaticWaves) k_select_static(
   if (blk >= a.n) return;  // wave-uniform: the waves never synchronise with each other
   body_select_static(WaveBlk{(int64_t*)mine}, blk, mine, a);
 }
+// Spread selections over the class orders (kp_kernels.h body_spread_order): one wave
+// per binding, kOrderWaves independent waves per workgroup.
+constexpr int kOrderWaves = 4;
+extern "C" __global__ void __launch_bounds__(64 * kOrderWaves) k_spread_order(KArgs a, OrderArgs o, int slice) {
+  KP_SMEM;
+  const int w = (int)(threadIdx.x >> 6);
+  unsigned char* mine = smem + (size_t)w * (size_t)slice;
+  const int blk = (int)blockIdx.x * kOrderWaves + w;
+  if (blk >= a.n) return;  // wave-uniform: the waves never synchronise with each other
+  body_spread_order(WaveBlk{(int64_t*)mine}, blk, mine, a, o);
+}
 // Each estimator class's row in (estimate desc, rank asc) order: LDS bitonic sort.
 extern "C" __global__ void __launch_bounds__(1024) k_class_order(SnapView s, const int32_t* rows, int P, uint64_t* ord,
                                                                 int64_t* tot, int32_t* ok) {
@@ -140,7 +151,7 @@ extern "C" __global__ void __launch_bounds__(1024) k_select_all_wide(KArgs a) {
 #define KP_SPREAD_KERNELS(SUF, T, MINW)                                                                          \
   extern "C" __global__ void __launch_bounds__(T, MINW) k_select_cluster##SUF(KArgs a, int cap) {              \
     KP_SMEM;                                                                                                   \
-    body_select_cluster(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, cap);                                \
+    KP_LIST_LOOP(body_select_cluster(GpuBlk{(int64_t*)smem}, a.sub ? a.sub[blk] : blk, smem, a, cap))         \
   }                                                                                                            \
   extern "C" __global__ void __launch_bounds__(T, MINW) k_region_a##SUF(KArgs a, RegionOut* rout, int32_t* rstat) { \
     KP_SMEM;                                                                                                   \
@@ -150,7 +161,7 @@ extern "C" __global__ void __launch_bounds__(1024) k_select_all_wide(KArgs a) {
                                                                       const int32_t* rnsel,                    \
                                                                       const RegionOut* rout, int cap) {        \
     KP_SMEM;                                                                                                   \
-    body_region_b(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, rsel, rnsel, rout, cap);                   \
+    KP_LIST_LOOP(body_region_b(GpuBlk{(int64_t*)smem}, a.sub ? a.sub[blk] : blk, smem, a, rsel, rnsel, rout, cap)) \
   }
 KP_SPREAD_KERNELS(, 256, 3)
 KP_SPREAD_KERNELS(_wide, 512, 4)
@@ -339,6 +350,9 @@ int filter(stream_t st, const SnapView& s, const BatchView& bv, uint64_t* fmask)
   return chk(hipGetLastError());
 }
 
+// one workgroup per list entry, or over a device-appended list a persistent grid
+static int spread_grid(const KArgs& a) { return a.n_dev ? std::min(a.n, 256 * 4) : a.n; }
+
 int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x) {
   if (a.n <= 0) return 0;
   hipStream_t h = (hipStream_t)st;
@@ -358,9 +372,9 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
       break;
     case SEL_LAUNCH_CLUSTER:
       if (smem > kLdsPerCu / 2)
-        hipLaunchKernelGGL(k_select_cluster_wide, dim3(a.n), dim3(512), smem, h, a, cap);
+        hipLaunchKernelGGL(k_select_cluster_wide, dim3(spread_grid(a)), dim3(512), smem, h, a, cap);
       else
-        hipLaunchKernelGGL(k_select_cluster, dim3(a.n), dim3(256), smem, h, a, cap);
+        hipLaunchKernelGGL(k_select_cluster, dim3(spread_grid(a)), dim3(256), smem, h, a, cap);
       break;
     case SEL_LAUNCH_REGION_A:
       if (smem > kLdsPerCu / 2)
@@ -370,9 +384,9 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
       break;
     case SEL_LAUNCH_REGION_B:
       if (smem > kLdsPerCu / 2)
-        hipLaunchKernelGGL(k_region_b_wide, dim3(a.n), dim3(512), smem, h, a, x.rsel, x.rnsel, x.rout, cap);
+        hipLaunchKernelGGL(k_region_b_wide, dim3(spread_grid(a)), dim3(512), smem, h, a, x.rsel, x.rnsel, x.rout, cap);
       else
-        hipLaunchKernelGGL(k_region_b, dim3(a.n), dim3(256), smem, h, a, x.rsel, x.rnsel, x.rout, cap);
+        hipLaunchKernelGGL(k_region_b, dim3(spread_grid(a)), dim3(256), smem, h, a, x.rsel, x.rnsel, x.rout, cap);
       break;
     case SEL_LAUNCH_SLOW:
       if (smem > 65536 &&
@@ -408,6 +422,17 @@ int select_top(stream_t st, const KArgs& a, const TopArgs& t, size_t slice) {
     return -1;
   hipLaunchKernelGGL(k_select_top, dim3((a.n + kTopWaves - 1) / kTopWaves), dim3(64 * kTopWaves), smem,
                      (hipStream_t)st, a, t, (int)slice);
+  return chk(hipGetLastError());
+}
+
+int spread_order(stream_t st, const KArgs& a, const OrderArgs& o, size_t slice) {
+  if (a.n <= 0) return 0;
+  const size_t smem = slice * kOrderWaves;
+  if (smem > 65536 &&
+      chk(hipFuncSetAttribute((const void*)k_spread_order, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)))
+    return -1;
+  hipLaunchKernelGGL(k_spread_order, dim3((a.n + kOrderWaves - 1) / kOrderWaves), dim3(64 * kOrderWaves), smem,
+                     (hipStream_t)st, a, o, (int)slice);
   return chk(hipGetLastError());
 }
 

@@ -14,6 +14,7 @@
 namespace kp {
 struct SetsArgs;
 struct TopArgs;
+struct OrderArgs;
 struct GradesArgs;
 struct NodeEstArgs;
 struct NodeView;
@@ -92,6 +93,9 @@ int node_est(stream_t st, const NodeEstArgs& A);
 // StaticWeight SEL_ALL bindings a.list[0, a.n) at class level (body_select_static),
 // one wave each with `slice` bytes of LDS.
 int select_static(stream_t st, const KArgs& a, size_t slice);
+// Spread selections over the estimator-class orders (body_spread_order), one wave
+// per binding, `slice` bytes of LDS each; unfinished list positions go to o.fb.
+int spread_order(stream_t st, const KArgs& a, const OrderArgs& o, size_t slice);
 // kp_node_max_component_sets: match[k * n + j] = MatchNode(node j, P[k]) (P in
 // device memory), then the first-fit set simulation by one wave (A in device memory).
 int node_match(stream_t st, const NodeView& v, const ClaimProg* P, int K, uint8_t* match);

@@ -725,33 +725,56 @@ KP_FI void body_select_all_stream(const BLK& B, int blk, unsigned char* smem, co
 // ---------------------------------------------------------------------------
 // Select stage: SEL_CLUSTER
 // ---------------------------------------------------------------------------
-// selectBestClustersByCluster (select_clusters_by_cluster.go:25-102) over the
-// binding's estimator-class order (k_class_order) instead of a gather and a radix
-// select. With no spec.Clusters (locality score 0, assigned replicas 0) and no
-// overflow tiers (order 0), the sortClusters key of every candidate reduces to
-// (estimate desc, name asc): the class order filtered by the feasibility row. The
-// first min(F, MaxGroups) feasible entries are then the selection, and the swap
-// step never fires (every rest cluster's AvailableReplicas is at most the last
-// selected one's, and it needs a strictly larger one), so only the resource check
-// remains. Returns false (nothing written) when the shortcut does not apply.
-template <class BLK>
-KP_FI bool cluster_by_order(const BLK& B, const KArgs& a, const SelCtx& x, uint32_t* hist, Item* items,
-                            unsigned char* scratch, int cap, size_t area_bytes) {
+// Outcome of a class-order selection (cluster_order_select, region_order_select).
+enum : int { ORD_NA = 0, ORD_DONE = 1, ORD_ITEMS = 2 };
+
+// The class-order selections apply to a binding without spec.Clusters (locality
+// score 0, assigned replicas 0) and without overflow tiers (order 0) whose class
+// row can be walked (k_class_order's ok: no MaxInt32, no negative estimate): its
+// sortClusters key is then (estimate desc, name asc), i.e. the class order filtered
+// by its feasibility row. Returns the class, or -1.
+KP_HD inline int32_t order_class(const KArgs& a, const SelCtx& x) {
   const BindHdr& h = *x.h;
-  if (!a.ord || !a.cok || !a.bcls) return false;
+  if (!a.ord || !a.cok || !a.bcls) return -1;
   const int32_t cls = a.bcls[x.b];
-  if (cls <= 0 || !a.cok[cls] || h.tgt_cnt != 0 || h.ovf_mode != OVF_ZERO || (h.flags & BF_BAD)) return false;
+  if (cls <= 0 || !a.cok[cls] || h.tgt_cnt != 0 || h.ovf_mode != OVF_ZERO || (h.flags & BF_BAD)) return -1;
+  return cls;
+}
+KP_HD inline Item order_item(uint64_t e) {
+  Item it;
+  it.rank = (uint32_t)e;
+  it.alloc = (int32_t)(e >> 32);  // est_at: the class row holds no MaxInt32 (ok), so no merge
+  it.avail = (int64_t)(int32_t)(e >> 32);
+  it.ovf = 0;
+  it.pad = 0;
+  return it;
+}
+
+// selectBestClustersByCluster (select_clusters_by_cluster.go:25-102) over the
+// binding's estimator-class order instead of a gather and a radix select: the
+// first min(F, MaxGroups) feasible entries are the selection, and the swap step
+// never fires (every rest cluster's AvailableReplicas is at most the last selected
+// one's, and a swap needs a strictly larger one), so only the resource check
+// remains. ORD_ITEMS: items[0, *n) in sortClusters order (at most max_items);
+// ORD_DONE: the status is written; ORD_NA: nothing written.
+template <class BLK>
+KP_FI int cluster_order_select(const BLK& B, const KArgs& a, const SelCtx& x, Item* items, int max_items, int* n_out) {
+  const BindHdr& h = *x.h;
+  const int32_t cls = order_class(a, x);
+  if (cls < 0) return ORD_NA;
+  KP_STAMP_INIT
   const SnapView& s = *x.s;
   int64_t F = 0;
   for (int w = B.tid(); w < s.W; w += B.nth()) F += popc64(x.frow[w]);
   F = B.sum64(F);
+  KP_STAMP(x, 37);
   if (F == 0) {  // FitError (generic_scheduler.go:84-89)
     if (B.tid() == 0) sink_error(x, KP_STATUS_FIT_ERROR, KP_ERR_FIT, s.C);
-    return true;
+    return ORD_DONE;
   }
   if (F < h.cluster_min) {
     if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_CLUSTER_MIN_GROUPS, 0);
-    return true;
+    return ORD_DONE;
   }
   int64_t needCnt = F < h.cluster_max ? F : h.cluster_max;
   if (needCnt < 0) needCnt = 0;
@@ -761,9 +784,9 @@ KP_FI bool cluster_by_order(const BLK& B, const KArgs& a, const SelCtx& x, uint3
       if (need == -1) sink_error(x, KP_STATUS_ERROR, KP_ERR_NO_CLUSTERS, 0);
       else sink_error(x, KP_STATUS_ERROR, KP_ERR_CLUSTER_RESOURCE, 0);
     }
-    return true;
+    return ORD_DONE;
   }
-  if (needCnt > kSmallMax) return false;
+  if (needCnt > max_items) return ORD_NA;
   // walk the class order, nth entries per step, keeping the feasible ones in order
   const uint64_t* ord = a.ord + (size_t)cls * s.Cp;
   int n = 0;
@@ -779,28 +802,21 @@ KP_FI bool cluster_by_order(const BLK& B, const KArgs& a, const SelCtx& x, uint3
     int32_t cnt;
     const int32_t pos = n + B.excl_scan(in ? 1 : 0, &cnt);
     if (in && pos < needCnt) {
-      Item it;
-      it.rank = (uint32_t)e;
-      it.alloc = (int32_t)(e >> 32);  // est_at: the row holds no MaxInt32 (cok), so no merge
-      it.avail = (int64_t)(int32_t)(e >> 32);
-      it.ovf = 0;
-      it.pad = 0;
-      items[pos] = it;
-      tot += it.avail;
+      items[pos] = order_item(e);
+      tot += (int32_t)(e >> 32);
     }
     n += cnt;
   }
   B.sync();
   if (n > needCnt) n = (int)needCnt;
   tot = B.sum64(tot);
+  KP_STAMP(x, 38);
   if (need != -1 && tot < (int64_t)need) {  // selectClustersByAvailableResource: no swap can help
     if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_CLUSTER_RESOURCE, needCnt);
-    return true;
+    return ORD_DONE;
   }
-  (void)hist;
-  if (B.tid() == 0 && a.n_order) kp_atomic_add(a.n_order, 1u);
-  assign_small(B, x, items, n, scratch, cap, area_bytes);
-  return true;
+  *n_out = n;
+  return ORD_ITEMS;
 }
 
 template <class BLK>
@@ -823,13 +839,94 @@ KP_FI void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const
   KP_STAMP(x, 26);
   const size_t area_bytes = 8 * (size_t)a.s.Cp > serial_scratch_bytes(scratch_cap) ? 8 * (size_t)a.s.Cp
                                                                                     : serial_scratch_bytes(scratch_cap);
-  if (cluster_by_order(B, a, x, hist, items, area, scratch_cap, area_bytes)) return;
+  {
+    int n = 0;
+    const int o = cluster_order_select(B, a, x, items, kSmallMax, &n);
+    if (o == ORD_DONE) return;
+    if (o == ORD_ITEMS) {
+      if (B.tid() == 0 && a.n_order) kp_atomic_add(a.n_order, 1u);
+      assign_small(B, x, items, n, area, scratch_cap, area_bytes);
+      KP_STAMP(x, 39);
+      return;
+    }
+  }
   cd.F = gather(B, x, cd, false);
   KP_STAMP(x, 27);
   if (pre_checks(B, x, cd.F)) return;
   if (!sel_cluster_fast(B, x, cd, hist, items, keys, area, scratch_cap, area_bytes)) {
     if (B.tid() == 0) flag_slow(a, b, SLOW_CLUSTER);
   }
+}
+
+// ---------------------------------------------------------------------------
+// k_spread_order: the class-order selections of the spread kernels
+// (cluster_order_select, region_order_select) and the assignment over the
+// selected list, one wave per binding with a small LDS slice (no Cp-sized
+// candidate arrays), so many bindings are resident per CU. A binding it does not
+// finish (ORD_NA, a list past kOrderItems, or an assignment sel_all_fast refuses)
+// is appended to a fallback list of list positions for the full kernel.
+// ---------------------------------------------------------------------------
+struct OrderArgs {
+  const RegionOut* rout;  // region stage B: stage A's per-region counts [n][R]
+  const int32_t* rsel;    // region stage B: selected region ids [n][R]
+  const int32_t* rnsel;   // region stage B: their count (-1000 finalised by stage A, < 0 an error)
+  int32_t* fb;            // list positions handed to the full kernel
+  uint32_t* fb_n;
+  int region;  // 0: cluster spread (k_select_cluster), 1: region stage B (k_region_b)
+};
+constexpr int kOrderItems = 64;  // selected-list capacity
+constexpr int kOrderEcap = 128;  // sel_all_fast's party list (>= 64 + kOrderItems)
+KP_HD inline size_t order_lds_bytes(int W, int R) {
+  return 64 + 8 * (size_t)R + 4 * (size_t)((R + 3) & ~3) + sizeof(Item) * kOrderItems + 8 * (size_t)W + 2048 +
+         1024 + 8 * (size_t)kOrderEcap;
+}
+template <class BLK>
+KP_FI void body_spread_order(const BLK& B, int blk, unsigned char* smem, const KArgs& a, const OrderArgs& o) {
+  if (blk >= a.n) return;
+  const int b = a.list[blk];
+  const int R = a.s.n_regions, W = a.s.W;
+  unsigned char* p = smem + 64;
+  unsigned long long* hpos = (unsigned long long*)p;
+  p += 8 * (size_t)R;
+  int32_t* rs = (int32_t*)p;
+  p += 4 * (size_t)((R + 3) & ~3);
+  Item* items = (Item*)p;
+  p += sizeof(Item) * kOrderItems;
+  uint64_t* selb = (uint64_t*)p;
+  SelCtx x = make_ctx(a, b, nullptr);  // no spec.Clusters on this path: the target bitset is never read
+  int n = 0, st = ORD_NA;
+  if (o.region) {
+    const int nsel = o.rnsel[blk];
+    if (nsel == -1000) return;  // stage A wrote the status
+    if (nsel >= 0)
+      st = region_order_select(B, a, x, o.rout + (size_t)blk * R, o.rsel + (size_t)blk * R, nsel, hpos, rs, items,
+                               kOrderItems, &n);
+  } else {
+    st = cluster_order_select(B, a, x, items, kOrderItems, &n);
+  }
+  if (st == ORD_DONE) return;
+  int why = SLOW_NONE + 1;
+  if (st == ORD_ITEMS) {  // assign_small's block-parallel assignment over the list
+    for (int w = B.tid(); w < W; w += B.nth()) selb[w] = 0;
+    B.sync();
+    uint32_t* sel32 = (uint32_t*)selb;
+    for (int i = B.tid(); i < n; i += B.nth()) kp_atomic_or(&sel32[items[i].rank >> 5], 1u << (items[i].rank & 31));
+    B.sync();
+    SelCtx y = x;
+    y.frow = selb;
+    SelScratch ss;
+    ss.whist = (unsigned long long*)(selb + W);
+    ss.hist = (uint32_t*)(ss.whist + 256);
+    ss.buf = (uint64_t*)(ss.hist + 256);
+    ss.cap = kOrderEcap;
+    why = sel_all_fast(B, y, ItemCands{items, n, B.tid(), B.nth(), &y, x.h->strategy == ST_STATIC}, ss);
+    B.sync();
+  }
+  if (why == SLOW_NONE) {
+    if (B.tid() == 0 && a.n_order) kp_atomic_add(a.n_order, 1u);
+    return;
+  }
+  if (B.tid() == 0) o.fb[kp_atomic_add(o.fb_n, 1u)] = blk;
 }
 
 // ---------------------------------------------------------------------------
@@ -892,29 +989,28 @@ KP_FI void body_region_a(const BLK& B, int blk, unsigned char* smem, const KArgs
 }
 
 // selectBestClustersByRegion (select_clusters_by_region.go:41-63) over the
-// binding's estimator-class order, for the bindings cluster_by_order covers (no
-// spec.Clusters, no overflow tiers: the sortClusters order is the class order
-// filtered by the feasibility row). Each selected region's head is its first entry
-// in that order, the rest are the next restCnt entries of the selected regions that
-// are not heads, and the candidate count comes from stage A's per-region counts, so
-// the walk stops once the heads and the rest are found instead of gathering every
-// candidate. hpos: [R] LDS. Returns false (nothing written) when it does not apply.
+// binding's estimator-class order (order_class): each selected region's head is
+// its first entry in that order, the rest are the next restCnt entries of the
+// selected regions that are not heads, and the candidate count comes from stage
+// A's per-region counts, so the walk stops once the heads and the rest are found
+// instead of gathering every candidate. hpos, rsel: [R] LDS. ORD_ITEMS: items[0, *n)
+// = the heads in path order, then the rest in sortClusters order.
 template <class BLK>
-KP_FI bool region_b_by_order(const BLK& B, const KArgs& a, const SelCtx& x, const RegionOut* ro, const int32_t* sel,
-                             int nsel, unsigned long long* hpos, int32_t* rsel, Item* items, void* scratch, int cap,
-                             size_t area_bytes) {
+KP_FI int region_order_select(const BLK& B, const KArgs& a, const SelCtx& x, const RegionOut* ro, const int32_t* sel,
+                              int nsel, unsigned long long* hpos, int32_t* rsel, Item* items, int max_items,
+                              int* n_out) {
   const BindHdr& h = *x.h;
-  if (!a.ord || !a.cok || !a.bcls || !ro) return false;
-  const int32_t cls = a.bcls[x.b];
-  if (cls <= 0 || !a.cok[cls] || h.tgt_cnt != 0 || h.ovf_mode != OVF_ZERO || (h.flags & BF_BAD)) return false;
+  const int32_t cls = order_class(a, x);
+  if (cls < 0 || !ro) return ORD_NA;
+  KP_STAMP_INIT
   const SnapView& s = *x.s;
   const int R = s.n_regions;
   int64_t total = 0;
   for (int j = 0; j < nsel; j++) total += ro[sel[j]].count;
-  int64_t needCnt = total < h.cluster_max ? total : h.cluster_max;
+  const int64_t needCnt = total < h.cluster_max ? total : h.cluster_max;
   const int64_t restCnt = needCnt - nsel;
-  if (restCnt > kSmallMax - nsel) return false;  // the general path reports the engine limit
   const int64_t want = restCnt > 0 ? restCnt : 0;
+  if (nsel + want > max_items) return ORD_NA;  // the general path (and its engine limit)
   for (int r = B.tid(); r < R; r += B.nth()) {
     hpos[r] = ~0ull;
     rsel[r] = -1;
@@ -923,6 +1019,7 @@ KP_FI bool region_b_by_order(const BLK& B, const KArgs& a, const SelCtx& x, cons
   for (int j = B.tid(); j < nsel; j += B.nth()) rsel[sel[j]] = j;
   B.sync();
   const uint64_t* ord = a.ord + (size_t)cls * s.Cp;
+  KP_STAMP(x, 32);
   int nh = 0, nr = 0;
   for (int i0 = 0; i0 < s.C && (nh < nsel || nr < want); i0 += B.nth()) {
     const int i = i0 + B.tid();
@@ -944,32 +1041,19 @@ KP_FI bool region_b_by_order(const BLK& B, const KArgs& a, const SelCtx& x, cons
     int32_t cnt;
     const int32_t pk = B.excl_scan((rest ? 1 : 0) | (head ? 1 << 16 : 0), &cnt);
     const int32_t pos = nr + (pk & 0xffff);
-    if (rest && pos < want) {
-      Item& it = items[nsel + pos];
-      it.rank = (uint32_t)e;
-      it.alloc = (int32_t)(e >> 32);  // est_at: the class row holds no MaxInt32 (cok)
-      it.avail = (int64_t)(int32_t)(e >> 32);
-      it.ovf = 0;
-      it.pad = 0;
-    }
+    if (rest && pos < want) items[nsel + pos] = order_item(e);
     nr += cnt & 0xffff;
     nh += cnt >> 16;
+    KP_COUNT(x, 36, 1);
   }
   B.sync();
-  if (nh < nsel || nr < want) return false;  // a selected region without a feasible cluster
-  for (int j = B.tid(); j < nsel; j += B.nth()) {
-    const uint64_t e = ord[hpos[sel[j]]];
-    Item& it = items[j];
-    it.rank = (uint32_t)e;
-    it.alloc = (int32_t)(e >> 32);
-    it.avail = (int64_t)(int32_t)(e >> 32);
-    it.ovf = 0;
-    it.pad = 0;
-  }
+  KP_STAMP(x, 33);
+  if (nh < nsel || nr < want) return ORD_NA;  // a selected region without a feasible cluster
+  for (int j = B.tid(); j < nsel; j += B.nth()) items[j] = order_item(ord[hpos[sel[j]]]);
   B.sync();
-  if (B.tid() == 0 && a.n_order) kp_atomic_add(a.n_order, 1u);
-  assign_small(B, x, items, nsel + (int)want, scratch, cap, area_bytes);
-  return true;
+  KP_STAMP(x, 34);
+  *n_out = nsel + (int)want;
+  return ORD_ITEMS;
 }
 
 // Region stage B. rsel: [n][n_regions] selected region ids (path order); rnsel[n]:
@@ -1015,9 +1099,16 @@ KP_FI void body_region_b(const BLK& B, int blk, unsigned char* smem, const KArgs
   KP_STAMP(x, 16);
   const size_t area_bytes = 8 * (size_t)a.s.Cp > serial_scratch_bytes(scratch_cap) ? 8 * (size_t)a.s.Cp
                                                                                     : serial_scratch_bytes(scratch_cap);
-  if (region_b_by_order(B, a, x, rout ? rout + (size_t)blk * R : nullptr, rsel + (size_t)blk * R, nsel, heads, rs,
-                        items, p, scratch_cap, area_bytes))
-    return;
+  {
+    int n = 0;
+    if (region_order_select(B, a, x, rout ? rout + (size_t)blk * R : nullptr, rsel + (size_t)blk * R, nsel, heads, rs,
+                            items, kSmallMax, &n) == ORD_ITEMS) {
+      if (B.tid() == 0 && a.n_order) kp_atomic_add(a.n_order, 1u);
+      assign_small(B, x, items, n, p, scratch_cap, area_bytes);
+      KP_STAMP(x, 35);
+      return;
+    }
+  }
   cd.F = gather(B, x, cd, false);
   region_of_cands(B, a.s, cd);
   KP_STAMP(x, 17);

@@ -32,6 +32,9 @@ struct KArgs {
   const uint64_t* ord = nullptr;
   const int32_t* cok = nullptr;
   uint32_t* n_order = nullptr;  // count of the bindings that took it
+  // set (with n_dev): loop index j stands for list position sub[j] (a device-appended
+  // fallback list of positions, so per-position arrays such as rsel stay aligned)
+  const int32_t* sub = nullptr;
 };
 
 enum : int {

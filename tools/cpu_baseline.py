@@ -57,6 +57,7 @@ def main():
             n, dt = sample(u, O.REFSHAPE, th, args.budget)
             out["configs"].setdefault(str(cfg), {})[f"refshape_{th}t"] = {"bindings": n, "s": round(dt, 3),
                                                                             "per_s": round(n / dt, 2)}
+            print(f"config {cfg} {th}t: {n} bindings in {dt:.2f} s", file=sys.stderr, flush=True)
     out["configs"]["3"]["faithful_pairs_1t"] = faithful_pairs(args.budget)
     print(json.dumps(out))
 
