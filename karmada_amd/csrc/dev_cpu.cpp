@@ -149,8 +149,9 @@ int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const Sele
       });
       break;
     case SEL_LAUNCH_REGION_A:
-      grid(a.n, smem,
-           [&](int blk, unsigned char* sm) { body_region_a(CpuBlk{(int64_t*)sm}, blk, sm, a, x.rout, x.rstat); });
+      grid(a.n_dev ? (int)*a.n_dev : a.n, smem, [&](int j, unsigned char* sm) {
+        body_region_a(CpuBlk{(int64_t*)sm}, a.sub ? a.sub[j] : j, sm, a, x.rout, x.rstat);
+      });
       break;
     case SEL_LAUNCH_REGION_B:
       grid(a.n_dev ? (int)*a.n_dev : a.n, smem, [&](int j, unsigned char* sm) {
@@ -227,6 +228,14 @@ int node_est(stream_t, const NodeEstArgs& A) {
 
 int spread_order(stream_t, const KArgs& a, const OrderArgs& o, size_t slice) {
   grid(a.n, slice, [&](int blk, unsigned char* sm) { body_spread_order(CpuBlk{(int64_t*)sm}, blk, sm, a, o); });
+  return 0;
+}
+
+int region_a_order(stream_t, const KArgs& a, RegionOut* rout, int32_t* rstat, int32_t* fb, uint32_t* fb_n,
+                   size_t slice) {
+  grid(a.n, slice, [&](int blk, unsigned char* sm) {
+    body_region_a_order(CpuBlk{(int64_t*)sm}, blk, sm, a, rout, rstat, fb, fb_n);
+  });
   return 0;
 }
 

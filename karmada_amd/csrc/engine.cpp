@@ -250,6 +250,7 @@ struct kp_batch {
   int64_t* d_ctot = nullptr;
   int32_t *d_cok = nullptr, *d_fb = nullptr;
   int32_t *d_fbc = nullptr, *d_fbr = nullptr;  // k_spread_order's fallback lists (cluster / region positions)
+  int32_t* d_fba = nullptr;                     // k_region_a_order's fallback list
   std::vector<int32_t> sets_cls, l_sets;
   std::vector<SetsArgs> sets_args;
   SetsArgs* d_sets_args = nullptr;
@@ -266,7 +267,7 @@ struct kp_batch {
   unsigned long long* dbg = nullptr;
   uint32_t h_stats[16] = {};  // [0..7] slow-path counts, [8] component-set simulation overflow, [9] k_select_top
                               // fallbacks, [10] / [11] cluster- / region-spread bindings selected over the class order,
-                              // [12] / [13] k_spread_order's fallback list lengths
+                              // [12] / [13] k_spread_order's fallback list lengths, [14] k_region_a_order's
   uint32_t* out_idx = nullptr;
   int32_t* out_rep = nullptr;
   uint64_t* offsets_d = nullptr;
@@ -2248,6 +2249,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
     a.add(&bt->d_fb, std::max(1, bt->n_all_dyn));
     a.add(&bt->d_fbc, std::max<size_t>(1, bt->l_cluster.size()));
     a.add(&bt->d_fbr, std::max(1, nr));
+    a.add(&bt->d_fba, std::max(1, nr));
   }
   // component-set classes: per cluster rank its node-run scratch (one run per model
   // node at most, capped at kSetsRunsMax) for k_sets_rows, reused class after class
@@ -2508,7 +2510,18 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
       k.cok = bt->d_cok;
       k.n_order = bt->stats + 11;
     }
-    HIPCHK(dev::select(st, SEL_LAUNCH_REGION_A, k, smem_region_a(s), cap, sx));
+    if (orders) {  // stage A of the order-eligible bindings, one wave each; the rest below
+      KArgs ko = k;
+      ko.n_order = nullptr;
+      HIPCHK(dev::region_a_order(st, ko, bt->rout, bt->rstat, bt->d_fba, bt->stats + 14,
+                                 (region_a_order_lds_bytes(R) + 15) & ~(size_t)15));
+      KArgs kf = k;
+      kf.sub = bt->d_fba;
+      kf.n_dev = bt->stats + 14;
+      HIPCHK(dev::select(st, SEL_LAUNCH_REGION_A, kf, smem_region_a(s), cap, sx));
+    } else {
+      HIPCHK(dev::select(st, SEL_LAUNCH_REGION_A, k, smem_region_a(s), cap, sx));
+    }
     // selectGroups: on the device (one thread per binding) unless the snapshot
     // has more regions than its arrays hold; bindings whose DFS exceeds the node
     // budget, and every binding on the other route, take the host DFS.
@@ -2663,9 +2676,9 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   if (getenv("KP_DEBUG_SLOW"))
     fprintf(stderr,
             "kp slow: total %u overflow/dup %u scale-down %u wrap %u tie %u weight %u cluster %u "
-            "(ties resolved block-parallel %u); class-order spread fallbacks: cluster %u region %u\n",
+            "(ties resolved block-parallel %u); class-order spread fallbacks: cluster %u region %u (stage A %u)\n",
             bt->h_stats[0], bt->h_stats[1], bt->h_stats[2], bt->h_stats[3], bt->h_stats[4], bt->h_stats[5],
-            bt->h_stats[6], bt->h_stats[7], bt->h_stats[12], bt->h_stats[13]);
+            bt->h_stats[6], bt->h_stats[7], bt->h_stats[12], bt->h_stats[13], bt->h_stats[14]);
   tm.pair_ms = ms_pair;
   tm.select_ms = ms_sel;
   tm.host_ms = th1 - th0;

@@ -119,6 +119,16 @@ extern "C" __global__ void __launch_bounds__(64 * kOrderWaves) k_spread_order(KA
   if (blk >= a.n) return;  // wave-uniform: the waves never synchronise with each other
   body_spread_order(WaveBlk{(int64_t*)mine}, blk, mine, a, o);
 }
+extern "C" __global__ void __launch_bounds__(64 * kOrderWaves) k_region_a_order(KArgs a, RegionOut* rout,
+                                                                               int32_t* rstat, int32_t* fb,
+                                                                               uint32_t* fb_n, int slice) {
+  KP_SMEM;
+  const int w = (int)(threadIdx.x >> 6);
+  unsigned char* mine = smem + (size_t)w * (size_t)slice;
+  const int blk = (int)blockIdx.x * kOrderWaves + w;
+  if (blk >= a.n) return;  // wave-uniform
+  body_region_a_order(WaveBlk{(int64_t*)mine}, blk, mine, a, rout, rstat, fb, fb_n);
+}
 // Each estimator class's row in (estimate desc, rank asc) order: LDS bitonic sort.
 extern "C" __global__ void __launch_bounds__(1024) k_class_order(SnapView s, const int32_t* rows, int P, uint64_t* ord,
                                                                 int64_t* tot, int32_t* ok) {
@@ -155,7 +165,7 @@ extern "C" __global__ void __launch_bounds__(1024) k_select_all_wide(KArgs a) {
   }                                                                                                            \
   extern "C" __global__ void __launch_bounds__(T, MINW) k_region_a##SUF(KArgs a, RegionOut* rout, int32_t* rstat) { \
     KP_SMEM;                                                                                                   \
-    body_region_a(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, a, rout, rstat);                              \
+    KP_LIST_LOOP(body_region_a(GpuBlk{(int64_t*)smem}, a.sub ? a.sub[blk] : blk, smem, a, rout, rstat))       \
   }                                                                                                            \
   extern "C" __global__ void __launch_bounds__(T, MINW) k_region_b##SUF(KArgs a, const int32_t* rsel,           \
                                                                       const int32_t* rnsel,                    \
@@ -378,9 +388,9 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
       break;
     case SEL_LAUNCH_REGION_A:
       if (smem > kLdsPerCu / 2)
-        hipLaunchKernelGGL(k_region_a_wide, dim3(a.n), dim3(512), smem, h, a, x.rout, x.rstat);
+        hipLaunchKernelGGL(k_region_a_wide, dim3(spread_grid(a)), dim3(512), smem, h, a, x.rout, x.rstat);
       else
-        hipLaunchKernelGGL(k_region_a, dim3(a.n), dim3(256), smem, h, a, x.rout, x.rstat);
+        hipLaunchKernelGGL(k_region_a, dim3(spread_grid(a)), dim3(256), smem, h, a, x.rout, x.rstat);
       break;
     case SEL_LAUNCH_REGION_B:
       if (smem > kLdsPerCu / 2)
@@ -433,6 +443,15 @@ int spread_order(stream_t st, const KArgs& a, const OrderArgs& o, size_t slice) 
     return -1;
   hipLaunchKernelGGL(k_spread_order, dim3((a.n + kOrderWaves - 1) / kOrderWaves), dim3(64 * kOrderWaves), smem,
                      (hipStream_t)st, a, o, (int)slice);
+  return chk(hipGetLastError());
+}
+
+int region_a_order(stream_t st, const KArgs& a, RegionOut* rout, int32_t* rstat, int32_t* fb, uint32_t* fb_n,
+                   size_t slice) {
+  if (a.n <= 0) return 0;
+  const size_t smem = slice * kOrderWaves;
+  hipLaunchKernelGGL(k_region_a_order, dim3((a.n + kOrderWaves - 1) / kOrderWaves), dim3(64 * kOrderWaves), smem,
+                     (hipStream_t)st, a, rout, rstat, fb, fb_n, (int)slice);
   return chk(hipGetLastError());
 }
 

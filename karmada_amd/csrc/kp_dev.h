@@ -15,6 +15,7 @@ namespace kp {
 struct SetsArgs;
 struct TopArgs;
 struct OrderArgs;
+struct RegionOut;
 struct GradesArgs;
 struct NodeEstArgs;
 struct NodeView;
@@ -96,6 +97,10 @@ int select_static(stream_t st, const KArgs& a, size_t slice);
 // Spread selections over the estimator-class orders (body_spread_order), one wave
 // per binding, `slice` bytes of LDS each; unfinished list positions go to o.fb.
 int spread_order(stream_t st, const KArgs& a, const OrderArgs& o, size_t slice);
+// Region stage A of the order-eligible bindings (body_region_a_order), one wave per
+// binding; the other list positions go to fb.
+int region_a_order(stream_t st, const KArgs& a, RegionOut* rout, int32_t* rstat, int32_t* fb, uint32_t* fb_n,
+                   size_t slice);
 // kp_node_max_component_sets: match[k * n + j] = MatchNode(node j, P[k]) (P in
 // device memory), then the first-fit set simulation by one wave (A in device memory).
 int node_match(stream_t st, const NodeView& v, const ClaimProg* P, int K, uint8_t* match);

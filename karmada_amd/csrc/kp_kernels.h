@@ -929,6 +929,75 @@ KP_FI void body_spread_order(const BLK& B, int blk, unsigned char* smem, const K
   if (B.tid() == 0) o.fb[kp_atomic_add(o.fb_n, 1u)] = blk;
 }
 
+// Region stage A for the order-eligible bindings (order_class), one wave per
+// binding: their AvailableReplicas are the class row's estimates (all >= 0) and
+// their cluster scores are 0, so every region's calcGroupScore walk is free
+// (region_walk_free) and calcGroupScoreForDuplicate counts only the valid
+// clusters; both need per-region sums over the feasible clusters, taken here
+// straight from the feasibility row and the class row (no candidate arrays).
+// LDS slice: [red 64 B | cnt R | dvalid R | sum 8R]. The others go to fb.
+KP_HD inline size_t region_a_order_lds_bytes(int R) { return 64 + 8 * (size_t)((R + 1) & ~1) + 8 * (size_t)R; }
+template <class BLK>
+KP_FI void body_region_a_order(const BLK& B, int blk, unsigned char* smem, const KArgs& a, RegionOut* rout,
+                               int32_t* rstat, int32_t* fb, uint32_t* fb_n) {
+  if (blk >= a.n) return;
+  const int b = a.list[blk];
+  SelCtx x = make_ctx(a, b, nullptr);  // no spec.Clusters on this path
+  const int32_t cls = order_class(a, x);
+  if (cls < 0) {
+    if (B.tid() == 0) fb[kp_atomic_add(fb_n, 1u)] = blk;
+    return;
+  }
+  const SnapView& s = a.s;
+  const BindHdr& h = *x.h;
+  const int R = s.n_regions;
+  int32_t* cnt = (int32_t*)(smem + 64);
+  int32_t* dvalid = cnt + R;
+  unsigned long long* sum = (unsigned long long*)(smem + 64 + 8 * (size_t)((R + 1) & ~1));
+  for (int r = B.tid(); r < R; r += B.nth()) {
+    cnt[r] = 0;
+    dvalid[r] = 0;
+    sum[r] = 0;
+  }
+  B.sync();
+  const bool dup = (h.flags & BF_GROUP_DUP) != 0;
+  const int32_t* row = x.erow;
+  int64_t F = 0;
+  for (int w = 0; w < s.W; w++) {  // word by word (one wave-uniform load), a lane per cluster
+    const uint64_t m = x.frow[w];
+    if (!m) continue;
+    for (int l = B.tid(); l < 64; l += B.nth()) {
+      if (!((m >> l) & 1ull)) continue;
+      const int c = w * 64 + l;
+      F++;
+      const int r = s.region_idx[c];
+      if (r >= 0) {
+        const int32_t e = row[c];
+        kp_atomic_add(&cnt[r], 1);
+        kp_atomic_add(&sum[r], (unsigned long long)e);
+        if (dup && e >= h.replicas) kp_atomic_add(&dvalid[r], 1);
+      }
+    }
+  }
+  F = B.sum64(F);  // (its reduction also orders the LDS sums before the reads below)
+  if (F == 0) {  // FitError (generic_scheduler.go:84-89), as pre_checks
+    if (B.tid() == 0) {
+      sink_error(x, KP_STATUS_FIT_ERROR, KP_ERR_FIT, s.C);
+      rstat[blk] = -1;
+    }
+    return;
+  }
+  RegionOut* out = rout + (size_t)blk * R;
+  const int64_t target = go_ceil_div_i64(h.replicas, h.region_min);
+  for (int r = B.tid(); r < R; r += B.nth()) {
+    out[r].count = cnt[r];
+    if (dup) out[r].score = dvalid[r] == 0 ? 0 : mul64((int64_t)dvalid[r], 1000);
+    else out[r].score = region_score_totals(cnt[r], (int64_t)sum[r], 0, target);
+  }
+  if (a.n_order && B.tid() == 0) kp_atomic_add(a.n_order, 1u);
+  if (B.tid() == 0) rstat[blk] = 0;
+}
+
 // ---------------------------------------------------------------------------
 // Region stage A: per-region count and group score for the host selectGroups.
 // rout: [n][n_regions]; rstat[blk] = -1 when the final status is already written.
