@@ -79,6 +79,27 @@ def test_webster_par_matches_reference_heap(seed):
             assert got == want, (votes[:20], N, desc, ecap)
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_webster_first_seat_case(seed):
+    """webster_par's first-seat case (P >= N and vmax < 3 v_N: t* = v_N from a rank select
+    of the compacted list): votes in a narrow band, ties at v_N, and the boundary vmax =
+    3 v_N where a second seat ties with v_N (the general path)."""
+    rng = random.Random(100 + seed)
+    cases = [([300, 100, 100], 2), ([299, 100, 100], 2), ([300, 100, 100, 100], 3), ([7, 7, 7, 7], 2)]
+    for _ in range(40):
+        n = rng.choice([2, 5, 13, 40, 100, 127])
+        lo = rng.randint(1, 5000)
+        v = [rng.randint(lo, 3 * lo - 1) for _ in range(n)]
+        if rng.random() < 0.5:  # a tie group straddling the N-th place
+            v += [sorted(v)[n // 2]] * rng.randint(1, 5)
+        cases.append((v, rng.randint(1, len(v))))
+    for votes, N in cases:
+        for desc in (False, True):
+            want = oracle_webster(votes, N, desc)
+            for ecap in (64, 256, 4096):
+                assert sim_webster(votes, N, desc, ecap) == want, (votes[:20], N, desc, ecap)
+
+
 def test_wsel_max_brute_force():
     rng = random.Random(7)
     for _ in range(300):
