@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 12
+#define KP_ABI_VERSION 13
 
 /* ------------------------------------------------------------------------- */
 /* Object model                                                              */
@@ -276,6 +276,15 @@ typedef struct kp_options {
   uint8_t customized_cluster_resource_modeling; /* feature gate, default on */
   uint8_t multiple_pod_templates_scheduling;    /* feature gate MultiplePodTemplatesScheduling, alpha, default off */
   uint32_t enabled_plugins;                     /* KP_PLUGIN_* bitmask (--plugins) */
+  /* Filter or score plugins the scheduler's registry holds beyond the in-tree set
+   * (app.WithPlugin, cmd/scheduler/app/scheduler.go:90). RunFilterPlugins and
+   * RunScorePlugins (runtime/framework.go:93-170) run every registered plugin, so
+   * the batch path, which computes the in-tree set only, would place differently:
+   * kp_schedule_batch, kp_schedule_affinities and kp_multi_schedule return
+   * KP_ENOTSUP for a snapshot with n_out_of_tree_plugins > 0. The per-pair entry
+   * points (kp_filter_reasons, kp_score_batch, kp_max_available_replicas) still
+   * answer for the in-tree set, for the framework to combine with the others. */
+  uint32_t n_out_of_tree_plugins;
 } kp_options;
 
 /* ------------------------------------------------------------------------- */
@@ -589,6 +598,58 @@ int kp_node_max_component_sets(kp_engine* e, const kp_node* nodes, uint64_t n_no
 
 /* Last schedule call's stage timings. */
 int kp_last_stage_times(const kp_engine* e, kp_stage_times* out);
+
+/* Host threads an engine packs a batch on (kp_batch_create); default: the
+ * hardware threads, at most 16. */
+int kp_engine_set_threads(kp_engine* e, int n_threads);
+
+/* A replica of snapshot `src` (of another engine, on another device) on engine e's
+ * device: the packed device image copied device to device (hipMemcpyPeer, over xGMI
+ * between the GPUs of one node) instead of re-packed and re-uploaded. The replica
+ * schedules exactly as `src` does. */
+int kp_snapshot_replicate(kp_engine* e, const kp_snapshot* src, kp_snapshot** out);
+
+/* ---- one scheduler process over N GPUs (SURVEY §8(b) Threading, §8(e)) ------------
+ * Replaces the reference scheduler's single worker (pkg/scheduler/scheduler.go:327):
+ * a kp_multi owns one engine per device (own HIP streams); its snapshot is packed on
+ * the first device and replicated onto the others (kp_snapshot_replicate); a batch
+ * is cut into contiguous binding shards at equal prefix sums of the §8(e) cost
+ * C + Replicas*log2 C, one per device; kp_multi_schedule runs the shards
+ * concurrently (one host thread per device, no cross-device traffic) and returns one
+ * CSR in binding order, identical to kp_schedule_batch over the whole batch on one
+ * device. Result buffers belong to the batch and stay valid until its next
+ * kp_multi_schedule or destruction. */
+typedef struct kp_multi kp_multi;
+typedef struct kp_multi_snapshot kp_multi_snapshot;
+typedef struct kp_multi_batch kp_multi_batch;
+
+int kp_multi_create(const int* devices, uint32_t n_devices, kp_multi** out);
+void kp_multi_destroy(kp_multi* m);
+const char* kp_multi_last_error(const kp_multi* m);
+uint32_t kp_multi_devices(const kp_multi* m);
+/* The engine of the i-th device (stage times, diagnosis entry points); owned by m. */
+kp_engine* kp_multi_engine(kp_multi* m, uint32_t i);
+
+int kp_multi_snapshot_create(kp_multi* m, const kp_cluster* clusters, uint64_t n_clusters, const kp_options* opts,
+                             kp_multi_snapshot** out);
+/* kp_snapshot_update on every replica (same semantics, same dict_grew). */
+int kp_multi_snapshot_update(kp_multi* m, kp_multi_snapshot* s, const kp_cluster* clusters, uint64_t n_clusters,
+                             int* dict_grew);
+void kp_multi_snapshot_destroy(kp_multi_snapshot* s);
+/* The i-th device's replica; owned by s. */
+kp_snapshot* kp_multi_snapshot_replica(kp_multi_snapshot* s, uint32_t i);
+
+/* The shard cuts kp_multi_batch_create uses: starts[0..n_shards], starts[0] = 0,
+ * starts[n_shards] = n_bindings. */
+int kp_multi_shard_cuts(const kp_binding* bindings, uint64_t n_bindings, uint64_t n_clusters, uint32_t n_shards,
+                        uint64_t* starts);
+int kp_multi_batch_create(kp_multi* m, const kp_multi_snapshot* s, const kp_binding* bindings, uint64_t n_bindings,
+                          kp_multi_batch** out);
+void kp_multi_batch_destroy(kp_multi_batch* b);
+/* The batch's shard cuts (n_devices + 1 entries). */
+int kp_multi_batch_shards(const kp_multi_batch* b, uint64_t* starts);
+/* genericScheduler.Schedule for every binding, the shards on their devices at once. */
+int kp_multi_schedule(kp_multi* m, kp_multi_batch* b, kp_results* out);
 
 #ifdef __cplusplus
 }

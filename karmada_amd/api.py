@@ -163,7 +163,8 @@ class kp_options(C.Structure):
     _fields_ = [("enable_empty_workload_propagation", u8),
                 ("customized_cluster_resource_modeling", u8),
                 ("multiple_pod_templates_scheduling", u8),
-                ("enabled_plugins", u32)]
+                ("enabled_plugins", u32),
+                ("n_out_of_tree_plugins", u32)]
 
 
 class kp_results(C.Structure):
@@ -250,10 +251,11 @@ ERR_NAMES = {
 
 
 def options(empty_workload_propagation=False, models_gate=True, plugins=PLUGIN_ALL,
-            multi_templates=False) -> kp_options:
+            multi_templates=False, out_of_tree_plugins=0) -> kp_options:
     return kp_options(enable_empty_workload_propagation=int(empty_workload_propagation),
                       customized_cluster_resource_modeling=int(models_gate),
-                      multiple_pod_templates_scheduling=int(multi_templates), enabled_plugins=plugins)
+                      multiple_pod_templates_scheduling=int(multi_templates), enabled_plugins=plugins,
+                      n_out_of_tree_plugins=int(out_of_tree_plugins))
 
 
 class World:

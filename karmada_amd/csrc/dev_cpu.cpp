@@ -26,17 +26,30 @@ int threads() {
   int n = e ? atoi(e) : 1;
   return n < 1 ? 1 : n;
 }
+// GPU LDS is not zeroed at launch and keeps whatever the previous workgroup on
+// the CU left: every "workgroup" here starts from a poison pattern (0xA5 bytes,
+// KP_CPUSIM_POISON=0 turns it off), so a read of LDS the kernel never wrote
+// gives garbage here as it would on the device, not a convenient zero.
+bool poison() {
+  static const bool on = [] {
+    const char* e = getenv("KP_CPUSIM_POISON");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 // Runs fn(blk, smem) for blk in [0, n) on the configured host threads.
 template <class F>
 void grid(int n, size_t smem_bytes, F fn) {
   int T = threads();
   if (T > n) T = n;
   std::atomic<int> next(0);
+  const bool pz = poison();
   auto work = [&]() {
     std::vector<int64_t> smem((smem_bytes + kRedBytes + 7) / 8);
     for (;;) {
       int b = next.fetch_add(1);
       if (b >= n) break;
+      if (pz) memset(smem.data(), 0xA5, smem.size() * 8);
       fn(b, (unsigned char*)smem.data());
     }
   };
@@ -53,7 +66,12 @@ struct Ev {
 };
 }  // namespace
 
-int device_count() { return 1; }
+// Emulated devices (the multi-device engine's tests): KP_CPUSIM_DEVICES, default 8.
+int device_count() {
+  const char* e = getenv("KP_CPUSIM_DEVICES");
+  const int n = e ? atoi(e) : 8;
+  return n < 1 ? 1 : n;
+}
 int set_device(int) { return 0; }
 size_t max_lds_per_block(int) { return 160 * 1024; }
 const char* last_error() { return "cpusim error"; }
@@ -73,9 +91,13 @@ int event_record(event_t e, stream_t) {
   return 0;
 }
 int stream_wait(stream_t, event_t) { return 0; }
+int event_sync(event_t) { return 0; }
 float event_ms(event_t a, event_t b) { return (float)(((Ev*)b)->ms - ((Ev*)a)->ms); }
+// Device memory is poisoned like LDS: a pooled arena block on the GPU holds the
+// previous batch's data, so nothing may rely on a zeroed allocation.
 int alloc(void** p, size_t bytes) {
-  *p = calloc(1, bytes ? bytes : 1);
+  *p = malloc(bytes ? bytes : 1);
+  if (*p && poison()) memset(*p, 0xA5, bytes ? bytes : 1);
   return *p ? 0 : -1;
 }
 void release(void* p) { free(p); }
@@ -86,6 +108,10 @@ int h2d(void* dst, const void* src, size_t bytes, stream_t) {
   return 0;
 }
 int d2h(void* dst, const void* src, size_t bytes, stream_t) {
+  if (bytes) memcpy(dst, src, bytes);
+  return 0;
+}
+int peer_copy(void* dst, int, const void* src, int, size_t bytes, stream_t) {
   if (bytes) memcpy(dst, src, bytes);
   return 0;
 }
@@ -158,11 +184,26 @@ int select(stream_t, int which, const KArgs& a, size_t smem, int cap, const Sele
         body_region_b(CpuBlk{(int64_t*)sm}, a.sub ? a.sub[j] : j, sm, a, x.rsel, x.rnsel, x.rout, cap);
       });
       break;
-    case SEL_LAUNCH_SLOW:
-      grid(x.grid, smem, [&](int blk, unsigned char* sm) {
-        body_slow(CpuBlk{(int64_t*)sm}, blk, x.grid, sm, a, x.scratch, x.slot_bytes, cap, x.lds_area, x.lds_sort);
+    case SEL_LAUNCH_SLOW: {
+      // On the GPU the flagged list's order is the order of the device atomics that
+      // appended it, so which bindings follow each other in one workgroup's slot
+      // varies from run to run. KP_CPUSIM_SLOW_SHUFFLE=<seed> permutes the list and
+      // KP_CPUSIM_SLOW_GRID=<g> narrows the grid, to replay such orders here.
+      if (const char* sh = getenv("KP_CPUSIM_SLOW_SHUFFLE")) {
+        uint64_t r = (uint64_t)atoll(sh) * 0x9E3779B97F4A7C15ull + 1;
+        const int ns = (int)std::min<uint32_t>(a.stats[0], (uint32_t)a.n);
+        for (int i = ns - 1; i > 0; i--) {
+          r ^= r << 13, r ^= r >> 7, r ^= r << 17;
+          std::swap(a.slow_ids[i], a.slow_ids[(int)(r % (uint64_t)(i + 1))]);
+        }
+      }
+      int g = x.grid;
+      if (const char* sg = getenv("KP_CPUSIM_SLOW_GRID")) g = std::max(1, std::min(g, atoi(sg)));
+      grid(g, smem, [&](int blk, unsigned char* sm) {
+        body_slow(CpuBlk{(int64_t*)sm}, blk, g, sm, a, x.scratch, x.slot_bytes, cap, x.lds_area, x.lds_sort);
       });
       break;
+    }
     default:
       return -1;
   }

@@ -146,6 +146,13 @@ struct Arena {
     }
     return 0;
   }
+  // One block of `bytes` with no sub-buffers (a replica's copy of another arena).
+  int alloc_raw(size_t bytes) {
+    req.clear();
+    total = bytes ? bytes : 256;
+    got = total;
+    return dev::alloc(&base, total);
+  }
   void drop() {
     if (!base) return;
     if (pool_dev >= 0) buf_pool().put(pool_dev, base, got);
@@ -292,7 +299,28 @@ struct kp_batch {
   int32_t* h_crep = nullptr;
   uint64_t h_res_cap = 0;
   size_t h_cidx_bytes = 0, h_crep_bytes = 0;  // their pooled block sizes
+  // The batch's device arena and page-locked buffers go back to the process-wide
+  // pools on destruction, where another batch (of any engine) may take them at
+  // once. An entry point that fails part-way leaves kernels queued that still
+  // use them: it records these events on the engine's streams (batch_fence), and
+  // destruction waits for them. kp_batch_create does the same through
+  // create_stream while it runs.
+  dev::event_t fence[3] = {};
+  bool fenced = false;
+  dev::stream_t create_stream = nullptr;
+  void quiesce() {
+    if (create_stream) (void)dev::sync(create_stream);
+    create_stream = nullptr;
+    for (auto& ev : fence)
+      if (ev) {
+        if (fenced) (void)dev::event_sync(ev);
+        dev::event_destroy(ev);
+        ev = nullptr;
+      }
+    fenced = false;
+  }
   ~kp_batch() {
+    quiesce();
     buf_pool().put(-1, h_cidx, h_cidx_bytes);
     buf_pool().put(-1, h_crep, h_crep_bytes);
     if (est) dev::release(est);
@@ -1511,7 +1539,7 @@ int snapshot_est_kind(const kp_snapshot* s) {
 // Packed-snapshot bytes: pack once on one rank, broadcast the bytes, import on
 // the others. Host-endian; same engine build on every rank.
 namespace {
-const char kSnapMagic[8] = {'K', 'P', 'S', 'N', 'A', 'P', '0', '3'};
+const char kSnapMagic[8] = {'K', 'P', 'S', 'N', 'A', 'P', '0', '4'};
 struct Wr {
   std::vector<unsigned char>& b;
   void raw(const void* p, size_t n) { b.insert(b.end(), (const unsigned char*)p, (const unsigned char*)p + n); }
@@ -1680,6 +1708,12 @@ void kp_engine_destroy(kp_engine* e) {
 
 const char* kp_last_error(const kp_engine* e) { return e ? e->err.c_str() : "null engine"; }
 
+int kp_engine_set_threads(kp_engine* e, int n_threads) {
+  if (!e || n_threads < 1) return KP_EINVAL;
+  e->n_threads = std::min(n_threads, 256);
+  return KP_OK;
+}
+
 int kp_snapshot_create(kp_engine* e, const kp_cluster* clusters, uint64_t n, const kp_options* opts,
                        kp_snapshot** out) {
   if (!e || !out || (n && !clusters)) return KP_EINVAL;
@@ -1809,6 +1843,8 @@ int kp_snapshot_export(const kp_snapshot* cs, const void** bytes, uint64_t* n_by
   w.u64(s->opts.enable_empty_workload_propagation);
   w.u64(s->opts.customized_cluster_resource_modeling);
   w.u64(s->opts.enabled_plugins);
+  w.u64(s->opts.multiple_pod_templates_scheduling);
+  w.u64(s->opts.n_out_of_tree_plugins);
   w.u64((uint64_t)(int64_t)s->rid_cpu);
   w.u64((uint64_t)(int64_t)s->rid_mem);
   w.u64((uint64_t)(int64_t)s->rid_eph);
@@ -1849,17 +1885,15 @@ int kp_snapshot_export(const kp_snapshot* cs, const void** bytes, uint64_t* n_by
   return KP_OK;
 }
 
-int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_snapshot** out) {
-  if (!e || !bytes || !out) return KP_EINVAL;
+// The host half of kp_snapshot_import: every host column from the byte image
+// (no device work).
+static int import_host(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_snapshot* s) {
   Rd r{(const unsigned char*)bytes, (const unsigned char*)bytes + n_bytes};
   char magic[8];
   if (!r.raw(magic, 8) || memcmp(magic, kSnapMagic, 8) != 0) {
     e->err = "not a kp snapshot";
     return KP_EINVAL;
   }
-  (void)dev::set_device(e->device);
-  auto* s = new kp_snapshot();
-  std::unique_ptr<kp_snapshot> guard(s);
   s->e = e;
   s->C = (int)r.u64();
   s->Cp = s->C ? ((s->C + 63) / 64) * 64 : 64;
@@ -1867,6 +1901,8 @@ int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_sna
   s->opts.enable_empty_workload_propagation = (uint8_t)r.u64();
   s->opts.customized_cluster_resource_modeling = (uint8_t)r.u64();
   s->opts.enabled_plugins = (uint32_t)r.u64();
+  s->opts.multiple_pod_templates_scheduling = (uint8_t)r.u64();
+  s->opts.n_out_of_tree_plugins = (uint32_t)r.u64();
   s->rid_cpu = (int32_t)(int64_t)r.u64();
   s->rid_mem = (int32_t)(int64_t)r.u64();
   s->rid_eph = (int32_t)(int64_t)r.u64();
@@ -1911,8 +1947,52 @@ int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_sna
     s->rank_of[s->names[rk]] = rk;
     if (s->perm[rk] < (uint32_t)s->C) s->inv[s->perm[rk]] = rk;
   }
-  int rc = upload_snapshot(e, s);
+  return KP_OK;
+}
+
+int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_snapshot** out) {
+  if (!e || !bytes || !out) return KP_EINVAL;
+  (void)dev::set_device(e->device);
+  auto* s = new kp_snapshot();
+  std::unique_ptr<kp_snapshot> guard(s);
+  int rc = import_host(e, bytes, n_bytes, s);
   if (rc != KP_OK) return rc;
+  rc = upload_snapshot(e, s);
+  if (rc != KP_OK) return rc;
+  *out = guard.release();
+  return KP_OK;
+}
+
+// A replica of `src` on engine e's device: the host columns from its byte image
+// and the device arena copied device to device (hipMemcpyPeer: over xGMI between
+// the GPUs of one node), its views rebased onto the copy. Nothing is re-derived.
+int kp_snapshot_replicate(kp_engine* e, const kp_snapshot* src, kp_snapshot** out) {
+  if (!e || !src || !out) return KP_EINVAL;
+  const void* bytes = nullptr;
+  uint64_t n_bytes = 0;
+  int rc = kp_snapshot_export(src, &bytes, &n_bytes);
+  if (rc != KP_OK) return rc;
+  (void)dev::set_device(e->device);
+  auto* s = new kp_snapshot();
+  std::unique_ptr<kp_snapshot> guard(s);
+  rc = import_host(e, bytes, n_bytes, s);
+  if (rc != KP_OK) return rc;
+  const size_t total = src->dev.total;
+  HIPCHK(s->dev.alloc_raw(total));
+  HIPCHK(dev::peer_copy(s->dev.base, e->device, src->dev.base, src->e->device, total, e->stream));
+  HIPCHK(dev::sync(e->stream));
+  s->view = src->view;
+  const char* b0 = (const char*)src->dev.base;
+  char* b1 = (char*)s->dev.base;
+  auto rb = [&](auto& p) {
+    if (p) p = (std::remove_reference_t<decltype(p)>)(b1 + ((const char*)p - b0));
+  };
+  SnapView& v = s->view;
+  rb(v.flags), rb(v.perm), rb(v.provider), rb(v.region), rb(v.region_idx), rb(v.provider_int), rb(v.region_int);
+  rb(v.zone_off), rb(v.zone_ids), rb(v.label_val), rb(v.taint_off), rb(v.taint_key), rb(v.taint_val);
+  rb(v.taint_eff), rb(v.taint_set), rb(v.tset_rep), rb(v.api_bits), rb(v.allowed), rb(v.avail), rb(v.qa);
+  rb(v.mg_tid), rb(v.mg_cnt), rb(v.tmpl), rb(v.mt_cnt), rb(v.bits), rb(v.bkey), rb(v.bval);
+  s->est_kind = src->est_kind;
   *out = guard.release();
   return KP_OK;
 }
@@ -2194,6 +2274,10 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   bt->slow_slot = (bt->slow_slot + 255) & ~(size_t)255;
   // k_slow: one workgroup per CU pass over the flagged bindings (appended on device)
   bt->slow_grid = (int)std::max<size_t>(1, std::min<size_t>(256, bt->l_slow.size()));
+  // diagnostics: KP_SLOW_GRID=<g> caps k_slow's grid, KP_SLOW_LDS=0 keeps its sort
+  // keys and scale-down scratch in the global slot (no LDS sort, no wave sort.Sort)
+  if (const char* g = getenv("KP_SLOW_GRID")) bt->slow_grid = std::max(1, std::min(bt->slow_grid, atoi(g)));
+  if (const char* g = getenv("KP_SLOW_LDS"); g && g[0] == '0') bt->slow_sort = bt->slow_lds = 0;
   bt->fast_ok = batch_fast_ok(bt);
   Arena& a = bt->dev;
   a.pool_dev = e->device;
@@ -2226,7 +2310,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->count, B);
   a.add(&bt->counter, 1);
   a.add(&bt->stats, 16);
-#ifdef KP_STAMPS
+#if defined(KP_STAMPS) || defined(KP_SLOW_CHECK)
   a.add(&bt->dbg, 64);
 #endif
   // [0, out_cap): per-binding slots; [out_cap, 2 out_cap): serial results past their slot
@@ -2270,6 +2354,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   }
   const auto tp1 = std::chrono::steady_clock::now();
   HIPCHK(a.alloc());
+  bt->create_stream = e->stream;  // (an early return below waits for the uploads queued so far)
   const auto tp2 = std::chrono::steady_clock::now();
   auto up = [&](void* d, const void* h, size_t bytes) {
     return dev::h2d(d, h, bytes, e->stream);
@@ -2311,11 +2396,29 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   v.tols = d_tols;
   v.progs = d_progs;
   v.instrs = d_instrs;
+  bt->create_stream = nullptr;
   *out = guard.release();
   return KP_OK;
 }
 
 void kp_batch_destroy(kp_batch* b) { delete b; }
+
+// After a failed entry point: the work it queued on the engine's streams may still
+// use the batch's buffers, so destruction must wait for it (kp_batch::quiesce).
+static int batch_fence(kp_engine* e, kp_batch* bt, int rc) {
+  if (rc == KP_OK || !e || !bt) return rc;
+  const dev::stream_t ss[3] = {e->stream, e->stream2, e->stream3};
+  for (int i = 0; i < 3; i++) {
+    if (!bt->fence[i] && dev::event_create(&bt->fence[i])) {
+      bt->fence[i] = nullptr;
+      (void)dev::sync(ss[i]);  // no event: wait here instead
+      continue;
+    }
+    if (dev::event_record(bt->fence[i], ss[i])) (void)dev::sync(ss[i]);
+  }
+  bt->fenced = true;
+  return rc;
+}
 
 // The per-binding [B][Cp] calAvailableReplicas rows, allocated on first use (the
 // pair-row mode and the diagnosis entry points; the default path never needs them).
@@ -2330,8 +2433,18 @@ static int ensure_rows(kp_engine* e, kp_batch* bt) {
   return 0;
 }
 
-int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
+// The batch path computes the in-tree plugin set only (kp_options.n_out_of_tree_plugins).
+static int refuse_out_of_tree(kp_engine* e, const kp_snapshot* s) {
+  if (s->opts.n_out_of_tree_plugins == 0) return KP_OK;
+  e->err = "the scheduler registry holds " + std::to_string(s->opts.n_out_of_tree_plugins) +
+           " filter/score plugin(s) outside the in-tree set: the batch path would ignore them "
+           "(schedule through the framework with the per-pair entry points)";
+  return KP_ENOTSUP;
+}
+
+static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   if (!e || !bt || !out) return KP_EINVAL;
+  if (int rc = refuse_out_of_tree(e, bt->snap)) return rc;
   (void)dev::set_device(e->device);
   kp_snapshot* s = bt->snap;
   const int B = bt->B;
@@ -2369,7 +2482,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   ka.stats = bt->stats;
   ka.slow_ids = bt->d_slowlist;
   ka.dbg = bt->dbg;
-#ifdef KP_STAMPS
+#if defined(KP_STAMPS) || defined(KP_SLOW_CHECK)
   HIPCHK(dev::fill(bt->dbg, 0, 64 * 8, st));
 #endif
   dev::stream_t sp = e->stream2;
@@ -2662,7 +2775,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   tm.cluster_kernel_ms = bt->l_cluster.empty() ? 0.f : dev::event_ms(e->ev[14], e->ev[15]);
   tm.n_region = (uint32_t)bt->l_region.size();
   tm.n_region_order = orders ? bt->h_stats[11] : 0u;
-#ifdef KP_STAMPS
+#if defined(KP_STAMPS) || defined(KP_SLOW_CHECK)
   {
     unsigned long long h[64];
     HIPCHK(dev::d2h(h, bt->dbg, sizeof(h), st));
@@ -2676,9 +2789,10 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   if (getenv("KP_DEBUG_SLOW"))
     fprintf(stderr,
             "kp slow: total %u overflow/dup %u scale-down %u wrap %u tie %u weight %u cluster %u "
-            "(ties resolved block-parallel %u); class-order spread fallbacks: cluster %u region %u (stage A %u)\n",
+            "(ties resolved block-parallel %u); class-order spread fallbacks: cluster %u region %u (stage A %u)"
+            " check %u\n",
             bt->h_stats[0], bt->h_stats[1], bt->h_stats[2], bt->h_stats[3], bt->h_stats[4], bt->h_stats[5],
-            bt->h_stats[6], bt->h_stats[7], bt->h_stats[12], bt->h_stats[13], bt->h_stats[14]);
+            bt->h_stats[6], bt->h_stats[7], bt->h_stats[12], bt->h_stats[13], bt->h_stats[14], bt->h_stats[15]);
   tm.pair_ms = ms_pair;
   tm.select_ms = ms_sel;
   tm.host_ms = th1 - th0;
@@ -2695,6 +2809,7 @@ int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) {
   out->n_targets = tot;
   return KP_OK;
 }
+int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) { return batch_fence(e, bt, schedule_batch_impl(e, bt, out)); }
 
 // Runs the pair kernel and returns the rank-ordered device row pointers.
 static int run_pair(kp_engine* e, kp_batch* bt, int64_t* score, int est_mode, int b0, int nb) {
@@ -2706,7 +2821,7 @@ static int run_pair(kp_engine* e, kp_batch* bt, int64_t* score, int est_mode, in
   return KP_OK;
 }
 
-int kp_filter_batch(kp_engine* e, kp_batch* bt, uint64_t* out_mask) {
+static int filter_batch_impl(kp_engine* e, kp_batch* bt, uint64_t* out_mask) {
   if (!e || !bt || !out_mask) return KP_EINVAL;
   (void)dev::set_device(e->device);
   kp_snapshot* s = bt->snap;
@@ -2730,8 +2845,9 @@ int kp_filter_batch(kp_engine* e, kp_batch* bt, uint64_t* out_mask) {
       }
   return KP_OK;
 }
+int kp_filter_batch(kp_engine* e, kp_batch* bt, uint64_t* out_mask) { return batch_fence(e, bt, filter_batch_impl(e, bt, out_mask)); }
 
-int kp_filter_reasons(kp_engine* e, kp_batch* bt, uint32_t* out_reasons) {
+static int filter_reasons_impl(kp_engine* e, kp_batch* bt, uint32_t* out_reasons) {
   if (!e || !bt || !out_reasons) return KP_EINVAL;
   (void)dev::set_device(e->device);
   kp_snapshot* s = bt->snap;
@@ -2761,6 +2877,7 @@ int kp_filter_reasons(kp_engine* e, kp_batch* bt, uint32_t* out_reasons) {
   if (rc) return rc;
   return KP_OK;
 }
+int kp_filter_reasons(kp_engine* e, kp_batch* bt, uint32_t* out_reasons) { return batch_fence(e, bt, filter_reasons_impl(e, bt, out_reasons)); }
 
 }  // extern "C"
 
@@ -2876,7 +2993,7 @@ int kp_max_available_component_sets(kp_engine* e, const kp_snapshot* sc, const k
   return KP_OK;
 }
 
-int kp_score_batch(kp_engine* e, kp_batch* bt, int64_t* out_scores) {
+static int score_batch_impl(kp_engine* e, kp_batch* bt, int64_t* out_scores) {
   if (!e || !bt || !out_scores) return KP_EINVAL;
   (void)dev::set_device(e->device);
   kp_snapshot* s = bt->snap;
@@ -2893,9 +3010,10 @@ int kp_score_batch(kp_engine* e, kp_batch* bt, int64_t* out_scores) {
     for (int r = 0; r < s->C; r++) out_scores[(size_t)b * s->C + s->perm[r]] = h[(size_t)b * s->C + r];
   return KP_OK;
 }
+int kp_score_batch(kp_engine* e, kp_batch* bt, int64_t* out_scores) { return batch_fence(e, bt, score_batch_impl(e, bt, out_scores)); }
 
-int kp_max_available_replicas(kp_engine* e, kp_batch* bt, uint64_t binding, const uint32_t* cluster_idx, uint64_t n,
-                              int32_t* out) {
+static int max_available_replicas_impl(kp_engine* e, kp_batch* bt, uint64_t binding, const uint32_t* cluster_idx, uint64_t n,
+                                       int32_t* out) {
   if (!e || !bt || (n && (!cluster_idx || !out)) || binding >= (uint64_t)bt->B) return KP_EINVAL;
   (void)dev::set_device(e->device);
   kp_snapshot* s = bt->snap;
@@ -2909,6 +3027,10 @@ int kp_max_available_replicas(kp_engine* e, kp_batch* bt, uint64_t binding, cons
     out[i] = row[s->inv[cluster_idx[i]]];
   }
   return KP_OK;
+}
+int kp_max_available_replicas(kp_engine* e, kp_batch* bt, uint64_t binding, const uint32_t* cluster_idx, uint64_t n,
+                              int32_t* out) {
+  return batch_fence(e, bt, max_available_replicas_impl(e, bt, binding, cluster_idx, n, out));
 }
 
 // ---------------------------------------------------------------------------
@@ -3516,6 +3638,7 @@ static uint32_t affinity_index_of(const kp_binding& b) {
 int kp_schedule_affinities(kp_engine* e, const kp_snapshot* s, const kp_binding* bs, uint64_t n,
                            kp_affinity_results* out) {
   if (!e || !s || !out || (n && !bs)) return KP_EINVAL;
+  if (int rc = refuse_out_of_tree(e, s)) return rc;
   auto& A = e->aff;
   A.status.assign(n, KP_STATUS_OK);
   A.err.assign(n, KP_ERR_NONE);

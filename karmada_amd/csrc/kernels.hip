@@ -21,6 +21,50 @@
 
 using namespace kp;
 
+// The kernels are compiled in parallel translation units: the Makefile builds this
+// file once per group with -DKP_TU=<group>, and each build defines only its group's
+// kernels (the others are declared, so the device interface below, built with
+// group 1, launches them by their host stubs). KP_TU=0 (or unset) defines all.
+#ifndef KP_TU
+#define KP_TU 0
+#endif
+#define KP_K(G) (KP_TU == 0 || KP_TU == (G))
+#if KP_K(1)
+#define KP_IMPL1(...) __VA_ARGS__
+#else
+#define KP_IMPL1(...) ;
+#endif
+#if KP_K(5)
+#define KP_IMPL5(...) __VA_ARGS__
+#else
+#define KP_IMPL5(...) ;
+#endif
+#if KP_K(9)
+#define KP_IMPL9(...) __VA_ARGS__
+#else
+#define KP_IMPL9(...) ;
+#endif
+#if KP_K(10)
+#define KP_IMPL10(...) __VA_ARGS__
+#else
+#define KP_IMPL10(...) ;
+#endif
+#if KP_K(11)
+#define KP_IMPL11(...) __VA_ARGS__
+#else
+#define KP_IMPL11(...) ;
+#endif
+#if KP_K(12)
+#define KP_IMPL12(...) __VA_ARGS__
+#else
+#define KP_IMPL12(...) ;
+#endif
+#if KP_K(13)
+#define KP_IMPL13(...) __VA_ARGS__
+#else
+#define KP_IMPL13(...) ;
+#endif
+
 #define KP_SMEM extern __shared__ __align__(16) unsigned char smem[]
 // k_select_all: workgroup size bound and minimum waves per SIMD. Its LDS (~53 KB at
 // C = 5k with KP_ECAP_MAX = 1024) allows 3 workgroups per CU. 256-thread workgroups
@@ -40,18 +84,24 @@ constexpr size_t kLdsPerCu = 160 * 1024;  // gfx950 LDS per CU
 
 extern "C" __global__ void __launch_bounds__(kBlock) k_pair(SnapView s, BatchView bv, const int32_t* list, int b0,
                                                             uint64_t* fmask, int32_t* est, int64_t* score,
-                                                            int est_mode, int md_cap) {
+                                                            int est_mode, int md_cap)
+#if KP_K(1)
+{
   KP_SMEM;
   body_pair<EST_GENERIC>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, list, b0, fmask, est, score, est_mode,
                          md_cap);
 }
+#else
+;
+#endif
 #define KP_PAIR_FAST(NAME, KIND)                                                                              \
   extern "C" __global__ void __launch_bounds__(kBlock, KP_PAIR_MIN_WAVES)                                     \
-      NAME(SnapView s, BatchView bv, const int32_t* list, int b0, uint64_t* fmask, int32_t* est, int md_cap) { \
-    KP_SMEM;                                                                                                  \
-    body_pair<KIND>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, list, b0, fmask, est, nullptr, 0,   \
-                    md_cap);                                                                                  \
-  }
+      NAME(SnapView s, BatchView bv, const int32_t* list, int b0, uint64_t* fmask, int32_t* est, int md_cap)   \
+      KP_IMPL1({                                                                                              \
+        KP_SMEM;                                                                                              \
+        body_pair<KIND>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, list, b0, fmask, est, nullptr, 0, \
+                        md_cap);                                                                              \
+      })
 KP_PAIR_FAST(k_pair_fast, EST_MIXED)
 KP_PAIR_FAST(k_pair_fast_summary, EST_SUMMARY)
 KP_PAIR_FAST(k_pair_fast_m8, EST_MODEL8)
@@ -59,21 +109,27 @@ KP_PAIR_FAST(k_pair_fast_m16, EST_MODEL16)
 // Estimator-class rows (kp_filter.h), one instance per estimator kind.
 #define KP_EST_CLASS(NAME, KIND)                                                                              \
   extern "C" __global__ void __launch_bounds__(kBlock) NAME(SnapView s, BatchView bv, const int32_t* rep,      \
-                                                             int32_t* rows) {                                 \
-    KP_SMEM;                                                                                                  \
-    body_est_class<KIND>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, rep, rows);                    \
-  }
+                                                             int32_t* rows)                                   \
+      KP_IMPL1({                                                                                              \
+        KP_SMEM;                                                                                              \
+        body_est_class<KIND>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, rep, rows);                \
+      })
 KP_EST_CLASS(k_est_class, EST_MIXED)
 KP_EST_CLASS(k_est_class_summary, EST_SUMMARY)
 KP_EST_CLASS(k_est_class_m8, EST_MODEL8)
 KP_EST_CLASS(k_est_class_m16, EST_MODEL16)
 // Feasibility rows by bitset algebra: one wave64 per binding, kFilterWaves per workgroup.
 constexpr int kFilterWaves = 4;
-extern "C" __global__ void __launch_bounds__(64 * kFilterWaves) k_filter(SnapView s, BatchView bv, uint64_t* fmask) {
+extern "C" __global__ void __launch_bounds__(64 * kFilterWaves) k_filter(SnapView s, BatchView bv, uint64_t* fmask)
+#if KP_K(1)
+{
   const int b = (int)(blockIdx.x * kFilterWaves + (threadIdx.x >> 6));
   if (b >= bv.B) return;  // wave-uniform
   body_filter(GpuBlk{nullptr}, b, s, bv, fmask);
 }
+#else
+;
+#endif
 // A launch over a device-appended list (a.n_dev) runs a grid-stride loop; otherwise
 // one workgroup per list entry (one iteration).
 #define KP_LIST_LOOP(BODY)                                                       \
@@ -82,14 +138,21 @@ extern "C" __global__ void __launch_bounds__(64 * kFilterWaves) k_filter(SnapVie
     BODY;                                                                        \
     __syncthreads();                                                             \
   }
-extern "C" __global__ void __launch_bounds__(KP_SEL_MAX_THREADS, KP_SEL_MIN_WAVES) k_select_all(KArgs a) {
+extern "C" __global__ void __launch_bounds__(KP_SEL_MAX_THREADS, KP_SEL_MIN_WAVES) k_select_all(KArgs a)
+#if KP_K(2)
+{
   KP_SMEM;
   KP_LIST_LOOP(body_select_all(GpuBlk{(int64_t*)smem}, blk, smem, a))
 }
+#else
+;
+#endif
 // SEL_ALL DynamicWeight / Aggregated over the candidates that can matter (kp_top.h):
 // kTopWaves independent waves per workgroup, one binding each, no workgroup barrier.
 constexpr int kTopWaves = 2;  // small workgroups: LDS is granted per workgroup
-extern "C" __global__ void __launch_bounds__(64 * kTopWaves) k_select_top(KArgs a, TopArgs t, int slice) {
+extern "C" __global__ void __launch_bounds__(64 * kTopWaves) k_select_top(KArgs a, TopArgs t, int slice)
+#if KP_K(4)
+{
   KP_SMEM;
   const int w = (int)(threadIdx.x >> 6);
   unsigned char* mine = smem + (size_t)w * (size_t)slice;
@@ -97,10 +160,15 @@ extern "C" __global__ void __launch_bounds__(64 * kTopWaves) k_select_top(KArgs 
   if (blk >= a.n) return;  // wave-uniform: the waves never synchronise with each other
   body_select_top(WaveBlk{(int64_t*)mine}, blk, mine, a, t);
 }
+#else
+;
+#endif
 // StaticWeight SEL_ALL at class level (kp_kernels.h body_select_static): one wave per
 // binding, kStaticWaves independent waves per workgroup.
 constexpr int kStaticWaves = 4;
-extern "C" __global__ void __launch_bounds__(64 * kStaticWaves) k_select_static(KArgs a, int slice) {
+extern "C" __global__ void __launch_bounds__(64 * kStaticWaves) k_select_static(KArgs a, int slice)
+#if KP_K(4)
+{
   KP_SMEM;
   const int w = (int)(threadIdx.x >> 6);
   unsigned char* mine = smem + (size_t)w * (size_t)slice;
@@ -108,10 +176,15 @@ extern "C" __global__ void __launch_bounds__(64 * kStaticWaves) k_select_static(
   if (blk >= a.n) return;  // wave-uniform: the waves never synchronise with each other
   body_select_static(WaveBlk{(int64_t*)mine}, blk, mine, a);
 }
+#else
+;
+#endif
 // Spread selections over the class orders (kp_kernels.h body_spread_order): one wave
 // per binding, kOrderWaves independent waves per workgroup.
 constexpr int kOrderWaves = 4;
-extern "C" __global__ void __launch_bounds__(64 * kOrderWaves) k_spread_order(KArgs a, OrderArgs o, int slice) {
+extern "C" __global__ void __launch_bounds__(64 * kOrderWaves) k_spread_order(KArgs a, OrderArgs o, int slice)
+#if KP_K(6)
+{
   KP_SMEM;
   const int w = (int)(threadIdx.x >> 6);
   unsigned char* mine = smem + (size_t)w * (size_t)slice;
@@ -119,9 +192,14 @@ extern "C" __global__ void __launch_bounds__(64 * kOrderWaves) k_spread_order(KA
   if (blk >= a.n) return;  // wave-uniform: the waves never synchronise with each other
   body_spread_order(WaveBlk{(int64_t*)mine}, blk, mine, a, o);
 }
+#else
+;
+#endif
 extern "C" __global__ void __launch_bounds__(64 * kOrderWaves) k_region_a_order(KArgs a, RegionOut* rout,
                                                                                int32_t* rstat, int32_t* fb,
-                                                                               uint32_t* fb_n, int slice) {
+                                                                               uint32_t* fb_n, int slice)
+#if KP_K(6)
+{
   KP_SMEM;
   const int w = (int)(threadIdx.x >> 6);
   unsigned char* mine = smem + (size_t)w * (size_t)slice;
@@ -129,12 +207,20 @@ extern "C" __global__ void __launch_bounds__(64 * kOrderWaves) k_region_a_order(
   if (blk >= a.n) return;  // wave-uniform
   body_region_a_order(WaveBlk{(int64_t*)mine}, blk, mine, a, rout, rstat, fb, fb_n);
 }
+#else
+;
+#endif
 // Each estimator class's row in (estimate desc, rank asc) order: LDS bitonic sort.
 extern "C" __global__ void __launch_bounds__(1024) k_class_order(SnapView s, const int32_t* rows, int P, uint64_t* ord,
-                                                                int64_t* tot, int32_t* ok) {
+                                                                int64_t* tot, int32_t* ok)
+#if KP_K(4)
+{
   KP_SMEM;
   body_class_order(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, (uint64_t*)(smem + kRedBytes), P, s, rows, ord, tot, ok);
 }
+#else
+;
+#endif
 // SEL_ALL over streamed candidates: ~15 KB LDS at C = 5k, so LDS no longer bounds
 // the workgroups per CU; KP_STREAM_MIN_WAVES waves per SIMD bounds the VGPRs.
 #ifndef KP_STREAM_THREADS
@@ -143,111 +229,189 @@ extern "C" __global__ void __launch_bounds__(1024) k_class_order(SnapView s, con
 #ifndef KP_STREAM_MIN_WAVES
 #define KP_STREAM_MIN_WAVES 6
 #endif
-extern "C" __global__ void __launch_bounds__(KP_STREAM_THREADS, KP_STREAM_MIN_WAVES) k_select_all_stream(KArgs a) {
+extern "C" __global__ void __launch_bounds__(KP_STREAM_THREADS, KP_STREAM_MIN_WAVES) k_select_all_stream(KArgs a)
+#if KP_K(3)
+{
   KP_SMEM;
   KP_LIST_LOOP(body_select_all_stream(GpuBlk{(int64_t*)smem}, blk, smem, a))
 }
+#else
+;
+#endif
 // Large snapshots (C ~ 10k): the candidate arrays alone take 8 B per cluster, so a
 // single workgroup fits a CU; 1024 threads then keep 16 waves in flight instead of 8.
-extern "C" __global__ void __launch_bounds__(1024) k_select_all_wide(KArgs a) {
+extern "C" __global__ void __launch_bounds__(1024) k_select_all_wide(KArgs a)
+#if KP_K(2)
+{
   KP_SMEM;
   KP_LIST_LOOP(body_select_all(GpuBlk{(int64_t*)smem}, blk, smem, a))
 }
+#else
+;
+#endif
 // Spread-constraint selection kernels: workgroup size (their LDS, ~8 B per cluster
 // of gathered candidates, bounds the workgroups per CU; wider ones hide latency).
 // Two instances each: 256 threads while the LDS leaves several workgroups per CU
 // (C up to ~8.6k; fewer waves per barrier), 512 when it leaves one (wider hides
 // latency). 4 / 3 waves per SIMD bound the VGPRs at 128 / 168.
-#define KP_SPREAD_KERNELS(SUF, T, MINW)                                                                          \
-  extern "C" __global__ void __launch_bounds__(T, MINW) k_select_cluster##SUF(KArgs a, int cap) {              \
+#define KP_SPREAD_KERNELS(SUF, T, MINW, IC, IA, IB)                                                                  \
+  extern "C" __global__ void __launch_bounds__(T, MINW) k_select_cluster##SUF(KArgs a, int cap) IC({            \
     KP_SMEM;                                                                                                   \
     KP_LIST_LOOP(body_select_cluster(GpuBlk{(int64_t*)smem}, a.sub ? a.sub[blk] : blk, smem, a, cap))         \
-  }                                                                                                            \
-  extern "C" __global__ void __launch_bounds__(T, MINW) k_region_a##SUF(KArgs a, RegionOut* rout, int32_t* rstat) { \
-    KP_SMEM;                                                                                                   \
-    KP_LIST_LOOP(body_region_a(GpuBlk{(int64_t*)smem}, a.sub ? a.sub[blk] : blk, smem, a, rout, rstat))       \
-  }                                                                                                            \
+  })                                                                                                           \
+  extern "C" __global__ void __launch_bounds__(T, MINW) k_region_a##SUF(KArgs a, RegionOut* rout, int32_t* rstat) \
+      IA({                                                                                                     \
+        KP_SMEM;                                                                                               \
+        KP_LIST_LOOP(body_region_a(GpuBlk{(int64_t*)smem}, a.sub ? a.sub[blk] : blk, smem, a, rout, rstat))   \
+      })                                                                                                       \
   extern "C" __global__ void __launch_bounds__(T, MINW) k_region_b##SUF(KArgs a, const int32_t* rsel,           \
                                                                       const int32_t* rnsel,                    \
-                                                                      const RegionOut* rout, int cap) {        \
-    KP_SMEM;                                                                                                   \
-    KP_LIST_LOOP(body_region_b(GpuBlk{(int64_t*)smem}, a.sub ? a.sub[blk] : blk, smem, a, rsel, rnsel, rout, cap)) \
-  }
-KP_SPREAD_KERNELS(, 256, 3)
-KP_SPREAD_KERNELS(_wide, 512, 4)
+                                                                      const RegionOut* rout, int cap)          \
+      IB({                                                                                                     \
+        KP_SMEM;                                                                                               \
+        KP_LIST_LOOP(body_region_b(GpuBlk{(int64_t*)smem}, a.sub ? a.sub[blk] : blk, smem, a, rsel, rnsel, rout, cap)) \
+      })
+KP_SPREAD_KERNELS(, 256, 3, KP_IMPL5, KP_IMPL10, KP_IMPL12)
+KP_SPREAD_KERNELS(_wide, 512, 4, KP_IMPL9, KP_IMPL11, KP_IMPL13)
 extern "C" __global__ void __launch_bounds__(256) k_region_groups(const RegionOut* rout, const int32_t* rstat,
                                                                   const BindHdr* hdr, const int32_t* list, int n, int R,
-                                                                  int32_t* rsel, int32_t* rnsel, uint32_t* nhost) {
+                                                                  int32_t* rsel, int32_t* rnsel, uint32_t* nhost)
+#if KP_K(6)
+{
   const int j = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (j >= n) return;
   const int32_t k = region_groups_one(rout + (size_t)j * R, rstat[j], hdr[list[j]], R, rsel + (size_t)j * R);
   if (k == kGroupsHost) atomicAdd(nhost, 1u);
   rnsel[j] = k;
 }
+#else
+;
+#endif
 extern "C" __global__ void __launch_bounds__(kSlowBlock) k_slow(KArgs a, unsigned char* scratch, size_t slot_bytes,
-                                                                int cap, int lds_area, int lds_sort) {
+                                                                int cap, int lds_area, int lds_sort)
+#if KP_K(7)
+{
   KP_SMEM;
-  body_slow(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, (int)gridDim.x, smem, a, scratch, slot_bytes, cap, lds_area, lds_sort);
+  body_slow(GpuBlkG{(int64_t*)smem}, (int)blockIdx.x, (int)gridDim.x, smem, a, scratch, slot_bytes, cap, lds_area, lds_sort);
 }
+#else
+;
+#endif
 extern "C" __global__ void __launch_bounds__(64) k_sets(SnapView s, const SetsArgs* A, const int32_t* ranks, const int64_t* off,
-                                                       uint64_t n, int64_t* scratch, int32_t* out) {
+                                                       uint64_t n, int64_t* scratch, int32_t* out)
+#if KP_K(8)
+{
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) body_sets(s, A, ranks, off, i, scratch, out);
 }
+#else
+;
+#endif
 extern "C" __global__ void __launch_bounds__(64) k_sets_rows(SnapView s, const SetsArgs* A, const int64_t* off,
-                                                            int64_t* scratch, int32_t* row, uint32_t* ovf) {
+                                                            int64_t* scratch, int32_t* row, uint32_t* ovf)
+#if KP_K(8)
+{
   const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (r < s.C) body_sets_row(s, *A, off, r, scratch, row, ovf);
 }
+#else
+;
+#endif
 extern "C" __global__ void __launch_bounds__(256) k_rows_from_class(SnapView s, BatchView bv, const int32_t* list,
                                                                   const int32_t* bcls, const int32_t* cls_rows,
-                                                                  const uint64_t* fmask, int32_t* est) {
+                                                                  const uint64_t* fmask, int32_t* est)
+#if KP_K(1)
+{
   body_rows_from_class(GpuBlk{nullptr}, (int)blockIdx.x, s, bv, list, bcls, cls_rows, fmask, est);
 }
-extern "C" __global__ void __launch_bounds__(256) k_grades(GradesArgs A) {
+#else
+;
+#endif
+extern "C" __global__ void __launch_bounds__(256) k_grades(GradesArgs A)
+#if KP_K(8)
+{
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < A.n) body_grades(A, i);
 }
-extern "C" __global__ void __launch_bounds__(256) k_node_est(NodeEstArgs A) {
+#else
+;
+#endif
+extern "C" __global__ void __launch_bounds__(256) k_node_est(NodeEstArgs A)
+#if KP_K(8)
+{
   __shared__ int64_t red[128];
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const GpuBlk B{red};
   const int64_t s = B.sum64(i < A.v.n ? (int64_t)(uint32_t)node_replicas(A, i) : 0);
   if (threadIdx.x == 0) atomicAdd(A.sum, (uint32_t)(uint64_t)s);  // mod 2^32: Go's wrapping int32 adds
 }
+#else
+;
+#endif
 extern "C" __global__ void __launch_bounds__(256) k_node_match(NodeView v, const ClaimProg* P, uint64_t n,
-                                                               uint8_t* match) {
+                                                               uint8_t* match)
+#if KP_K(8)
+{
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) body_node_match(v, P, i, match);
 }
-extern "C" __global__ void __launch_bounds__(64) k_node_sets(const NodeSetsArgs* A) {
+#else
+;
+#endif
+extern "C" __global__ void __launch_bounds__(64) k_node_sets(const NodeSetsArgs* A)
+#if KP_K(8)
+{
   __shared__ int64_t red[2];
   node_sets(WaveBlk{red}, *A);
 }
-extern "C" __global__ void __launch_bounds__(256) k_reasons(SnapView s, BatchView bv, int b0, uint64_t n, uint32_t* out) {
+#else
+;
+#endif
+extern "C" __global__ void __launch_bounds__(256) k_reasons(SnapView s, BatchView bv, int b0, uint64_t n, uint32_t* out)
+#if KP_K(8)
+{
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     body_reasons(s, bv, b0, i, out);
 }
+#else
+;
+#endif
 extern "C" __global__ void __launch_bounds__(kOffThreads) k_offsets_a(const int32_t* status, const uint32_t* count, int n,
-                                                                    uint64_t* offsets, uint64_t* part) {
+                                                                    uint64_t* offsets, uint64_t* part)
+#if KP_K(8)
+{
   __shared__ int64_t red[128];
   body_offsets_a(GpuBlk{red}, (int)blockIdx.x, status, count, n, offsets, part);
 }
-extern "C" __global__ void __launch_bounds__(kOffThreads) k_offsets_b(int n, uint64_t* offsets, const uint64_t* part) {
+#else
+;
+#endif
+extern "C" __global__ void __launch_bounds__(kOffThreads) k_offsets_b(int n, uint64_t* offsets, const uint64_t* part)
+#if KP_K(8)
+{
   __shared__ int64_t red[128];
   body_offsets_b(GpuBlk{red}, (int)blockIdx.x, (int)gridDim.x, n, offsets, part);
 }
+#else
+;
+#endif
 extern "C" __global__ void __launch_bounds__(64) k_compact(const uint64_t* start, const uint32_t* count,
                                                            const uint64_t* offsets, const uint32_t* in_idx,
                                                            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep,
-                                                           int n) {
+                                                           int n)
+#if KP_K(8)
+{
   __shared__ int64_t red[8];
   body_compact(GpuBlk{red}, (int)blockIdx.x, start, count, offsets, in_idx, in_rep, out_idx, out_rep, n);
 }
+#else
+;
+#endif
 
 // ---------------------------------------------------------------------------
 // Device interface (HIP)
 // ---------------------------------------------------------------------------
+#if KP_K(1)
 namespace kp {
 namespace dev {
 
@@ -300,6 +464,7 @@ int event_create(event_t* e) {
 }
 void event_destroy(event_t e) { (void)hipEventDestroy((hipEvent_t)e); }
 int event_record(event_t e, stream_t s) { return chk(hipEventRecord((hipEvent_t)e, (hipStream_t)s)); }
+int event_sync(event_t e) { return chk(hipEventSynchronize((hipEvent_t)e)); }
 int stream_wait(stream_t s, event_t e) { return chk(hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)e, 0)); }
 float event_ms(event_t a, event_t b) {
   float ms = 0;
@@ -318,6 +483,11 @@ int h2d(void* dst, const void* src, size_t bytes, stream_t s) {
 }
 int d2h(void* dst, const void* src, size_t bytes, stream_t s) {
   return bytes ? chk(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)s)) : 0;
+}
+int peer_copy(void* dst, int dst_dev, const void* src, int src_dev, size_t bytes, stream_t s) {
+  if (!bytes) return 0;
+  if (dst_dev == src_dev) return chk(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)s));
+  return chk(hipMemcpyPeerAsync(dst, dst_dev, src, src_dev, bytes, (hipStream_t)s));
 }
 int fill(void* dst, int value, size_t bytes, stream_t s) {
   return bytes ? chk(hipMemsetAsync(dst, value, bytes, (hipStream_t)s)) : 0;
@@ -547,3 +717,4 @@ int compact(stream_t st, const uint64_t* start, const uint32_t* count, const uin
 
 }  // namespace dev
 }  // namespace kp
+#endif  // KP_K(1)

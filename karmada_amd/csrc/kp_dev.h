@@ -37,6 +37,7 @@ int sync(stream_t s);
 int event_create(event_t* e);
 void event_destroy(event_t e);
 int event_record(event_t e, stream_t s);
+int event_sync(event_t e);  // host waits for e
 int stream_wait(stream_t s, event_t e);  // s waits for e (no host block)
 float event_ms(event_t a, event_t b);
 
@@ -48,6 +49,8 @@ void host_release(void* p);
 int h2d(void* dst, const void* src, size_t bytes, stream_t s);  // stream-ordered
 int d2h(void* dst, const void* src, size_t bytes, stream_t s);
 int fill(void* dst, int value, size_t bytes, stream_t s);
+// Device-to-device copy between GPUs (xGMI peer copy; same device: a local copy).
+int peer_copy(void* dst, int dst_dev, const void* src, int src_dev, size_t bytes, stream_t s);
 
 // fast: the estimator instance (EST_*); other than EST_GENERIC only for batches
 // that meet pair_fast_ok.

@@ -1281,6 +1281,36 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
     if (B.bcast(done)) continue;
     cd.F = gather(B, x, cd, false);
     const int F = cd.F;
+#ifdef KP_SLOW_CHECK
+    // diagnostic build: the gathered candidates against the feasibility row (count,
+    // rank sum and xor). dbg[0] += threads whose F differs, dbg[1] += bindings whose
+    // list differs, dbg[8 + 4k ..] = (binding, F, F0, wave) of the first ones.
+    {
+      int F0 = 0;
+      uint64_t s0 = 0, x0 = 0;
+      for (int c = 0; c < a.s.C; c++)
+        if (mask_test(x.frow, c)) F0++, s0 += (uint64_t)c, x0 ^= (uint64_t)c * 0x9E3779B97F4A7C15ull;
+      if (F0 != F) {
+        const unsigned long long k = kp_atomic_add(&a.dbg[0], 1ull);
+        if (k < 8 && (B.tid() & 63) == 0) {
+          a.dbg[8 + 4 * k] = (unsigned long long)b;
+          a.dbg[9 + 4 * k] = (unsigned long long)(int64_t)F;
+          a.dbg[10 + 4 * k] = (unsigned long long)F0;
+          a.dbg[11 + 4 * k] = (unsigned long long)B.wid();
+        }
+      }
+      if (B.tid() == 0) {
+        uint64_t s1 = 0, x1 = 0;
+        const int Fc = F < 0 ? 0 : (F > a.s.Cp ? a.s.Cp : F);
+        for (int i = 0; i < Fc; i++) {
+          const uint64_t c = c_rank(cd, i);
+          s1 += c, x1 ^= c * 0x9E3779B97F4A7C15ull;
+        }
+        if (s1 != s0 || x1 != x0) kp_atomic_add(&a.dbg[1], 1ull);
+      }
+      B.sync();
+    }
+#endif
     int PF = 1;
     while (PF < F) PF <<= 1;
     for (int i = B.tid(); i < PF; i += B.nth()) keys[i] = i < F ? cand_key(x, cd, i, cd.v[i]) : ~0ull;
@@ -1302,6 +1332,18 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
       }
     for (int i = B.tid(); i < F; i += B.nth()) items[i] = item_from_key(x, keys[i]);
     B.sync();
+#ifdef KP_SLOW_CHECK
+    if (B.tid() == 0) {  // dbg[2] += bindings whose sorted items differ, dbg[3] += ... whose keys differ
+      uint64_t s0 = 0, s1 = 0, k0 = 0;
+      for (int c = 0; c < a.s.C; c++)
+        if (mask_test(x.frow, c)) s0 += (uint64_t)c;
+      const int Fc = F < 0 ? 0 : (F > a.s.Cp ? a.s.Cp : F);
+      for (int i = 0; i < Fc; i++) s1 += items[i].rank, k0 += key_rank(keys[i]);
+      if (s1 != s0) kp_atomic_add(&a.dbg[2], 1ull);
+      if (k0 != s0) kp_atomic_add(&a.dbg[3], 1ull);
+    }
+    B.sync();
+#endif
     KP_STAMP(x, 6);
     SerialScratch sc = serial_scratch_carve(ser, scratch_cap);
     if (pdq_lds && presort_dynamic(B, x, items, F, sarea, pos, sc) && why == SLOW_TIE && tie_lds) {

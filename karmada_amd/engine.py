@@ -25,7 +25,7 @@ from karmada_amd import api
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libkp.so")
-KP_ABI_VERSION = 12
+KP_ABI_VERSION = 13
 
 _LIBS = {}
 
@@ -36,6 +36,11 @@ EXPORTS = (
     "kp_batch_destroy",
     "kp_schedule_batch", "kp_schedule_affinities", "kp_filter_batch", "kp_filter_reasons", "kp_score_batch", "kp_max_available_replicas", "kp_max_available_component_sets",
     "kp_model_grades", "kp_node_max_replicas", "kp_node_max_component_sets", "kp_last_stage_times",
+    "kp_engine_set_threads", "kp_snapshot_replicate",
+    "kp_multi_create", "kp_multi_destroy", "kp_multi_last_error", "kp_multi_devices", "kp_multi_engine",
+    "kp_multi_snapshot_create", "kp_multi_snapshot_update", "kp_multi_snapshot_destroy", "kp_multi_snapshot_replica",
+    "kp_multi_shard_cuts", "kp_multi_batch_create", "kp_multi_batch_destroy", "kp_multi_batch_shards",
+    "kp_multi_schedule",
 )
 
 KP_OK, KP_EINVAL, KP_ENOMEM, KP_EDEVICE, KP_ENOTSUP, KP_ESTATE = 0, -1, -2, -3, -4, -5
@@ -86,6 +91,28 @@ def load_library(path: str = LIB_PATH):
     L.kp_snapshot_export.argtypes = [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
     L.kp_snapshot_import.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(vp)]
     L.kp_snapshot_update.argtypes = [vp, vp, C.POINTER(api.kp_cluster), C.c_uint64, C.POINTER(C.c_int)]
+    L.kp_engine_set_threads.argtypes = [vp, C.c_int]
+    L.kp_snapshot_replicate.argtypes = [vp, vp, C.POINTER(vp)]
+    L.kp_multi_create.argtypes = [C.POINTER(C.c_int), C.c_uint32, C.POINTER(vp)]
+    L.kp_multi_destroy.argtypes = [vp]
+    L.kp_multi_last_error.restype = C.c_char_p
+    L.kp_multi_last_error.argtypes = [vp]
+    L.kp_multi_devices.restype = C.c_uint32
+    L.kp_multi_devices.argtypes = [vp]
+    L.kp_multi_engine.restype = vp
+    L.kp_multi_engine.argtypes = [vp, C.c_uint32]
+    L.kp_multi_snapshot_create.argtypes = [vp, C.POINTER(api.kp_cluster), C.c_uint64, C.POINTER(api.kp_options),
+                                           C.POINTER(vp)]
+    L.kp_multi_snapshot_update.argtypes = [vp, vp, C.POINTER(api.kp_cluster), C.c_uint64, C.POINTER(C.c_int)]
+    L.kp_multi_snapshot_destroy.argtypes = [vp]
+    L.kp_multi_snapshot_replica.restype = vp
+    L.kp_multi_snapshot_replica.argtypes = [vp, C.c_uint32]
+    L.kp_multi_shard_cuts.argtypes = [C.POINTER(api.kp_binding), C.c_uint64, C.c_uint64, C.c_uint32,
+                                      C.POINTER(C.c_uint64)]
+    L.kp_multi_batch_create.argtypes = [vp, vp, C.POINTER(api.kp_binding), C.c_uint64, C.POINTER(vp)]
+    L.kp_multi_batch_destroy.argtypes = [vp]
+    L.kp_multi_batch_shards.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.kp_multi_schedule.argtypes = [vp, vp, C.POINTER(api.kp_results)]
     if L.kp_abi_version() != KP_ABI_VERSION:
         raise EngineError("libkp.so ABI version mismatch")
     _LIBS[path] = L
@@ -289,6 +316,117 @@ class Batch:
         r = self.schedule_raw()
         return api.results_to_python(r.status, r.err_code, r.err_arg, r.offsets, r.cluster_idx, r.replicas,
                                      r.n_bindings)
+
+
+class MultiEngine:
+    """One scheduler process over N GPUs (kp_multi): an engine per device, the snapshot
+    replicated device to device, each batch sharded by cost across the devices and
+    scheduled concurrently, results merged in binding order. Replaces the reference
+    scheduler's single worker (pkg/scheduler/scheduler.go:327)."""
+
+    def __init__(self, devices: Sequence[int], lib_path: str = LIB_PATH):
+        self.L = load_library(lib_path)
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        rc = self.L.kp_multi_create(devs, len(devices), C.byref(h))
+        if rc != KP_OK:
+            raise EngineError(f"kp_multi_create(devices={list(devices)}) failed: rc={rc}")
+        self.h = h
+        self.n_devices = int(self.L.kp_multi_devices(h))
+
+    def _check(self, rc: int, what: str):
+        if rc != KP_OK:
+            raise EngineError(f"{what}: rc={rc}: {self.L.kp_multi_last_error(self.h).decode(errors='replace')}")
+
+    def stage_times(self, i: int) -> Dict[str, float]:
+        """kp_last_stage_times of device i's engine (its shard's last schedule)."""
+        t = api.kp_stage_times()
+        e = self.L.kp_multi_engine(self.h, i)
+        if self.L.kp_last_stage_times(e, C.byref(t)) != KP_OK:
+            raise EngineError("kp_last_stage_times")
+        return {k: getattr(t, k) for k, _ in api.kp_stage_times._fields_}
+
+    def snapshot(self, ca, n: int, opts: api.kp_options) -> "MultiSnapshot":
+        return MultiSnapshot(self, ca, n, opts)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.kp_multi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MultiSnapshot:
+    """kp_multi_snapshot: packed on the first device, replicas on the others."""
+
+    def __init__(self, m: MultiEngine, ca, n: int, opts: api.kp_options):
+        self.m, self.opts, self.n_clusters = m, opts, n
+        h = C.c_void_p()
+        m._check(m.L.kp_multi_snapshot_create(m.h, ca, n, C.byref(opts), C.byref(h)), "kp_multi_snapshot_create")
+        self.h = h
+
+    def update_structs(self, ca, n: int) -> bool:
+        grew = C.c_int(0)
+        self.m._check(self.m.L.kp_multi_snapshot_update(self.m.h, self.h, ca, n, C.byref(grew)),
+                      "kp_multi_snapshot_update")
+        return bool(grew.value)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.m.L.kp_multi_snapshot_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MultiBatch:
+    """kp_multi_batch: a batch cut into per-device shards."""
+
+    def __init__(self, snap: MultiSnapshot, structs):
+        self.snap = snap
+        m = snap.m
+        ba, n = structs
+        self.n = n
+        h = C.c_void_p()
+        m._check(m.L.kp_multi_batch_create(m.h, snap.h, ba, n, C.byref(h)), "kp_multi_batch_create")
+        self.h = h
+
+    def shards(self) -> List[int]:
+        D = self.snap.m.n_devices
+        out = (C.c_uint64 * (D + 1))()
+        self.snap.m._check(self.snap.m.L.kp_multi_batch_shards(self.h, out), "kp_multi_batch_shards")
+        return [int(out[i]) for i in range(D + 1)]
+
+    def schedule_raw(self) -> api.kp_results:
+        r = api.kp_results()
+        m = self.snap.m
+        m._check(m.L.kp_multi_schedule(m.h, self.h, C.byref(r)), "kp_multi_schedule")
+        return r
+
+    def schedule(self) -> List[dict]:
+        r = self.schedule_raw()
+        return api.results_to_python(r.status, r.err_code, r.err_arg, r.offsets, r.cluster_idx, r.replicas,
+                                     r.n_bindings)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.snap.m.L.kp_multi_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class GenericScheduler:
