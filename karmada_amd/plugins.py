@@ -20,12 +20,14 @@ INTEGRATION.md implements them (the Python mirror the tests drive):
                                   enabled_plugins bitmask
 
 A batch is keyed by binding slot: the shim computes the device arrays once per batch
-and every per-pair call is a lookup. The product path is the C-ABI; nothing here
+and every per-pair call is a lookup. Shim mirrors the Go shim's spec -> slot index,
+its estimator cache keyed by request content, and their release / invalidation. The product path is the C-ABI; nothing here
 computes a filter, score or estimate itself.
 """
 from __future__ import annotations
 
 import ctypes as C
+import json
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 from karmada_amd import api
@@ -234,3 +236,122 @@ class KpEstimator:
         eng._check(eng.L.kp_max_available_component_sets(eng.h, self.snap.h, ca, nc, ci, len(clusters), out),
                    "kp_max_available_component_sets")
         return [(n, int(out[i])) for i, n in enumerate(clusters)]
+
+
+def out_of_tree_plugins(registry_names: Sequence[str], shim_name: str = "KpPlacement") -> int:
+    """kp_options.n_out_of_tree_plugins: the registered plugins that are neither in-tree
+    nor the shim itself (RunFilterPlugins / RunScorePlugins would run them too)."""
+    return sum(1 for n in registry_names if n not in IN_TREE and n != shim_name)
+
+
+def requirements_key(requirements: Optional[dict]) -> str:
+    """The estimator cache key of a ReplicaRequirements: its content, canonically
+    ordered (two requests with equal content share one device answer)."""
+    return json.dumps(requirements, sort_keys=True, separators=(",", ":"))
+
+
+class Shim:
+    """The Go shim's state (plugins.go): the engine, the current
+    snapshot, the spec -> (view, slot) index of the batches packed this cycle, and the
+    estimator's requirements -> (view, slot) cache.
+
+    * schedule_batch(specs) packs and schedules a batch (ScheduleBatch) and registers
+      every spec of it, so Filter/Score for those specs are lookups;
+    * slot_of(spec) finds a spec by identity (the Go map is keyed by *ResourceBindingSpec);
+      an unseen spec is packed as a one-binding batch once;
+    * max_available_replicas(requirements, clusters) answers from a one-binding batch
+      per distinct requirements content, reused by every later equal request;
+    * release(specs) ends those specs' cycle: a view whose specs are all released is
+      destroyed (kp_batch_destroy);
+    * update(clusters) applies cluster events and destroys every view (their device
+      arrays describe the old snapshot).
+    The batch path refuses a registry with out-of-tree filter/score plugins
+    (kp_options.n_out_of_tree_plugins, KP_ENOTSUP); the per-pair answers stay available.
+    """
+
+    def __init__(self, engine, clusters: Sequence[dict], opts: Optional[api.kp_options] = None,
+                 registry_names: Sequence[str] = ()):
+        opts = opts or api.options()
+        opts.n_out_of_tree_plugins = out_of_tree_plugins(registry_names)
+        self.clusters = list(clusters)
+        self.snap = Snapshot(engine, self.clusters, opts)
+        self.by: Dict[int, Tuple[BatchView, int]] = {}   # id(spec) -> (view, slot)
+        self.keep: Dict[int, dict] = {}                  # id(spec) -> spec (ids stay unique while held)
+        self.est: Dict[str, Tuple[BatchView, int]] = {}  # requirements content -> (view, slot)
+        self.live: Dict[int, int] = {}                   # id(view) -> specs still registered
+        self.batches_created = 0
+
+    def _view(self, specs: Sequence[dict]) -> BatchView:
+        b = Batch(self.snap, list(specs))
+        self.batches_created += 1
+        return BatchView(self.snap, b, self.clusters)
+
+    def _register(self, view: BatchView, specs: Sequence[dict]):
+        for i, sp in enumerate(specs):
+            self.by[id(sp)] = (view, i)
+            self.keep[id(sp)] = sp
+        self.live[id(view)] = self.live.get(id(view), 0) + len(specs)
+
+    def schedule_batch(self, specs: Sequence[dict]) -> List[dict]:
+        view = self._view(specs)
+        self._register(view, specs)
+        return view.batch.schedule()
+
+    def slot_of(self, spec: dict) -> Tuple[BatchView, int]:
+        hit = self.by.get(id(spec))
+        if hit is not None and self.keep.get(id(spec)) is spec:
+            return hit
+        view = self._view([spec])
+        self._register(view, [spec])
+        return view, 0
+
+    def filter(self, spec: dict, cluster: str) -> Optional[Result]:
+        view, slot = self.slot_of(spec)
+        return KpFilter(view).filter((slot, cluster))
+
+    def score(self, spec: dict, cluster: str) -> Tuple[int, Optional[Result]]:
+        view, slot = self.slot_of(spec)
+        return view.score(slot, cluster), None
+
+    def max_available_replicas(self, requirements: Optional[dict], clusters: Sequence[str]) -> List[Tuple[str, int]]:
+        key = requirements_key(requirements)
+        hit = self.est.get(key)
+        if hit is None:
+            spec = {"replicas": 1}
+            if requirements is not None:
+                spec["replicaRequirements"] = requirements
+            view = self._view([spec])
+            hit = self.est[key] = (view, 0)
+        view, slot = hit
+        return KpEstimator(self.snap, view.batch).max_available_replicas(slot, clusters)
+
+    def release(self, specs: Sequence[dict]):
+        for sp in specs:
+            hit = self.by.pop(id(sp), None)
+            self.keep.pop(id(sp), None)
+            if hit is None:
+                continue
+            view = hit[0]
+            self.live[id(view)] -= 1
+            if self.live[id(view)] == 0:
+                del self.live[id(view)]
+                view.batch.close()
+
+    def update(self, clusters: Sequence[dict]) -> bool:
+        grew = self.snap.update(clusters)
+        by_name = {c["name"]: c for c in clusters}
+        self.clusters = [by_name.get(c["name"], c) for c in self.clusters]
+        for view, _ in list(self.by.values()) + list(self.est.values()):
+            view.batch.close()
+        self.by.clear()
+        self.keep.clear()
+        self.est.clear()
+        self.live.clear()
+        return grew
+
+    def close(self):
+        for view, _ in list(self.by.values()) + list(self.est.values()):
+            view.batch.close()
+        self.by.clear()
+        self.est.clear()
+        self.snap.close()

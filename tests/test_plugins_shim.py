@@ -207,3 +207,102 @@ def test_kp_estimator_component_sets(cpusim_engine):
         c = u.names.index(n)
         assert sets == OL.kpo_max_available_component_sets(C.pointer(u.clusters[c]), ca, nc, C.byref(opts), O.FAST)
     snap.close()
+
+
+# ---- the shim's spec -> slot index and estimator cache (plugins.Shim) ----
+APIS = [{"groupVersion": "apps/v1", "resources": [{"kind": "Deployment"}]}]
+
+
+def shim_clusters(cpu=("4", "8", "2")):
+    return [{"name": f"m{i}", "apiEnablements": APIS, "labels": {"env": "prod" if i % 2 == 0 else "dev"},
+             "resourceSummary": {"allocatable": {"cpu": c, "memory": "64Gi", "pods": "100"},
+                                 "allocated": {}, "allocating": {}}} for i, c in enumerate(cpu)]
+
+
+def shim_spec(replicas=3, env=None):
+    p = {"replicaScheduling": {"replicaSchedulingType": "Divided", "replicaDivisionPreference": "Weighted",
+                               "weightPreference": {"dynamicWeight": "AvailableReplicas"}}}
+    if env:
+        p["clusterAffinity"] = {"labelSelector": {"matchLabels": {"env": env}}}
+    return {"replicas": replicas, "replicaRequirements": {"resourceRequest": {"cpu": "1"}}, "placement": p,
+            "clusters": [{"name": "m0", "replicas": 1}]}
+
+
+def test_shim_spec_slot_lookup(cpusim_engine):
+    """ScheduleBatch registers every spec it packs; Filter/Score for them are lookups
+    (no batch packed); an unseen spec is packed once as a one-binding batch; the Go map
+    is keyed by pointer, so an equal-content copy is a different spec."""
+    sh = plugins.Shim(cpusim_engine, shim_clusters())
+    a, b = shim_spec(env="prod"), shim_spec(env="dev")
+    res = sh.schedule_batch([a, b])
+    assert len(res) == 2 and sh.batches_created == 1
+    for c in ("m0", "m1", "m2"):
+        fa, fb = sh.filter(a, c), sh.filter(b, c)
+        assert (fa is None) == (c in ("m0", "m2")) and (fb is None) == (c == "m1")
+        assert sh.score(a, c)[0] == (100 if c == "m0" else 0)
+    assert sh.batches_created == 1
+    cold = shim_spec(env="prod")
+    assert sh.filter(cold, "m0") is None and sh.batches_created == 2
+    assert sh.filter(cold, "m1") is not None and sh.batches_created == 2
+    sh.release([a, b, cold])
+    assert not sh.by and not sh.live
+    sh.close()
+
+
+def test_shim_release_destroys_batches(cpusim_engine):
+    sh = plugins.Shim(cpusim_engine, shim_clusters())
+    a, b = shim_spec(), shim_spec()
+    sh.schedule_batch([a, b])
+    view = sh.by[id(a)][0]
+    sh.release([a])
+    assert view.batch.h  # b still holds the view
+    sh.release([b])
+    assert not view.batch.h
+    sh.close()
+
+
+def test_shim_estimator_cache_by_content(cpusim_engine):
+    """MaxAvailableReplicas builds a one-binding batch per distinct ReplicaRequirements
+    content and reuses it (the r3 shim packed a fresh spec on every call and never
+    freed it); answers are the GeneralEstimator's (cpu allocatable / request)."""
+    sh = plugins.Shim(cpusim_engine, shim_clusters())
+    req = {"resourceRequest": {"cpu": "1"}}
+    assert sh.max_available_replicas(req, ["m2", "m0", "m1"]) == [("m2", 2), ("m0", 4), ("m1", 8)]
+    assert sh.max_available_replicas({"resourceRequest": {"cpu": "1"}}, ["m1"]) == [("m1", 8)]
+    assert sh.batches_created == 1
+    assert sh.max_available_replicas({"resourceRequest": {"cpu": "2"}}, ["m1", "m0"]) == [("m1", 4), ("m0", 2)]
+    assert sh.batches_created == 2
+    assert sh.max_available_replicas(None, ["m0"]) == [("m0", 100)]  # no requirements: allowed pods
+    sh.close()
+
+
+def test_shim_update_invalidates(cpusim_engine):
+    """Cluster events re-pack the snapshot and drop every cached view: the next answers
+    come from the new snapshot, never a stale batch."""
+    sh = plugins.Shim(cpusim_engine, shim_clusters())
+    req = {"resourceRequest": {"cpu": "1"}}
+    a = shim_spec()
+    sh.schedule_batch([a])
+    assert sh.max_available_replicas(req, ["m0"]) == [("m0", 4)]
+    sh.update(shim_clusters(cpu=("16", "8", "2"))[:1])
+    assert not sh.by and not sh.est
+    assert sh.max_available_replicas(req, ["m0"]) == [("m0", 16)]
+    sh.close()
+
+
+def test_shim_refuses_out_of_tree_plugins(cpusim_engine):
+    """A registry with an out-of-tree score plugin: the batch path refuses (KP_ENOTSUP,
+    kp_options.n_out_of_tree_plugins) instead of placing without that plugin's scores;
+    the per-pair answers, which the framework combines with the other plugin, remain."""
+    from karmada_amd.engine import EngineError
+    names = list(plugins.IN_TREE) + ["KpPlacement", "MyScore"]
+    assert plugins.out_of_tree_plugins(names) == 1
+    sh = plugins.Shim(cpusim_engine, shim_clusters(), registry_names=names)
+    a = shim_spec()
+    with pytest.raises(EngineError, match="rc=-4"):
+        sh.schedule_batch([a])
+    assert sh.filter(a, "m0") is None
+    sh.close()
+    sh = plugins.Shim(cpusim_engine, shim_clusters(), registry_names=list(plugins.IN_TREE) + ["KpPlacement"])
+    assert len(sh.schedule_batch([shim_spec()])) == 1
+    sh.close()
