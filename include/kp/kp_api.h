@@ -315,9 +315,13 @@ enum {
   KP_ERR_SCALE_DOWN_NOT_ENOUGH = 11, /* assignment.go:228-231; arg = available */
   KP_ERR_SCALE_UP_NOT_ENOUGH = 12,   /* assignment.go:236-239; arg = available */
   KP_ERR_UNDEFINED_STRATEGY = 13,    /* division_algorithm.go:97-99 */
-  KP_ERR_RESULT_CAPACITY = 14        /* engine limit, no reference site: a serial result list
+  KP_ERR_RESULT_CAPACITY = 14,       /* engine limit, no reference site: a serial result list
                                         outgrew the batch's result pool (arg = its length);
                                         never expected, reported instead of written */
+  KP_ERR_SETS_CAPACITY = 15          /* engine limit, no reference site: the binding's
+                                        MaxAvailableComponentSets simulation needed more than
+                                        the device's node runs in one cluster (arg = the
+                                        cluster's caller index); only that binding fails */
 };
 
 /* Per-batch results, engine-owned, valid until the next call on the engine.

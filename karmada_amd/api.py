@@ -246,7 +246,7 @@ ERR_NAMES = {
     0: "none", 1: "fit", 2: "region_min_groups", 3: "region_cluster_min", 4: "cluster_min_groups",
     5: "cluster_resource", 6: "spread_unsupported", 7: "no_clusters", 8: "unsupported_strategy",
     9: "overflow_not_enough", 10: "fresh_not_enough", 11: "scale_down_not_enough",
-    12: "scale_up_not_enough", 13: "undefined_strategy", 14: "result_capacity",
+    12: "scale_up_not_enough", 13: "undefined_strategy", 14: "result_capacity", 15: "sets_capacity",
 }
 
 

@@ -70,11 +70,16 @@ struct Dict {
 // and its page-locked result buffers go back here on kp_batch_destroy and the next
 // batch of a fitting size takes them, so a stream of batches pays hipMalloc /
 // hipHostMalloc (and the frees) once. A block is reused for requests of at least
-// half its size; each pool keeps at most kPoolKeep blocks.
+// half its size. Each pool (one per device, one for page-locked host memory) keeps
+// at most kPoolKeep blocks and kPoolBytes (device) / kPoolHostBytes (host) bytes,
+// oldest evicted first: several engines' batches in flight (bench lanes, kp_multi)
+// each hold an arena and two host buffers.
 struct BufPool {
-  static constexpr size_t kPoolKeep = 8;
+  static constexpr size_t kPoolKeep = 32;
+  static constexpr size_t kPoolBytes = (size_t)16 << 30;     // per device (288 GB of HBM)
+  static constexpr size_t kPoolHostBytes = (size_t)4 << 30;  // page-locked host memory
   std::mutex mu;
-  std::vector<std::tuple<int, void*, size_t>> free;  // (device or -1 for host, pointer, bytes)
+  std::vector<std::tuple<int, void*, size_t>> free;  // (device or -1 for host, pointer, bytes), oldest first
   void* get(int dev_id, size_t bytes, size_t* got) {
     std::lock_guard<std::mutex> g(mu);
     size_t best = (size_t)-1;
@@ -91,18 +96,27 @@ struct BufPool {
   }
   void put(int dev_id, void* p, size_t bytes) {
     if (!p) return;
-    std::tuple<int, void*, size_t> drop{-2, nullptr, 0};
+    std::vector<std::tuple<int, void*, size_t>> drop;
     {
       std::lock_guard<std::mutex> g(mu);
       free.emplace_back(dev_id, p, bytes);
-      if (free.size() > kPoolKeep) {  // the oldest goes
-        drop = free.front();
-        free.erase(free.begin());
+      size_t cnt = 0, tot = 0;
+      for (auto& f : free)
+        if (std::get<0>(f) == dev_id) cnt++, tot += std::get<2>(f);
+      const size_t cap = dev_id < 0 ? kPoolHostBytes : kPoolBytes;
+      for (size_t i = 0; i < free.size() && (cnt > kPoolKeep || tot > cap);) {  // the oldest of this pool go
+        if (std::get<0>(free[i]) != dev_id) {
+          i++;
+          continue;
+        }
+        cnt--, tot -= std::get<2>(free[i]);
+        drop.push_back(free[i]);
+        free.erase(free.begin() + (long)i);
       }
     }
-    if (std::get<1>(drop)) {
-      if (std::get<0>(drop) < 0) dev::host_release(std::get<1>(drop));
-      else dev::release(std::get<1>(drop));
+    for (auto& d : drop) {
+      if (std::get<0>(d) < 0) dev::host_release(std::get<1>(d));
+      else dev::release(std::get<1>(d));
     }
   }
 };
@@ -262,6 +276,7 @@ struct kp_batch {
   std::vector<SetsArgs> sets_args;
   SetsArgs* d_sets_args = nullptr;
   int64_t *d_sets_off = nullptr, *d_sets_scratch = nullptr;
+  uint32_t* d_sets_ovf = nullptr;  // [sets_cls] per component-set class: overflowing rank + 1, or 0
   int32_t* d_sets_list = nullptr;
   std::string err;  // packing error text
   int32_t *d_all = nullptr, *d_cluster = nullptr, *d_region = nullptr, *d_slowlist = nullptr, *d_cs = nullptr;
@@ -2326,7 +2341,10 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->rnsel, std::max(1, nr));
   a.add(&bt->nhost, 1);
   a.add(&bt->slow_scratch, bt->slow_slot * bt->slow_grid);
-  if (s->C <= 16384 && !bt->crep.empty()) {  // k_select_top (bits mode): class orders, fallback list
+  // k_select_top (bits mode): class orders, fallback list. k_class_order sorts a class
+  // row in LDS (kRedBytes + 8 * nextpow2(C)): a device with less LDS per workgroup
+  // keeps the full-candidate kernels instead of failing the launch.
+  if (s->C <= 16384 && !bt->crep.empty() && kRedBytes + 8 * (size_t)P <= e->max_lds) {
     a.add(&bt->d_ord, bt->crep.size() * (size_t)s->Cp);
     a.add(&bt->d_ctot, bt->crep.size());
     a.add(&bt->d_cok, bt->crep.size());
@@ -2342,14 +2360,17 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
     for (uint64_t i = 0; i < n; i++)
       if (bt->hdr[i].flags & BF_SETS) bt->l_sets.push_back((int32_t)i);
     sets_off.assign((size_t)s->C + 1, 0);
+    int64_t runs_cap = kSetsRunsMax;  // (KP_SETS_RUNS_CAP lowers it: tests of the overflow report)
+    if (const char* v = getenv("KP_SETS_RUNS_CAP")) runs_cap = std::max<int64_t>(1, std::min<int64_t>(atoll(v), kSetsRunsMax));
     for (int r = 0; r < s->C; r++) {
       int64_t nodes = 0;
       for (int g = s->mgrp_off[r]; g < s->mgrp_off[r + 1]; g++) nodes += s->mgrp_cnt[g];
-      sets_off[r + 1] = sets_off[r] + std::max<int64_t>(1, std::min<int64_t>(nodes, kSetsRunsMax));
+      sets_off[r + 1] = sets_off[r] + std::max<int64_t>(1, std::min<int64_t>(nodes, runs_cap));
     }
     a.add(&bt->d_sets_args, bt->sets_args.size());
     a.add(&bt->d_sets_off, sets_off.size());
     a.add(&bt->d_sets_scratch, (size_t)sets_off.back() * (1 + kSetsSlots));
+    a.add(&bt->d_sets_ovf, bt->sets_cls.size());
     a.add(&bt->d_sets_list, bt->l_sets.size());
   }
   const auto tp1 = std::chrono::steady_clock::now();
@@ -2464,6 +2485,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   if (batch_lds_check(e, s, bt)) return KP_ENOTSUP;
   HIPCHK(dev::h2d(bt->counter, &bt->out_cap, sizeof(unsigned long long), st));  // the shared area's start
   HIPCHK(dev::fill(bt->stats, 0, sizeof(bt->h_stats), st));
+  if (!bt->sets_cls.empty()) HIPCHK(dev::fill(bt->d_sets_ovf, 0, 4 * bt->sets_cls.size(), st));
   KArgs ka;
   ka.s = s->view;
   ka.bv = bt->view;
@@ -2522,16 +2544,23 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   // mode those bindings' own rows rebuilt from them (feasible clusters only)
   for (size_t j = 0; j < bt->sets_cls.size(); j++)
     HIPCHK(dev::sets_rows(sp, s->view, bt->d_sets_args + j, bt->d_sets_off, bt->d_sets_scratch,
-                          bt->cls_rows + (size_t)bt->sets_cls[j] * s->Cp, bt->stats + 8));
+                          bt->cls_rows + (size_t)bt->sets_cls[j] * s->Cp, bt->d_sets_ovf + j));
   if (!bits && !bt->l_sets.empty())
     HIPCHK(dev::rows_from_class(sp, s->view, bt->view, bt->d_sets_list, (int)bt->l_sets.size(), bt->d_bcls,
                                 bt->cls_rows, bt->fmask, bt->est));
   // SEL_ALL DynamicWeight / Aggregated over the deciding candidates (kp_top.h): the
   // class rows' orders first
-  const bool top = bits && e->top_on && bt->d_ord != nullptr && bt->n_all_dyn > 0;
-  // class orders: k_select_top's walk, and the cluster-spread shortcut (cluster_by_order)
-  const bool orders = bits && e->top_on && bt->d_ord != nullptr &&
-                      (bt->n_all_dyn > 0 || !bt->l_cluster.empty() || !bt->l_region.empty());
+  const bool top = bits && e->top_on && bt->d_ord != nullptr && bt->n_all_dyn > 0 &&
+                   kTopWaves * ((top_lds_bytes(s->Cp, e->top_cap) + 15) & ~(size_t)15) <= e->max_lds;
+  // class orders: k_select_top's walk, and the spread selections over them
+  // (k_spread_order, k_region_a_order), each where its LDS slices fit the device
+  const bool spread_orders = bits && e->top_on && bt->d_ord != nullptr &&
+                             (!bt->l_cluster.empty() || !bt->l_region.empty()) &&
+                             kOrderWaves * ((order_lds_bytes(s->view.W, s->view.n_regions) + 15) & ~(size_t)15) <=
+                                 e->max_lds &&
+                             kOrderWaves * ((region_a_order_lds_bytes(s->view.n_regions) + 15) & ~(size_t)15) <=
+                                 e->max_lds;
+  const bool orders = top || spread_orders;
   if (orders)
     HIPCHK(dev::class_order(sp, s->view, bt->cls_rows, (int)bt->crep.size(), bt->d_ord, bt->d_ctot, bt->d_cok));
   HIPCHK(dev::event_record(e->ev[4], sp));
@@ -2576,7 +2605,8 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     // the rest: StaticWeight at class level (k_select_static) where it applies, then
     // the streamed kernel
     int rest0 = top ? bt->n_all_dyn : na;
-    if (bits && rest0 == bt->n_all_dyn && bt->n_static > 0) {
+    if (bits && rest0 == bt->n_all_dyn && bt->n_static > 0 &&
+        kStaticWaves * ((static_lds_bytes(s->view.W) + 15) & ~(size_t)15) <= e->max_lds) {
       KArgs g = k;
       g.list = bt->d_all + rest0;
       g.n = bt->n_static;
@@ -2598,7 +2628,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     k.list = bt->d_cluster;
     k.n = (int)bt->l_cluster.size();
     HIPCHK(dev::event_record(e->ev[14], s3));
-    if (orders) {
+    if (spread_orders) {
       // the class-order selection, one wave per binding; what it hands back runs below
       k.ord = bt->d_ord;
       k.cok = bt->d_cok;
@@ -2618,12 +2648,12 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     KArgs k = ka;
     k.list = bt->d_region;
     k.n = nr;
-    if (orders) {  // region_b_by_order
+    if (spread_orders) {  // region_b_by_order
       k.ord = bt->d_ord;
       k.cok = bt->d_cok;
       k.n_order = bt->stats + 11;
     }
-    if (orders) {  // stage A of the order-eligible bindings, one wave each; the rest below
+    if (spread_orders) {  // stage A of the order-eligible bindings, one wave each; the rest below
       KArgs ko = k;
       ko.n_order = nullptr;
       HIPCHK(dev::region_a_order(st, ko, bt->rout, bt->rstat, bt->d_fba, bt->stats + 14,
@@ -2690,7 +2720,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       HIPCHK(dev::h2d(bt->rsel, bt->h_rsel.data(), 4 * bt->h_rsel.size(), st));
       HIPCHK(dev::h2d(bt->rnsel, bt->h_rnsel.data(), 4 * nr, st));
     }
-    if (orders) {
+    if (spread_orders) {
       OrderArgs oa{bt->rout, bt->rsel, bt->rnsel, bt->d_fbr, bt->stats + 13, 1};
       HIPCHK(dev::spread_order(st, k, oa, (order_lds_bytes(s->view.W, R) + 15) & ~(size_t)15));
       k.sub = bt->d_fbr;
@@ -2723,10 +2753,10 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   HIPCHK(dev::d2h(bt->h_offsets.data(), bt->offsets_d, 8 * (size_t)(B + 1), st));
   HIPCHK(dev::d2h(bt->h_stats, bt->stats, sizeof(bt->h_stats), st));
   HIPCHK(dev::sync(st));
-  if (bt->h_stats[8]) {
-    e->err = "kp_schedule_batch: a MaxAvailableComponentSets simulation needs more than " +
-             std::to_string(kSetsRunsMax) + " node runs in one cluster";
-    return KP_ENOTSUP;
+  std::vector<uint32_t> sets_ovf(bt->sets_cls.size(), 0);
+  if (!sets_ovf.empty()) {
+    HIPCHK(dev::d2h(sets_ovf.data(), bt->d_sets_ovf, 4 * sets_ovf.size(), st));
+    HIPCHK(dev::sync(st));
   }
   double tc0 = now_ms();
   const uint64_t tot = bt->h_offsets[B];
@@ -2750,6 +2780,33 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     HIPCHK(dev::d2h(bt->h_crep, bt->crep_d, 4 * tot, st));
   }
   HIPCHK(dev::sync(st));
+  // A component-set class whose simulation outgrew the device's node runs in some
+  // cluster (kSetsRunsMax): its bindings report KP_ERR_SETS_CAPACITY, every other
+  // binding keeps its result (the CSR is re-packed without their targets).
+  for (size_t j = 0; j < sets_ovf.size(); j++) {
+    if (!sets_ovf[j]) continue;
+    const int32_t cls = bt->sets_cls[j];
+    for (int32_t b : bt->l_sets)
+      if (bt->bcls[b] == cls) {
+        bt->h_status[b] = KP_STATUS_ERROR;
+        bt->h_err[b] = KP_ERR_SETS_CAPACITY;
+        bt->h_arg[b] = (int64_t)s->perm[sets_ovf[j] - 1];
+      }
+  }
+  if (std::any_of(sets_ovf.begin(), sets_ovf.end(), [](uint32_t v) { return v != 0; })) {
+    uint64_t w = 0;
+    for (int b = 0; b < B; b++) {
+      const uint64_t lo = bt->h_offsets[b], hi = bt->h_offsets[b + 1];
+      bt->h_offsets[b] = w;
+      if (bt->h_status[b] != KP_STATUS_OK) continue;
+      for (uint64_t k = lo; k < hi; k++, w++) {
+        bt->h_cidx[w] = bt->h_cidx[k];
+        bt->h_crep[w] = bt->h_crep[k];
+      }
+    }
+    bt->h_offsets[B] = w;
+  }
+  const uint64_t tot_out = bt->h_offsets[B];
   double t1 = now_ms();
   // pair: the pair launch, or k_est_class + k_filter (stream2; filter: k_filter
   // alone); select: from the point where they are complete to the end of the last
@@ -2771,10 +2828,10 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   tm.n_top_fallback = top ? bt->h_stats[9] : 0u;
   tm.top_kernel_ms = top ? dev::event_ms(e->ev[12], e->ev[13]) : 0.f;
   tm.n_cluster = (uint32_t)bt->l_cluster.size();
-  tm.n_cluster_order = orders ? bt->h_stats[10] : 0u;
+  tm.n_cluster_order = spread_orders ? bt->h_stats[10] : 0u;
   tm.cluster_kernel_ms = bt->l_cluster.empty() ? 0.f : dev::event_ms(e->ev[14], e->ev[15]);
   tm.n_region = (uint32_t)bt->l_region.size();
-  tm.n_region_order = orders ? bt->h_stats[11] : 0u;
+  tm.n_region_order = spread_orders ? bt->h_stats[11] : 0u;
 #if defined(KP_STAMPS) || defined(KP_SLOW_CHECK)
   {
     unsigned long long h[64];
@@ -2806,7 +2863,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   out->offsets = bt->h_offsets.data();
   out->cluster_idx = bt->h_cidx;
   out->replicas = bt->h_crep;
-  out->n_targets = tot;
+  out->n_targets = tot_out;
   return KP_OK;
 }
 int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) { return batch_fence(e, bt, schedule_batch_impl(e, bt, out)); }

@@ -149,7 +149,6 @@ extern "C" __global__ void __launch_bounds__(KP_SEL_MAX_THREADS, KP_SEL_MIN_WAVE
 #endif
 // SEL_ALL DynamicWeight / Aggregated over the candidates that can matter (kp_top.h):
 // kTopWaves independent waves per workgroup, one binding each, no workgroup barrier.
-constexpr int kTopWaves = 2;  // small workgroups: LDS is granted per workgroup
 extern "C" __global__ void __launch_bounds__(64 * kTopWaves) k_select_top(KArgs a, TopArgs t, int slice)
 #if KP_K(4)
 {
@@ -165,7 +164,6 @@ extern "C" __global__ void __launch_bounds__(64 * kTopWaves) k_select_top(KArgs 
 #endif
 // StaticWeight SEL_ALL at class level (kp_kernels.h body_select_static): one wave per
 // binding, kStaticWaves independent waves per workgroup.
-constexpr int kStaticWaves = 4;
 extern "C" __global__ void __launch_bounds__(64 * kStaticWaves) k_select_static(KArgs a, int slice)
 #if KP_K(4)
 {
@@ -181,7 +179,6 @@ extern "C" __global__ void __launch_bounds__(64 * kStaticWaves) k_select_static(
 #endif
 // Spread selections over the class orders (kp_kernels.h body_spread_order): one wave
 // per binding, kOrderWaves independent waves per workgroup.
-constexpr int kOrderWaves = 4;
 extern "C" __global__ void __launch_bounds__(64 * kOrderWaves) k_spread_order(KArgs a, OrderArgs o, int slice)
 #if KP_K(6)
 {

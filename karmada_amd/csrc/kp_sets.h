@@ -187,7 +187,7 @@ KP_HD inline void body_sets_row(const SnapView& s, const SetsArgs& A, const int6
                                 int32_t* row, uint32_t* ovf) {
   const int32_t v = sets_one(s, A, r, scratch + (size_t)off[r] * (1 + kSetsSlots), (int)(off[r + 1] - off[r]));
   if (v == kSetsOverflow) {
-    *ovf = 1u;
+    *ovf = (uint32_t)r + 1u;  // (any overflowing cluster's rank + 1)
     row[r] = 0;
   } else {
     row[r] = v;

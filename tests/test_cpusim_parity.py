@@ -175,3 +175,25 @@ def test_cpusim_top_subsets(top_env):
                 assert times[0]["n_top_fallback"] > 0
     finally:
         e.close()
+
+
+def test_cpusim_sets_overflow_is_per_binding(engine):
+    """A component-set simulation that outgrows its node runs (KP_SETS_RUNS_CAP=1 here;
+    kSetsRunsMax on the device) fails only the bindings of that component-set class
+    (KP_ERR_SETS_CAPACITY, arg = a caller cluster index); every other binding keeps
+    the oracle's result (the whole batch used to fail with KP_ENOTSUP)."""
+    u = synth.Universe(9, 1, 300, 0, 600)
+    opts = api.options(multi_templates=True)
+    want = O.schedule_c(u.clusters, u.n_clusters, u.bindings, u.n_bindings, opts, O.FAST, 8)
+    os.environ["KP_SETS_RUNS_CAP"] = "1"
+    try:
+        got = run(engine, u, opts)
+    finally:
+        os.environ.pop("KP_SETS_RUNS_CAP", None)
+    failed = [i for i, g in enumerate(got) if g["err"] == 15]
+    assert failed, "no component-set class overflowed: the test needs another cap or universe"
+    for i in failed:
+        assert got[i]["status"] == api.STATUS_ERROR and got[i]["targets"] == [] and 0 <= got[i]["arg"] < 300
+    ok = [i for i in range(len(got)) if i not in set(failed)]
+    assert ok  # (most of the multi-template bindings overflow at a cap of one run)
+    compare([got[i] for i in ok], [want[i] for i in ok], "sets overflow: the other bindings")
