@@ -63,10 +63,46 @@ def compulsory_bytes(n_bind, n_all, n_clusters, n_targets, snap_bytes, n_classes
     return pair, sel
 
 
+def kernel_bytes(name, units, Cp, n_classes, n_bind, n_targets, snap_bytes, R):
+    """Compulsory HBM bytes of one kernel over the units (bindings or class rows) its
+    launches covered: the records and feasibility rows it must read
+    (256 + Cp/8 B per binding), the class rows (4 B/cluster) and orders (8 B/cluster)
+    it reads once, the results it writes (8 B per target, 28 B per binding)."""
+    if units == 0 and name not in ("k_offsets", "k_compact"):
+        return 0.0  # (an empty fallback list: the launch found nothing to do)
+    rec = B_BIND + Cp / 8.0
+    share = n_targets * units / max(1, n_bind)  # its bindings' share of the targets
+    if name.startswith("k_est_class"):
+        return snap_bytes + 4.0 * Cp * units
+    if name.startswith("k_pair"):
+        return snap_bytes + units * (B_BIND + Cp / 8.0 + 4.0 * Cp)
+    if name == "k_filter":
+        return units * rec
+    if name == "k_class_order":
+        return 12.0 * Cp * units
+    if name == "k_select_top":
+        return units * (rec + 28) + 12.0 * Cp * n_classes + 8.0 * share
+    if name == "k_select_static":
+        return units * (rec + 28) + 8.0 * share
+    if name in ("k_spread_order", "k_region_a_order"):
+        return units * (rec + 28) + 12.0 * Cp * n_classes + 8.0 * share
+    if name == "k_region_groups":
+        return units * (B_BIND + 16.0 * max(1, R))
+    if name == "k_slow":
+        return units * (rec + 4.0 * Cp + 28) + 8.0 * share
+    if name == "k_offsets":
+        return n_bind * 16.0
+    if name == "k_compact":
+        return n_bind * 20.0 + 16.0 * n_targets
+    # k_select_all*, k_select_cluster*, k_region_a*, k_region_b*: the bindings' records,
+    # feasibility rows and class rows, their results
+    return units * (rec + 28) + 4.0 * Cp * n_classes + 8.0 * share
+
+
 def load_pmc(config, kernel):
     """Per-launch PMC figures of `kernel` from the committed summary (same bench
     command, default sizes): {hbm_bytes (FETCH_SIZE*2 + WRITE_SIZE), valu_insts, ...}."""
-    for rnd in ("r03", "r02"):  # the newest summary that holds the kernel
+    for rnd in ("r04", "r03", "r02"):  # the newest summary that holds the kernel
         try:
             with open(os.path.join(ROOT, "profiles", f"{rnd}_pmc_config{config}.json")) as f:
                 k = json.load(f).get("kernels", {}).get(kernel)
@@ -323,6 +359,14 @@ def main():
             r = batch.schedule_raw()
             st_ser.append(eng.stage_times())
         barrier_sync()
+        # then every kernel of the step timed by its own HIP event pair (on the stream it
+        # runs on), one batch at a time, for the per-kernel ranking and the roofline
+        eng.set_profile(True)
+        kt_runs = []
+        for _ in range(n_ser):
+            batch.schedule_raw()
+            kt_runs.append(eng.kernel_times())
+        eng.set_profile(False)
         st_all = st_ser  # per-stage HIP event times without another batch's kernels beside them
         serial_ms = 1e3 * (time.perf_counter() - t1) / n_ser
         if dist is not None:
@@ -333,6 +377,12 @@ def main():
     # ---- after the timed region ----
     if len(lanes) == 1:
         r = results[0]
+        eng.set_profile(True)
+        kt_runs = []
+        for _ in range(max(1, min(args.steps, 50))):
+            batch.schedule_raw()
+            kt_runs.append(eng.kernel_times())
+        eng.set_profile(False)
     csr = Csr.from_results(r)
     res = csr.to_python()
     n_ok = int((csr.status == 0).sum())
@@ -414,20 +464,25 @@ def main():
     bits = last["bits"] == 1
     pair_b, sel_b = compulsory_bytes(B_rank, int(last["n_sel_all"]), C_, n_targets_rank, snap_bytes,
                                      int(last["n_classes"]) if bits else 0)
-    stage = "k_est_class+k_filter" if bits else PAIR_KERNELS.get(last["pair_kind"], "k_pair")
     top_ms = avg("top_kernel_ms")
-    n_top, n_fb, n_all = int(last["n_top"]), int(last["n_top_fallback"]), max(1, int(last["n_sel_all"]))
-    if top_ms > 0 and n_top > 0:
-        # k_select_top alone: its bindings' records and feasibility rows, each class
-        # row and its order (4 B + 4 B per cluster) once, the targets it writes
-        Cp = (C_ + 63) // 64 * 64
-        top_b = (n_top * (B_BIND + Cp / 8.0 + 28) + 8.0 * Cp * int(last["n_classes"])
-                 + 8.0 * n_targets_rank * (n_top - n_fb) / n_all)
-        cands = [(stage, pair_ms, pair_b), ("k_select_top", top_ms, top_b),
-                 ("SEL_ALL rest (k_class_order + k_select_all fallback + streamed)", sel_all_ms - top_ms,
-                  sel_b - top_b)]
-    else:
-        cands = [(stage, pair_ms, pair_b), ("k_select_all", sel_all_ms, sel_b)]
+    # every kernel of the step, ranked by its HIP-event time (averaged over the profiled
+    # serial steps), with its compulsory bytes
+    Cp = (C_ + 63) // 64 * 64
+    n_cls = int(last["n_classes"]) if bits else 0
+    kern = {}
+    for run in kt_runs:
+        for name, v in run.items():
+            k = kern.setdefault(name, {"ms": 0.0, "launches": 0, "units": 0})
+            k["ms"] += v["ms"] / len(kt_runs)
+            k["launches"] = v["launches"]
+            k["units"] = v["units"]
+    kernels = []
+    for name, v in kern.items():
+        by = kernel_bytes(name, v["units"], Cp, n_cls, B_rank, n_targets_rank, snap_bytes, 0)
+        kernels.append({"kernel": name, "ms": round(v["ms"], 4), "launches": v["launches"], "units": v["units"],
+                        "bytes": round(by), "gbs": round(by / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None})
+    kernels.sort(key=lambda x: -x["ms"])
+    cands = [(k["kernel"], k["ms"], k["bytes"]) for k in kernels] or [("step", ms_per_step, pair_b + sel_b)]
     kname, kms, kbytes = max(cands, key=lambda x: x[1])
     achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     profiled = (C_, B) == tuple(synth.CONFIGS[cfg])
@@ -467,6 +522,9 @@ def main():
                    "parallelism": f"binding-shard x{world}" + (" (cost-balanced, RCCL snapshot broadcast + "
                                                                "CSR all-gather)" if world > 1 else "")},
         "roofline": roof,
+        # every kernel of one step (serial, profiled): HIP-event ms, launches, bindings (or
+        # class rows) covered, compulsory bytes and the rate they imply, slowest first
+        "kernels": kernels,
         # compulsory bytes of the whole step (every kernel) over the whole step's time
         "step_roofline": {"achieved": round(step_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(step_gbs / HBM_PEAK_GBS, 4), "bytes": round(step_bytes)},

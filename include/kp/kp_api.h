@@ -603,6 +603,20 @@ int kp_node_max_component_sets(kp_engine* e, const kp_node* nodes, uint64_t n_no
 /* Last schedule call's stage timings. */
 int kp_last_stage_times(const kp_engine* e, kp_stage_times* out);
 
+/* Per-kernel times of the last kp_schedule_batch, with profiling on
+ * (kp_engine_set_profile(e, 1): an event pair around every launch on its own
+ * stream; off by default). One entry per kernel name: the summed HIP-event time of
+ * its launches, their count, and the bindings (or class rows) they covered. */
+typedef struct kp_kernel_time {
+  char name[32];
+  float ms;
+  uint32_t launches;
+  uint64_t units;
+} kp_kernel_time;
+int kp_engine_set_profile(kp_engine* e, int on);
+/* *n_out = the number of entries; at most `cap` are written to out. */
+int kp_last_kernel_times(const kp_engine* e, kp_kernel_time* out, uint32_t cap, uint32_t* n_out);
+
 /* Host threads an engine packs a batch on (kp_batch_create); default: the
  * hardware threads, at most 16. */
 int kp_engine_set_threads(kp_engine* e, int n_threads);

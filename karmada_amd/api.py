@@ -178,6 +178,10 @@ class kp_affinity_results(C.Structure):
                 ("rounds", C.c_uint32)]
 
 
+class kp_kernel_time(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("ms", C.c_float), ("launches", u32), ("units", u64)]
+
+
 class kp_stage_times(C.Structure):
     _fields_ = [("pair_ms", C.c_double), ("select_ms", C.c_double), ("host_ms", C.c_double),
                 ("copy_ms", C.c_double), ("total_ms", C.c_double),

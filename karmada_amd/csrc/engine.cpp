@@ -215,6 +215,17 @@ struct kp_engine {
   // KP_TOP=0 / KP_TOP_CAP=<n> at engine creation (tests, tuning)
   bool top_on = true;
   int top_cap = 512;
+  // per-kernel timing of kp_schedule_batch (kp_engine_set_profile): an event pair
+  // around every launch on its own stream, folded by kernel name after the batch
+  struct KProf {
+    const char* name;
+    uint64_t units;  // bindings (or rows) the launch covered
+    int units_stat;  // >= 0: the count is device-side, h_stats[units_stat]
+  };
+  bool prof = false;
+  std::vector<dev::event_t> pev;
+  std::vector<KProf> pk;
+  std::vector<kp_kernel_time> ktimes;
 };
 
 struct kp_snapshot {
@@ -1715,6 +1726,7 @@ void kp_engine_destroy(kp_engine* e) {
   (void)dev::set_device(e->device);
   for (auto& ev : e->ev)
     if (ev) dev::event_destroy(ev);
+  for (auto& ev : e->pev) dev::event_destroy(ev);
   if (e->stream) dev::stream_destroy(e->stream);
   if (e->stream2) dev::stream_destroy(e->stream2);
   if (e->stream3) dev::stream_destroy(e->stream3);
@@ -1722,6 +1734,20 @@ void kp_engine_destroy(kp_engine* e) {
 }
 
 const char* kp_last_error(const kp_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+int kp_engine_set_profile(kp_engine* e, int on) {
+  if (!e) return KP_EINVAL;
+  e->prof = on != 0;
+  e->ktimes.clear();
+  return KP_OK;
+}
+
+int kp_last_kernel_times(const kp_engine* e, kp_kernel_time* out, uint32_t cap, uint32_t* n_out) {
+  if (!e || !n_out || (cap && !out)) return KP_EINVAL;
+  *n_out = (uint32_t)e->ktimes.size();
+  for (uint32_t i = 0; i < cap && i < e->ktimes.size(); i++) out[i] = e->ktimes[i];
+  return KP_OK;
+}
 
 int kp_engine_set_threads(kp_engine* e, int n_threads) {
   if (!e || n_threads < 1) return KP_EINVAL;
@@ -2454,6 +2480,84 @@ static int ensure_rows(kp_engine* e, kp_batch* bt) {
   return 0;
 }
 
+// Per-kernel profiling (kp_engine_set_profile): prof_begin records the start event of
+// launch i on its stream, prof_end its end event and what it covered.
+static int prof_begin(kp_engine* e, dev::stream_t st) {
+  if (!e->prof) return -1;
+  const size_t i = e->pk.size();
+  while (e->pev.size() < 2 * i + 2) {
+    dev::event_t ev = nullptr;
+    if (dev::event_create(&ev)) return -1;
+    e->pev.push_back(ev);
+  }
+  if (dev::event_record(e->pev[2 * i], st)) return -1;
+  e->pk.push_back({"", 0, -1});
+  return (int)i;
+}
+static void prof_end(kp_engine* e, int i, dev::stream_t st, const char* name, uint64_t units, int units_stat = -1) {
+  if (i < 0) return;
+  (void)dev::event_record(e->pev[2 * (size_t)i + 1], st);
+  e->pk[i] = {name, units, units_stat};
+}
+// After the batch's final sync: each kernel's launches folded by name.
+static void prof_fold(kp_engine* e, const uint32_t* h_stats) {
+  e->ktimes.clear();
+  for (size_t i = 0; i < e->pk.size(); i++) {
+    const auto& k = e->pk[i];
+    const float ms = dev::event_ms(e->pev[2 * i], e->pev[2 * i + 1]);
+    const uint64_t units = k.units_stat >= 0 ? h_stats[k.units_stat] : k.units;
+    kp_kernel_time* t = nullptr;
+    for (auto& x : e->ktimes)
+      if (strncmp(x.name, k.name, sizeof(x.name)) == 0) t = &x;
+    if (!t) {
+      e->ktimes.push_back(kp_kernel_time{});
+      t = &e->ktimes.back();
+      snprintf(t->name, sizeof(t->name), "%s", k.name);
+    }
+    t->ms += ms > 0 ? ms : 0.f;
+    t->launches++;
+    t->units += units;
+  }
+  e->pk.clear();
+}
+#define KPROF(ST, NAME, UNITS, STAT, CALL)           \
+  do {                                               \
+    const int pi_ = prof_begin(e, ST);               \
+    HIPCHK(CALL);                                    \
+    prof_end(e, pi_, ST, NAME, (uint64_t)(UNITS), STAT); \
+  } while (0)
+// launch names of the select kernels (kernels.hip picks the wide instance past half
+// the CU's LDS, as here)
+static const char* sel_name(int which, size_t smem) {
+  const bool wide = smem > 80 * 1024;
+  switch (which) {
+    case SEL_LAUNCH_ALL: return wide ? "k_select_all_wide" : "k_select_all";
+    case SEL_LAUNCH_ALL_STREAM: return "k_select_all_stream";
+    case SEL_LAUNCH_CLUSTER: return wide ? "k_select_cluster_wide" : "k_select_cluster";
+    case SEL_LAUNCH_REGION_A: return wide ? "k_region_a_wide" : "k_region_a";
+    case SEL_LAUNCH_REGION_B: return wide ? "k_region_b_wide" : "k_region_b";
+    case SEL_LAUNCH_SLOW: return "k_slow";
+  }
+  return "k_select";
+}
+static const char* pair_name(int fast) {
+  switch (fast) {
+    case EST_MIXED: return "k_pair_fast";
+    case EST_SUMMARY: return "k_pair_fast_summary";
+    case EST_MODEL8: return "k_pair_fast_m8";
+    case EST_MODEL16: return "k_pair_fast_m16";
+  }
+  return "k_pair";
+}
+static const char* est_class_name(int fast) {
+  switch (fast) {
+    case EST_SUMMARY: return "k_est_class_summary";
+    case EST_MODEL8: return "k_est_class_m8";
+    case EST_MODEL16: return "k_est_class_m16";
+  }
+  return "k_est_class";
+}
+
 // The batch path computes the in-tree plugin set only (kp_options.n_out_of_tree_plugins).
 static int refuse_out_of_tree(kp_engine* e, const kp_snapshot* s) {
   if (s->opts.n_out_of_tree_plugins == 0) return KP_OK;
@@ -2483,6 +2587,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     return KP_ESTATE;
   }
   if (batch_lds_check(e, s, bt)) return KP_ENOTSUP;
+  e->pk.clear();
   HIPCHK(dev::h2d(bt->counter, &bt->out_cap, sizeof(unsigned long long), st));  // the shared area's start
   HIPCHK(dev::fill(bt->stats, 0, sizeof(bt->h_stats), st));
   if (!bt->sets_cls.empty()) HIPCHK(dev::fill(bt->d_sets_ovf, 0, 4 * bt->sets_cls.size(), st));
@@ -2533,21 +2638,25 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   const int cap = kSmallMax + kTgtSmallMax + 16;
   HIPCHK(dev::event_record(e->ev[3], sp));
   if (bits) {
-    HIPCHK(dev::est_class(sp, s->view, bt->view, bt->d_crep, (int)bt->crep.size(), bt->cls_rows, fast));
+    KPROF(sp, est_class_name(fast), bt->crep.size(), -1,
+          dev::est_class(sp, s->view, bt->view, bt->d_crep, (int)bt->crep.size(), bt->cls_rows, fast));
     HIPCHK(dev::event_record(e->ev[5], sp));
-    HIPCHK(dev::filter(sp, s->view, bt->view, bt->fmask));
+    KPROF(sp, "k_filter", B, -1, dev::filter(sp, s->view, bt->view, bt->fmask));
   } else {
-    HIPCHK(dev::pair(sp, s->view, bt->view, nullptr, 0, B, bt->fmask, bt->est, nullptr, 0, md_cap, smem_pair(s, md_cap),
-                     fast));
+    KPROF(sp, pair_name(fast), B, -1,
+          dev::pair(sp, s->view, bt->view, nullptr, 0, B, bt->fmask, bt->est, nullptr, 0, md_cap, smem_pair(s, md_cap),
+                    fast));
   }
   // component-set classes (BF_SETS bindings): their class rows, and in the pair-row
   // mode those bindings' own rows rebuilt from them (feasible clusters only)
   for (size_t j = 0; j < bt->sets_cls.size(); j++)
-    HIPCHK(dev::sets_rows(sp, s->view, bt->d_sets_args + j, bt->d_sets_off, bt->d_sets_scratch,
-                          bt->cls_rows + (size_t)bt->sets_cls[j] * s->Cp, bt->d_sets_ovf + j));
+    KPROF(sp, "k_sets_rows", 1, -1,
+          dev::sets_rows(sp, s->view, bt->d_sets_args + j, bt->d_sets_off, bt->d_sets_scratch,
+                         bt->cls_rows + (size_t)bt->sets_cls[j] * s->Cp, bt->d_sets_ovf + j));
   if (!bits && !bt->l_sets.empty())
-    HIPCHK(dev::rows_from_class(sp, s->view, bt->view, bt->d_sets_list, (int)bt->l_sets.size(), bt->d_bcls,
-                                bt->cls_rows, bt->fmask, bt->est));
+    KPROF(sp, "k_rows_from_class", bt->l_sets.size(), -1,
+          dev::rows_from_class(sp, s->view, bt->view, bt->d_sets_list, (int)bt->l_sets.size(), bt->d_bcls,
+                               bt->cls_rows, bt->fmask, bt->est));
   // SEL_ALL DynamicWeight / Aggregated over the deciding candidates (kp_top.h): the
   // class rows' orders first
   const bool top = bits && e->top_on && bt->d_ord != nullptr && bt->n_all_dyn > 0 &&
@@ -2562,7 +2671,8 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
                                  e->max_lds;
   const bool orders = top || spread_orders;
   if (orders)
-    HIPCHK(dev::class_order(sp, s->view, bt->cls_rows, (int)bt->crep.size(), bt->d_ord, bt->d_ctot, bt->d_cok));
+    KPROF(sp, "k_class_order", bt->crep.size(), -1,
+          dev::class_order(sp, s->view, bt->cls_rows, (int)bt->crep.size(), bt->d_ord, bt->d_ctot, bt->d_cok));
   HIPCHK(dev::event_record(e->ev[4], sp));
   HIPCHK(dev::stream_wait(st, e->ev[4]));  // every pair row precedes the rest
   HIPCHK(dev::event_record(e->ev[1], st));
@@ -2589,18 +2699,20 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       TopArgs ta{bt->d_ord, bt->d_ctot, bt->d_cok, bt->d_fb, bt->stats + 9, e->top_cap};
       const size_t slice = (top_lds_bytes(s->Cp, e->top_cap) + 15) & ~(size_t)15;
       HIPCHK(dev::event_record(e->ev[12], sp));
-      HIPCHK(dev::select_top(sp, g, ta, slice));
+      KPROF(sp, "k_select_top", g.n, -1, dev::select_top(sp, g, ta, slice));
       HIPCHK(dev::event_record(e->ev[13], sp));
       KArgs f = k;
       f.list = bt->d_fb;
       f.n = bt->n_all_dyn;
       f.n_dev = bt->stats + 9;
-      if (stream_all) HIPCHK(dev::select(sp, SEL_LAUNCH_ALL_STREAM, f, sel_stream_lds_bytes(s->Cp), cap, sx));
-      else HIPCHK(dev::select(sp, SEL_LAUNCH_ALL, f, smem_all(s), cap, sx));
+      if (stream_all)
+        KPROF(sp, "k_select_all_stream", 0, 9, dev::select(sp, SEL_LAUNCH_ALL_STREAM, f, sel_stream_lds_bytes(s->Cp), cap, sx));
+      else
+        KPROF(sp, sel_name(SEL_LAUNCH_ALL, smem_all(s)), 0, 9, dev::select(sp, SEL_LAUNCH_ALL, f, smem_all(s), cap, sx));
     } else if (na > 0) {
       KArgs g = k;
       g.n = na;
-      HIPCHK(dev::select(sp, SEL_LAUNCH_ALL, g, smem_all(s), cap, sx));
+      KPROF(sp, sel_name(SEL_LAUNCH_ALL, smem_all(s)), g.n, -1, dev::select(sp, SEL_LAUNCH_ALL, g, smem_all(s), cap, sx));
     }
     // the rest: StaticWeight at class level (k_select_static) where it applies, then
     // the streamed kernel
@@ -2610,14 +2722,14 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       KArgs g = k;
       g.list = bt->d_all + rest0;
       g.n = bt->n_static;
-      HIPCHK(dev::select_static(sp, g, (static_lds_bytes(s->view.W) + 15) & ~(size_t)15));
+      KPROF(sp, "k_select_static", g.n, -1, dev::select_static(sp, g, (static_lds_bytes(s->view.W) + 15) & ~(size_t)15));
       rest0 += bt->n_static;
     }
     if (k.n - rest0 > 0) {
       KArgs g = k;
       g.list = bt->d_all + rest0;
       g.n = k.n - rest0;
-      HIPCHK(dev::select(sp, SEL_LAUNCH_ALL_STREAM, g, sel_stream_lds_bytes(s->Cp), cap, sx));
+      KPROF(sp, "k_select_all_stream", g.n, -1, dev::select(sp, SEL_LAUNCH_ALL_STREAM, g, sel_stream_lds_bytes(s->Cp), cap, sx));
     }
   }
   HIPCHK(dev::event_record(e->ev[8], sp));  // k_select_all alone: ev[7] -> ev[8]
@@ -2634,11 +2746,13 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       k.cok = bt->d_cok;
       k.n_order = bt->stats + 10;
       OrderArgs oa{nullptr, nullptr, nullptr, bt->d_fbc, bt->stats + 12, 0};
-      HIPCHK(dev::spread_order(s3, k, oa, (order_lds_bytes(s->view.W, s->view.n_regions) + 15) & ~(size_t)15));
+      KPROF(s3, "k_spread_order", k.n, -1,
+            dev::spread_order(s3, k, oa, (order_lds_bytes(s->view.W, s->view.n_regions) + 15) & ~(size_t)15));
       k.sub = bt->d_fbc;
       k.n_dev = bt->stats + 12;
     }
-    HIPCHK(dev::select(s3, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sx));
+    KPROF(s3, sel_name(SEL_LAUNCH_CLUSTER, smem_cluster(s, cap)), k.n_dev ? 0 : k.n, k.n_dev ? 12 : -1,
+          dev::select(s3, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sx));
     HIPCHK(dev::event_record(e->ev[15], s3));
   }
   HIPCHK(dev::event_record(e->ev[9], s3));
@@ -2656,14 +2770,16 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     if (spread_orders) {  // stage A of the order-eligible bindings, one wave each; the rest below
       KArgs ko = k;
       ko.n_order = nullptr;
-      HIPCHK(dev::region_a_order(st, ko, bt->rout, bt->rstat, bt->d_fba, bt->stats + 14,
+      KPROF(st, "k_region_a_order", ko.n, -1, dev::region_a_order(st, ko, bt->rout, bt->rstat, bt->d_fba, bt->stats + 14,
                                  (region_a_order_lds_bytes(R) + 15) & ~(size_t)15));
       KArgs kf = k;
       kf.sub = bt->d_fba;
       kf.n_dev = bt->stats + 14;
-      HIPCHK(dev::select(st, SEL_LAUNCH_REGION_A, kf, smem_region_a(s), cap, sx));
+      KPROF(st, sel_name(SEL_LAUNCH_REGION_A, smem_region_a(s)), 0, 14,
+            dev::select(st, SEL_LAUNCH_REGION_A, kf, smem_region_a(s), cap, sx));
     } else {
-      HIPCHK(dev::select(st, SEL_LAUNCH_REGION_A, k, smem_region_a(s), cap, sx));
+      KPROF(st, sel_name(SEL_LAUNCH_REGION_A, smem_region_a(s)), k.n, -1,
+            dev::select(st, SEL_LAUNCH_REGION_A, k, smem_region_a(s), cap, sx));
     }
     // selectGroups: on the device (one thread per binding) unless the snapshot
     // has more regions than its arrays hold; bindings whose DFS exceeds the node
@@ -2672,7 +2788,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     uint32_t nh = 0;
     if (dev_groups) {
       HIPCHK(dev::fill(bt->nhost, 0, 4, st));
-      HIPCHK(dev::region_groups(st, bt->rout, bt->rstat, bt->view.hdr, bt->d_region, nr, R, bt->rsel, bt->rnsel,
+      KPROF(st, "k_region_groups", nr, -1, dev::region_groups(st, bt->rout, bt->rstat, bt->view.hdr, bt->d_region, nr, R, bt->rsel, bt->rnsel,
                                 bt->nhost));
       HIPCHK(dev::d2h(&nh, bt->nhost, 4, st));
       HIPCHK(dev::sync(st));
@@ -2722,11 +2838,12 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     }
     if (spread_orders) {
       OrderArgs oa{bt->rout, bt->rsel, bt->rnsel, bt->d_fbr, bt->stats + 13, 1};
-      HIPCHK(dev::spread_order(st, k, oa, (order_lds_bytes(s->view.W, R) + 15) & ~(size_t)15));
+      KPROF(st, "k_spread_order", k.n, -1, dev::spread_order(st, k, oa, (order_lds_bytes(s->view.W, R) + 15) & ~(size_t)15));
       k.sub = bt->d_fbr;
       k.n_dev = bt->stats + 13;
     }
-    HIPCHK(dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sx));
+    KPROF(st, sel_name(SEL_LAUNCH_REGION_B, smem_region_b(s, cap)), k.n_dev ? 0 : k.n, k.n_dev ? 13 : -1,
+          dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sx));
   }
   HIPCHK(dev::stream_wait(st, e->ev[8]));  // every fast-path flag precedes k_slow
   HIPCHK(dev::stream_wait(st, e->ev[9]));
@@ -2734,15 +2851,16 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     KArgs k = ka;
     k.list = bt->d_slowlist;
     k.n = (int)bt->l_slow.size();
-    HIPCHK(dev::select(st, SEL_LAUNCH_SLOW, k, kRedBytes + 512 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area +
+    KPROF(st, "k_slow", 0, 0, dev::select(st, SEL_LAUNCH_SLOW, k, kRedBytes + 512 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area +
                                                       sx.lds_sort,
                        bt->slow_cap, sx));
   }
   HIPCHK(dev::event_record(e->ev[2], st));
   // results -> host, compacted to CSR: offsets scanned and results compacted on
   // the device, then the per-binding arrays and the CSR copied back
-  HIPCHK(dev::offsets(st, bt->status, bt->count, B, bt->offsets_d, bt->off_part));
-  HIPCHK(dev::compact(st, bt->start, bt->count, bt->offsets_d, bt->out_idx, bt->out_rep, bt->cidx_d, bt->crep_d, B));
+  KPROF(st, "k_offsets", B, -1, dev::offsets(st, bt->status, bt->count, B, bt->offsets_d, bt->off_part));
+  KPROF(st, "k_compact", B, -1,
+        dev::compact(st, bt->start, bt->count, bt->offsets_d, bt->out_idx, bt->out_rep, bt->cidx_d, bt->crep_d, B));
   bt->h_status.resize(B);
   bt->h_err.resize(B);
   bt->h_arg.resize(B);
@@ -2808,6 +2926,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   }
   const uint64_t tot_out = bt->h_offsets[B];
   double t1 = now_ms();
+  if (e->prof) prof_fold(e, bt->h_stats);
   // pair: the pair launch, or k_est_class + k_filter (stream2; filter: k_filter
   // alone); select: from the point where they are complete to the end of the last
   // select kernel.

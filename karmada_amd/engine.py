@@ -36,7 +36,7 @@ EXPORTS = (
     "kp_batch_destroy",
     "kp_schedule_batch", "kp_schedule_affinities", "kp_filter_batch", "kp_filter_reasons", "kp_score_batch", "kp_max_available_replicas", "kp_max_available_component_sets",
     "kp_model_grades", "kp_node_max_replicas", "kp_node_max_component_sets", "kp_last_stage_times",
-    "kp_engine_set_threads", "kp_snapshot_replicate",
+    "kp_engine_set_threads", "kp_snapshot_replicate", "kp_engine_set_profile", "kp_last_kernel_times",
     "kp_multi_create", "kp_multi_destroy", "kp_multi_last_error", "kp_multi_devices", "kp_multi_engine",
     "kp_multi_snapshot_create", "kp_multi_snapshot_update", "kp_multi_snapshot_destroy", "kp_multi_snapshot_replica",
     "kp_multi_shard_cuts", "kp_multi_batch_create", "kp_multi_batch_destroy", "kp_multi_batch_shards",
@@ -92,6 +92,8 @@ def load_library(path: str = LIB_PATH):
     L.kp_snapshot_import.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(vp)]
     L.kp_snapshot_update.argtypes = [vp, vp, C.POINTER(api.kp_cluster), C.c_uint64, C.POINTER(C.c_int)]
     L.kp_engine_set_threads.argtypes = [vp, C.c_int]
+    L.kp_engine_set_profile.argtypes = [vp, C.c_int]
+    L.kp_last_kernel_times.argtypes = [vp, C.POINTER(api.kp_kernel_time), C.c_uint32, C.POINTER(C.c_uint32)]
     L.kp_snapshot_replicate.argtypes = [vp, vp, C.POINTER(vp)]
     L.kp_multi_create.argtypes = [C.POINTER(C.c_int), C.c_uint32, C.POINTER(vp)]
     L.kp_multi_destroy.argtypes = [vp]
@@ -210,6 +212,19 @@ class Engine:
         t = api.kp_stage_times()
         self._check(self.L.kp_last_stage_times(self.h, C.byref(t)), "kp_last_stage_times")
         return {k: getattr(t, k) for k, _ in api.kp_stage_times._fields_}
+
+    def set_profile(self, on: bool = True):
+        """Per-kernel HIP-event timing of kp_schedule_batch (kp_engine_set_profile)."""
+        self._check(self.L.kp_engine_set_profile(self.h, int(on)), "kp_engine_set_profile")
+
+    def kernel_times(self) -> Dict[str, dict]:
+        """{kernel name: {ms, launches, units}} of the last kp_schedule_batch (profiling on)."""
+        n = C.c_uint32()
+        self._check(self.L.kp_last_kernel_times(self.h, None, 0, C.byref(n)), "kp_last_kernel_times")
+        arr = (api.kp_kernel_time * max(1, n.value))()
+        self._check(self.L.kp_last_kernel_times(self.h, arr, n.value, C.byref(n)), "kp_last_kernel_times")
+        return {arr[i].name.decode(): {"ms": arr[i].ms, "launches": arr[i].launches, "units": arr[i].units}
+                for i in range(n.value)}
 
 
 class Snapshot:

@@ -30,7 +30,8 @@ def test_library_exports_every_declared_symbol():
 STRUCTS = ("kp_str", "kp_label", "kp_requirement", "kp_cluster_affinity", "kp_affinity_term", "kp_toleration",
            "kp_taint", "kp_spread_constraint", "kp_static_weight", "kp_resource", "kp_target_cluster", "kp_binding",
            "kp_api_enablement", "kp_model_range", "kp_resource_model", "kp_allocatable_modeling", "kp_cluster",
-           "kp_options", "kp_results", "kp_affinity_results", "kp_stage_times", "kp_component")
+           "kp_options", "kp_results", "kp_affinity_results", "kp_stage_times", "kp_component",
+           "kp_kernel_time")
 
 
 def test_abi_version_and_struct_sizes(tmp_path):

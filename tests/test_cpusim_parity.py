@@ -197,3 +197,33 @@ def test_cpusim_sets_overflow_is_per_binding(engine):
     ok = [i for i in range(len(got)) if i not in set(failed)]
     assert ok  # (most of the multi-template bindings overflow at a cap of one run)
     compare([got[i] for i in ok], [want[i] for i in ok], "sets overflow: the other bindings")
+
+
+def test_cpusim_kernel_times():
+    """kp_engine_set_profile: every kernel of the step is timed by its own event pair and
+    reported by name with its launches and the bindings it covered (the bench ranks the
+    step's kernels by these times); results are unchanged with profiling on."""
+    e = Engine(0, lib_path=CPUSIM)
+    try:
+        e.set_profile(True)
+        for config, seed, C_, B_, must in [
+            (3, 3, 200, 300, {"k_est_class_m8", "k_filter", "k_class_order", "k_select_top", "k_offsets", "k_compact"}),
+            (4, 4, 400, 500, {"k_spread_order", "k_region_a_order", "k_region_groups"}),
+            (8, 4, 64, 300, {"k_slow"}),
+        ]:
+            u = synth.Universe(config, seed, C_, 0, B_)
+            opts = api.options()
+            want = O.schedule_c(u.clusters, u.n_clusters, u.bindings, u.n_bindings, opts, O.FAST, 8)
+            compare(run(e, u, opts), want, f"profiled config {config}")
+            kt = e.kernel_times()
+            assert must <= set(kt), (config, sorted(kt))
+            assert all(v["launches"] >= 1 and v["ms"] >= 0 for v in kt.values())
+            assert kt["k_filter"]["units"] == B_ if "k_filter" in kt else True
+            if config == 8:
+                assert kt["k_slow"]["units"] == e.stage_times()["n_slow"] > 0
+        e.set_profile(False)
+        u = synth.Universe(3, 3, 200, 0, 100)
+        run(e, u, api.options())
+        assert e.kernel_times() == {}
+    finally:
+        e.close()
