@@ -915,6 +915,18 @@ struct Packer {
   std::vector<Instr> tmp_out;
   std::vector<int32_t> tmp_vals;
   std::vector<std::pair<std::string_view, std::string_view>> tmp_ml;
+  std::vector<int32_t> tmp_filt, tmp_ovf, tmp_ov, tmp_ids, tmp_ev;
+  std::vector<int64_t> tmp_ws;
+  // compiled programs by affinity content (a batch repeats a policy's placement across
+  // its bindings): the instructions with their list references relative to the lists
+  // they own, re-emitted into the pools on a hit
+  struct CProg {
+    std::vector<Instr> ins;
+    std::vector<int32_t> lists;
+  };
+  SvMap<int32_t> cmemo;
+  std::vector<CProg> cprogs;
+  std::string ckey;
 
   bool scalar(std::string_view nm) {
     auto it = scalar_cache.find(nm);
@@ -988,8 +1000,81 @@ struct Packer {
       if (!k8s::label_value(SV(v[i]))) ok = false;
     return ok;
   }
-  // util.ClusterMatches compiled to a conjunction program (selector.go:97-155)
+  static bool list_ref_a(int32_t op) { return op == OP_EXCLUDE || op == OP_NAMES; }
+  static bool list_ref_b(int32_t op) {
+    return op == OP_LBL_IN || op == OP_LBL_NOTIN || op == OP_FLD_IN || op == OP_FLD_NOTIN || op == OP_ZONE_IN ||
+           op == OP_ZONE_NOTIN;
+  }
+  // The affinity's content as a key: every field, strings length-prefixed.
+  void affinity_key(const kp_cluster_affinity& a) {
+    std::string& k = ckey;
+    k.clear();
+    auto u32 = [&](uint32_t v) { k.append((const char*)&v, 4); };
+    auto str = [&](const kp_str& x) {
+      u32(x.len);
+      if (x.len) k.append(x.ptr, x.len);
+    };
+    auto strs = [&](const kp_str* v, uint32_t n) {
+      u32(n);
+      for (uint32_t i = 0; i < n; i++) str(v[i]);
+    };
+    auto reqs = [&](const kp_requirement* r, uint32_t n) {
+      u32(n);
+      for (uint32_t i = 0; i < n; i++) {
+        str(r[i].key);
+        str(r[i].op);
+        strs(r[i].values, r[i].n_values);
+      }
+    };
+    u32(a.has_label_selector);
+    u32(a.n_match_labels);
+    for (uint32_t i = 0; i < a.n_match_labels; i++) {
+      str(a.match_labels[i].key);
+      str(a.match_labels[i].value);
+    }
+    reqs(a.match_expressions, a.n_match_expressions);
+    u32(a.has_field_selector);
+    reqs(a.field_expressions, a.n_field_expressions);
+    strs(a.cluster_names, a.n_cluster_names);
+    strs(a.exclude_clusters, a.n_exclude_clusters);
+  }
+  // util.ClusterMatches compiled to a conjunction program (selector.go:97-155),
+  // memoized by content
   int32_t compile(const kp_cluster_affinity& a) {
+    affinity_key(a);
+    auto it = cmemo.find(std::string_view(ckey));
+    if (it != cmemo.end()) {
+      const CProg& c = cprogs[it->second];
+      const int32_t base = (int32_t)bt->ipool.size();
+      bt->ipool.insert(bt->ipool.end(), c.lists.begin(), c.lists.end());
+      Prog p;
+      p.ins_off = (int32_t)bt->instrs.size();
+      p.ins_cnt = (int32_t)c.ins.size();
+      for (Instr x : c.ins) {
+        if (list_ref_a(x.op)) x.a += base;
+        else if (list_ref_b(x.op)) x.b += base;
+        bt->instrs.push_back(x);
+      }
+      bt->progs.push_back(p);
+      return (int32_t)bt->progs.size() - 1;
+    }
+    const int32_t ip0 = (int32_t)bt->ipool.size();
+    const int32_t id = compile_new(a);
+    if (cprogs.size() < 4096) {
+      CProg c;
+      const Prog& p = bt->progs[id];
+      c.lists.assign(bt->ipool.begin() + ip0, bt->ipool.end());
+      c.ins.assign(bt->instrs.begin() + p.ins_off, bt->instrs.begin() + p.ins_off + p.ins_cnt);
+      for (Instr& x : c.ins) {
+        if (list_ref_a(x.op)) x.a -= ip0;
+        else if (list_ref_b(x.op)) x.b -= ip0;
+      }
+      cmemo.emplace(ckey, (int32_t)cprogs.size());
+      cprogs.push_back(std::move(c));
+    }
+    return id;
+  }
+  int32_t compile_new(const kp_cluster_affinity& a) {
     std::vector<Instr>& out = tmp_out;
     out.clear();
     bool never = false;
@@ -1170,7 +1255,12 @@ struct Packer {
       if (b.n_clusters > 0 && (o.enabled_plugins & KP_PLUGIN_CLUSTER_LOCALITY)) f |= BF_SCORE_LOCALITY;
     }
     {
-      auto r = ranks(b.eviction_from, b.n_eviction_from);
+      auto& r = tmp_ev;
+      r.clear();
+      for (uint32_t i = 0; i < b.n_eviction_from; i++) {
+        auto it = s->rank_of.find(SV(b.eviction_from[i]));
+        if (it != s->rank_of.end()) r.push_back(it->second);
+      }
       h.evict_off = list(r);
       h.evict_cnt = (int32_t)r.size();
     }
@@ -1200,16 +1290,18 @@ struct Packer {
     h.tol_cnt = (int32_t)bt->tols.size() - h.tol_off;
     // ClusterAffinity filter list + overflow order programs
     {
-      std::vector<int32_t> filt, ovf;
+      auto &filt = tmp_filt, &ovf = tmp_ovf;
+      filt.clear();
+      ovf.clear();
       bool have = false;
       const kp_affinity_term* term = nullptr;
       if (b.has_cluster_affinity) {
         filt.push_back(compile(b.cluster_affinity));
         have = true;
       } else {
-        std::string obs = S(b.observed_affinity_name);
+        const std::string_view obs = SV(b.observed_affinity_name);
         for (uint32_t i = 0; i < b.n_cluster_affinities; i++)
-          if (S(b.cluster_affinities[i].affinity_name) == obs) {
+          if (SV(b.cluster_affinities[i].affinity_name) == obs) {
             term = &b.cluster_affinities[i];
             break;
           }
@@ -1217,7 +1309,8 @@ struct Packer {
           have = true;
           ovf.push_back(compile(term->affinity));
           filt.push_back(ovf[0]);
-          std::vector<int32_t> ov;
+          auto& ov = tmp_ov;
+          ov.clear();
           for (uint32_t j = 0; j < term->n_overflow; j++) ov.push_back(compile(term->overflow[j]));
           ovf.insert(ovf.end(), ov.begin(), ov.end());
           bool workload = b.replicas > 0 || b.has_replica_requirements || b.n_components >= 1;
@@ -1239,8 +1332,10 @@ struct Packer {
     }
     // static weights
     {
-      std::vector<int32_t> ids;
-      std::vector<int64_t> ws;
+      auto& ids = tmp_ids;
+      auto& ws = tmp_ws;
+      ids.clear();
+      ws.clear();
       for (uint32_t i = 0; i < b.n_static_weights; i++) {
         ids.push_back(compile(b.static_weights[i].target));
         ws.push_back(b.static_weights[i].weight);
@@ -2076,7 +2171,14 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
   bt->bcls.assign(n, 0);
   std::vector<std::vector<std::string>> tkeys(T);
   std::vector<std::string> terr(T);
+  std::vector<double> tms(T, 0.0);
   auto run = [&](int t) {
+    const auto tt0 = std::chrono::steady_clock::now();
+    struct Stamp {
+      std::chrono::steady_clock::time_point t0;
+      double* out;
+      ~Stamp() { *out = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+    } stamp{tt0, &tms[t]};
     Packer pk{s, &pl[t]};
     std::unordered_map<std::string, int32_t> ids;
     std::string key;
@@ -2197,8 +2299,10 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
   }
   if (getenv("KP_PACK_TIMING")) {
     auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
-    fprintf(stderr, "pack_parallel: %d threads, pack %.1f ms, merge+classes %.1f ms\n", T, ms(tq0, tq1),
+    fprintf(stderr, "pack_parallel: %d threads, pack %.1f ms, merge+classes %.1f ms; per thread", T, ms(tq0, tq1),
             ms(tq1, std::chrono::steady_clock::now()));
+    for (double x : tms) fprintf(stderr, " %.1f", x);
+    fprintf(stderr, "\n");
   }
   return true;
 }
