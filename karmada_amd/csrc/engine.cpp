@@ -2229,54 +2229,71 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       bt->err = x;
       return false;
     }
-  size_t ni = 0, nl = 0, nt = 0, np = 0, nn = 0;
-  for (auto& q : pl) ni += q.ipool.size(), nl += q.lpool.size(), nt += q.tols.size(), np += q.progs.size(),
-                     nn += q.instrs.size();
-  if (ni > (size_t)INT32_MAX || nl > (size_t)INT32_MAX || nt > (size_t)INT32_MAX || np > (size_t)INT32_MAX ||
-      nn > (size_t)INT32_MAX)
-    return false;  // pool offsets are int32
-  bt->ipool.reserve(ni);
-  bt->lpool.reserve(nl);
-  bt->tols.reserve(nt);
-  bt->progs.reserve(np);
-  bt->instrs.reserve(nn);
+  // pools concatenated in thread order: each thread's bases are the prefix sums of
+  // the pool sizes before it; every thread rebases its own headers and instructions
+  // and copies its pools into place, in parallel
+  std::vector<size_t> bi(T + 1, 0), bl(T + 1, 0), bo(T + 1, 0), bp(T + 1, 0), bn(T + 1, 0);
   for (int t = 0; t < T; t++) {
+    bi[t + 1] = bi[t] + pl[t].ipool.size();
+    bl[t + 1] = bl[t] + pl[t].lpool.size();
+    bo[t + 1] = bo[t] + pl[t].tols.size();
+    bp[t + 1] = bp[t] + pl[t].progs.size();
+    bn[t + 1] = bn[t] + pl[t].instrs.size();
+  }
+  if (bi[T] > (size_t)INT32_MAX || bl[T] > (size_t)INT32_MAX || bo[T] > (size_t)INT32_MAX ||
+      bp[T] > (size_t)INT32_MAX || bn[T] > (size_t)INT32_MAX)
+    return false;  // pool offsets are int32
+  bt->ipool.resize(bi[T]);
+  bt->lpool.resize(bl[T]);
+  bt->tols.resize(bo[T]);
+  bt->progs.resize(bp[T]);
+  bt->instrs.resize(bn[T]);
+  auto merge = [&](int t) {
     Pools& q = pl[t];
-    const int32_t bi = (int32_t)bt->ipool.size(), bl = (int32_t)bt->lpool.size(), bo = (int32_t)bt->tols.size(),
-                  bp = (int32_t)bt->progs.size(), bn = (int32_t)bt->instrs.size();
+    const int32_t oi = (int32_t)bi[t], ol = (int32_t)bl[t], oo = (int32_t)bo[t], op = (int32_t)bp[t],
+                  on = (int32_t)bn[t];
     if (t > 0) {
       for (int i = lo[t]; i < lo[t + 1]; i++) {
         BindHdr& h = bt->hdr[i];
-        for (int j = 0; j < h.filt_cnt; j++) q.ipool[h.filt_off + j] += bp;
-        for (int j = 0; j < h.ovf_cnt; j++) q.ipool[h.ovf_off + j] += bp;
-        for (int j = 0; j < h.sw_cnt; j++) q.ipool[h.sw_off + j] += bp;
-        h.tgt_off += bi, h.evict_off += bi, h.filt_off += bi, h.ovf_off += bi, h.sw_off += bi;
-        h.sreq_off += bi, h.mreq_off += bi, h.ip_beg += bi, h.ip_end += bi;
-        h.sw_w_off += bl, h.sreq_q_off += bl, h.mreq_q_off += bl;
-        h.tol_off += bo;
-        h.pr_beg += bp, h.pr_end += bp;
-        h.in_beg += bn, h.in_end += bn;
+        for (int j = 0; j < h.filt_cnt; j++) q.ipool[h.filt_off + j] += op;
+        for (int j = 0; j < h.ovf_cnt; j++) q.ipool[h.ovf_off + j] += op;
+        for (int j = 0; j < h.sw_cnt; j++) q.ipool[h.sw_off + j] += op;
+        h.tgt_off += oi, h.evict_off += oi, h.filt_off += oi, h.ovf_off += oi, h.sw_off += oi;
+        h.sreq_off += oi, h.mreq_off += oi, h.ip_beg += oi, h.ip_end += oi;
+        h.sw_w_off += ol, h.sreq_q_off += ol, h.mreq_q_off += ol;
+        h.tol_off += oo;
+        h.pr_beg += op, h.pr_end += op;
+        h.in_beg += on, h.in_end += on;
       }
-      for (Prog& p : q.progs) p.ins_off += bn;
+      for (Prog& p : q.progs) p.ins_off += on;
       for (Instr& x : q.instrs) {
-        if (x.op == OP_EXCLUDE || x.op == OP_NAMES) x.a += bi;
+        if (x.op == OP_EXCLUDE || x.op == OP_NAMES) x.a += oi;
         else if (x.op == OP_LBL_IN || x.op == OP_LBL_NOTIN || x.op == OP_FLD_IN || x.op == OP_FLD_NOTIN ||
                  x.op == OP_ZONE_IN || x.op == OP_ZONE_NOTIN)
-          x.b += bi;
+          x.b += oi;
       }
     }
-    bt->ipool.insert(bt->ipool.end(), q.ipool.begin(), q.ipool.end());
-    bt->lpool.insert(bt->lpool.end(), q.lpool.begin(), q.lpool.end());
-    bt->tols.insert(bt->tols.end(), q.tols.begin(), q.tols.end());
-    bt->progs.insert(bt->progs.end(), q.progs.begin(), q.progs.end());
-    bt->instrs.insert(bt->instrs.end(), q.instrs.begin(), q.instrs.end());
+    std::copy(q.ipool.begin(), q.ipool.end(), bt->ipool.begin() + (long)bi[t]);
+    std::copy(q.lpool.begin(), q.lpool.end(), bt->lpool.begin() + (long)bl[t]);
+    std::copy(q.tols.begin(), q.tols.end(), bt->tols.begin() + (long)bo[t]);
+    std::copy(q.progs.begin(), q.progs.end(), bt->progs.begin() + (long)bp[t]);
+    std::copy(q.instrs.begin(), q.instrs.end(), bt->instrs.begin() + (long)bn[t]);
     q = Pools();
+  };
+  if (T == 1) {
+    merge(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++) th.emplace_back(merge, t);
+    for (auto& x : th) x.join();
   }
   // global class ids (1-based; 0 = non-workload) and one representative per class
   std::unordered_map<std::string, int32_t> gid;
   bt->crep.assign(1, 0);
+  std::vector<std::vector<int32_t>> remaps(T);
   for (int t = 0; t < T; t++) {
-    std::vector<int32_t> remap(tkeys[t].size());
+    std::vector<int32_t>& remap = remaps[t];
+    remap.resize(tkeys[t].size());
     for (size_t j = 0; j < tkeys[t].size(); j++) {
       auto it = gid.emplace(tkeys[t][j], (int32_t)gid.size() + 1).first;
       remap[j] = it->second;
@@ -2291,10 +2308,26 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
         }
       }
     }
-    for (int i = lo[t]; i < lo[t + 1]; i++) {
-      const int32_t g = bt->bcls[i] < 0 ? 0 : remap[bt->bcls[i]];
-      bt->bcls[i] = g;
-      if (g && bt->crep[g] < 0) bt->crep[g] = i;
+  }
+  // each binding's global class id (per thread range, in parallel); a class's
+  // representative is its first binding
+  auto remap_range = [&](int t) {
+    const std::vector<int32_t>& remap = remaps[t];
+    for (int i = lo[t]; i < lo[t + 1]; i++) bt->bcls[i] = bt->bcls[i] < 0 ? 0 : remap[bt->bcls[i]];
+  };
+  if (T == 1) {
+    remap_range(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++) th.emplace_back(remap_range, t);
+    for (auto& x : th) x.join();
+  }
+  size_t left = bt->crep.size() - 1;  // first binding of each class, in binding order
+  for (int i = 0; i < n && left; i++) {
+    const int32_t g = bt->bcls[i];
+    if (g && bt->crep[g] < 0) {
+      bt->crep[g] = i;
+      left--;
     }
   }
   if (getenv("KP_PACK_TIMING")) {
