@@ -214,7 +214,8 @@ struct kp_engine {
   // k_select_top (kp_top.h): on, and its subset capacity per binding (LDS entries);
   // KP_TOP=0 / KP_TOP_CAP=<n> at engine creation (tests, tuning)
   bool top_on = true;
-  int top_cap = 512;
+  int top_cap = 1024;      // subset capacity of the large slice
+  int top_cap_small = 256;  // ... and of the small one (bindings needing <= kTopSmallNeed)
   // per-kernel timing of kp_schedule_batch (kp_engine_set_profile): an event pair
   // around every launch on its own stream, folded by kernel name after the batch
   struct KProf {
@@ -263,6 +264,7 @@ struct kp_batch {
   std::vector<Instr> instrs;
   std::vector<int32_t> l_all, l_cluster, l_region, l_slow, l_cs;  // l_cs: cluster + region bindings
   int n_all_dyn = 0;  // l_all = [other strategies | StaticWeight]: the first n_all_dyn are not StaticWeight
+  int n_top_small = 0;  // of those, the first n_top_small take k_select_top's small slice
   int n_static = 0;   // of the StaticWeight ones, the first n_static take k_select_static (static_ok)
   uint64_t out_cap = 0;
   Arena dev;
@@ -1809,7 +1811,10 @@ int kp_engine_create(int device, kp_engine** out) {
   for (auto& ev : e->ev) (void)dev::event_create(&ev);
   e->max_lds = dev::max_lds_per_block(device);
   if (const char* v = getenv("KP_TOP")) e->top_on = atoi(v) != 0;
-  if (const char* v = getenv("KP_TOP_CAP")) e->top_cap = std::max(64, std::min(1024, atoi(v) & ~63));
+  if (const char* v = getenv("KP_TOP_CAP")) {  // (tests: one capacity for both slices)
+    e->top_cap = std::max(64, std::min(1024, atoi(v) & ~63));
+    e->top_cap_small = std::min(e->top_cap_small, e->top_cap);
+  }
   unsigned hc = std::thread::hardware_concurrency();
   e->n_threads = (int)std::max(1u, std::min(16u, hc));
   *out = e;
@@ -2387,6 +2392,16 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
     for (int i = 0; i < bt->n_all_dyn; i++) out[(size_t)cnt[(size_t)std::max(0, bt->bcls[bt->l_all[i]])]++] = bt->l_all[i];
     std::copy(out.begin(), out.end(), bt->l_all.begin());
   }
+  // ... and split by the subset each is likely to need (k_select_top runs twice: a
+  // small LDS slice for the first n_top_small, a large one for the rest): a
+  // DynamicWeight / Aggregated subset holds the scheduled clusters and about as many
+  // walked parties as the target replicas
+  bt->n_top_small = (int)(std::stable_partition(bt->l_all.begin(), bt->l_all.begin() + bt->n_all_dyn,
+                                                [&](int32_t i) {
+                                                  const BindHdr& h = bt->hdr[i];
+                                                  return (int64_t)h.replicas + h.tgt_cnt <= kTopSmallNeed;
+                                                }) -
+                          bt->l_all.begin());
   // StaticWeight bindings the class-level kernel covers first (bits mode only)
   {
     const kp_snapshot* sn = bt->snap;
@@ -2796,8 +2811,12 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
                                bt->cls_rows, bt->fmask, bt->est));
   // SEL_ALL DynamicWeight / Aggregated over the deciding candidates (kp_top.h): the
   // class rows' orders first
+  // the large slice's capacity, lowered until the slices fit the device's LDS
+  int top_cap = e->top_cap;
+  while (top_cap > 64 && kTopWaves * ((top_lds_bytes(s->Cp, top_cap) + 15) & ~(size_t)15) > e->max_lds) top_cap /= 2;
+  const int top_cap_small = std::min(e->top_cap_small, top_cap);
   const bool top = bits && e->top_on && bt->d_ord != nullptr && bt->n_all_dyn > 0 &&
-                   kTopWaves * ((top_lds_bytes(s->Cp, e->top_cap) + 15) & ~(size_t)15) <= e->max_lds;
+                   kTopWaves * ((top_lds_bytes(s->Cp, top_cap) + 15) & ~(size_t)15) <= e->max_lds;
   // class orders: k_select_top's walk, and the spread selections over them
   // (k_spread_order, k_region_a_order), each where its LDS slices fit the device
   const bool spread_orders = bits && e->top_on && bt->d_ord != nullptr &&
@@ -2829,14 +2848,20 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     const bool stream_w = bits;
     const int na = stream_all ? 0 : (stream_w ? bt->n_all_dyn : k.n);
     if (top) {
-      // k_select_top over [0, n_all_dyn); the bindings it hands back (other strategies,
-      // subsets past capacity, ...) run with every candidate from its fallback list
-      KArgs g = k;
-      g.n = bt->n_all_dyn;
-      TopArgs ta{bt->d_ord, bt->d_ctot, bt->d_cok, bt->d_fb, bt->stats + 9, e->top_cap};
-      const size_t slice = (top_lds_bytes(s->Cp, e->top_cap) + 15) & ~(size_t)15;
+      // k_select_top over [0, n_all_dyn), small slices for [0, n_top_small); the
+      // bindings it hands back (other strategies, subsets past capacity, ...) run with
+      // every candidate from its fallback list
       HIPCHK(dev::event_record(e->ev[12], sp));
-      KPROF(sp, "k_select_top", g.n, -1, dev::select_top(sp, g, ta, slice));
+      for (int part = 0; part < 2; part++) {
+        KArgs g = k;
+        const int cap_p = part == 0 ? top_cap_small : top_cap;
+        g.list = bt->d_all + (part == 0 ? 0 : bt->n_top_small);
+        g.n = part == 0 ? bt->n_top_small : bt->n_all_dyn - bt->n_top_small;
+        if (g.n <= 0) continue;
+        TopArgs ta{bt->d_ord, bt->d_ctot, bt->d_cok, bt->d_fb, bt->stats + 9, cap_p};
+        const size_t slice = (top_lds_bytes(s->Cp, cap_p) + 15) & ~(size_t)15;
+        KPROF(sp, "k_select_top", g.n, -1, dev::select_top(sp, g, ta, slice));
+      }
       HIPCHK(dev::event_record(e->ev[13], sp));
       KArgs f = k;
       f.list = bt->d_fb;

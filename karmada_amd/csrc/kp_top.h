@@ -87,6 +87,8 @@ struct TopArgs {
 // Webster's party list / enumeration buffer of the subset path (u64 entries): larger
 // party sets take its uncompacted passes over the subset (exact, kp_select.h).
 constexpr int kTopEcap = 256;
+// bindings whose Replicas + len(spec.Clusters) is at most this take the small slice
+constexpr int64_t kTopSmallNeed = 160;
 KP_HD inline int top_ecap(int cap) { return cap < kTopEcap ? cap : kTopEcap; }
 // LDS slice of one binding: [red 64 B | frow W u64 | tgt bits | S ranks cap | S votes cap | SelScratch]
 KP_HD inline size_t top_lds_bytes(int Cp, int cap) {
@@ -216,6 +218,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
 #endif
     for (int q = 0; q < kTopAhead; q++) ring[q] = lane + q * ww < s.C ? ord[lane + q * ww] : 0;
     int64_t walked = 0, wsum = 0;
+    const int32_t n0 = n;  // the scheduled clusters lead the subset
     bool tie = false;
     int32_t tie_v = 0;
     // (Aggregated: the prior clusters alone may already reach the target; no walk)
@@ -270,6 +273,22 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
       const int32_t vmin = cnt > 0 ? B.wread(v, 63 - __builtin_clzll(m)) : 0;
       walked += cnt;
       wsum += add;
+      // DynamicWeight: the subset (scheduled clusters + every walked party) holds at
+      // least N seat priorities strictly above vmin, so the N-th largest priority t* is
+      // above vmin, and every unwalked party (vote <= vmin) has all its priorities below
+      // t*: no seat, no tie (#{k : v/(2k+1) > vmin} = ((v-1)/vmin + 1)/2 for v > vmin,
+      // integers; float64 priorities order the same way for votes below 2^31). The rule
+      // is pinned against the reference heap in tests/test_cpusim_units.py.
+      if (!agg && cnt > 0 && vmin > 0 && tsum + wsum >= (int64_t)target) {
+        B.wsync();  // this chunk's subset entries, written by their lanes, before the reads
+        int64_t above = 0;
+        for (int q = lane; q < n; q += ww) {
+          int64_t vq = cd.v[q];
+          if (q < n0 && fresh) vq += sched_rep_of(x, cd.r[q]);
+          above += vq > vmin ? ((vq - 1) / vmin + 1) / 2 : 0;
+        }
+        if (B.sum64(above) >= (int64_t)target) break;  // (wave-uniform)
+      }
       // covered: the subset's votes reach the target (the availability check passes on
       // every candidate too) and the walked ones decide the division: the N-th largest
       // party vote (DynamicWeight) or the cut value (Aggregated) is >= vmin

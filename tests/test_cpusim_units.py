@@ -186,3 +186,73 @@ def test_select_groups_device_form_matches_oracle(seed):
             assert [out[i] for i in range(got)] == want, (vals, wts, min_c, max_c, target)
         else:
             assert got == want, (vals, wts, min_c, max_c, target, got)
+
+
+# ---- k_select_top's DynamicWeight stop rule (kp_top.h), pinned against the reference heap ----
+def oracle_webster_named(votes, names, N, desc):
+    """AllocateWebsterSeats over parties named c<index> (the tie order), the faithful heap."""
+    L = O.lib()
+    w = api.World()
+    n = len(votes)
+    arr, _ = w.arr(api.kp_str, [w.s(f"c{i:06d}") for i in names])
+    vv = (C.c_int64 * max(1, n))(*votes)
+    out = (C.c_int32 * max(1, n))()
+    assert L.kpo_allocate_webster(N, arr, vv, n, None, None, 0, 2 if desc else 1, api.kp_str(None, 0), out, n) == n
+    return dict(zip(names, (out[i] for i in range(n))))
+
+
+def seats_above(v, vmin):
+    """#{k >= 0 : v / (2k+1) > vmin} for integers v, vmin > 0 (exact; for v < 2^31 the
+    float64 priority compares the same way, its distance to vmin being > 2^-31 relative)."""
+    return ((v - 1) // vmin + 1) // 2 if v > vmin else 0
+
+
+def top_stop_subset(votes, N, chunk=64):
+    """The walk of k_select_top for a DynamicWeight binding with no scheduled clusters:
+    parties in (votes desc, name asc) order, 64 per step; it stops once the walked votes
+    cover N and the walked parties hold >= N seat priorities strictly above the
+    smallest walked vote vmin (then t* > vmin >= every unwalked priority)."""
+    order = sorted(range(len(votes)), key=lambda i: (-votes[i], i))
+    for end in range(chunk, len(order) + chunk, chunk):
+        sub = order[:end]
+        vmin = votes[sub[-1]]
+        if vmin > 0 and sum(votes[i] for i in sub) >= N and sum(seats_above(votes[i], vmin) for i in sub) >= N:
+            return sub
+    return order
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_top_dynamic_stop_rule_vs_heap(seed):
+    """Adversarial vote sets: votes at odd multiples of vmin (+-1), ties at vmin spanning
+    the chunk and the stop, a few huge votes over many small ones, N at the count
+    boundary. Webster over the stopped subset gives every party of the full set its
+    seats, and every party left out gets none."""
+    rng = random.Random(500 + seed)
+    for _ in range(40):
+        kind = rng.choice(["odd_multiples", "ties", "heavy_head", "uniform", "boundary"])
+        n = rng.choice([65, 130, 300, 700, 2000])
+        if kind == "odd_multiples":
+            base = rng.randint(1, 50)
+            votes = [(2 * rng.randint(0, 20) + 1) * base + rng.choice([-1, 0, 1]) for _ in range(n)]
+        elif kind == "ties":
+            votes = [rng.choice([7, 21, 35, 63]) for _ in range(n)]
+        elif kind == "heavy_head":
+            votes = [rng.randint(10**6, 10**7) for _ in range(5)] + [rng.randint(1, 30) for _ in range(n - 5)]
+        elif kind == "uniform":
+            votes = [rng.randint(0, 1000) for _ in range(n)]
+        else:
+            base = rng.randint(2, 9)
+            votes = [base * rng.choice([1, 3, 5, 9]) for _ in range(n)]
+        votes = [max(0, v) for v in votes]
+        tot = sum(votes)
+        if tot == 0:
+            continue
+        N = min(rng.choice([1, 5, 64, 200, 1000, 5000, tot]), tot, 20000)
+        desc = rng.random() < 0.5
+        full = oracle_webster_named(votes, list(range(n)), N, desc)
+        sub = top_stop_subset(votes, N)
+        sub = sorted(sub)  # (the parties in name order, as oracle_webster passes them)
+        part = oracle_webster_named([votes[i] for i in sub], sub, N, desc)
+        assert all(full[i] == part[i] for i in sub), (kind, n, N)
+        left = set(range(n)) - set(sub)
+        assert all(full[i] == 0 for i in left), (kind, n, N)
