@@ -2345,6 +2345,15 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
   return true;
 }
 
+// Bindings per estimator class below which a batch skips the class orders.
+static int64_t order_amort() {
+  static const int64_t v = [] {
+    const char* e = getenv("KP_ORDER_AMORT");
+    return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)4;
+  }();
+  return v;
+}
+
 int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindings, uint64_t n, kp_batch** out) {
   if (!e || !sc || !out || (n && !bindings)) return KP_EINVAL;
   if (n > (uint64_t)INT32_MAX) return KP_ENOTSUP;
@@ -2522,7 +2531,11 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   // k_select_top (bits mode): class orders, fallback list. k_class_order sorts a class
   // row in LDS (kRedBytes + 8 * nextpow2(C)): a device with less LDS per workgroup
   // keeps the full-candidate kernels instead of failing the launch.
-  if (s->C <= 16384 && !bt->crep.empty() && kRedBytes + 8 * (size_t)P <= e->max_lds) {
+  // Class orders pay off when each order serves several bindings: a batch of nearly
+  // one class per binding (per-binding requests) sorts a Cp row per binding instead,
+  // so it keeps the full-candidate kernels (KP_ORDER_AMORT: bindings per class needed)
+  const bool orders_pay = (int64_t)bt->crep.size() * order_amort() <= (int64_t)B;
+  if (s->C <= 16384 && !bt->crep.empty() && orders_pay && kRedBytes + 8 * (size_t)P <= e->max_lds) {
     a.add(&bt->d_ord, bt->crep.size() * (size_t)s->Cp);
     a.add(&bt->d_ctot, bt->crep.size());
     a.add(&bt->d_cok, bt->crep.size());

@@ -21,6 +21,9 @@
 //      GetSumOfReplicas, dynamicDivideReplicas and the Aggregated prefix wrap
 //      (SURVEY hazard H5), StaticWeight weights >= 2^31, spec.Clusters replicas
 //      near 2^31 and seat counts up to MaxInt32; parity only.
+//  10  "distinct": config 3 with every binding's requests drawn independently (cpu
+//      milli uniform over [100, 4000], memory MiB over [128, 16384]), so nearly every
+//      binding is its own estimator class; performance only.
 //   9  "templates": multi-template workloads (spec.Components) for the
 //      MultiplePodTemplatesScheduling gate: most carry a cluster spread constraint
 //      with MinGroups = MaxGroups = 1 (isMultiTemplateSchedulingApplicable), over
@@ -144,7 +147,7 @@ void gvk(int g, std::string* gv, std::string* kind) {
 
 void gen_cluster(kps_world& w, uint32_t i, kp_cluster& c) {
   Rng r(key(w.seed, 1, i));
-  const int cfg = w.config;
+  const int cfg = w.config == 10 ? 3 : w.config;  // config 10: config-3 clusters
   c.name = w.s(w.cname(i));
   // labels: 8 distinct keys of 16
   c.labels = w.a.alloc<kp_label>(8);
@@ -302,6 +305,8 @@ void gen_binding(kps_world& w, uint64_t i, kp_binding& b) {
   Rng r(key(w.seed, 2, i));
   int cfg = w.config;
   if (cfg == 5) cfg = 2 + (int)(i % 3);
+  const bool distinct = cfg == 10;  // config 10: config 3 with per-binding requests
+  if (distinct) cfg = 3;
   const uint32_t C = w.C;
   char ub[40];
   snprintf(ub, sizeof ub, "%08x-%04x-4%03x-%04x-%012llx", (unsigned)r.next(), (unsigned)(r.next() & 0xffff),
@@ -321,8 +326,16 @@ void gen_binding(kps_world& w, uint64_t i, kp_binding& b) {
   b.has_replica_requirements = 1;
   int nreq = (cfg == 3 && r.p(0.1)) ? 3 : 2;
   kp_resource* rq = w.a.alloc<kp_resource>(nreq);
-  rq[0] = {w.s("cpu"), w.s(kCpu[r.below(6)])};
-  rq[1] = {w.s("memory"), w.s(kMem[r.below(7)])};
+  if (distinct) {  // cpu milli uniform over [100, 4000], memory MiB uniform over [128, 16384]
+    char cb[24], mb[24];
+    snprintf(cb, sizeof cb, "%dm", (int)r.range(100, 4000));
+    snprintf(mb, sizeof mb, "%dMi", (int)r.range(128, 16384));
+    rq[0] = {w.s("cpu"), w.s(cb)};
+    rq[1] = {w.s("memory"), w.s(mb)};
+  } else {
+    rq[0] = {w.s("cpu"), w.s(kCpu[r.below(6)])};
+    rq[1] = {w.s("memory"), w.s(kMem[r.below(7)])};
+  }
   if (nreq == 3) rq[2] = {w.s("nvidia.com/gpu"), w.s("1")};
   b.resource_request = rq;
   b.n_resource_request = nreq;
