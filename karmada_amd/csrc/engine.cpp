@@ -191,6 +191,28 @@ struct Arena {
 
 }  // namespace
 
+// std::allocator that leaves trivial elements uninitialized on resize: the packer
+// writes every BindHdr itself (in parallel, so the pages are first touched there),
+// and a value-initializing resize would zero 160 B per binding on one thread.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new ((void*)p) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+};
+
 // ============================================================================
 // Engine / snapshot / batch objects
 // ============================================================================
@@ -256,7 +278,7 @@ struct kp_snapshot {
 struct kp_batch {
   kp_snapshot* snap = nullptr;
   int B = 0;
-  std::vector<BindHdr> hdr;
+  std::vector<BindHdr, NoInitAlloc<BindHdr>> hdr;
   std::vector<int32_t> ipool;
   std::vector<int64_t> lpool;
   std::vector<Tol> tols;
@@ -2169,14 +2191,20 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
   int T = host_cpus();
   if (const char* v = getenv("KP_PACK_THREADS")) T = atoi(v);
   T = std::max(1, std::min(T, n / 4096));
-  std::vector<Pools> pl(T);
-  std::vector<int> lo(T + 1);
-  for (int t = 0; t <= T; t++) lo[t] = (int)((int64_t)n * t / T);
+  // Chunks of kPackChunk bindings taken from a shared counter (a thread that meets heavy
+  // bindings takes fewer chunks); each chunk packs into its own pools, concatenated in
+  // chunk order below. Packer caches and class-id maps are per thread.
+  constexpr int kPackChunk = 1024;
+  const int K = std::max(1, (n + kPackChunk - 1) / kPackChunk);
+  std::vector<Pools> pl(K);
+  std::vector<int> lo(K + 1), owner(K, 0);
+  for (int k = 0; k <= K; k++) lo[k] = std::min(n, k * kPackChunk);
   // estimator classes: thread-local ids (bt->bcls) and keys, unified below
-  bt->bcls.assign(n, 0);
+  bt->bcls.resize(n);
   std::vector<std::vector<std::string>> tkeys(T);
   std::vector<std::string> terr(T);
   std::vector<double> tms(T, 0.0);
+  std::atomic<int> next_chunk(0);
   auto run = [&](int t) {
     const auto tt0 = std::chrono::steady_clock::now();
     struct Stamp {
@@ -2184,115 +2212,85 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       double* out;
       ~Stamp() { *out = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
     } stamp{tt0, &tms[t]};
-    Packer pk{s, &pl[t]};
+    Packer pk{s, nullptr};
     std::unordered_map<std::string, int32_t> ids;
     std::string key;
     SetsArgs A;
-    for (int i = lo[t]; i < lo[t + 1]; i++) {
-      pk.pack(bindings[i], bt->hdr[i]);
-      if (bt->hdr[i].flags & BF_NONWORKLOAD_EST) {
-        bt->bcls[i] = -1;
-        continue;
-      }
-      if (bt->hdr[i].flags & BF_SETS) {
-        // a component-set class: key 'S' + the resolved SetsArgs (est_key's keys
-        // start with the 0/1 ReplicaRequirements word, never 'S')
-        std::string err;
-        const int rc = build_sets_args(s, bindings[i].components, bindings[i].n_components, &A, &err);
-        if (rc == KP_EINVAL) {
-          bt->hdr[i].flags = (bt->hdr[i].flags & ~(uint32_t)BF_SETS) | BF_BAD;  // status ERROR, as a bad request
-        } else if (rc != KP_OK) {
-          if (terr[t].empty()) terr[t] = err;
-          bt->hdr[i].flags &= ~(uint32_t)BF_SETS;
+    for (;;) {
+      const int k = next_chunk.fetch_add(1);
+      if (k >= K) break;
+      owner[k] = t;
+      pk.bt = &pl[k];
+      for (int i = lo[k]; i < lo[k + 1]; i++) {
+        pk.pack(bindings[i], bt->hdr[i]);
+        if (bt->hdr[i].flags & BF_NONWORKLOAD_EST) {
+          bt->bcls[i] = -1;
+          continue;
         }
+        if (bt->hdr[i].flags & BF_SETS) {
+          // a component-set class: key 'S' + the resolved SetsArgs (est_key's keys
+          // start with the 0/1 ReplicaRequirements word, never 'S')
+          std::string err;
+          const int rc = build_sets_args(s, bindings[i].components, bindings[i].n_components, &A, &err);
+          if (rc == KP_EINVAL) {
+            bt->hdr[i].flags = (bt->hdr[i].flags & ~(uint32_t)BF_SETS) | BF_BAD;  // status ERROR, as a bad request
+          } else if (rc != KP_OK) {
+            if (terr[t].empty()) terr[t] = err;
+            bt->hdr[i].flags &= ~(uint32_t)BF_SETS;
+          }
+        }
+        if (bt->hdr[i].flags & BF_SETS) {
+          key.assign(1, 'S');
+          key.append((const char*)&A, sizeof(A));
+        } else {
+          est_key(bt->hdr[i], pl[k], &key);
+        }
+        auto it = ids.find(key);
+        if (it == ids.end()) {
+          it = ids.emplace(key, (int32_t)tkeys[t].size()).first;
+          tkeys[t].push_back(key);
+        }
+        bt->bcls[i] = it->second;
       }
-      if (bt->hdr[i].flags & BF_SETS) {
-        key.assign(1, 'S');
-        key.append((const char*)&A, sizeof(A));
-      } else {
-        est_key(bt->hdr[i], pl[t], &key);
-      }
-      auto it = ids.find(key);
-      if (it == ids.end()) {
-        it = ids.emplace(key, (int32_t)tkeys[t].size()).first;
-        tkeys[t].push_back(key);
-      }
-      bt->bcls[i] = it->second;
     }
   };
-  const auto tq0 = std::chrono::steady_clock::now();
-  if (T == 1) {
-    run(0);
-  } else {
+  auto on_threads = [&](auto fn) {
+    if (T == 1) {
+      fn(0);
+      return;
+    }
     std::vector<std::thread> th;
-    for (int t = 0; t < T; t++) th.emplace_back(run, t);
+    for (int t = 0; t < T; t++) th.emplace_back(fn, t);
     for (auto& x : th) x.join();
-  }
+  };
+  const auto tq0 = std::chrono::steady_clock::now();
+  on_threads(run);
   const auto tq1 = std::chrono::steady_clock::now();
   for (auto& x : terr)
     if (!x.empty()) {
       bt->err = x;
       return false;
     }
-  // pools concatenated in thread order: each thread's bases are the prefix sums of
-  // the pool sizes before it; every thread rebases its own headers and instructions
-  // and copies its pools into place, in parallel
-  std::vector<size_t> bi(T + 1, 0), bl(T + 1, 0), bo(T + 1, 0), bp(T + 1, 0), bn(T + 1, 0);
-  for (int t = 0; t < T; t++) {
-    bi[t + 1] = bi[t] + pl[t].ipool.size();
-    bl[t + 1] = bl[t] + pl[t].lpool.size();
-    bo[t + 1] = bo[t] + pl[t].tols.size();
-    bp[t + 1] = bp[t] + pl[t].progs.size();
-    bn[t + 1] = bn[t] + pl[t].instrs.size();
+  // pools concatenated in chunk order: each chunk's bases are the prefix sums of the
+  // pool sizes before it; the threads rebase the chunks' headers and instructions
+  // and copy their pools into place, chunk by chunk from a shared counter
+  std::vector<size_t> bi(K + 1, 0), bl(K + 1, 0), bo(K + 1, 0), bp(K + 1, 0), bn(K + 1, 0);
+  for (int k = 0; k < K; k++) {
+    bi[k + 1] = bi[k] + pl[k].ipool.size();
+    bl[k + 1] = bl[k] + pl[k].lpool.size();
+    bo[k + 1] = bo[k] + pl[k].tols.size();
+    bp[k + 1] = bp[k] + pl[k].progs.size();
+    bn[k + 1] = bn[k] + pl[k].instrs.size();
   }
-  if (bi[T] > (size_t)INT32_MAX || bl[T] > (size_t)INT32_MAX || bo[T] > (size_t)INT32_MAX ||
-      bp[T] > (size_t)INT32_MAX || bn[T] > (size_t)INT32_MAX)
+  if (bi[K] > (size_t)INT32_MAX || bl[K] > (size_t)INT32_MAX || bo[K] > (size_t)INT32_MAX ||
+      bp[K] > (size_t)INT32_MAX || bn[K] > (size_t)INT32_MAX)
     return false;  // pool offsets are int32
-  bt->ipool.resize(bi[T]);
-  bt->lpool.resize(bl[T]);
-  bt->tols.resize(bo[T]);
-  bt->progs.resize(bp[T]);
-  bt->instrs.resize(bn[T]);
-  auto merge = [&](int t) {
-    Pools& q = pl[t];
-    const int32_t oi = (int32_t)bi[t], ol = (int32_t)bl[t], oo = (int32_t)bo[t], op = (int32_t)bp[t],
-                  on = (int32_t)bn[t];
-    if (t > 0) {
-      for (int i = lo[t]; i < lo[t + 1]; i++) {
-        BindHdr& h = bt->hdr[i];
-        for (int j = 0; j < h.filt_cnt; j++) q.ipool[h.filt_off + j] += op;
-        for (int j = 0; j < h.ovf_cnt; j++) q.ipool[h.ovf_off + j] += op;
-        for (int j = 0; j < h.sw_cnt; j++) q.ipool[h.sw_off + j] += op;
-        h.tgt_off += oi, h.evict_off += oi, h.filt_off += oi, h.ovf_off += oi, h.sw_off += oi;
-        h.sreq_off += oi, h.mreq_off += oi, h.ip_beg += oi, h.ip_end += oi;
-        h.sw_w_off += ol, h.sreq_q_off += ol, h.mreq_q_off += ol;
-        h.tol_off += oo;
-        h.pr_beg += op, h.pr_end += op;
-        h.in_beg += on, h.in_end += on;
-      }
-      for (Prog& p : q.progs) p.ins_off += on;
-      for (Instr& x : q.instrs) {
-        if (x.op == OP_EXCLUDE || x.op == OP_NAMES) x.a += oi;
-        else if (x.op == OP_LBL_IN || x.op == OP_LBL_NOTIN || x.op == OP_FLD_IN || x.op == OP_FLD_NOTIN ||
-                 x.op == OP_ZONE_IN || x.op == OP_ZONE_NOTIN)
-          x.b += oi;
-      }
-    }
-    std::copy(q.ipool.begin(), q.ipool.end(), bt->ipool.begin() + (long)bi[t]);
-    std::copy(q.lpool.begin(), q.lpool.end(), bt->lpool.begin() + (long)bl[t]);
-    std::copy(q.tols.begin(), q.tols.end(), bt->tols.begin() + (long)bo[t]);
-    std::copy(q.progs.begin(), q.progs.end(), bt->progs.begin() + (long)bp[t]);
-    std::copy(q.instrs.begin(), q.instrs.end(), bt->instrs.begin() + (long)bn[t]);
-    q = Pools();
-  };
-  if (T == 1) {
-    merge(0);
-  } else {
-    std::vector<std::thread> th;
-    for (int t = 0; t < T; t++) th.emplace_back(merge, t);
-    for (auto& x : th) x.join();
-  }
-  // global class ids (1-based; 0 = non-workload) and one representative per class
+  bt->ipool.resize(bi[K]);
+  bt->lpool.resize(bl[K]);
+  bt->tols.resize(bo[K]);
+  bt->progs.resize(bp[K]);
+  bt->instrs.resize(bn[K]);
+  // global class ids (1-based; 0 = non-workload): the threads' keys in thread order
   std::unordered_map<std::string, int32_t> gid;
   bt->crep.assign(1, 0);
   std::vector<std::vector<int32_t>> remaps(T);
@@ -2304,30 +2302,59 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       remap[j] = it->second;
       if ((size_t)it->second == bt->crep.size()) {
         bt->crep.push_back(-1);
-        const std::string& k = tkeys[t][j];
-        if (!k.empty() && k[0] == 'S') {  // component-set class: its rows come from k_sets_rows
+        const std::string& key = tkeys[t][j];
+        if (!key.empty() && key[0] == 'S') {  // component-set class: its rows come from k_sets_rows
           SetsArgs A;
-          memcpy(&A, k.data() + 1, sizeof(A));
+          memcpy(&A, key.data() + 1, sizeof(A));
           bt->sets_cls.push_back(it->second);
           bt->sets_args.push_back(A);
         }
       }
     }
   }
-  // each binding's global class id (per thread range, in parallel); a class's
-  // representative is its first binding
-  auto remap_range = [&](int t) {
-    const std::vector<int32_t>& remap = remaps[t];
-    for (int i = lo[t]; i < lo[t + 1]; i++) bt->bcls[i] = bt->bcls[i] < 0 ? 0 : remap[bt->bcls[i]];
+  std::atomic<int> next_merge(0);
+  auto merge = [&](int) {
+    for (;;) {
+      const int k = next_merge.fetch_add(1);
+      if (k >= K) break;
+      Pools& q = pl[k];
+      const int32_t oi = (int32_t)bi[k], ol = (int32_t)bl[k], oo = (int32_t)bo[k], op = (int32_t)bp[k],
+                    on = (int32_t)bn[k];
+      const std::vector<int32_t>& remap = remaps[owner[k]];
+      for (int i = lo[k]; i < lo[k + 1]; i++) {
+        BindHdr& h = bt->hdr[i];
+        bt->bcls[i] = bt->bcls[i] < 0 ? 0 : remap[bt->bcls[i]];
+        if (k == 0) continue;
+        for (int j = 0; j < h.filt_cnt; j++) q.ipool[h.filt_off + j] += op;
+        for (int j = 0; j < h.ovf_cnt; j++) q.ipool[h.ovf_off + j] += op;
+        for (int j = 0; j < h.sw_cnt; j++) q.ipool[h.sw_off + j] += op;
+        h.tgt_off += oi, h.evict_off += oi, h.filt_off += oi, h.ovf_off += oi, h.sw_off += oi;
+        h.sreq_off += oi, h.mreq_off += oi, h.ip_beg += oi, h.ip_end += oi;
+        h.sw_w_off += ol, h.sreq_q_off += ol, h.mreq_q_off += ol;
+        h.tol_off += oo;
+        h.pr_beg += op, h.pr_end += op;
+        h.in_beg += on, h.in_end += on;
+      }
+      if (k > 0) {
+        for (Prog& p : q.progs) p.ins_off += on;
+        for (Instr& x : q.instrs) {
+          if (x.op == OP_EXCLUDE || x.op == OP_NAMES) x.a += oi;
+          else if (x.op == OP_LBL_IN || x.op == OP_LBL_NOTIN || x.op == OP_FLD_IN || x.op == OP_FLD_NOTIN ||
+                   x.op == OP_ZONE_IN || x.op == OP_ZONE_NOTIN)
+            x.b += oi;
+        }
+      }
+      std::copy(q.ipool.begin(), q.ipool.end(), bt->ipool.begin() + (long)bi[k]);
+      std::copy(q.lpool.begin(), q.lpool.end(), bt->lpool.begin() + (long)bl[k]);
+      std::copy(q.tols.begin(), q.tols.end(), bt->tols.begin() + (long)bo[k]);
+      std::copy(q.progs.begin(), q.progs.end(), bt->progs.begin() + (long)bp[k]);
+      std::copy(q.instrs.begin(), q.instrs.end(), bt->instrs.begin() + (long)bn[k]);
+      q = Pools();
+    }
   };
-  if (T == 1) {
-    remap_range(0);
-  } else {
-    std::vector<std::thread> th;
-    for (int t = 0; t < T; t++) th.emplace_back(remap_range, t);
-    for (auto& x : th) x.join();
-  }
-  size_t left = bt->crep.size() - 1;  // first binding of each class, in binding order
+  on_threads(merge);
+  // a class's representative: its first binding
+  size_t left = bt->crep.size() - 1;
   for (int i = 0; i < n && left; i++) {
     const int32_t g = bt->bcls[i];
     if (g && bt->crep[g] < 0) {
@@ -2337,8 +2364,8 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
   }
   if (getenv("KP_PACK_TIMING")) {
     auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
-    fprintf(stderr, "pack_parallel: %d threads, pack %.1f ms, merge+classes %.1f ms; per thread", T, ms(tq0, tq1),
-            ms(tq1, std::chrono::steady_clock::now()));
+    fprintf(stderr, "pack_parallel: %d threads, %d chunks, pack %.1f ms, merge+classes %.1f ms; per thread", T, K,
+            ms(tq0, tq1), ms(tq1, std::chrono::steady_clock::now()));
     for (double x : tms) fprintf(stderr, " %.1f", x);
     fprintf(stderr, "\n");
   }
