@@ -2957,6 +2957,17 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
           dev::select(s3, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sx));
     HIPCHK(dev::event_record(e->ev[15], s3));
   }
+  // k_slow after every kernel that flags bindings (SEL_ALL on stream2, cluster spread
+  // here; the region chain flags none), so it runs beside the region chain
+  HIPCHK(dev::stream_wait(s3, e->ev[8]));
+  if (!bt->l_slow.empty()) {
+    KArgs k = ka;
+    k.list = bt->d_slowlist;
+    k.n = (int)bt->l_slow.size();
+    KPROF(s3, "k_slow", 0, 0, dev::select(s3, SEL_LAUNCH_SLOW, k, kRedBytes + 512 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area +
+                                                      sx.lds_sort,
+                       bt->slow_cap, sx));
+  }
   HIPCHK(dev::event_record(e->ev[9], s3));
   double th0 = 0, th1 = 0;
   if (!bt->l_region.empty()) {
@@ -3047,16 +3058,8 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     KPROF(st, sel_name(SEL_LAUNCH_REGION_B, smem_region_b(s, cap)), k.n_dev ? 0 : k.n, k.n_dev ? 13 : -1,
           dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sx));
   }
-  HIPCHK(dev::stream_wait(st, e->ev[8]));  // every fast-path flag precedes k_slow
-  HIPCHK(dev::stream_wait(st, e->ev[9]));
-  if (!bt->l_slow.empty()) {
-    KArgs k = ka;
-    k.list = bt->d_slowlist;
-    k.n = (int)bt->l_slow.size();
-    KPROF(st, "k_slow", 0, 0, dev::select(st, SEL_LAUNCH_SLOW, k, kRedBytes + 512 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area +
-                                                      sx.lds_sort,
-                       bt->slow_cap, sx));
-  }
+  HIPCHK(dev::stream_wait(st, e->ev[8]));
+  HIPCHK(dev::stream_wait(st, e->ev[9]));  // k_slow (stream3) and every select kernel precede the results
   HIPCHK(dev::event_record(e->ev[2], st));
   // results -> host, compacted to CSR: offsets scanned and results compacted on
   // the device, then the per-binding arrays and the CSR copied back

@@ -944,24 +944,38 @@ KP_HD int pdq_choose_pivot(const D& d, int a, int b, int* hint) {
 }
 // The loop state (wasBalanced, wasPartitioned) is a parameter so that a
 // segment handed over mid-loop (pdq_wave) resumes exactly where Go would.
+//
+// Go recurses into the smaller side and loops on the larger one. Here the larger
+// side's continuation goes on an explicit stack and the loop descends into the
+// smaller side, so the depth stays <= log2(n) + 1 and, above all, the function does
+// not recurse: a recursive device function gives its kernel a dynamic call stack the
+// runtime does not size, and k_slow's thread 0 (the serial emulation) overran its
+// stack into the next wave's scratch, corrupting threads 64-65's spilled state
+// (round 4: config 8 seed 6). Disjoint segments are independent (the
+// only read outside a segment, a[-1] in partitionEqual, is a placed pivot), so the
+// order in which they are finished does not change the permutation.
+struct PdqTaskGo {
+  int a, b, limit;
+  bool wasBalanced, wasPartitioned;
+};
+constexpr int kPdqGoStack = 40;  // > log2(2^31) + 1 pending continuations
 template <class D>
 KP_HD void pdqsort_go(const D& d, int a, int b, int limit, bool wasBalanced = true, bool wasPartitioned = true) {
+  PdqTaskGo st[kPdqGoStack];
+  int sp = 0;
   for (;;) {
     int length = b - a;
-    if (length <= 12) {
-      pdq_insertion(d, a, b);
-      return;
+    bool done = length <= 12 || limit == 0;  // (Go: return from this segment)
+    if (done) {
+      if (length <= 12) pdq_insertion(d, a, b);
+      else pdq_heapsort(d, a, b);
     }
-    if (limit == 0) {
-      pdq_heapsort(d, a, b);
-      return;
-    }
-    if (!wasBalanced) {
+    if (!done && !wasBalanced) {
       pdq_break_patterns(d, a, b);
       limit--;
     }
-    int hint;
-    int pivot = pdq_choose_pivot(d, a, b, &hint);
+    int hint = 0, pivot = 0;
+    if (!done) pivot = pdq_choose_pivot(d, a, b, &hint);
     if (hint == 2) {
       int i = a, j = b - 1;
       while (i < j) {
@@ -972,7 +986,7 @@ KP_HD void pdqsort_go(const D& d, int a, int b, int limit, bool wasBalanced = tr
       pivot = (b - 1) - (pivot - a);
       hint = 1;
     }
-    if (wasBalanced && wasPartitioned && hint == 1) {  // partialInsertionSort
+    if (!done && wasBalanced && wasPartitioned && hint == 1) {  // partialInsertionSort
       int i = a + 1;
       bool sorted = false;
       for (int step = 0; step < 5; step++) {
@@ -996,7 +1010,13 @@ KP_HD void pdqsort_go(const D& d, int a, int b, int limit, bool wasBalanced = tr
           }
         }
       }
-      if (sorted) return;
+      done = sorted;
+    }
+    if (done) {  // the segment is sorted: resume the innermost pending continuation
+      if (sp == 0) return;
+      const PdqTaskGo& t = st[--sp];
+      a = t.a, b = t.b, limit = t.limit, wasBalanced = t.wasBalanced, wasPartitioned = t.wasPartitioned;
+      continue;
     }
     if (a > 0 && !d.Less(a - 1, pivot)) {  // partitionEqual
       d.Swap(a, pivot);
@@ -1041,15 +1061,18 @@ KP_HD void pdqsort_go(const D& d, int a, int b, int limit, bool wasBalanced = tr
     wasPartitioned = already;
     int leftLen = mid - a, rightLen = b - mid;
     int balanceThreshold = length / 8;
+    // Go: recurse into the smaller side with fresh state, then loop on the larger one
     if (leftLen < rightLen) {
       wasBalanced = leftLen >= balanceThreshold;
-      pdqsort_go(d, a, mid, limit);
-      a = mid + 1;
+      if (sp < kPdqGoStack) st[sp++] = PdqTaskGo{mid + 1, b, limit, wasBalanced, wasPartitioned};
+      b = mid;
     } else {
       wasBalanced = rightLen >= balanceThreshold;
-      pdqsort_go(d, mid + 1, b, limit);
-      b = mid;
+      if (sp < kPdqGoStack) st[sp++] = PdqTaskGo{a, mid, limit, wasBalanced, wasPartitioned};
+      a = mid + 1;
     }
+    wasBalanced = true;  // the smaller side starts as Go's recursive call does
+    wasPartitioned = true;
   }
 }
 KP_HD inline void sort_tcl(uint32_t* name, int32_t* rep, int n) {

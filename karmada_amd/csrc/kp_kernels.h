@@ -1279,8 +1279,10 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
       done = 1;
     }
     if (B.bcast(done)) continue;
+    KP_STAMP(x, 49);
     cd.F = gather(B, x, cd, false);
     const int F = cd.F;
+    KP_STAMP(x, 50);
 #ifdef KP_SLOW_CHECK
     // diagnostic build: the gathered candidates against the feasibility row (count,
     // rank sum and xor). dbg[0] += threads whose F differs, dbg[1] += bindings whose
@@ -1346,13 +1348,17 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
 #endif
     KP_STAMP(x, 6);
     SerialScratch sc = serial_scratch_carve(ser, scratch_cap);
-    if (pdq_lds && presort_dynamic(B, x, items, F, sarea, pos, sc) && why == SLOW_TIE && tie_lds) {
+    const bool pre = pdq_lds && presort_dynamic(B, x, items, F, sarea, pos, sc);
+    KP_STAMP(x, 51);
+    if (pre && why == SLOW_TIE && tie_lds) {
       // The Aggregated tie group straddled the cut: with sort.Sort's output
       // order known, the block-parallel path decides it exactly.
       for (int i = B.tid(); i < F; i += B.nth()) pos[sc.an[i]] = i;
       B.sync();
       const SelScratch ss = carve_sel_scratch(sarea, a.s.Cp);
       const int w2 = sel_all_fast(B, x, PosCands{&cd, pos, B.tid(), B.nth()}, ss);
+      KP_STAMP(x, 52);
+      KP_COUNT(x, 53, F);
       B.sync();  // every thread's last read of pos (emit) precedes the reset
       for (int i = B.tid(); i < F; i += B.nth()) pos[sc.an[i]] = -1;
       B.sync();

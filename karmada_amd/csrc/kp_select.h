@@ -774,6 +774,67 @@ KP_FI uint64_t rank_select(const BLK& B, const uint64_t* keys, int E, int64_t k,
 struct WebPre {
   int64_t V, vmax, P;
 };
+// webster_par's last steps from t*: the seats strictly above t*, then the tie group
+// at t* ordered by (seats asc, name) as the heap's tie-breaker orders it.
+constexpr int kWebFirstMax = 128;  // compacted lists rank-selected for the first-seat case
+template <class BLK, class Parties>
+KP_FI WebRes webster_tail(const BLK& B, WebRes r, Parties parties, double tstar, int32_t N, bool desc,
+                          const SelScratch& sc, int ecap, bool compact, int32_t np, int64_t Lb, uint64_t* pl) {
+  r.t = tstar;
+  r.rt = 1.0 / tstar;
+  r.compact = compact;
+  r.np = np;
+  r.Lb = Lb;
+  r.pl = pl;
+  KP_STAMP_INIT
+  KP_STAMPD(sc.dbg, 12);
+  // seats strictly above t*, then the tie group at t* ordered by (k asc, name)
+  int64_t S = 0, T = 0;
+  const double rts = 1.0 / tstar;
+  parties([&](uint32_t, int64_t v) {
+    int64_t base = w_count_r(v, tstar, rts, (int64_t)N + 1, false);
+    S += base;
+    if (w_prio(v, base) == tstar) T++;
+  });
+  B.sum2(S, T);
+  const int64_t M = (int64_t)N - S;
+  KP_STAMPD(sc.dbg, 13);
+  if (M >= T) {
+    r.tie = ~0ull;
+  } else if (T <= (int64_t)ecap) {
+    int32_t mine = 0;
+    parties([&](uint32_t, int64_t v) {
+      int64_t base = w_count_r(v, tstar, rts, (int64_t)N + 1, false);
+      if (w_prio(v, base) == tstar) mine++;
+    });
+    int32_t n;
+    int32_t pos = B.excl_scan(mine, &n);
+    parties([&](uint32_t rk, int64_t v) {
+      int64_t base = w_count_r(v, tstar, rts, (int64_t)N + 1, false);
+      if (w_prio(v, base) == tstar) sc.buf[pos++] = tie_key(base, rk, desc);
+    });
+    B.sync();
+    r.tie = rank_select(B, sc.buf, n, M, false, (uint64_t*)sc.whist);
+  } else {
+    uint64_t tlo = 0, thi = (uint64_t)1 << 62;  // smallest x with count(tk <= x) >= M
+    while (tlo < thi) {
+      uint64_t mid = tlo + (thi - tlo) / 2;
+      int64_t c = 0;
+      parties([&](uint32_t rk, int64_t v) {
+        int64_t base = w_count_r(v, tstar, rts, (int64_t)N + 1, false);
+        if (w_prio(v, base) == tstar && tie_key(base, rk, desc) <= mid) c++;
+      });
+      c = B.sum64(c);
+      if (c >= M) thi = mid;
+      else tlo = mid + 1;
+    }
+    r.tie = tlo;
+  }
+  KP_STAMPD(sc.dbg, 14);
+  B.sync();  // buf[0, 64) / whist are free again for the caller; pl stays
+  return r;
+}
+
 KP_HD inline uint32_t* web_ctr(const SelScratch& sc) { return (uint32_t*)sc.whist + 511; }  // party list fill counter
 template <class BLK, class Parties>
 KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc, const SelScratch& sc,
@@ -866,6 +927,29 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   };
   KP_STAMPD(sc.dbg, 9);
   const int64_t capN = (int64_t)N;
+  // Every seat a first seat: with P >= N parties of positive votes and the largest
+  // vote below 3 v_N (v_N = the N-th largest vote), every second priority vmax/3 is
+  // below v_N (exactly: fl(vmax/3) < v_N by far more than its rounding), so the N
+  // largest priorities are first priorities and t* = v_N. v_N is rank-selected from
+  // the compacted list (every vote >= v_N is in it: Lb <= v_N).
+  if (compact && P >= (int64_t)N && np <= kWebFirstMax) {
+    int64_t* slot = (int64_t*)sc.whist;
+    for (int i = B.tid(); i < np; i += B.nth()) {
+      const int64_t v = (int64_t)(uint32_t)pl[i];
+      int64_t before = 0, upto = 0;
+      for (int j = 0; j < np; j++) {
+        const int64_t y = (int64_t)(uint32_t)pl[j];
+        before += y > v ? 1 : 0;
+        upto += y == v ? 1 : 0;
+      }
+      upto += before;
+      if (before < (int64_t)N && (int64_t)N <= upto) *slot = v;  // every writer writes the same value
+    }
+    B.sync();
+    const int64_t vN = *slot;
+    B.sync();
+    if (vmax < 3 * vN) return webster_tail(B, r, parties, (double)vN, N, desc, sc, ecap, compact, np, Lb, pl);
+  }
   auto cnt2 = [&](double ta, double tb, int64_t* ca, int64_t* cb) {
     int64_t a = 0, b = 0;
     const double ra = 1.0 / ta, rb = 1.0 / tb;
@@ -941,58 +1025,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     B.sync();
     tstar = bitsd(rank_select(B, sc.buf, E, (int64_t)N - chi, true, (uint64_t*)sc.whist));
   }
-  r.t = tstar;
-  r.rt = 1.0 / tstar;
-  r.compact = compact;
-  r.np = np;
-  r.Lb = Lb;
-  r.pl = pl;
-  KP_STAMPD(sc.dbg, 12);
-  // seats strictly above t*, then the tie group at t* ordered by (k asc, name)
-  int64_t S = 0, T = 0;
-  const double rts = 1.0 / tstar;
-  parties([&](uint32_t, int64_t v) {
-    int64_t base = w_count_r(v, tstar, rts, (int64_t)N + 1, false);
-    S += base;
-    if (w_prio(v, base) == tstar) T++;
-  });
-  B.sum2(S, T);
-  const int64_t M = (int64_t)N - S;
-  KP_STAMPD(sc.dbg, 13);
-  if (M >= T) {
-    r.tie = ~0ull;
-  } else if (T <= (int64_t)ecap) {
-    int32_t mine = 0;
-    parties([&](uint32_t, int64_t v) {
-      int64_t base = w_count_r(v, tstar, rts, (int64_t)N + 1, false);
-      if (w_prio(v, base) == tstar) mine++;
-    });
-    int32_t n;
-    int32_t pos = B.excl_scan(mine, &n);
-    parties([&](uint32_t rk, int64_t v) {
-      int64_t base = w_count_r(v, tstar, rts, (int64_t)N + 1, false);
-      if (w_prio(v, base) == tstar) sc.buf[pos++] = tie_key(base, rk, desc);
-    });
-    B.sync();
-    r.tie = rank_select(B, sc.buf, n, M, false, (uint64_t*)sc.whist);
-  } else {
-    uint64_t tlo = 0, thi = (uint64_t)1 << 62;  // smallest x with count(tk <= x) >= M
-    while (tlo < thi) {
-      uint64_t mid = tlo + (thi - tlo) / 2;
-      int64_t c = 0;
-      parties([&](uint32_t rk, int64_t v) {
-        int64_t base = w_count_r(v, tstar, rts, (int64_t)N + 1, false);
-        if (w_prio(v, base) == tstar && tie_key(base, rk, desc) <= mid) c++;
-      });
-      c = B.sum64(c);
-      if (c >= M) thi = mid;
-      else tlo = mid + 1;
-    }
-    r.tie = tlo;
-  }
-  KP_STAMPD(sc.dbg, 14);
-  B.sync();  // buf[0, 64) / whist are free again for the caller; pl stays
-  return r;
+  return webster_tail(B, r, parties, tstar, N, desc, sc, ecap, compact, np, Lb, pl);
 }
 
 // Largest value v* over a value set (values in [0, 2^31)) such that the values

@@ -142,7 +142,8 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   ss.cap = top_ecap(t.cap);
   ss.dbg = a.dbg;
   SelCtx x = make_ctx(a, b, tgt);
-  build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
+  // (every read of the target bitset is behind tgt_cnt > 0)
+  if (h->tgt_cnt > 0) build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
   int64_t F = 0;
   for (int w = B.tid(); w < s.W; w += B.nth()) {
     const uint64_t m = x.frow[w];
@@ -159,10 +160,11 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   const bool fresh = (fl & BF_FRESH) != 0;
   const bool agg = st == ST_AGGREGATED;
   uint32_t* ctr = (uint32_t*)smem;  // subset length
-  if (B.tid() == 0) *ctr = 0;
-  B.sync();
   int64_t asum = 0, apos = 0, tsum = 0;
-  {
+  int32_t n = 0;
+  if (h->tgt_cnt > 0) {  // (none: an empty subset and zero sums, no reductions)
+    if (B.tid() == 0) *ctr = 0;
+    B.sync();
     int32_t mine = 0;
     for (int j = B.tid(); j < h->tgt_cnt; j += B.nth())
       mine += mask_test(x.frow, (int)kp_ldu(a.bv.ipool + h->tgt_off + 2 * j)) ? 1 : 0;
@@ -181,10 +183,10 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
       apos += sr > 0 ? 1 : 0;
       tsum += fresh ? add32(e, sr) : e;
     }
+    B.sum2(asum, apos);
+    tsum = B.sum64(tsum);
+    n = (int32_t)*ctr;  // (the reductions ordered the reservation)
   }
-  B.sum2(asum, apos);
-  tsum = B.sum64(tsum);
-  int32_t n = (int32_t)*ctr;  // (the reductions ordered the reservation)
   if (n > t.cap) {
     top_fallback(B, a, t, b);
     return;
