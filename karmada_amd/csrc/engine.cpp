@@ -238,6 +238,8 @@ struct kp_engine {
   bool top_on = true;
   int top_cap = 1024;      // subset capacity of the large slice
   int top_cap_small = 256;  // ... and of the small one (bindings needing <= kTopSmallNeed)
+  bool top_split = true;    // the two slices' launches on two streams (KP_TOP_SPLIT=0: one)
+  bool slow_order = true;   // k_slow orders candidates from the class orders (KP_SLOW_ORDER=0: sorts)
   // per-kernel timing of kp_schedule_batch (kp_engine_set_profile): an event pair
   // around every launch on its own stream, folded by kernel name after the batch
   struct KProf {
@@ -289,6 +291,8 @@ struct kp_batch {
   int n_top_small = 0;  // of those, the first n_top_small take k_select_top's small slice
   int n_static = 0;   // of the StaticWeight ones, the first n_static take k_select_static (static_ok)
   uint64_t out_cap = 0;
+  std::vector<uint8_t> route;     // RT_* per binding (pack_parallel)
+  int max_tgt = 0, max_tiers = 1;  // over the batch's headers (pack_parallel)
   Arena dev;
   BatchView view{};
   // device work buffers
@@ -1833,6 +1837,8 @@ int kp_engine_create(int device, kp_engine** out) {
   for (auto& ev : e->ev) (void)dev::event_create(&ev);
   e->max_lds = dev::max_lds_per_block(device);
   if (const char* v = getenv("KP_TOP")) e->top_on = atoi(v) != 0;
+  if (const char* v = getenv("KP_TOP_SPLIT")) e->top_split = atoi(v) != 0;
+  if (const char* v = getenv("KP_SLOW_ORDER")) e->slow_order = atoi(v) != 0;
   if (const char* v = getenv("KP_TOP_CAP")) {  // (tests: one capacity for both slices)
     e->top_cap = std::max(64, std::min(1024, atoi(v) & ~63));
     e->top_cap_small = std::min(e->top_cap_small, e->top_cap);
@@ -2187,6 +2193,30 @@ void est_key(const BindHdr& h, const Pools& p, std::string* k) {
   }
 }
 
+// A binding's route through kp_schedule_batch, recorded while packing so that the
+// batch's lists come from one pass over n bytes instead of passes over the headers.
+enum : uint8_t { RT_CLUSTER = 1, RT_REGION = 2, RT_DYN = 4, RT_SMALL = 8, RT_STATIC_OK = 16 };
+KP_HD inline bool route_static_ok(const SnapView& v, const BindHdr& h, const int64_t* lpool) {
+  if (h.sel != SEL_ALL || h.strategy != ST_STATIC || h.replicas < 0 || (int64_t)h.replicas >= kSeatWrap) return false;
+  if (!(h.flags & BF_WORKLOAD_ASSIGN) || (h.flags & (BF_OVERFLOW | BF_DUP_TARGETS | BF_BAD))) return false;
+  if (v.C >= 65536) return false;  // packed class counts
+  if (h.flags & BF_HAS_WP) {
+    if (h.sw_cnt > kSwRules || v.n_bits <= 0) return false;
+    for (int j = 0; j < h.sw_cnt; j++)
+      if (lpool[h.sw_w_off + j] >= (int64_t)kInt32Max) return false;  // saturated votes: SLOW_WEIGHT
+  }
+  return true;
+}
+inline uint8_t route_of(const SnapView& v, const BindHdr& h, const int64_t* lpool) {
+  uint8_t r = h.sel == SEL_CLUSTER ? RT_CLUSTER : h.sel == SEL_REGION ? RT_REGION : 0;
+  if (!r) {
+    if (h.strategy != ST_STATIC) r |= RT_DYN;
+    if ((int64_t)h.replicas + h.tgt_cnt <= kTopSmallNeed) r |= RT_SMALL;
+    if (route_static_ok(v, h, lpool)) r |= RT_STATIC_OK;
+  }
+  return r;
+}
+
 bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* bt) {
   int T = host_cpus();
   if (const char* v = getenv("KP_PACK_THREADS")) T = atoi(v);
@@ -2205,6 +2235,9 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
   std::vector<std::string> terr(T);
   std::vector<double> tms(T, 0.0);
   std::atomic<int> next_chunk(0);
+  bt->route.resize(n);
+  std::vector<uint64_t> chunk_cap(K + 1, 0);  // result slots per chunk (out_off prefix sums)
+  std::vector<int> tmax_tgt(T, 0), tmax_tiers(T, 1);
   auto run = [&](int t) {
     const auto tt0 = std::chrono::steady_clock::now();
     struct Stamp {
@@ -2221,8 +2254,17 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       if (k >= K) break;
       owner[k] = t;
       pk.bt = &pl[k];
+      uint64_t cap = 0;
       for (int i = lo[k]; i < lo[k + 1]; i++) {
         pk.pack(bindings[i], bt->hdr[i]);
+        {
+          const BindHdr& h = bt->hdr[i];
+          cap += h.out_cap;
+          bt->route[i] = route_of(s->view, h, pl[k].lpool.data());  // (chunk-relative pool offsets)
+          tmax_tgt[t] = std::max(tmax_tgt[t], (int)h.tgt_cnt);
+          tmax_tiers[t] = std::max(tmax_tiers[t], (int)h.ovf_cnt + 2);  // primary, each overflow term, unmatched
+        }
+        chunk_cap[k + 1] = cap;
         if (bt->hdr[i].flags & BF_NONWORKLOAD_EST) {
           bt->bcls[i] = -1;
           continue;
@@ -2238,6 +2280,7 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
             if (terr[t].empty()) terr[t] = err;
             bt->hdr[i].flags &= ~(uint32_t)BF_SETS;
           }
+          bt->route[i] = route_of(s->view, bt->hdr[i], pl[k].lpool.data());  // (flags changed)
         }
         if (bt->hdr[i].flags & BF_SETS) {
           key.assign(1, 'S');
@@ -2312,6 +2355,10 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       }
     }
   }
+  for (int k = 0; k < K; k++) chunk_cap[k + 1] += chunk_cap[k];
+  bt->out_cap = chunk_cap[K];
+  bt->max_tgt = *std::max_element(tmax_tgt.begin(), tmax_tgt.end());
+  bt->max_tiers = *std::max_element(tmax_tiers.begin(), tmax_tiers.end());
   std::atomic<int> next_merge(0);
   auto merge = [&](int) {
     for (;;) {
@@ -2321,9 +2368,12 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       const int32_t oi = (int32_t)bi[k], ol = (int32_t)bl[k], oo = (int32_t)bo[k], op = (int32_t)bp[k],
                     on = (int32_t)bn[k];
       const std::vector<int32_t>& remap = remaps[owner[k]];
+      uint64_t off = chunk_cap[k];
       for (int i = lo[k]; i < lo[k + 1]; i++) {
         BindHdr& h = bt->hdr[i];
         bt->bcls[i] = bt->bcls[i] < 0 ? 0 : remap[bt->bcls[i]];
+        h.out_off = off;  // private result slots: no atomic on the emit path
+        off += h.out_cap;
         if (k == 0) continue;
         for (int j = 0; j < h.filt_cnt; j++) q.ipool[h.filt_off + j] += op;
         for (int j = 0; j < h.ovf_cnt; j++) q.ipool[h.ovf_off + j] += op;
@@ -2403,64 +2453,62 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
     e->err = bt->err.empty() ? "batch pools exceed 2^31 entries" : bt->err;
     return KP_ENOTSUP;
   }
-  for (uint64_t i = 0; i < n; i++) {
-    bt->hdr[i].out_off = bt->out_cap;  // private result slots: no atomic on the emit path
-    bt->out_cap += bt->hdr[i].out_cap;
-    const BindHdr& h = bt->hdr[i];
-    if (h.sel == SEL_CLUSTER) bt->l_cluster.push_back((int32_t)i);
-    else if (h.sel == SEL_REGION) bt->l_region.push_back((int32_t)i);
-    else bt->l_all.push_back((int32_t)i);
-  }
-  // SEL_ALL bindings: StaticWeight last (they take the streamed-candidate kernel, kp_kernels.h)
-  bt->n_all_dyn = (int)(std::stable_partition(bt->l_all.begin(), bt->l_all.end(),
-                                              [&](int32_t i) { return bt->hdr[i].strategy != ST_STATIC; }) -
-                        bt->l_all.begin());
-  // the non-StaticWeight SEL_ALL bindings grouped by estimator class (counting sort,
-  // stable): the workgroups resident at any moment then cover a short run of the
-  // list, i.e. few classes, whose orders and rows stay in every XCD's L2
-  // (k_select_top 1.23 -> 1.10 ms at config 3; mapping each XCD to one contiguous
-  // run of the list instead was slower, 1.33 ms)
-  if (bt->n_all_dyn > 1 && !bt->crep.empty()) {
-    const size_t ncls = bt->crep.size();
-    std::vector<int32_t> cnt(ncls + 1, 0), out((size_t)bt->n_all_dyn);
-    for (int i = 0; i < bt->n_all_dyn; i++) cnt[(size_t)std::max(0, bt->bcls[bt->l_all[i]]) + 1]++;
-    for (size_t k = 1; k <= ncls; k++) cnt[k] += cnt[k - 1];
-    for (int i = 0; i < bt->n_all_dyn; i++) out[(size_t)cnt[(size_t)std::max(0, bt->bcls[bt->l_all[i]])]++] = bt->l_all[i];
-    std::copy(out.begin(), out.end(), bt->l_all.begin());
-  }
-  // ... and split by the subset each is likely to need (k_select_top runs twice: a
-  // small LDS slice for the first n_top_small, a large one for the rest): a
-  // DynamicWeight / Aggregated subset holds the scheduled clusters and about as many
-  // walked parties as the target replicas
-  bt->n_top_small = (int)(std::stable_partition(bt->l_all.begin(), bt->l_all.begin() + bt->n_all_dyn,
-                                                [&](int32_t i) {
-                                                  const BindHdr& h = bt->hdr[i];
-                                                  return (int64_t)h.replicas + h.tgt_cnt <= kTopSmallNeed;
-                                                }) -
-                          bt->l_all.begin());
-  // StaticWeight bindings the class-level kernel covers first (bits mode only)
+  // the selection lists from the routes (binding order within each kind). SEL_ALL:
+  // [non-StaticWeight | StaticWeight]; the non-StaticWeight ones split by the subset
+  // they likely need (k_select_top's small LDS slice first: a DynamicWeight /
+  // Aggregated subset holds the scheduled clusters and about as many walked parties
+  // as the target replicas), each part grouped by estimator class (counting sort,
+  // stable: the workgroups resident at any moment then cover a short run of the list,
+  // i.e. few classes, whose orders and rows stay in every XCD's L2; k_select_top
+  // 1.23 -> 1.10 ms at config 3, mapping each XCD to one contiguous run of the list
+  // instead was slower, 1.33 ms); StaticWeight bindings the class-level kernel covers
+  // (bits mode) before the others.
   {
-    const kp_snapshot* sn = bt->snap;
-    auto static_ok = [&](int32_t i) {
-      const BindHdr& h = bt->hdr[i];
-      if (h.sel != SEL_ALL || h.strategy != ST_STATIC || h.replicas < 0 || (int64_t)h.replicas >= kSeatWrap) return false;
-      if (!(h.flags & BF_WORKLOAD_ASSIGN) || (h.flags & (BF_OVERFLOW | BF_DUP_TARGETS | BF_BAD))) return false;
-      if (sn->view.C >= 65536) return false;  // packed class counts
-      if (h.flags & BF_HAS_WP) {
-        if (h.sw_cnt > kSwRules || sn->view.n_bits <= 0) return false;
-        for (int j = 0; j < h.sw_cnt; j++)
-          if (bt->lpool[h.sw_w_off + j] >= (int64_t)kInt32Max) return false;  // saturated votes: SLOW_WEIGHT
+    const std::vector<uint8_t>& rt = bt->route;
+    const size_t ncls = std::max<size_t>(1, bt->crep.size());
+    std::vector<int32_t> cnt(2 * ncls + 1, 0);
+    int n_dyn = 0, n_small = 0, n_stat = 0, n_stat_ok = 0, n_cl = 0, n_rg = 0;
+    for (uint64_t i = 0; i < n; i++) {
+      const uint8_t r = rt[i];
+      if (r & RT_CLUSTER) n_cl++;
+      else if (r & RT_REGION) n_rg++;
+      else if (r & RT_DYN) {
+        n_dyn++;
+        const bool sm = (r & RT_SMALL) != 0;
+        n_small += sm;
+        cnt[(sm ? 0 : ncls) + (size_t)std::max(0, bt->bcls[i]) + 1]++;
+      } else {
+        n_stat++;
+        n_stat_ok += (r & RT_STATIC_OK) ? 1 : 0;
       }
-      return true;
-    };
-    bt->n_static = (int)(std::stable_partition(bt->l_all.begin() + bt->n_all_dyn, bt->l_all.end(), static_ok) -
-                         (bt->l_all.begin() + bt->n_all_dyn));
+    }
+    for (size_t k = 1; k <= 2 * ncls; k++) cnt[k] += cnt[k - 1];
+    bt->l_all.resize((size_t)n_dyn + n_stat);
+    bt->l_cluster.resize(n_cl);
+    bt->l_region.resize(n_rg);
+    bt->l_cs.resize((size_t)n_cl + n_rg);
+    int pc = 0, pr = 0, ps = n_dyn, pso = n_dyn + n_stat_ok, pcs = 0;
+    for (uint64_t i = 0; i < n; i++) {
+      const uint8_t r = rt[i];
+      const int32_t b = (int32_t)i;
+      if (r & (RT_CLUSTER | RT_REGION)) {
+        bt->l_cs[pcs++] = b;
+        if (r & RT_CLUSTER) bt->l_cluster[pc++] = b;
+        else bt->l_region[pr++] = b;
+      } else if (r & RT_DYN) {
+        bt->l_all[cnt[((r & RT_SMALL) ? 0 : ncls) + (size_t)std::max(0, bt->bcls[i])]++] = b;
+      } else if (r & RT_STATIC_OK) {
+        bt->l_all[ps++] = b;
+      } else {
+        bt->l_all[pso++] = b;
+      }
+    }
+    bt->n_all_dyn = n_dyn;
+    bt->n_top_small = n_small;
+    bt->n_static = n_stat_ok;
   }
   bt->l_slow = bt->l_all;
   bt->l_slow.insert(bt->l_slow.end(), bt->l_cluster.begin(), bt->l_cluster.end());
-  bt->l_cs = bt->l_cluster;
-  bt->l_cs.insert(bt->l_cs.end(), bt->l_region.begin(), bt->l_region.end());
-  std::sort(bt->l_cs.begin(), bt->l_cs.end());
   if (s->view.n_regions > kRegionMax && !bt->l_region.empty()) {
     e->err = "region spread over more than 256 regions is not supported";
     return KP_ENOTSUP;
@@ -2477,11 +2525,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   pad1(bt->instrs);
   const int B = bt->B ? bt->B : 1;
   const int nr = (int)bt->l_region.size(), R = std::max(1, s->view.n_regions);
-  int max_tgt = 0, max_tiers = 1;
-  for (auto& h : bt->hdr) {
-    max_tgt = std::max(max_tgt, (int)h.tgt_cnt);
-    max_tiers = std::max(max_tiers, (int)h.ovf_cnt + 2);  // primary, each overflow term, unmatched (1000)
-  }
+  const int max_tgt = bt->max_tgt, max_tiers = bt->max_tiers;
   // SerialAssign's result list: every candidate once, plus, per overflow tier, the
   // spec.Clusters entries MergeTargetClusters appends (common.go:97-139; util/binding.go:91-115).
   bt->slow_cap = s->Cp + max_tiers * max_tgt + 64;
@@ -2892,6 +2936,9 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       // bindings it hands back (other strategies, subsets past capacity, ...) run with
       // every candidate from its fallback list
       HIPCHK(dev::event_record(e->ev[12], sp));
+      // the two slices' launches run concurrently, the large one on stream3 (which the
+      // cluster-spread kernels use after it), so neither drains the CUs alone
+      const bool split = e->top_split && bt->n_top_small > 0 && bt->n_all_dyn > bt->n_top_small;
       for (int part = 0; part < 2; part++) {
         KArgs g = k;
         const int cap_p = part == 0 ? top_cap_small : top_cap;
@@ -2900,7 +2947,13 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
         if (g.n <= 0) continue;
         TopArgs ta{bt->d_ord, bt->d_ctot, bt->d_cok, bt->d_fb, bt->stats + 9, cap_p};
         const size_t slice = (top_lds_bytes(s->Cp, cap_p) + 15) & ~(size_t)15;
-        KPROF(sp, "k_select_top", g.n, -1, dev::select_top(sp, g, ta, slice));
+        dev::stream_t sx_ = split && part == 1 ? e->stream3 : sp;
+        if (split && part == 1) HIPCHK(dev::stream_wait(sx_, e->ev[4]));
+        KPROF(sx_, "k_select_top", g.n, -1, dev::select_top(sx_, g, ta, slice));
+        if (split && part == 1) {
+          HIPCHK(dev::event_record(e->ev[10], sx_));
+          HIPCHK(dev::stream_wait(sp, e->ev[10]));  // both slices' fallbacks precede k_select_all
+        }
       }
       HIPCHK(dev::event_record(e->ev[13], sp));
       KArgs f = k;
@@ -2964,6 +3017,9 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     KArgs k = ka;
     k.list = bt->d_slowlist;
     k.n = (int)bt->l_slow.size();
+    k.ord = orders ? bt->d_ord : nullptr;  // sortClusters order from the class orders (kp_kernels.h)
+    k.cok = orders ? bt->d_cok : nullptr;
+    if (!e->slow_order) k.ord = nullptr;
     KPROF(s3, "k_slow", 0, 0, dev::select(s3, SEL_LAUNCH_SLOW, k, kRedBytes + 512 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area +
                                                       sx.lds_sort,
                        bt->slow_cap, sx));

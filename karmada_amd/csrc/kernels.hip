@@ -149,7 +149,10 @@ extern "C" __global__ void __launch_bounds__(KP_SEL_MAX_THREADS, KP_SEL_MIN_WAVE
 #endif
 // SEL_ALL DynamicWeight / Aggregated over the candidates that can matter (kp_top.h):
 // kTopWaves independent waves per workgroup, one binding each, no workgroup barrier.
-extern "C" __global__ void __launch_bounds__(64 * kTopWaves) k_select_top(KArgs a, TopArgs t, int slice)
+#ifndef KP_TOP_MIN_WAVES
+#define KP_TOP_MIN_WAVES 1
+#endif
+extern "C" __global__ void __launch_bounds__(64 * kTopWaves, KP_TOP_MIN_WAVES) k_select_top(KArgs a, TopArgs t, int slice)
 #if KP_K(4)
 {
   KP_SMEM;

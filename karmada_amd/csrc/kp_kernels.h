@@ -1240,6 +1240,79 @@ KP_FI bool presort_dynamic(const BLK& B, const SelCtx& x, const Item* items, int
   return true;
 }
 
+// The candidates in sortClusters order (items[0, F)) without sorting them: a
+// non-target candidate's key is (overflow 0, score 0, estimate, rank), which ascends
+// along its estimator class's order (k_class_order: estimate desc, rank asc), so the
+// class order filtered by the binding's feasibility row is that part of the list,
+// already sorted; the few feasible spec.Clusters entries (their locality score and
+// scheduled replicas in the key) are merged in by binary search. O(C) per binding
+// instead of the bitonic sort's O(C log^2 C). Returns false, with nothing written to
+// items, when it does not apply (no class orders, overflow tiers, a class whose row
+// the order cannot stand for, many or duplicate targets) or when the filtered order
+// is not ascending in the keys; the caller then sorts.
+constexpr int kSlowOrdTargets = 64;
+template <class BLK>
+KP_FI bool slow_items_from_order(const BLK& B, const KArgs& a, const SelCtx& x, int b, const uint32_t* tgt, int F,
+                                 uint64_t* keys, Item* items) {
+  const BindHdr& h = *x.h;
+  if (!a.ord || !a.cok || !a.bcls || h.ovf_mode != OVF_ZERO || (h.flags & BF_DUP_TARGETS) ||
+      h.tgt_cnt > kSlowOrdTargets)
+    return false;
+  const int32_t cls = a.bcls[b];
+  if (cls <= 0 || !a.cok[cls]) return false;
+  const uint64_t* ord = a.ord + (size_t)cls * a.s.Cp;
+  const int C = a.s.C;
+  int N = 0;
+  for (int base = 0; base < C; base += B.nth()) {  // stream compaction of the class order
+    const int i = base + B.tid();
+    int32_t in = 0;
+    uint32_t r = 0;
+    if (i < C) {
+      r = (uint32_t)ord[i];
+      in = mask_test(x.frow, (int)r) && !(h.tgt_cnt > 0 && bit_test(tgt, (int)r)) ? 1 : 0;
+    }
+    int32_t tot;
+    const int32_t off = B.excl_scan(in, &tot);
+    if (in) keys[N + off] = sort_key(0, 0, (int64_t)est_at(x, (int)r), r);
+    N += tot;
+  }
+  int T = 0;  // the feasible targets, appended after the others (thread 0: at most kSlowOrdTargets)
+  if (h.tgt_cnt > 0) {
+    if (B.tid() == 0)
+      for (int j = 0; j < h.tgt_cnt; j++) {
+        const uint32_t r = (uint32_t)x.bv->ipool[h.tgt_off + 2 * j];
+        if (!mask_test(x.frow, (int)r)) continue;
+        const int64_t avail = (int64_t)est_at(x, (int)r) + (int64_t)assigned_of(*x.bv, h, x.tgt_bits, r);
+        keys[N + T++] = sort_key(0, locality_score(h, x.tgt_bits, r), avail, r);
+      }
+    T = B.bcast(T);
+  }
+  B.sync();
+  int64_t bad = N + T != F ? 1 : 0;
+  for (int p = B.tid() + 1; p < N; p += B.nth()) bad |= keys[p - 1] >= keys[p] ? 1 : 0;
+  if (B.sum64(bad) != 0) return false;  // (also orders every key write before the reads below)
+  for (int p = B.tid(); p < N + T; p += B.nth()) {
+    const uint64_t k = keys[p];
+    int pos = 0;
+    for (int q = 0; q < T; q++) pos += keys[N + q] < k ? 1 : 0;  // targets before it
+    if (p < N) {
+      pos += p;
+    } else {
+      int lo = 0, hi = N;  // non-targets before it
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] < k) lo = mid + 1;
+        else hi = mid;
+      }
+      pos += lo;
+    }
+    items[pos] = item_from_key(x, k);
+  }
+  B.sync();
+  if (B.tid() == 0) KP_COUNT(x, 54, 1);
+  return true;
+}
+
 template <class BLK>
 KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const KArgs& a, unsigned char* scratch,
                      size_t slot_bytes, int scratch_cap, int lds_area, int lds_sort) {
@@ -1313,27 +1386,29 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
       B.sync();
     }
 #endif
-    int PF = 1;
-    while (PF < F) PF <<= 1;
-    for (int i = B.tid(); i < PF; i += B.nth()) keys[i] = i < F ? cand_key(x, cd, i, cd.v[i]) : ~0ull;
-    B.sync();
-    for (int k = 2; k <= PF; k <<= 1)  // bitonic sort (ascending)
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = B.tid(); i < PF; i += B.nth()) {
-          int l = i ^ j;
-          if (l > i) {
-            uint64_t ki = keys[i], kl = keys[l];
-            bool up = (i & k) == 0;
-            if ((ki > kl) == up) {
-              keys[i] = kl;
-              keys[l] = ki;
+    if (!slow_items_from_order(B, a, x, b, tgt, F, keys, items)) {
+      int PF = 1;
+      while (PF < F) PF <<= 1;
+      for (int i = B.tid(); i < PF; i += B.nth()) keys[i] = i < F ? cand_key(x, cd, i, cd.v[i]) : ~0ull;
+      B.sync();
+      for (int k = 2; k <= PF; k <<= 1)  // bitonic sort (ascending)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = B.tid(); i < PF; i += B.nth()) {
+            int l = i ^ j;
+            if (l > i) {
+              uint64_t ki = keys[i], kl = keys[l];
+              bool up = (i & k) == 0;
+              if ((ki > kl) == up) {
+                keys[i] = kl;
+                keys[l] = ki;
+              }
             }
           }
+          B.sync();
         }
-        B.sync();
-      }
-    for (int i = B.tid(); i < F; i += B.nth()) items[i] = item_from_key(x, keys[i]);
-    B.sync();
+      for (int i = B.tid(); i < F; i += B.nth()) items[i] = item_from_key(x, keys[i]);
+      B.sync();
+    }
 #ifdef KP_SLOW_CHECK
     if (B.tid() == 0) {  // dbg[2] += bindings whose sorted items differ, dbg[3] += ... whose keys differ
       uint64_t s0 = 0, s1 = 0, k0 = 0;

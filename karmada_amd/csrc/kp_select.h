@@ -121,9 +121,16 @@ KP_HD inline int32_t est_at(const SelCtx& x, int c) { return est_merge(x, x.erow
 #define KP_STAMPD(dbg, i) \
   do {                    \
   } while (0)
+#if defined(KP_STAMPS)  // host build with -DKP_STAMPS: the counters only (one thread per block)
+#define KP_COUNT(ctx_, i, v)                                                                        \
+  do {                                                                                              \
+    if ((ctx_).dbg) __atomic_fetch_add(&(ctx_).dbg[i], (unsigned long long)(v), __ATOMIC_RELAXED); \
+  } while (0)
+#else
 #define KP_COUNT(x, i, v) \
   do {                    \
   } while (0)
+#endif
 #endif
 
 struct SerialOut {

@@ -322,6 +322,8 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   }
   KP_STAMP(x, 11);
   KP_COUNT(x, 14, n);
+  KP_COUNT(x, 40 + (n <= 16 ? 0 : n <= 32 ? 1 : n <= 64 ? 2 : n <= 128 ? 3 : n <= 256 ? 4 : n <= 512 ? 5 : 6), 1);
+  KP_COUNT(x, 47 + (agg ? 1 : 0), 1);
   cd.F = n;
   B.sync();
   const TopInfo ti{F, complete};
