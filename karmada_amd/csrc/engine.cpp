@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -41,13 +42,76 @@ double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// std::string-keyed hash table with string_view lookups (no key copy per probe).
-struct SvHash {
-  using is_transparent = void;
-  size_t operator()(std::string_view v) const { return std::hash<std::string_view>()(v); }
-};
+// String-keyed hash table with string_view lookups for the packing hot path (names,
+// dictionary strings, memo keys): open addressing with linear probing over a
+// power-of-two slot array kept at most half full, one multiply-xorshift hash over
+// 8-byte words per lookup, entries in a deque (stable addresses). find() returns the
+// entry or nullptr (== end()); it->first / it->second as with std::unordered_map.
+inline uint64_t sv_hash(std::string_view v) {
+  const unsigned char* p = (const unsigned char*)v.data();
+  size_t n = v.size();
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+  for (; n >= 8; n -= 8, p += 8) {
+    uint64_t w;
+    memcpy(&w, p, 8);
+    h = (h ^ w) * 0xff51afd7ed558ccdull;
+    h ^= h >> 32;
+  }
+  uint64_t w = 0;
+  memcpy(&w, p, n);
+  h = (h ^ w) * 0xc4ceb9fe1a85ec53ull;
+  h ^= h >> 29;
+  return h | 1;  // 0 marks an empty slot
+}
 template <class V>
-using SvMap = std::unordered_map<std::string, V, SvHash, std::equal_to<>>;
+class SvMap {
+ public:
+  struct Entry {
+    std::string first;
+    V second;
+  };
+  Entry* find(std::string_view k) {
+    if (slots_.empty()) return nullptr;
+    const uint64_t h = sv_hash(k);
+    for (size_t i = h & mask_;; i = (i + 1) & mask_) {
+      const Slot& sl = slots_[i];
+      if (sl.h == 0) return nullptr;
+      if (sl.h == h && ent_[sl.i].first == k) return &ent_[sl.i];
+    }
+  }
+  const Entry* find(std::string_view k) const { return const_cast<SvMap*>(this)->find(k); }
+  Entry* end() const { return nullptr; }
+  template <class K, class W>
+  std::pair<Entry*, bool> emplace(K&& k, W&& v) {
+    if (Entry* e = find(std::string_view(k))) return {e, false};
+    if (2 * (ent_.size() + 1) > slots_.size()) grow();
+    ent_.push_back(Entry{std::string(std::forward<K>(k)), V(std::forward<W>(v))});
+    put(sv_hash(ent_.back().first), (uint32_t)(ent_.size() - 1));
+    return {&ent_.back(), true};
+  }
+  V& operator[](std::string_view k) { return emplace(std::string(k), V()).first->second; }
+  size_t size() const { return ent_.size(); }
+
+ private:
+  struct Slot {
+    uint64_t h = 0;
+    uint32_t i = 0;
+  };
+  std::vector<Slot> slots_;
+  std::deque<Entry> ent_;
+  size_t mask_ = 0;
+  void put(uint64_t h, uint32_t i) {
+    size_t j = h & mask_;
+    while (slots_[j].h != 0) j = (j + 1) & mask_;
+    slots_[j] = Slot{h, i};
+  }
+  void grow() {
+    const size_t cap = std::max<size_t>(16, 2 * slots_.size());
+    slots_.assign(cap, Slot{});
+    mask_ = cap - 1;
+    for (uint32_t i = 0; i < (uint32_t)ent_.size(); i++) put(sv_hash(ent_[i].first), i);
+  }
+};
 
 struct Dict {
   SvMap<int32_t> m;
@@ -928,6 +992,22 @@ struct Pools {
   std::vector<Instr> instrs;
 };
 
+// Diagnostic build (-DKP_PACK_PROF): cycles per section of Packer::pack, summed over
+// the process and printed by pack_parallel under KP_PACK_TIMING.
+#ifdef KP_PACK_PROF
+#include <x86intrin.h>
+std::atomic<uint64_t> g_pack_cyc[8];
+#define KP_PACK_MARK_INIT uint64_t kp_c0 = __rdtsc()
+#define KP_PACK_MARK(i)                                                  \
+  do {                                                                   \
+    const uint64_t kp_c1 = __rdtsc();                                    \
+    g_pack_cyc[i].fetch_add(kp_c1 - kp_c0, std::memory_order_relaxed); \
+    kp_c0 = kp_c1;                                                       \
+  } while (0)
+#else
+#define KP_PACK_MARK_INIT
+#define KP_PACK_MARK(i)
+#endif
 struct Packer {
   kp_snapshot* s;
   Pools* bt;  // this packer's pools (one per packing thread, merged by kp_batch_create)
@@ -1222,6 +1302,7 @@ struct Packer {
   }
 
   void pack(const kp_binding& b, BindHdr& h) {
+    KP_PACK_MARK_INIT;
     memset(&h, 0, sizeof(h));
     h.ip_beg = (int32_t)bt->ipool.size();
     h.pr_beg = (int32_t)bt->progs.size();
@@ -1262,6 +1343,7 @@ struct Packer {
         if (gvk_cache.size() < 4096) gvk_cache.emplace(gvkey, h.gvk);
       }
     }
+    KP_PACK_MARK(0);
     // spec.Clusters
     h.n_targets_all = (int32_t)b.n_clusters;
     {
@@ -1292,6 +1374,7 @@ struct Packer {
       h.evict_off = list(r);
       h.evict_cnt = (int32_t)r.size();
     }
+    KP_PACK_MARK(1);
     // tolerations
     h.tol_off = (int32_t)bt->tols.size();
     for (uint32_t i = 0; i < b.n_tolerations; i++) {
@@ -1316,6 +1399,7 @@ struct Packer {
       bt->tols.push_back(x);
     }
     h.tol_cnt = (int32_t)bt->tols.size() - h.tol_off;
+    KP_PACK_MARK(2);
     // ClusterAffinity filter list + overflow order programs
     {
       auto &filt = tmp_filt, &ovf = tmp_ovf;
@@ -1358,6 +1442,7 @@ struct Packer {
           term->n_overflow > 0)
         f |= BF_OVERFLOW;
     }
+    KP_PACK_MARK(3);
     // static weights
     {
       auto& ids = tmp_ids;
@@ -1373,6 +1458,7 @@ struct Packer {
       h.sw_w_off = (int32_t)bt->lpool.size();
       bt->lpool.insert(bt->lpool.end(), ws.begin(), ws.end());
     }
+    KP_PACK_MARK(4);
     // requests
     {
       // the ResourceList as (name, quantity) in name order, a repeated name's last
@@ -1427,6 +1513,7 @@ struct Packer {
       h.mreq_q_off = (int32_t)bt->lpool.size();
       bt->lpool.insert(bt->lpool.end(), mq.begin(), mq.end());
     }
+    KP_PACK_MARK(5);
     // spread constraints: filter presence + selection kind (select_clusters.go:28-80)
     const std::string_view rst = b.has_replica_scheduling ? SV(b.replica_scheduling_type) : std::string_view("Duplicated");
     const std::string_view div = SV(b.replica_division_preference);
@@ -1494,6 +1581,7 @@ struct Packer {
     h.ip_end = (int32_t)bt->ipool.size();
     h.pr_end = (int32_t)bt->progs.size();
     h.in_end = (int32_t)bt->instrs.size();
+    KP_PACK_MARK(6);
   }
 };
 
@@ -2217,6 +2305,54 @@ inline uint8_t route_of(const SnapView& v, const BindHdr& h, const int64_t* lpoo
   return r;
 }
 
+// Packing reads each binding's struct and the strings and arrays it points to once,
+// scattered over the caller's memory: cache misses, not the parsing, bound it (about
+// 3k cycles per config-3 binding, spread evenly over the struct's sections). So the
+// loop prefetches three levels ahead of the binding it packs: the struct of i + 3,
+// the arrays and strings i + 2 points to, the strings inside i + 1's arrays.
+inline void pf(const void* p) {
+  if (p) __builtin_prefetch(p, 0, 3);
+}
+inline void pf_struct(const kp_binding* b) {
+  for (size_t o = 0; o < sizeof(kp_binding); o += 64) pf((const char*)b + o);
+}
+inline void pf_affinity(const kp_cluster_affinity& a) {
+  pf(a.match_labels);
+  pf(a.match_expressions);
+  pf(a.field_expressions);
+  pf(a.cluster_names);
+  pf(a.exclude_clusters);
+}
+inline void pf_arrays(const kp_binding& b) {
+  pf(b.uid.ptr);
+  pf(b.api_version.ptr);
+  pf(b.kind.ptr);
+  pf(b.resource_request);
+  pf(b.clusters);
+  pf(b.eviction_from);
+  pf(b.tolerations);
+  pf(b.spread_constraints);
+  pf(b.static_weights);
+  pf(b.cluster_affinities);
+  if (b.has_cluster_affinity) pf_affinity(b.cluster_affinity);
+}
+inline void pf_strings(const kp_binding& b) {
+  for (uint32_t j = 0; j < b.n_resource_request && j < 4; j++) {
+    pf(b.resource_request[j].name.ptr);
+    pf(b.resource_request[j].quantity.ptr);
+  }
+  for (uint32_t j = 0; j < b.n_clusters && j < 4; j++) pf(b.clusters[j].name.ptr);
+  for (uint32_t j = 0; j < b.n_tolerations && j < 2; j++) {
+    pf(b.tolerations[j].key.ptr);
+    pf(b.tolerations[j].value.ptr);
+  }
+  if (b.has_cluster_affinity)
+    for (uint32_t j = 0; j < b.cluster_affinity.n_match_expressions && j < 2; j++) {
+      pf(b.cluster_affinity.match_expressions[j].key.ptr);
+      pf(b.cluster_affinity.match_expressions[j].values);
+    }
+}
+
 bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* bt) {
   int T = host_cpus();
   if (const char* v = getenv("KP_PACK_THREADS")) T = atoi(v);
@@ -2254,17 +2390,23 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       if (k >= K) break;
       owner[k] = t;
       pk.bt = &pl[k];
-      uint64_t cap = 0;
-      for (int i = lo[k]; i < lo[k + 1]; i++) {
+      uint64_t cap = 0;  // (chunk and thread totals kept in registers: the shared arrays are
+      int max_tgt = 0, max_tiers = 1;  // written once per chunk, not once per binding)
+      const int hi = lo[k + 1];
+      for (int q = lo[k]; q < std::min(hi, lo[k] + 3); q++) pf_struct(&bindings[q]);
+      if (lo[k] + 1 < hi) pf_arrays(bindings[lo[k] + 1]);
+      for (int i = lo[k]; i < hi; i++) {
+        if (i + 3 < hi) pf_struct(&bindings[i + 3]);
+        if (i + 2 < hi) pf_arrays(bindings[i + 2]);
+        if (i + 1 < hi) pf_strings(bindings[i + 1]);
         pk.pack(bindings[i], bt->hdr[i]);
         {
           const BindHdr& h = bt->hdr[i];
           cap += h.out_cap;
           bt->route[i] = route_of(s->view, h, pl[k].lpool.data());  // (chunk-relative pool offsets)
-          tmax_tgt[t] = std::max(tmax_tgt[t], (int)h.tgt_cnt);
-          tmax_tiers[t] = std::max(tmax_tiers[t], (int)h.ovf_cnt + 2);  // primary, each overflow term, unmatched
+          max_tgt = std::max(max_tgt, (int)h.tgt_cnt);
+          max_tiers = std::max(max_tiers, (int)h.ovf_cnt + 2);  // primary, each overflow term, unmatched
         }
-        chunk_cap[k + 1] = cap;
         if (bt->hdr[i].flags & BF_NONWORKLOAD_EST) {
           bt->bcls[i] = -1;
           continue;
@@ -2295,6 +2437,9 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
         }
         bt->bcls[i] = it->second;
       }
+      chunk_cap[k + 1] = cap;
+      tmax_tgt[t] = std::max(tmax_tgt[t], max_tgt);
+      tmax_tiers[t] = std::max(tmax_tiers[t], max_tiers);
     }
   };
   auto on_threads = [&](auto fn) {
@@ -2418,6 +2563,11 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
             ms(tq0, tq1), ms(tq1, std::chrono::steady_clock::now()));
     for (double x : tms) fprintf(stderr, " %.1f", x);
     fprintf(stderr, "\n");
+#ifdef KP_PACK_PROF
+    fprintf(stderr, "pack sections (Mcycles, cumulative): gvk %.1f targets %.1f tolerations %.1f affinity %.1f "
+            "static %.1f requests %.1f rest %.1f\n", g_pack_cyc[0] / 1e6, g_pack_cyc[1] / 1e6, g_pack_cyc[2] / 1e6,
+            g_pack_cyc[3] / 1e6, g_pack_cyc[4] / 1e6, g_pack_cyc[5] / 1e6, g_pack_cyc[6] / 1e6);
+#endif
   }
   return true;
 }

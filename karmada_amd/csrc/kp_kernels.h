@@ -946,6 +946,13 @@ KP_FI void body_region_a_order(const BLK& B, int blk, unsigned char* smem, const
   const int32_t cls = order_class(a, x);
   if (cls < 0) {
     if (B.tid() == 0) fb[kp_atomic_add(fb_n, 1u)] = blk;
+#ifdef KP_STAMPS
+    if (B.tid() == 0) {  // why: 55 no orders, 56 class 0, 57 row not walkable, 58 spec.Clusters, 59 other
+      const BindHdr& h0 = *x.h;
+      const int32_t c0 = a.bcls && a.ord ? a.bcls[b] : -1;
+      KP_COUNT(x, !a.ord || !a.bcls ? 55 : c0 <= 0 ? 56 : !a.cok[c0] ? 57 : h0.tgt_cnt != 0 ? 58 : 59, 1);
+    }
+#endif
     return;
   }
   const SnapView& s = a.s;
@@ -1267,13 +1274,16 @@ KP_FI bool slow_items_from_order(const BLK& B, const KArgs& a, const SelCtx& x, 
     const int i = base + B.tid();
     int32_t in = 0;
     uint32_t r = 0;
+    int32_t e = 0;
     if (i < C) {
-      r = (uint32_t)ord[i];
+      const uint64_t o = ord[i];
+      r = (uint32_t)o;
+      e = (int32_t)(o >> 32);  // the class row's estimate: est_at's value (a walkable row: no merge)
       in = mask_test(x.frow, (int)r) && !(h.tgt_cnt > 0 && bit_test(tgt, (int)r)) ? 1 : 0;
     }
     int32_t tot;
     const int32_t off = B.excl_scan(in, &tot);
-    if (in) keys[N + off] = sort_key(0, 0, (int64_t)est_at(x, (int)r), r);
+    if (in) keys[N + off] = sort_key(0, 0, (int64_t)e, r);
     N += tot;
   }
   int T = 0;  // the feasible targets, appended after the others (thread 0: at most kSlowOrdTargets)
@@ -1306,7 +1316,17 @@ KP_FI bool slow_items_from_order(const BLK& B, const KArgs& a, const SelCtx& x, 
       }
       pos += lo;
     }
-    items[pos] = item_from_key(x, k);
+    if (p < N) {  // (no scheduled replicas: allocatable = available = the estimate)
+      Item it;
+      it.rank = key_rank(k);
+      it.alloc = (int32_t)key_avail(k);
+      it.avail = key_avail(k);
+      it.ovf = 0;
+      it.pad = 0;
+      items[pos] = it;
+    } else {
+      items[pos] = item_from_key(x, k);
+    }
   }
   B.sync();
   if (B.tid() == 0) KP_COUNT(x, 54, 1);
