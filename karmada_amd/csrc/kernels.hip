@@ -292,7 +292,7 @@ extern "C" __global__ void __launch_bounds__(kSlowBlock) k_slow(KArgs a, unsigne
 #if KP_K(7)
 {
   KP_SMEM;
-  body_slow(GpuBlkG{(int64_t*)smem}, (int)blockIdx.x, (int)gridDim.x, smem, a, scratch, slot_bytes, cap, lds_area, lds_sort);
+  body_slow(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, (int)gridDim.x, smem, a, scratch, slot_bytes, cap, lds_area, lds_sort);
 }
 #else
 ;

@@ -65,17 +65,10 @@ KP_INLINE T kp_readlane(T v, int l) {
 // primitive needs a single barrier: a thread can only write an area again after
 // passing the next primitive's barrier, which every thread reaches only once it
 // has read the previous contents. Every primitive must be called in block-
-// uniform control flow, in the same sequence by all threads.
-//
-// kGlobal: the workgroup also exchanges data through GLOBAL memory (k_slow's
-// per-workgroup scratch slot, which a workgroup reuses binding after binding).
-// __syncthreads' workgroup-scope fences do not order those accesses on gfx950:
-// a wave read back, after the barrier, the previous binding's candidate entries
-// that another wave of the workgroup had just overwritten (config 8 seed 6,
-// DESIGN.md §2). Every barrier of such a workgroup is bracketed by agent-scope
-// fences (the stores complete, the vector L1 is invalidated).
-template <bool kGlobal = false>
-struct GpuBlkT {
+// uniform control flow, in the same sequence by all threads. Workgroup-scope
+// barriers also order the workgroup's exchanges through global memory (k_slow's
+// scratch slot): its waves share one CU's vector L1, which the stores write through.
+struct GpuBlk {
   int64_t* red;  // kRedBytes of LDS
   mutable int ph = 0;
 
@@ -84,15 +77,7 @@ struct GpuBlkT {
   KP_INLINE int lane() const { return (int)(threadIdx.x & 63); }
   KP_INLINE int wid() const { return (int)(threadIdx.x >> 6); }
   KP_INLINE int nwaves() const { return (int)(blockDim.x >> 6); }
-  KP_INLINE void sync() const {
-    if constexpr (kGlobal) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    } else {
-      __syncthreads();
-    }
-  }
+  KP_INLINE void sync() const { __syncthreads(); }
   KP_INLINE int64_t* area() const {
     int64_t* a = red + (ph ? 64 : 0);
     ph ^= 1;
@@ -303,8 +288,6 @@ struct GpuBlkT {
     return (T)a[0];
   }
 };
-using GpuBlk = GpuBlkT<false>;
-using GpuBlkG = GpuBlkT<true>;  // k_slow: global-memory exchanges (see kGlobal)
 
 // Block policy of ONE wave64 working alone (several such "blocks" share a
 // workgroup, each on its own binding and LDS slice): every reduction and scan is

@@ -155,6 +155,10 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   KP_STAMP(x, 9);
   KP_COUNT(x, 15, 1);
   if (pre_checks(B, x, (int)F)) return;
+#if defined(KP_TOP_EXIT) && KP_TOP_EXIT == 1  // timing experiments only: phases cut off (wrong results)
+  if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, 0);
+  return;
+#endif
   // the scheduled clusters among the candidates (spec.Clusters ∩ feasible): always
   // in the subset, with the votes the division gives them
   const bool fresh = (fl & BF_FRESH) != 0;
@@ -281,13 +285,18 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
       // t*: no seat, no tie (#{k : v/(2k+1) > vmin} = ((v-1)/vmin + 1)/2 for v > vmin,
       // integers; float64 priorities order the same way for votes below 2^31). The rule
       // is pinned against the reference heap in tests/test_cpusim_units.py.
-      if (!agg && cnt > 0 && vmin > 0 && tsum + wsum >= (int64_t)target) {
+      // The count is bounded by (S / vmin + n) / 2 (S = the subset's vote sum), so the
+      // exact pass runs only once the bound reaches the target; votes stay below 2^30
+      // (eligibility), so it divides in 32 bits.
+      if (!agg && cnt > 0 && vmin > 0 && tsum + wsum >= (int64_t)target &&
+          (int64_t)((double)(tsum + wsum) / (double)vmin) / 2 + n / 2 + 2 >= (int64_t)target) {
         B.wsync();  // this chunk's subset entries, written by their lanes, before the reads
+        const uint32_t vm = (uint32_t)vmin;
         int64_t above = 0;
         for (int q = lane; q < n; q += ww) {
-          int64_t vq = cd.v[q];
-          if (q < n0 && fresh) vq += sched_rep_of(x, cd.r[q]);
-          above += vq > vmin ? ((vq - 1) / vmin + 1) / 2 : 0;
+          uint32_t vq = (uint32_t)cd.v[q];
+          if (q < n0 && fresh) vq += (uint32_t)sched_rep_of(x, cd.r[q]);
+          above += vq > vm ? ((vq - 1) / vm + 1) / 2 : 0;
         }
         if (B.sum64(above) >= (int64_t)target) break;  // (wave-uniform)
       }
@@ -321,6 +330,10 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     }
   }
   KP_STAMP(x, 11);
+#if defined(KP_TOP_EXIT) && KP_TOP_EXIT == 2
+  if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, n);
+  return;
+#endif
   KP_COUNT(x, 14, n);
   KP_COUNT(x, 40 + (n <= 16 ? 0 : n <= 32 ? 1 : n <= 64 ? 2 : n <= 128 ? 3 : n <= 256 ? 4 : n <= 512 ? 5 : 6), 1);
   KP_COUNT(x, 47 + (agg ? 1 : 0), 1);
