@@ -1451,7 +1451,7 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
       for (int i = B.tid(); i < F; i += B.nth()) pos[sc.an[i]] = i;
       B.sync();
       const SelScratch ss = carve_sel_scratch(sarea, a.s.Cp);
-      const int w2 = sel_all_fast(B, x, PosCands{&cd, pos, B.tid(), B.nth()}, ss);
+      const int w2 = sel_all_fast<true>(B, x, PosCands{&cd, pos, B.tid(), B.nth()}, ss);
       KP_STAMP(x, 52);
       KP_COUNT(x, 53, F);
       B.sync();  // every thread's last read of pos (emit) precedes the reset

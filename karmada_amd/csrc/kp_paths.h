@@ -301,19 +301,27 @@ struct TopInfo {
 // Returns SLOW_NONE when the result (or error) is written, else the reason the
 // binding needs the exact serial path (nothing written).
 // ----------------------------------------------------------------------------
-template <class BLK, class CS>
+// kDynOnly: the caller's bindings are DynamicWeight / Aggregated workloads (k_select_top,
+// k_slow's tie route); anything else returns SLOW_TOP_FULL without writing, and the
+// other strategies' code is not instantiated (k_select_top: 46k -> 20k instructions).
+template <bool kDynOnly = false, class BLK, class CS>
 KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScratch& ss,
                        const TopInfo* top = nullptr) {
   KP_STAMP_INIT
   const BindHdr& h = *x.h;
   const bool desc = (h.flags & BF_UID_DESC) != 0;
   const bool prop = (h.flags & BF_EMPTY_PROP) != 0;
+  const int st = h.strategy;
+  if constexpr (kDynOnly) {
+    if (!(h.flags & BF_WORKLOAD_ASSIGN) || (h.flags & (BF_OVERFLOW | BF_DUP_TARGETS)) ||
+        (st != ST_DYNAMIC && st != ST_AGGREGATED))
+      return SLOW_TOP_FULL;
+  } else {
   if (!(h.flags & BF_WORKLOAD_ASSIGN)) {  // non-workload: all candidates, 0 replicas (common.go:72-82)
     emit_each(B, x, cs, [&](uint32_t, int32_t) { return (int32_t)0; }, true);
     return SLOW_NONE;
   }
   if (h.flags & (BF_OVERFLOW | BF_DUP_TARGETS)) return SLOW_OVERFLOW_DUP;
-  const int st = h.strategy;
   if (st == ST_NONE) {
     if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_UNSUPPORTED_STRATEGY, 0);
     return SLOW_NONE;
@@ -346,6 +354,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
         },
         prop);
     return SLOW_NONE;
+  }
   }
   // Dynamic / Aggregated (assignment.go:213-244)
   // GetSumOfReplicas(scheduledClusters) wraps in int32; the int64 sum taken
@@ -400,6 +409,12 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
     ds.np = pn >> 32;
   }
   ds.valid = true;
+#if defined(KP_TOP_EXIT) && KP_TOP_EXIT == 3  // timing experiments only (wrong results)
+  if (top) {
+    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, ds.vtot);
+    return SLOW_NONE;
+  }
+#endif
   if (top) ds.nparty = top->F;  // the whole TargetClustersList (SLOW_TIE's n > 12 test)
   const int32_t assigned = wrap32(asum);
   const bool anyPriorPos = apos != 0;

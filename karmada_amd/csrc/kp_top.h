@@ -212,12 +212,21 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     const uint64_t* ord = t.ord + (size_t)cls * s.Cp;
     const int lane = B.tid() % B.wwidth();
     const int ww = B.wwidth();
-    // the walk's loads run kTopAhead chunks ahead (a register ring): the class
-    // order is read once, in order, and its L2 latency overlaps the chunk work
+    // The walk takes kTopGroup chunks of the class order per step: their feasibility
+    // tests (LDS lookups of the binding's row) are issued together, their entries are
+    // appended in order, and coverage is decided once per step over the group, with its
+    // smallest walked vote as vmin. A coarser step only adds candidates with votes >= a
+    // smaller vmin to the subset (plus the whole tie group at it), which the subset
+    // argument allows; it divides the dependent reductions and decisions per entry by
+    // kTopGroup. The loads run kTopAhead chunks ahead in a register ring.
 #ifndef KP_TOP_AHEAD
-#define KP_TOP_AHEAD 4
+#define KP_TOP_AHEAD 8
 #endif
-    constexpr int kTopAhead = KP_TOP_AHEAD;
+#ifndef KP_TOP_GROUP
+#define KP_TOP_GROUP 4
+#endif
+    constexpr int kTopAhead = KP_TOP_AHEAD, kTopGroup = KP_TOP_GROUP;
+    static_assert(kTopAhead % kTopGroup == 0, "the ring holds whole groups");
     uint64_t ring[kTopAhead];
 #if defined(__clang__)
 #pragma unroll
@@ -231,52 +240,98 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     const bool cov0 = agg && tsum >= (int64_t)target && psum >= (int64_t)target;
     int i0_last = -B.wwidth();  // (the stamps build counts the walked chunks)
     (void)i0_last;
-    for (int i0 = 0; !cov0; i0 += ww) {
-      i0_last = i0;
-      if (i0 >= s.C) {
+    // Hopeless: every unwalked candidate's vote is at most the last walked one (the
+    // order is votes desc), so once the subset's votes plus vmin times the feasible
+    // candidates not yet walked stay below the target, no candidate set covers it:
+    // dynamicDivideReplicas' availability error (division_algorithm.go:75-78), whose
+    // argument (the votes' sum) one parallel pass below takes instead of walking the
+    // rest of the order. F - n0: the feasible candidates that are not scheduled.
+    const int64_t unsched = F - (int64_t)n0;
+    bool hopeless = false;
+    for (int g0 = 0; !cov0; g0 += kTopGroup * ww) {
+      i0_last = g0 + (kTopGroup - 1) * ww;
+      if (g0 >= s.C) {
         complete = true;
         break;
       }
-      const int i = i0 + lane;
-      const uint64_t e = ring[0];
+      uint32_t rg[kTopGroup];
+      int32_t vg[kTopGroup];
+      uint64_t mg[kTopGroup];
+      bool fg[kTopGroup];
+      bool past = false;
 #if defined(__clang__)
 #pragma unroll
 #endif
-      for (int q = 0; q + 1 < kTopAhead; q++) ring[q] = ring[q + 1];
-      ring[kTopAhead - 1] = i + kTopAhead * ww < s.C ? ord[i + kTopAhead * ww] : 0;
-      bool in = false, past = false;
-      int32_t v = 0;
-      uint32_t r = 0;
-      if (i < s.C) {
-        r = (uint32_t)e;
-        v = (int32_t)(e >> 32);
-        in = ((frow[r >> 6] >> (r & 63)) & 1ull) && !(h->tgt_cnt > 0 && bit_test(tgt, (int)r));
-        if (tie) {
-          past = v < tie_v;
-          in = in && v == tie_v;
+      for (int q = 0; q < kTopGroup; q++) {
+        const uint64_t e = ring[q];
+        rg[q] = (uint32_t)e;
+        vg[q] = (int32_t)(e >> 32);
+        const bool valid = g0 + q * ww + lane < s.C;
+        fg[q] = valid && ((frow[rg[q] >> 6] >> (rg[q] & 63)) & 1ull) && !(h->tgt_cnt > 0 && bit_test(tgt, (int)rg[q]));
+        if (tie && valid) {
+          past = past || vg[q] < tie_v;
+          fg[q] = fg[q] && vg[q] == tie_v;
         }
       }
-      const uint64_t m = B.wballot(in);
+#if defined(__clang__)
+#pragma unroll
+#endif
+      for (int q = 0; q + kTopGroup < kTopAhead; q++) ring[q] = ring[q + kTopGroup];
+#if defined(__clang__)
+#pragma unroll
+#endif
+      for (int q = 0; q < kTopGroup; q++) {
+        const int i = g0 + (kTopAhead + q) * ww + lane;
+        ring[kTopAhead - kTopGroup + q] = i < s.C ? ord[i] : 0;
+      }
+      int cnt = 0, last = -1;
+#if defined(__clang__)
+#pragma unroll
+#endif
+      for (int q = 0; q < kTopGroup; q++) {
+        mg[q] = B.wballot(fg[q]);
+        cnt += popc64(mg[q]);
+        if (mg[q]) last = q;
+      }
       const bool any_past = B.wballot(past) != 0;
-      const int cnt = popc64(m);
       if (n + cnt > t.cap) {
         n += cnt;
         break;
       }
-      if (in) {
-        const int pos = n + popc64(m & B.wlt());
-        cd.r[pos] = r;
-        cd.v[pos] = v;
+      int base = n;
+#if defined(__clang__)
+#pragma unroll
+#endif
+      for (int q = 0; q < kTopGroup; q++) {
+        if (fg[q]) {
+          const int pos = base + popc64(mg[q] & B.wlt());
+          cd.r[pos] = rg[q];
+          cd.v[pos] = vg[q];
+        }
+        base += popc64(mg[q]);
       }
       n += cnt;
       if (tie) {
         if (any_past) break;
         continue;
       }
-      // the chunk's sum (int32: the class row's total is below 2^30) and its smallest
-      // walked vote: the last walked lane's, the order being votes desc
-      const int32_t add = B.wsum32(in ? v : 0);
-      const int32_t vmin = cnt > 0 ? B.wread(v, 63 - __builtin_clzll(m)) : 0;
+      // the group's sum (int32: the class row's total is below 2^30) and its smallest
+      // walked vote: the last walked lane's of its last chunk with one, votes desc
+      int32_t mine = 0;
+#if defined(__clang__)
+#pragma unroll
+#endif
+      for (int q = 0; q < kTopGroup; q++) mine += fg[q] ? vg[q] : 0;
+      const int32_t add = B.wsum32(mine);
+      int32_t vmin = 0;
+      if (cnt > 0) {
+        int32_t vl = vg[0];
+#if defined(__clang__)
+#pragma unroll
+#endif
+        for (int q = 1; q < kTopGroup; q++) vl = last == q ? vg[q] : vl;
+        vmin = B.wread(vl, 63 - __builtin_clzll(mg[last]));
+      }
       walked += cnt;
       wsum += add;
       // DynamicWeight: the subset (scheduled clusters + every walked party) holds at
@@ -290,12 +345,12 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
       // (eligibility), so it divides in 32 bits.
       if (!agg && cnt > 0 && vmin > 0 && tsum + wsum >= (int64_t)target &&
           (int64_t)((double)(tsum + wsum) / (double)vmin) / 2 + n / 2 + 2 >= (int64_t)target) {
-        B.wsync();  // this chunk's subset entries, written by their lanes, before the reads
+        B.wsync();  // this group's subset entries, written by their lanes, before the reads
         const uint32_t vm = (uint32_t)vmin;
         int64_t above = 0;
-        for (int q = lane; q < n; q += ww) {
-          uint32_t vq = (uint32_t)cd.v[q];
-          if (q < n0 && fresh) vq += (uint32_t)sched_rep_of(x, cd.r[q]);
+        for (int j = lane; j < n; j += ww) {
+          uint32_t vq = (uint32_t)cd.v[j];
+          if (j < n0 && fresh) vq += (uint32_t)sched_rep_of(x, cd.r[j]);
           above += vq > vm ? ((vq - 1) / vm + 1) / 2 : 0;
         }
         if (B.sum64(above) >= (int64_t)target) break;  // (wave-uniform)
@@ -307,10 +362,14 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
       if (cov) {  // then the rest of the tie group at the last (smallest) vote
         tie = true;
         tie_v = vmin;
+      } else if (cnt > 0 && (int64_t)target < kSeatWrap &&
+                 tsum + wsum + (int64_t)vmin * (unsched - walked) < (int64_t)target) {
+        hopeless = true;
+        break;
       }
     }
     KP_COUNT(x, 13, (i0_last + B.wwidth()) / B.wwidth());
-    if (n > t.cap) {
+    if (n > t.cap || hopeless) {
       // Past capacity before covering the target: when every candidate's votes together
       // stay below it, the answer is dynamicDivideReplicas' availability error
       // (division_algorithm.go:75-78; the sum cannot wrap: the class total is below
@@ -340,7 +399,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   cd.F = n;
   B.sync();
   const TopInfo ti{F, complete};
-  const int why = sel_all_fast(B, x, LdsCands{&cd, B.tid(), B.nth()}, ss, &ti);
+  const int why = sel_all_fast<true>(B, x, LdsCands{&cd, B.tid(), B.nth()}, ss, &ti);
   KP_STAMP(x, 12);
   if (why == SLOW_TOP_FULL) top_fallback(B, a, t, b);
   else if (why != SLOW_NONE && B.tid() == 0) flag_slow(a, b, why);
