@@ -341,6 +341,7 @@ struct kp_snapshot {
   SnapView view{};
 };
 
+constexpr int kDbgSlots = 96;  // diagnostic builds: phase stamps and counters (kp_select.h)
 struct kp_batch {
   kp_snapshot* snap = nullptr;
   int B = 0;
@@ -2734,7 +2735,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->counter, 1);
   a.add(&bt->stats, 16);
 #if defined(KP_STAMPS) || defined(KP_SLOW_CHECK)
-  a.add(&bt->dbg, 64);
+  a.add(&bt->dbg, kDbgSlots);
 #endif
   // [0, out_cap): per-binding slots; [out_cap, 2 out_cap): serial results past their slot
   a.add(&bt->out_idx, std::max<uint64_t>(1, 2 * bt->out_cap));
@@ -2996,7 +2997,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   ka.slow_ids = bt->d_slowlist;
   ka.dbg = bt->dbg;
 #if defined(KP_STAMPS) || defined(KP_SLOW_CHECK)
-  HIPCHK(dev::fill(bt->dbg, 0, 64 * 8, st));
+  HIPCHK(dev::fill(bt->dbg, 0, kDbgSlots * 8, st));
 #endif
   dev::stream_t sp = e->stream2;
   HIPCHK(dev::event_record(e->ev[0], st));
@@ -3364,11 +3365,11 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   tm.n_region_order = spread_orders ? bt->h_stats[11] : 0u;
 #if defined(KP_STAMPS) || defined(KP_SLOW_CHECK)
   {
-    unsigned long long h[64];
+    unsigned long long h[kDbgSlots];
     HIPCHK(dev::d2h(h, bt->dbg, sizeof(h), st));
     HIPCHK(dev::sync(st));
     fprintf(stderr, "kp stamps (s_memtime ticks, summed over workgroups):");
-    for (int i = 0; i < 64; i++)
+    for (int i = 0; i < kDbgSlots; i++)
       if (h[i]) fprintf(stderr, " [%d]=%llu", i, h[i]);
     fprintf(stderr, "\n");
   }

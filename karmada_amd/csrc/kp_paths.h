@@ -558,6 +558,10 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
     }
   }
   KP_STAMP(x, 3);
+#if defined(KP_TOP_EXIT) && KP_TOP_EXIT == 5  // timing experiments only (wrong results)
+  if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, vstar);
+  return SLOW_NONE;
+#endif
   auto member = [&](uint32_t rk, int64_t v, int32_t v0) {
     if (st != ST_AGGREGATED) return true;
     const bool p = prior(rk);
@@ -577,6 +581,10 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
   const WebPre wp{pre ? pre->vtot : 0, pre ? pre->vmax : 0, pre ? pre->P : 0};
   WebRes w = webster_par(B, parties, target, desc, ss, pre && st != ST_AGGREGATED ? &wp : nullptr);
   KP_STAMP(x, 4);
+#if defined(KP_TOP_EXIT) && KP_TOP_EXIT == 4
+  if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, (int64_t)w.tie);
+  return SLOW_NONE;
+#endif
   if (w.mode == 2 && w.compact && !prop) {
     // Only parties take seats, and every party with a seat is in Webster's compacted
     // list (votes >= Lb <= t*): emit from it, plus the prior targets outside it

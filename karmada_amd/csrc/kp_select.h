@@ -794,7 +794,7 @@ KP_FI WebRes webster_tail(const BLK& B, WebRes r, Parties parties, double tstar,
   r.Lb = Lb;
   r.pl = pl;
   KP_STAMP_INIT
-  KP_STAMPD(sc.dbg, 12);
+  KP_STAMPD(sc.dbg, 67);
   // seats strictly above t*, then the tie group at t* ordered by (k asc, name)
   int64_t S = 0, T = 0;
   const double rts = 1.0 / tstar;
@@ -805,7 +805,7 @@ KP_FI WebRes webster_tail(const BLK& B, WebRes r, Parties parties, double tstar,
   });
   B.sum2(S, T);
   const int64_t M = (int64_t)N - S;
-  KP_STAMPD(sc.dbg, 13);
+  KP_STAMPD(sc.dbg, 68);
   if (M >= T) {
     r.tie = ~0ull;
   } else if (T <= (int64_t)ecap) {
@@ -837,7 +837,7 @@ KP_FI WebRes webster_tail(const BLK& B, WebRes r, Parties parties, double tstar,
     }
     r.tie = tlo;
   }
-  KP_STAMPD(sc.dbg, 14);
+  KP_STAMPD(sc.dbg, 69);
   B.sync();  // buf[0, 64) / whist are free again for the caller; pl stays
   return r;
 }
@@ -932,7 +932,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
       });
     }
   };
-  KP_STAMPD(sc.dbg, 9);
+  KP_STAMPD(sc.dbg, 64);
   const int64_t capN = (int64_t)N;
   // Every seat a first seat: with P >= N parties of positive votes and the largest
   // vote below 3 v_N (v_N = the N-th largest vote), every second priority vmax/3 is
@@ -1000,7 +1000,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     }
     if (clo < 0) clo = cnt1(bitsd(lo));
   }
-  KP_STAMPD(sc.dbg, 10);
+  KP_STAMPD(sc.dbg, 65);
   while (hi - lo > 1 && clo - chi > (int64_t)ecap) {
     uint64_t mid = lo + (hi - lo) / 2;
     int64_t c = cnt1(bitsd(mid));
@@ -1012,7 +1012,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
       chi = c;
     }
   }
-  KP_STAMPD(sc.dbg, 11);
+  KP_STAMPD(sc.dbg, 66);
   double tstar;
   if (hi - lo <= 1) {
     tstar = bitsd(lo);
