@@ -888,7 +888,8 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   const int pcap = sc.cap > 64 ? sc.cap - 64 : 0;
   uint64_t* pl = sc.buf + 64;
   int64_t Lb = 1;
-  if (P > (int64_t)N) {  // lower edge of the octave bin holding the N-th largest vote
+  // (few parties: all of them go to the list, where the quota search below needs no Lb)
+  if (P > (int64_t)N && (P > (int64_t)ecap || pcap < ecap)) {  // lower edge of the octave bin holding the N-th largest vote
     int64_t before;
     Lb = vote_bin_floor(B.find_bin(sc.hist, (int64_t)N, &before, true));
   }
@@ -934,6 +935,57 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   };
   KP_STAMPD(sc.dbg, 64);
   const int64_t capN = (int64_t)N;
+  // Few parties (the compacted list fits the enumeration area): t* by adjusting the
+  // quota counts. At t0 = V / 2N each party holds s = #{k : prio(v, k) >= t0} =
+  // floor(N v / V + 1/2) <= N priorities, within np/2 of N in total. With C of them,
+  // t* (the N-th largest priority) is found by dropping the C - N smallest held ones
+  // (each party's smallest held priority is prio(v, s - 1)) or adding the N - C
+  // largest next ones (prio(v, s)), one block-wide min or max per step. Parties
+  // below Lb hold no priority >= t* (t* >= the N-th largest vote >= Lb, or Lb = 1),
+  // so the list decides t*. The held counts live in buf[0, np) until webster_tail.
+  if (compact && np > 0 && np <= ecap) {
+    constexpr int64_t kAdjMax = 64;
+    const double t0 = (double)V / (2.0 * (double)N);
+    int64_t C = 0;
+    for (int i = B.tid(); i < np; i += B.nth()) {
+      const int64_t s = w_count((int64_t)(uint32_t)pl[i], t0, capN + 1, true);
+      sc.buf[i] = (uint64_t)s;
+      C += s;
+    }
+    C = B.sum64(C);  // (its barrier also orders the counts before the steps read them)
+    const int64_t steps = C >= (int64_t)N ? C - (int64_t)N : (int64_t)N - C;
+    if (steps <= kAdjMax) {
+      const bool drop = C >= (int64_t)N;
+      double tstar = 0;
+      for (int64_t left = steps;; left--) {
+        // this thread's best held (drop: smallest) or next (add: largest) priority
+        uint64_t best = drop ? ~0ull : 0ull;
+        int64_t bi = INT64_MAX;
+        for (int i = B.tid(); i < np; i += B.nth()) {
+          const int64_t v = (int64_t)(uint32_t)pl[i], s = (int64_t)sc.buf[i];
+          if (drop && s == 0) continue;
+          const uint64_t p = kp_dbits(w_prio(v, drop ? s - 1 : s));  // positive doubles order as their bits
+          if (drop ? p < best : p > best) {
+            best = p;
+            bi = i;
+          }
+        }
+        const uint64_t ext = drop ? B.minu64(best) : (uint64_t)B.max64((int64_t)best);
+        if (drop && left == 0) {
+          tstar = kp_bitsd(ext);
+          break;
+        }
+        const int64_t win = B.min64(best == ext ? bi : INT64_MAX);  // one party holding it
+        if (win != INT64_MAX && win % B.nth() == B.tid()) sc.buf[win] += drop ? ~0ull : 1ull;
+        if (!drop && left == 1) {
+          tstar = kp_bitsd(ext);
+          break;
+        }
+      }
+      B.sync();  // every step's reads of buf precede webster_tail's use of it
+      return webster_tail(B, r, parties, tstar, N, desc, sc, ecap, compact, np, Lb, pl);
+    }
+  }
   // Every seat a first seat: with P >= N parties of positive votes and the largest
   // vote below 3 v_N (v_N = the N-th largest vote), every second priority vmax/3 is
   // below v_N (exactly: fl(vmax/3) < v_N by far more than its rounding), so the N

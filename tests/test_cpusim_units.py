@@ -80,6 +80,36 @@ def test_webster_par_matches_reference_heap(seed):
 
 
 @pytest.mark.parametrize("seed", range(4))
+def test_webster_quota_adjust(seed):
+    """webster_par's few-party search (compacted list within the enumeration area): t*
+    from the quota counts at V/2N, adjusted by dropping or adding single priorities; ties
+    across parties at t*, N far above and below the party count, one dominant party."""
+    rng = random.Random(500 + seed)
+    for _ in range(150):
+        n = rng.randint(1, 64)
+        kind = rng.choice(["uniform", "ties", "narrow", "one-big", "tiny"])
+        if kind == "uniform":
+            v = [rng.randint(1, 5000) for _ in range(n)]
+        elif kind == "ties":
+            v = [rng.choice([6, 10, 30, 42]) for _ in range(n)]
+        elif kind == "narrow":
+            lo = rng.randint(1, 300)
+            v = [rng.randint(lo, lo + 3) for _ in range(n)]
+        elif kind == "one-big":
+            v = [rng.randint(1, 3) for _ in range(n)]
+            v[rng.randrange(n)] = rng.randint(1000, 100000)
+        else:
+            v = [rng.randint(0, 2) for _ in range(n)]
+        if sum(v) == 0:
+            continue
+        N = rng.choice([1, 2, n // 2 + 1, n, n + 1, 3 * n, 97, 1000, 20000])
+        desc = rng.random() < 0.5
+        want = oracle_webster(v, N, desc)
+        for ecap in (64, 256):
+            assert sim_webster(v, N, desc, ecap) == want, (v, N, desc, ecap)
+
+
+@pytest.mark.parametrize("seed", range(4))
 def test_webster_first_seat_case(seed):
     """webster_par's first-seat case (P >= N and vmax < 3 v_N: t* = v_N from a rank select
     of the compacted list): votes in a narrow band, ties at v_N, and the boundary vmax =
