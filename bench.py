@@ -484,16 +484,20 @@ def main():
     kernels.sort(key=lambda x: -x["ms"])
     cands = [(k["kernel"], k["ms"], k["bytes"]) for k in kernels] or [("step", ms_per_step, pair_b + sel_b)]
     kname, kms, kbytes = max(cands, key=lambda x: x[1])
+    klaunch = next((k["launches"] for k in kernels if k["kernel"] == kname), 1) or 1
     achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     profiled = (C_, B) == tuple(synth.CONFIGS[cfg])
     pmc = load_pmc(cfg, kname) if profiled else None
 
+    # the PMC summary holds per-launch averages; the kernel's time and bytes here cover
+    # all its launches in a step (k_select_top: two), so both sides are per step
     def pmc_frac(key, peak):
         if not pmc or not pmc.get(key) or kms <= 0:
             return None
-        return round(pmc[key] / (kms * 1e-3) / 1e9 / peak, 4)
+        return round(pmc[key] * klaunch / (kms * 1e-3) / 1e9 / peak, 4)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc.get("hbm_bytes") if pmc else None,
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": round(pmc["hbm_bytes"] * klaunch) if pmc and pmc.get("hbm_bytes") else None,
             "kernel": kname, "kernel_ms": round(kms, 4), "algorithmic_bytes": round(kbytes),
             "dram_frac": pmc_frac("hbm_bytes", HBM_PEAK_GBS), "valu_frac": pmc_frac("valu_insts", VALU_PEAK_GINST)}
     step_bytes = pair_b + sel_b

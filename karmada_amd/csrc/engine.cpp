@@ -3089,7 +3089,8 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       HIPCHK(dev::event_record(e->ev[12], sp));
       // the two slices' launches run concurrently, the large one on stream3 (which the
       // cluster-spread kernels use after it), so neither drains the CUs alone
-      const bool split = e->top_split && bt->n_top_small > 0 && bt->n_all_dyn > bt->n_top_small;
+      // (profiled steps keep both on one stream: each launch's HIP-event time is then its own)
+      const bool split = e->top_split && !e->prof && bt->n_top_small > 0 && bt->n_all_dyn > bt->n_top_small;
       for (int part = 0; part < 2; part++) {
         KArgs g = k;
         const int cap_p = part == 0 ? top_cap_small : top_cap;

@@ -102,6 +102,15 @@ KP_FI void top_fallback(const BLK& B, const KArgs& a, const TopArgs& t, int b) {
   if (B.tid() == 0) t.fb[kp_atomic_add(t.fb_n, 1u)] = b;
 }
 
+#ifndef KP_TOP_AHEAD
+#define KP_TOP_AHEAD 8
+#endif
+#ifndef KP_TOP_GROUP
+#define KP_TOP_GROUP 4
+#endif
+constexpr int kTopAhead = KP_TOP_AHEAD, kTopGroup = KP_TOP_GROUP;
+static_assert(kTopAhead % kTopGroup == 0, "the ring holds whole groups");
+
 template <class BLK>
 KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KArgs& a, const TopArgs& t) {
   if (blk >= a.n) return;
@@ -114,6 +123,16 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   const uint32_t fl = h->flags;
   const int st = h->strategy;
   const int32_t cls = a.bcls ? a.bcls[b] : 0;
+  // the first chunks of the class order, loaded with the binding's header and row (the
+  // walk is the first to read them; a binding that does not walk wastes a few L2 hits)
+  const uint64_t* ord = t.ord + (size_t)cls * s.Cp;
+  const int lane = B.tid() % B.wwidth();
+  const int ww = B.wwidth();
+  uint64_t ring[kTopAhead];
+#if defined(__clang__)
+#pragma unroll
+#endif
+  for (int q = 0; q < kTopAhead; q++) ring[q] = lane + q * ww < s.C ? ord[lane + q * ww] : 0;
   bool elig = a.bcls != nullptr && h->sel == SEL_ALL && (st == ST_DYNAMIC || st == ST_AGGREGATED) &&
               (fl & BF_WORKLOAD_ASSIGN) && !(fl & (BF_EMPTY_PROP | BF_BAD | BF_DUP_TARGETS | BF_OVERFLOW)) &&
               h->ovf_mode == OVF_ZERO && h->replicas > 0 && t.ok[cls] != 0;
@@ -209,29 +228,14 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
         if (h->tgt_cnt > 0 && sched_rep_of(x, cd.r[i]) > 0) psum += cd.v[i];
       psum = B.sum64(psum);
     }
-    const uint64_t* ord = t.ord + (size_t)cls * s.Cp;
-    const int lane = B.tid() % B.wwidth();
-    const int ww = B.wwidth();
     // The walk takes kTopGroup chunks of the class order per step: their feasibility
     // tests (LDS lookups of the binding's row) are issued together, their entries are
     // appended in order, and coverage is decided once per step over the group, with its
     // smallest walked vote as vmin. A coarser step only adds candidates with votes >= a
     // smaller vmin to the subset (plus the whole tie group at it), which the subset
     // argument allows; it divides the dependent reductions and decisions per entry by
-    // kTopGroup. The loads run kTopAhead chunks ahead in a register ring.
-#ifndef KP_TOP_AHEAD
-#define KP_TOP_AHEAD 8
-#endif
-#ifndef KP_TOP_GROUP
-#define KP_TOP_GROUP 4
-#endif
-    constexpr int kTopAhead = KP_TOP_AHEAD, kTopGroup = KP_TOP_GROUP;
-    static_assert(kTopAhead % kTopGroup == 0, "the ring holds whole groups");
-    uint64_t ring[kTopAhead];
-#if defined(__clang__)
-#pragma unroll
-#endif
-    for (int q = 0; q < kTopAhead; q++) ring[q] = lane + q * ww < s.C ? ord[lane + q * ww] : 0;
+    // kTopGroup. The loads run kTopAhead chunks ahead in a register ring (its first
+    // loads were issued with the binding's own, above).
     int64_t walked = 0, wsum = 0;
     const int32_t n0 = n;  // the scheduled clusters lead the subset
     bool tie = false;
