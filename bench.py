@@ -359,6 +359,7 @@ def main():
             r = batch.schedule_raw()
             st_ser.append(eng.stage_times())
         barrier_sync()
+        serial_ms = 1e3 * (time.perf_counter() - t1) / n_ser
         # then every kernel of the step timed by its own HIP event pair (on the stream it
         # runs on), one batch at a time, for the per-kernel ranking and the roofline
         eng.set_profile(True)
@@ -368,7 +369,6 @@ def main():
             kt_runs.append(eng.kernel_times())
         eng.set_profile(False)
         st_all = st_ser  # per-stage HIP event times without another batch's kernels beside them
-        serial_ms = 1e3 * (time.perf_counter() - t1) / n_ser
         if dist is not None:
             import torch
             t = torch.tensor([serial_ms], dtype=torch.float64, device=tdev)
