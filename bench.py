@@ -80,7 +80,7 @@ def kernel_bytes(name, units, Cp, n_classes, n_bind, n_targets, snap_bytes, R):
         return units * rec
     if name == "k_class_order":
         return 12.0 * Cp * units
-    if name == "k_select_top":
+    if name in ("k_select_top", "k_select_top_wg"):
         return units * (rec + 28) + 12.0 * Cp * n_classes + 8.0 * share
     if name == "k_select_static":
         return units * (rec + 28) + 8.0 * share

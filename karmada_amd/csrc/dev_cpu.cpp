@@ -224,6 +224,12 @@ int select_top(stream_t, const KArgs& a, const TopArgs& t, size_t slice) {
   grid(a.n, slice, [&](int blk, unsigned char* sm) { body_select_top(CpuBlk{(int64_t*)sm}, blk, sm, a, t); });
   return 0;
 }
+int select_top_wg(stream_t, const KArgs& a, const TopArgs& t, size_t smem) {
+  grid(a.n, smem, [&](int blk, unsigned char* sm) {
+    body_select_top_wg(CpuBlk{(int64_t*)sm}, CpuBlk{(int64_t*)top_wg_slice(sm)}, blk, sm, a, t);
+  });
+  return 0;
+}
 
 int region_groups(stream_t, const RegionOut* rout, const int32_t* rstat, const BindHdr* hdr, const int32_t* list,
                   int n, int R, int32_t* rsel, int32_t* rnsel, uint32_t* nhost) {

@@ -304,6 +304,7 @@ struct kp_engine {
   int top_cap_small = 256;  // ... and of the small one (bindings needing <= kTopSmallNeed)
   bool top_split = true;    // the two slices' launches on two streams (KP_TOP_SPLIT=0: one)
   bool slow_order = true;   // k_slow orders candidates from the class orders (KP_SLOW_ORDER=0: sorts)
+  bool top_wg = true;       // large-subset bindings on k_select_top_wg (KP_TOP_WG=0: the one-wave kernel)
   // per-kernel timing of kp_schedule_batch (kp_engine_set_profile): an event pair
   // around every launch on its own stream, folded by kernel name after the batch
   struct KProf {
@@ -1928,6 +1929,7 @@ int kp_engine_create(int device, kp_engine** out) {
   if (const char* v = getenv("KP_TOP")) e->top_on = atoi(v) != 0;
   if (const char* v = getenv("KP_TOP_SPLIT")) e->top_split = atoi(v) != 0;
   if (const char* v = getenv("KP_SLOW_ORDER")) e->slow_order = atoi(v) != 0;
+  if (const char* v = getenv("KP_TOP_WG")) e->top_wg = atoi(v) != 0;
   if (const char* v = getenv("KP_TOP_CAP")) {  // (tests: one capacity for both slices)
     e->top_cap = std::max(64, std::min(1024, atoi(v) & ~63));
     e->top_cap_small = std::min(e->top_cap_small, e->top_cap);
@@ -3101,7 +3103,12 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
         const size_t slice = (top_lds_bytes(s->Cp, cap_p) + 15) & ~(size_t)15;
         dev::stream_t sx_ = split && part == 1 ? e->stream3 : sp;
         if (split && part == 1) HIPCHK(dev::stream_wait(sx_, e->ev[4]));
-        KPROF(sx_, "k_select_top", g.n, -1, dev::select_top(sx_, g, ta, slice));
+        // the large-subset bindings: a workgroup each (wave 0 walks, the workgroup divides)
+        const size_t wg_lds = (top_wg_lds_bytes(s->Cp, cap_p) + 15) & ~(size_t)15;
+        if (part == 1 && e->top_wg && wg_lds <= e->max_lds)
+          KPROF(sx_, "k_select_top_wg", g.n, -1, dev::select_top_wg(sx_, g, ta, wg_lds));
+        else
+          KPROF(sx_, "k_select_top", g.n, -1, dev::select_top(sx_, g, ta, slice));
         if (split && part == 1) {
           HIPCHK(dev::event_record(e->ev[10], sx_));
           HIPCHK(dev::stream_wait(sp, e->ev[10]));  // both slices' fallbacks precede k_select_all

@@ -165,6 +165,16 @@ extern "C" __global__ void __launch_bounds__(64 * kTopWaves, KP_TOP_MIN_WAVES) k
 #else
 ;
 #endif
+// The large-subset bindings: one workgroup each, wave 0 walks, the workgroup divides.
+extern "C" __global__ void __launch_bounds__(64 * kTopWgWaves) k_select_top_wg(KArgs a, TopArgs t)
+#if KP_K(4)
+{
+  KP_SMEM;
+  body_select_top_wg(GpuBlk{(int64_t*)smem}, WaveBlk{(int64_t*)top_wg_slice(smem)}, (int)blockIdx.x, smem, a, t);
+}
+#else
+;
+#endif
 // StaticWeight SEL_ALL at class level (kp_kernels.h body_select_static): one wave per
 // binding, kStaticWaves independent waves per workgroup.
 extern "C" __global__ void __launch_bounds__(64 * kStaticWaves) k_select_static(KArgs a, int slice)
@@ -602,6 +612,15 @@ int select_top(stream_t st, const KArgs& a, const TopArgs& t, size_t slice) {
     return -1;
   hipLaunchKernelGGL(k_select_top, dim3((a.n + kTopWaves - 1) / kTopWaves), dim3(64 * kTopWaves), smem,
                      (hipStream_t)st, a, t, (int)slice);
+  return chk(hipGetLastError());
+}
+
+int select_top_wg(stream_t st, const KArgs& a, const TopArgs& t, size_t smem) {
+  if (a.n <= 0) return 0;
+  if (smem > 65536 &&
+      chk(hipFuncSetAttribute((const void*)k_select_top_wg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)))
+    return -1;
+  hipLaunchKernelGGL(k_select_top_wg, dim3(a.n), dim3(64 * kTopWgWaves), smem, (hipStream_t)st, a, t);
   return chk(hipGetLastError());
 }
 

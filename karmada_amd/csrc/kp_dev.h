@@ -74,6 +74,8 @@ int class_order(stream_t st, const SnapView& s, const int32_t* rows, int n_rows,
 // candidates (body_select_top), `slice` bytes of LDS per binding; the others are
 // appended to t.fb.
 int select_top(stream_t st, const KArgs& a, const TopArgs& t, size_t slice);
+// k_select_top_wg: one workgroup per binding (the large-subset bindings), smem = top_wg_lds_bytes
+int select_top_wg(stream_t st, const KArgs& a, const TopArgs& t, size_t smem);
 // selectGroups for n region bindings (one thread each): rsel/rnsel as the host
 // step writes them; *nhost counts the bindings left to the host (kGroupsHost).
 int region_groups(stream_t st, const RegionOut* rout, const int32_t* rstat, const BindHdr* hdr, const int32_t* list,

@@ -62,6 +62,7 @@ constexpr int kBlock = 256;
 constexpr int kSlowBlock = 512;  // k_slow: wider for the LDS bitonic sort
 // waves per workgroup of the one-wave-per-binding kernels (each wave its own LDS slice)
 constexpr int kTopWaves = 2;     // k_select_top (small workgroups: LDS is granted per workgroup)
+constexpr int kTopWgWaves = 4;   // k_select_top_wg: one binding per workgroup of this many waves
 constexpr int kStaticWaves = 4;  // k_select_static
 constexpr int kOrderWaves = 4;   // k_spread_order, k_region_a_order
 constexpr int kPairStage = 4096;  // bytes of per-binding predicate data staged in LDS

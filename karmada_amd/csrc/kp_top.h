@@ -111,8 +111,41 @@ KP_FI void top_fallback(const BLK& B, const KArgs& a, const TopArgs& t, int b) {
 constexpr int kTopAhead = KP_TOP_AHEAD, kTopGroup = KP_TOP_GROUP;
 static_assert(kTopAhead % kTopGroup == 0, "the ring holds whole groups");
 
+// Hand-off of a binding from wave 0's walk to its workgroup's selection (k_select_top_wg).
+struct TopHand {
+  int32_t go, n, complete, pad;
+  int64_t F;
+};
+
+// The LDS slice of one binding: [red 64 B | frow W u64 | tgt bits | S ranks cap | S votes cap |
+// SelScratch], carved the same way by every wave that reads it.
+struct TopCarve {
+  uint64_t* frow;
+  uint32_t* tgt;
+  Cands cd;
+  SelScratch ss;
+};
+KP_HD inline TopCarve top_carve(unsigned char* smem, const SnapView& s, int cap, unsigned long long* dbg) {
+  const int words = (s.Cp + 31) >> 5;
+  TopCarve c;
+  unsigned char* p = smem + 64;
+  c.frow = (uint64_t*)p;
+  p += 8 * (size_t)s.W;
+  c.tgt = (uint32_t*)p;
+  p += 4 * (size_t)((words + 3) & ~3);
+  c.cd.r = (uint32_t*)p;
+  c.cd.v = (int32_t*)(c.cd.r + cap);
+  c.ss = carve_sel_scratch((unsigned char*)(c.cd.v + cap), 2 * cap);
+  c.ss.cap = top_ecap(cap);
+  c.ss.dbg = dbg;
+  return c;
+}
+
+// hand: wave 0 of a k_select_top_wg workgroup stops after the walk and leaves the
+// selection to the whole workgroup (the subset is in the slice, the counts in *hand).
 template <class BLK>
-KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KArgs& a, const TopArgs& t) {
+KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KArgs& a, const TopArgs& t,
+                           TopHand* hand = nullptr) {
   if (blk >= a.n) return;
   KP_STAMP_INIT
   const int b = a.list[blk];
@@ -148,18 +181,11 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     top_fallback(B, a, t, b);
     return;
   }
-  // LDS carve
-  unsigned char* p = smem + 64;
-  uint64_t* frow = (uint64_t*)p;
-  p += 8 * (size_t)s.W;
-  uint32_t* tgt = (uint32_t*)p;
-  p += 4 * (size_t)((words + 3) & ~3);
-  Cands cd;
-  cd.r = (uint32_t*)p;
-  cd.v = (int32_t*)(cd.r + t.cap);
-  SelScratch ss = carve_sel_scratch((unsigned char*)(cd.v + t.cap), 2 * t.cap);
-  ss.cap = top_ecap(t.cap);
-  ss.dbg = a.dbg;
+  TopCarve tc = top_carve(smem, s, t.cap, a.dbg);
+  uint64_t* frow = tc.frow;
+  uint32_t* tgt = tc.tgt;
+  Cands cd = tc.cd;
+  SelScratch ss = tc.ss;
   SelCtx x = make_ctx(a, b, tgt);
   // (every read of the target bitset is behind tgt_cnt > 0)
   if (h->tgt_cnt > 0) build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
@@ -402,11 +428,45 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   KP_COUNT(x, 47 + (agg ? 1 : 0), 1);
   cd.F = n;
   B.sync();
+  if (hand) {
+    if (B.tid() == 0) *hand = TopHand{1, n, complete ? 1 : 0, 0, F};
+    return;
+  }
   const TopInfo ti{F, complete};
   const int why = sel_all_fast<true>(B, x, LdsCands{&cd, B.tid(), B.nth()}, ss, &ti);
   KP_STAMP(x, 12);
   if (why == SLOW_TOP_FULL) top_fallback(B, a, t, b);
   else if (why != SLOW_NONE && B.tid() == 0) flag_slow(a, b, why);
+}
+
+// k_select_top_wg: one workgroup of kTopWgWaves waves per binding for the bindings that
+// need a large subset (the second launch): wave 0 runs the walk exactly as the one-wave
+// kernel does, then the whole workgroup runs the division over the subset, whose passes
+// (Webster over hundreds of parties) dominate such a binding. LDS: [GpuBlk red |
+// TopHand 64 B | the one-wave slice].
+KP_HD inline size_t top_wg_lds_bytes(int Cp, int cap) { return kRedBytes + 64 + top_lds_bytes(Cp, cap); }
+// W: wave 0's block policy over the slice (its red area = the slice's first 64 B).
+KP_HD inline unsigned char* top_wg_slice(unsigned char* smem) { return smem + kRedBytes + 64; }
+template <class GBLK, class WBLK>
+KP_FI void body_select_top_wg(const GBLK& G, const WBLK& W, int blk, unsigned char* smem, const KArgs& a,
+                              const TopArgs& t) {
+  if (blk >= a.n) return;  // (block-uniform)
+  TopHand* hand = (TopHand*)(smem + kRedBytes);
+  unsigned char* slice = top_wg_slice(smem);
+  if (G.tid() == 0) hand->go = 0;
+  if (G.wid() == 0) body_select_top(W, blk, slice, a, t, hand);
+  G.sync();
+  const TopHand hh = *hand;
+  if (!hh.go) return;  // wave 0 wrote the result or handed the binding on
+  const int b = a.list[blk];
+  TopCarve tc = top_carve(slice, a.s, t.cap, a.dbg);
+  SelCtx x = make_ctx(a, b, tc.tgt);
+  x.frow = tc.frow;
+  tc.cd.F = hh.n;
+  const TopInfo ti{hh.F, hh.complete != 0};
+  const int why = sel_all_fast<true>(G, x, LdsCands{&tc.cd, G.tid(), G.nth()}, tc.ss, &ti);
+  if (why == SLOW_TOP_FULL) top_fallback(G, a, t, b);
+  else if (why != SLOW_NONE && G.tid() == 0) flag_slow(a, b, why);
 }
 
 }  // namespace kp
