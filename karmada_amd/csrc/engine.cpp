@@ -304,7 +304,7 @@ struct kp_engine {
   int top_cap_small = 256;  // ... and of the small one (bindings needing <= kTopSmallNeed)
   bool top_split = true;    // the two slices' launches on two streams (KP_TOP_SPLIT=0: one)
   bool slow_order = true;   // k_slow orders candidates from the class orders (KP_SLOW_ORDER=0: sorts)
-  bool top_wg = true;       // large-subset bindings on k_select_top_wg (KP_TOP_WG=0: the one-wave kernel)
+  bool top_wg = false;      // large-subset bindings on k_select_top_wg (KP_TOP_WG=1; measured slower)
   // per-kernel timing of kp_schedule_batch (kp_engine_set_profile): an event pair
   // around every launch on its own stream, folded by kernel name after the batch
   struct KProf {
@@ -1035,6 +1035,16 @@ struct Packer {
     std::vector<int32_t> lists;
   };
   SvMap<int32_t> cmemo;
+  // ResourceRequest lists memoized by content (their names and quantity strings): a batch
+  // repeats a few request specs, so most bindings skip the parse, sort and name lookups
+  struct ReqMemo {
+    bool bad;
+    std::vector<int32_t> sr, mr;
+    std::vector<int64_t> sq, mq;
+  };
+  SvMap<int32_t> rmemo;
+  std::vector<ReqMemo> rlist;
+  std::string rkey;
   std::vector<CProg> cprogs;
   std::string ckey;
 
@@ -1462,14 +1472,33 @@ struct Packer {
     }
     KP_PACK_MARK(4);
     // requests
-    {
+    rkey.clear();
+    for (uint32_t i = 0; i < b.n_resource_request; i++) {
+      rkey.append(SV(b.resource_request[i].name));
+      rkey.push_back('\0');
+      rkey.append(SV(b.resource_request[i].quantity));
+      rkey.push_back('\0');
+    }
+    if (auto* m = rmemo.find(std::string_view(rkey))) {
+      const ReqMemo& q = rlist[m->second];
+      if (q.bad) f |= BF_BAD;
+      h.sreq_off = list(q.sr);
+      h.sreq_cnt = (int32_t)q.sr.size();
+      h.sreq_q_off = (int32_t)bt->lpool.size();
+      bt->lpool.insert(bt->lpool.end(), q.sq.begin(), q.sq.end());
+      h.mreq_off = list(q.mr);
+      h.mreq_cnt = (int32_t)q.mr.size();
+      h.mreq_q_off = (int32_t)bt->lpool.size();
+      bt->lpool.insert(bt->lpool.end(), q.mq.begin(), q.mq.end());
+    } else {
+      bool bad = false;
       // the ResourceList as (name, quantity) in name order, a repeated name's last
       // entry winning (the map the reference decodes), without per-entry allocation
       auto& rq = tmp_rq;
       rq.clear();
       for (uint32_t i = 0; i < b.n_resource_request; i++) {
         k8s::Qty q;
-        if (!qty(SV(b.resource_request[i].quantity), &q)) f |= BF_BAD;
+        if (!qty(SV(b.resource_request[i].quantity), &q)) bad = true;
         const std::string_view nm = SV(b.resource_request[i].name);
         bool dup = false;
         for (auto& kv : rq)
@@ -1514,6 +1543,11 @@ struct Packer {
       h.mreq_cnt = (int32_t)mr.size();
       h.mreq_q_off = (int32_t)bt->lpool.size();
       bt->lpool.insert(bt->lpool.end(), mq.begin(), mq.end());
+      if (bad) f |= BF_BAD;
+      if (rlist.size() < 4096) {
+        rmemo.emplace(rkey, (int32_t)rlist.size());
+        rlist.push_back(ReqMemo{bad, sr, mr, sq, mq});
+      }
     }
     KP_PACK_MARK(5);
     // spread constraints: filter presence + selection kind (select_clusters.go:28-80)
@@ -3171,19 +3205,6 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   }
   // k_slow after every kernel that flags bindings (SEL_ALL on stream2, cluster spread
   // here; the region chain flags none), so it runs beside the region chain
-  HIPCHK(dev::stream_wait(s3, e->ev[8]));
-  if (!bt->l_slow.empty()) {
-    KArgs k = ka;
-    k.list = bt->d_slowlist;
-    k.n = (int)bt->l_slow.size();
-    k.ord = orders ? bt->d_ord : nullptr;  // sortClusters order from the class orders (kp_kernels.h)
-    k.cok = orders ? bt->d_cok : nullptr;
-    if (!e->slow_order) k.ord = nullptr;
-    KPROF(s3, "k_slow", 0, 0, dev::select(s3, SEL_LAUNCH_SLOW, k, kRedBytes + 512 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area +
-                                                      sx.lds_sort,
-                       bt->slow_cap, sx));
-  }
-  HIPCHK(dev::event_record(e->ev[9], s3));
   double th0 = 0, th1 = 0;
   if (!bt->l_region.empty()) {
     const int nr = (int)bt->l_region.size(), R = s->view.n_regions;
@@ -3273,6 +3294,32 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     KPROF(st, sel_name(SEL_LAUNCH_REGION_B, smem_region_b(s, cap)), k.n_dev ? 0 : k.n, k.n_dev ? 13 : -1,
           dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sx));
   }
+  // k_slow after every kernel that flags bindings (SEL_ALL on stream2, cluster spread on
+  // stream3; the region chain, queued above, flags none), beside the region chain. The
+  // flagged count is read back first (the host waits for the flagging kernels only): a
+  // batch that flags none launches nothing, and a few flagged take a small grid, instead
+  // of up to 256 workgroups whose LDS slices wait for CUs behind the region kernels.
+  HIPCHK(dev::stream_wait(s3, e->ev[8]));
+  if (!bt->l_slow.empty()) {
+    uint32_t nslow = 0;
+    HIPCHK(dev::d2h(&nslow, bt->stats, 4, s3));
+    HIPCHK(dev::sync(s3));
+    if (nslow > 0) {
+      KArgs k = ka;
+      k.list = bt->d_slowlist;
+      k.n = (int)bt->l_slow.size();
+      k.ord = orders ? bt->d_ord : nullptr;  // sortClusters order from the class orders (kp_kernels.h)
+      k.cok = orders ? bt->d_cok : nullptr;
+      if (!e->slow_order) k.ord = nullptr;
+      SelectExtra sxs = sx;
+      sxs.grid = (int)std::min<uint32_t>((uint32_t)bt->slow_grid, nslow);
+      KPROF(s3, "k_slow", 0, 0,
+            dev::select(s3, SEL_LAUNCH_SLOW, k,
+                        kRedBytes + 512 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area + sx.lds_sort,
+                        bt->slow_cap, sxs));
+    }
+  }
+  HIPCHK(dev::event_record(e->ev[9], s3));
   HIPCHK(dev::stream_wait(st, e->ev[8]));
   HIPCHK(dev::stream_wait(st, e->ev[9]));  // k_slow (stream3) and every select kernel precede the results
   HIPCHK(dev::event_record(e->ev[2], st));
