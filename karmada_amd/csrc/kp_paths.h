@@ -106,6 +106,24 @@ struct LdsCands {  // candidates compacted in LDS (gather)
   KP_FI uint64_t okey(const SelCtx& x, uint32_t rk, int32_t v0) const { return cand_order_key(x, rk, v0); }
   static constexpr bool kExact = false;  // okey is sort.Sort's output order only for <= 12 (stable insertion)
 };
+// At most one candidate per lane, held in registers (k_select_top's subsets of at most
+// 64 on one wave): every pass of the division reads it without an LDS round trip.
+struct RegCands {
+  bool has;
+  uint32_t rk;
+  mutable int32_t v;
+  template <class Fn>
+  KP_FI void each(Fn fn) const {
+    if (has) fn(rk, v);
+  }
+  template <class Fn>
+  KP_FI void each_set(Fn fn) const {
+    if (has) v = fn(rk, v);
+  }
+  static constexpr bool kSettable = true;
+  KP_FI uint64_t okey(const SelCtx& x, uint32_t r, int32_t v0) const { return cand_order_key(x, r, v0); }
+  static constexpr bool kExact = false;
+};
 // Gathered candidates (any memory) whose sort.Sort output order is known:
 // pos[rank] = position after the emulated sort (k_slow, kp_pdq.h).
 struct PosCands {

@@ -433,7 +433,13 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     return;
   }
   const TopInfo ti{F, complete};
-  const int why = sel_all_fast<true>(B, x, LdsCands{&cd, B.tid(), B.nth()}, ss, &ti);
+  int why;
+  if (n <= B.nth()) {  // (wave-uniform) at most one candidate per lane, in registers
+    const bool has = B.tid() < n;
+    why = sel_all_fast<true>(B, x, RegCands{has, has ? cd.r[B.tid()] : 0u, has ? cd.v[B.tid()] : 0}, ss, &ti);
+  } else {
+    why = sel_all_fast<true>(B, x, LdsCands{&cd, B.tid(), B.nth()}, ss, &ti);
+  }
   KP_STAMP(x, 12);
   if (why == SLOW_TOP_FULL) top_fallback(B, a, t, b);
   else if (why != SLOW_NONE && B.tid() == 0) flag_slow(a, b, why);
