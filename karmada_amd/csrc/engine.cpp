@@ -3295,15 +3295,19 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
           dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sx));
   }
   // k_slow after every kernel that flags bindings (SEL_ALL on stream2, cluster spread on
-  // stream3; the region chain, queued above, flags none), beside the region chain. The
-  // flagged count is read back first (the host waits for the flagging kernels only): a
-  // batch that flags none launches nothing, and a few flagged take a small grid, instead
-  // of up to 256 workgroups whose LDS slices wait for CUs behind the region kernels.
+  // stream3; the region chain, queued above, flags none), beside the region chain. With a
+  // region chain the flagged count is read back first (the host waits for the flagging
+  // kernels only): a batch that flags none launches nothing, and a few flagged take a
+  // small grid, instead of up to 256 workgroups whose LDS slices wait for CUs behind the
+  // region kernels (config 4: 3.87 -> 3.74 ms). Without one the wait costs more than it
+  // saves (config 3: 2.00 -> 2.20 ms with four batches in flight), so k_slow is queued.
   HIPCHK(dev::stream_wait(s3, e->ev[8]));
   if (!bt->l_slow.empty()) {
-    uint32_t nslow = 0;
-    HIPCHK(dev::d2h(&nslow, bt->stats, 4, s3));
-    HIPCHK(dev::sync(s3));
+    uint32_t nslow = (uint32_t)bt->slow_grid;
+    if (!bt->l_region.empty()) {
+      HIPCHK(dev::d2h(&nslow, bt->stats, 4, s3));
+      HIPCHK(dev::sync(s3));
+    }
     if (nslow > 0) {
       KArgs k = ka;
       k.list = bt->d_slowlist;
