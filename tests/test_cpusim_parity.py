@@ -177,6 +177,34 @@ def test_cpusim_top_subsets(top_env):
         e.close()
 
 
+@pytest.mark.parametrize("slow_env", [{"KP_SLOW_ORDER": "1"}, {"KP_SLOW_ORDER": "0"}, {"KP_TOP_WG": "1"}],
+                         ids=["order", "sort", "top-wg"])
+def test_cpusim_slow_order_and_top_wg(slow_env):
+    """k_slow's candidate order from the class orders (kp_kernels.h slow_items_from_order:
+    the filtered class order, spec.Clusters merged in) against the bitonic sort it replaces,
+    and the workgroup form of k_select_top for the large subsets, on config 7 (Aggregated
+    tie groups straddling the cut: every tie binding goes through k_slow, 20% with
+    spec.Clusters) and config 3: the oracle's placements every way."""
+    old = {k: os.environ.get(k) for k in slow_env}
+    os.environ.update(slow_env)
+    try:
+        e = Engine(0, lib_path=CPUSIM)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    try:
+        for config, seed, C_, B_ in [(7, 71, 400, 500), (3, 72, 500, 700)]:
+            u = synth.Universe(config, seed, C_, 0, B_)
+            opts = api.options()
+            want = O.schedule_c(u.clusters, u.n_clusters, u.bindings, u.n_bindings, opts, O.FAST, 8)
+            compare(run(e, u, opts), want, f"{slow_env} config {config}")
+    finally:
+        e.close()
+
+
 def test_cpusim_sets_overflow_is_per_binding(engine):
     """A component-set simulation that outgrows its node runs (KP_SETS_RUNS_CAP=1 here;
     kSetsRunsMax on the device) fails only the bindings of that component-set class
