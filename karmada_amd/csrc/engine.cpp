@@ -2419,7 +2419,7 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       ~Stamp() { *out = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
     } stamp{tt0, &tms[t]};
     Packer pk{s, nullptr};
-    std::unordered_map<std::string, int32_t> ids;
+    SvMap<int32_t> ids;
     std::string key;
     SetsArgs A;
     for (;;) {
@@ -2516,7 +2516,7 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
   bt->progs.resize(bp[K]);
   bt->instrs.resize(bn[K]);
   // global class ids (1-based; 0 = non-workload): the threads' keys in thread order
-  std::unordered_map<std::string, int32_t> gid;
+  SvMap<int32_t> gid;
   bt->crep.assign(1, 0);
   std::vector<std::vector<int32_t>> remaps(T);
   for (int t = 0; t < T; t++) {
