@@ -2693,6 +2693,14 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
     bt->n_all_dyn = n_dyn;
     bt->n_top_small = n_small;
     bt->n_static = n_stat_ok;
+    // KP_TOP_LPT=1: the large-subset part heaviest first (replicas desc) instead of by class
+    static const bool lpt = [] {
+      const char* v = getenv("KP_TOP_LPT");
+      return v && atoi(v) != 0;
+    }();
+    if (lpt)
+      std::stable_sort(bt->l_all.begin() + n_small, bt->l_all.begin() + n_dyn,
+                       [&](int32_t x, int32_t y) { return bt->hdr[x].replicas > bt->hdr[y].replicas; });
   }
   bt->l_slow = bt->l_all;
   bt->l_slow.insert(bt->l_slow.end(), bt->l_cluster.begin(), bt->l_cluster.end());
