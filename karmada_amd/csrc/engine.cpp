@@ -2332,11 +2332,20 @@ KP_HD inline bool route_static_ok(const SnapView& v, const BindHdr& h, const int
   }
   return true;
 }
+// Replicas + len(spec.Clusters) up to which a binding takes k_select_top's small slice
+// (KP_TOP_SMALL_NEED overrides kTopSmallNeed, for measurement).
+inline int64_t top_small_need() {
+  static const int64_t v = [] {
+    const char* e = getenv("KP_TOP_SMALL_NEED");
+    return e ? std::max<int64_t>(0, atoll(e)) : kTopSmallNeed;
+  }();
+  return v;
+}
 inline uint8_t route_of(const SnapView& v, const BindHdr& h, const int64_t* lpool) {
   uint8_t r = h.sel == SEL_CLUSTER ? RT_CLUSTER : h.sel == SEL_REGION ? RT_REGION : 0;
   if (!r) {
     if (h.strategy != ST_STATIC) r |= RT_DYN;
-    if ((int64_t)h.replicas + h.tgt_cnt <= kTopSmallNeed) r |= RT_SMALL;
+    if ((int64_t)h.replicas + h.tgt_cnt <= top_small_need()) r |= RT_SMALL;
     if (route_static_ok(v, h, lpool)) r |= RT_STATIC_OK;
   }
   return r;
