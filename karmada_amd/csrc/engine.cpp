@@ -2702,6 +2702,21 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
     bt->n_all_dyn = n_dyn;
     bt->n_top_small = n_small;
     bt->n_static = n_stat_ok;
+    // the spread lists grouped by estimator class too (stable): their kernels read the
+    // class rows and orders as the SEL_ALL ones do (KP_SPREAD_GROUP=0: binding order)
+    static const bool spread_group = [] {
+      const char* v = getenv("KP_SPREAD_GROUP");
+      return !v || atoi(v) != 0;
+    }();
+    if (spread_group)
+      for (std::vector<int32_t>* lst : {&bt->l_cluster, &bt->l_region}) {
+        if (lst->size() < 2) continue;
+        std::vector<int32_t> c2(ncls + 1, 0), o2(lst->size());
+        for (int32_t b : *lst) c2[(size_t)std::max(0, bt->bcls[b]) + 1]++;
+        for (size_t k = 1; k <= ncls; k++) c2[k] += c2[k - 1];
+        for (int32_t b : *lst) o2[(size_t)c2[(size_t)std::max(0, bt->bcls[b])]++] = b;
+        lst->swap(o2);
+      }
     // KP_TOP_LPT=1: the large-subset part heaviest first (replicas desc) instead of by class
     static const bool lpt = [] {
       const char* v = getenv("KP_TOP_LPT");
