@@ -2702,11 +2702,11 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
     bt->n_all_dyn = n_dyn;
     bt->n_top_small = n_small;
     bt->n_static = n_stat_ok;
-    // the spread lists grouped by estimator class too (stable): their kernels read the
-    // class rows and orders as the SEL_ALL ones do (KP_SPREAD_GROUP=0: binding order)
+    // KP_SPREAD_GROUP=1: the spread lists grouped by estimator class too (stable), as the
+    // SEL_ALL list is; measured no better (config 4 3.84 vs 3.74 ms), so binding order
     static const bool spread_group = [] {
       const char* v = getenv("KP_SPREAD_GROUP");
-      return !v || atoi(v) != 0;
+      return v && atoi(v) != 0;
     }();
     if (spread_group)
       for (std::vector<int32_t>* lst : {&bt->l_cluster, &bt->l_region}) {
