@@ -12,9 +12,14 @@ universe against its own snapshot replica (weak scaling, no data-path
 collective); the per-rank CSR results are all-gathered after the timed region.
 
 In flight: --inflight engines (default 4), each with its own HIP streams and its
-own copy of the batch, are driven by as many host threads over the K steps, so one
-batch's host steps and result copy-back overlap another batch's kernels (a
-scheduler keeping two batches in flight); `serial_value` is one batch at a time.
+own copy of the batch, are driven by as many host threads, so one batch's host
+steps and result copy-back overlap another batch's kernels (a scheduler keeping
+several batches in flight); `serial_value` is one batch at a time. The lane
+threads issue the warm-up steps themselves and keep going: the timed region
+starts at the (W x lanes)-th completion, with every lane mid-stream, and ends at
+the K-th completion after it, before any lane runs dry. So K timed steps measure
+the steady state, not the pipeline's fill and drain (each lane's step in flight
+at the end finishes untimed).
 
 Roofline: the dominant kernel of the step (by its HIP-event time) against HBM
 peak with compulsory bytes, plus the counter-derived DRAM bytes
@@ -317,33 +322,55 @@ def main():
         e2 = Engine(local, lib_path=os.path.join(ROOT, args.lib)) if args.lib else Engine(local)
         s2 = Snapshot.from_bytes(e2, snap.to_bytes(), u.names)
         lanes.append((e2, s2, Batch(s2, structs=u.binding_slice(0, u.n_bindings))))
-    for _ in range(args.warmup):
-        for _, _, bt in lanes:
-            bt.schedule_raw()
     st_all = []
     results = [None] * len(lanes)
+    # completions counted over all lanes: the first n_warm are the warm-up (every lane
+    # issues `warmup` of them on average), the next K are timed; a lane stops issuing
+    # once the K-th timed step has completed
+    n_warm = args.warmup * len(lanes)
+    lock = threading.Lock()
+    clock = {"done": 0, "t0": None, "t1": None}
+    if n_warm == 0:
+        clock["t0"] = "at start"
 
-    def drive(k, n):
+    def drive(k):
         e_k, _, b_k = lanes[k]
         st = []
-        for _ in range(n):
-            results[k] = b_k.schedule_raw()
-            st.append(e_k.stage_times())
-        st_all.extend(st)
+        while True:
+            with lock:
+                if clock["done"] >= n_warm + args.steps:
+                    break
+            r = b_k.schedule_raw()
+            now = time.perf_counter()
+            with lock:
+                clock["done"] += 1
+                d = clock["done"]
+                if d == n_warm:
+                    clock["t0"] = now
+                elif d == n_warm + args.steps:
+                    clock["t1"] = now
+                timed = n_warm < d <= n_warm + args.steps
+            results[k] = r
+            if timed:
+                st.append(e_k.stage_times())
+        with lock:
+            st_all.extend(st)
 
-    per = [args.steps // len(lanes) + (1 if k < args.steps % len(lanes) else 0) for k in range(len(lanes))]
     barrier_sync()
-    t0 = time.perf_counter()
+    t_start = time.perf_counter()
+    if clock["t0"] == "at start":
+        clock["t0"] = t_start
     if len(lanes) == 1:
-        drive(0, per[0])
+        drive(0)
     else:
-        th = [threading.Thread(target=drive, args=(k, per[k])) for k in range(len(lanes)) if per[k] > 0]
+        th = [threading.Thread(target=drive, args=(k,)) for k in range(len(lanes))]
         for x in th:
             x.start()
         for x in th:
             x.join()
     barrier_sync()
-    elapsed = time.perf_counter() - t0
+    lanes_wall = time.perf_counter() - t_start
+    elapsed = clock["t1"] - clock["t0"]
     rank_ms = 1e3 * elapsed / args.steps
     # every lane's last result (engine-owned until that engine's next call), copied
     # now: the in-flight lanes are parity-checked too, not only the serial run below
@@ -360,6 +387,8 @@ def main():
             st_ser.append(eng.stage_times())
         barrier_sync()
         serial_ms = 1e3 * (time.perf_counter() - t1) / n_ser
+        # copied before the profiled runs below reuse the engine's result buffers
+        csr = Csr.from_results(r)
         # then every kernel of the step timed by its own HIP event pair (on the stream it
         # runs on), one batch at a time, for the per-kernel ranking and the roofline
         eng.set_profile(True)
@@ -376,14 +405,13 @@ def main():
             serial_ms = float(t.item())
     # ---- after the timed region ----
     if len(lanes) == 1:
-        r = results[0]
+        csr = Csr.from_results(results[0])  # before the profiled runs reuse the buffers
         eng.set_profile(True)
         kt_runs = []
         for _ in range(max(1, min(args.steps, 50))):
             batch.schedule_raw()
             kt_runs.append(eng.kernel_times())
         eng.set_profile(False)
-    csr = Csr.from_results(r)
     res = csr.to_python()
     n_ok = int((csr.status == 0).sum())
     n_targets_rank = n_targets = csr.n_targets
@@ -400,6 +428,9 @@ def main():
         whole = gather_csr(csr)  # two-phase CSR all-gather (counts, then padded arrays)
         n_ok = int((whole.status == 0).sum())
         n_targets = whole.n_targets
+        # the parity check reads this rank's range of the GATHERED CSR (so the
+        # collective's placement of every rank's block is checked too), not the local one
+        res = whole.slice(lo, hi).to_python()
 
     # the oracle re-checks a sample of the serial run and of every in-flight lane's
     # last batch (lanes run concurrently on separate engines and streams)
@@ -511,6 +542,11 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "inflight": len(lanes),
+        # the timed window: from the (warmup x inflight)-th completed step to the K-th
+        # completion after it, every lane mid-stream (module docstring)
+        "timed_window": {"warmup_completions": n_warm, "timed_completions": args.steps,
+                         "total_completions": clock["done"],
+                         "lanes_wall_s": round(lanes_wall, 3)},
         # one batch at a time on one engine (nothing overlapped): ms per batch and the rate
         "serial_ms_per_step": round(serial_ms, 3) if serial_ms else round(ms_per_step, 3),
         "serial_value": round(total / (serial_ms * 1e-3), 1) if serial_ms else round(value, 1),
@@ -561,6 +597,8 @@ def main():
         "parity_checked": n_chk,
         "parity_lanes": n_lanes_chk,  # result lists checked per rank: the serial run + each in-flight lane
         "parity_bad": n_bad,
+        "parity_source": "all-gathered CSR (each rank's range) + every in-flight lane" if dist is not None else
+                         "serial run + every in-flight lane",
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(u, opts, args.cpu_budget)

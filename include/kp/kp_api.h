@@ -650,7 +650,10 @@ kp_engine* kp_multi_engine(kp_multi* m, uint32_t i);
 
 int kp_multi_snapshot_create(kp_multi* m, const kp_cluster* clusters, uint64_t n_clusters, const kp_options* opts,
                              kp_multi_snapshot** out);
-/* kp_snapshot_update on every replica (same semantics, same dict_grew). */
+/* kp_snapshot_update on every replica (same semantics, same dict_grew). If it fails on
+ * any device the others may already have applied the rows, so the multi snapshot is
+ * marked invalid: this call, kp_multi_batch_create and kp_multi_schedule on it return
+ * KP_ESTATE until it is destroyed and created again. */
 int kp_multi_snapshot_update(kp_multi* m, kp_multi_snapshot* s, const kp_cluster* clusters, uint64_t n_clusters,
                              int* dict_grew);
 void kp_multi_snapshot_destroy(kp_multi_snapshot* s);

@@ -33,6 +33,9 @@ struct kp_multi_snapshot {
   kp_multi* m = nullptr;
   std::vector<kp_snapshot*> rep;  // replica per device (rep[0] packed, the others copied)
   uint64_t n_clusters = 0;
+  // set when an update failed on some device: the replicas may then describe different
+  // cluster states, so batches on it are refused (KP_ESTATE) until it is rebuilt
+  bool invalid = false;
   ~kp_multi_snapshot() {
     for (auto* s : rep) kp_snapshot_destroy(s);
   }
@@ -144,8 +147,13 @@ int kp_multi_snapshot_create(kp_multi* m, const kp_cluster* clusters, uint64_t n
 int kp_multi_snapshot_update(kp_multi* m, kp_multi_snapshot* s, const kp_cluster* clusters, uint64_t n,
                              int* dict_grew) {
   if (!m || !s || s->m != m || (n && !clusters)) return KP_EINVAL;
+  if (s->invalid) {
+    m->err = "multi snapshot is invalid after a failed update on one device: rebuild it";
+    return KP_ESTATE;
+  }
   std::vector<int> grew(m->eng.size(), 0);
   const int rc = each_device(m, [&](int d) { return kp_snapshot_update(m->eng[d], s->rep[d], clusters, n, &grew[d]); });
+  if (rc != KP_OK) s->invalid = true;  // the other devices may have applied it
   if (dict_grew) *dict_grew = grew[0];
   return rc;
 }
@@ -179,6 +187,10 @@ int kp_multi_shard_cuts(const kp_binding* bindings, uint64_t n, uint64_t n_clust
 int kp_multi_batch_create(kp_multi* m, const kp_multi_snapshot* s, const kp_binding* bindings, uint64_t n,
                           kp_multi_batch** out) {
   if (!m || !s || s->m != m || !out || (n && !bindings)) return KP_EINVAL;
+  if (s->invalid) {
+    m->err = "multi snapshot is invalid after a failed update on one device: rebuild it";
+    return KP_ESTATE;
+  }
   const uint32_t D = (uint32_t)m->eng.size();
   auto b = std::make_unique<kp_multi_batch>();
   b->snap = s;
@@ -203,6 +215,10 @@ int kp_multi_batch_shards(const kp_multi_batch* b, uint64_t* starts) {
 
 int kp_multi_schedule(kp_multi* m, kp_multi_batch* b, kp_results* out) {
   if (!m || !b || !out || b->snap->m != m) return KP_EINVAL;
+  if (b->snap->invalid) {
+    m->err = "multi snapshot is invalid after a failed update on one device: rebuild it";
+    return KP_ESTATE;
+  }
   const uint32_t D = (uint32_t)m->eng.size();
   std::vector<kp_results> r(D);
   int rc = each_device(m, [&](int d) { return kp_schedule_batch(m->eng[d], b->shard[d], &r[d]); });

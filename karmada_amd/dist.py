@@ -126,6 +126,12 @@ class Csr:
                    arr(r.offsets, n + 1, np.int64) if n else np.zeros(1, np.int64),
                    arr(r.cluster_idx, t, np.int32), arr(r.replicas, t, np.int32))
 
+    def slice(self, lo: int, hi: int) -> "Csr":
+        """Bindings [lo, hi) as their own CSR (offsets rebased to 0)."""
+        a, b = int(self.offsets[lo]), int(self.offsets[hi])
+        return Csr(self.status[lo:hi].copy(), self.err_code[lo:hi].copy(), self.err_arg[lo:hi].copy(),
+                   self.offsets[lo:hi + 1] - a, self.cluster_idx[a:b].copy(), self.replicas[a:b].copy())
+
     def to_python(self) -> List[dict]:
         from karmada_amd import api
         return api.results_to_python(self.status, self.err_code, self.err_arg, self.offsets, self.cluster_idx,

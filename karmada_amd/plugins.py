@@ -149,26 +149,57 @@ class Framework:
         return out, None
 
 
+class UnknownCluster(KeyError):
+    """A cluster name the engine's snapshot does not hold (added since the last
+    update): an error, never a silent answer for some other cluster."""
+
+
 class BatchView:
-    """One batch's device answers, fetched once and looked up per (binding slot, cluster).
-    `clusters` are the snapshot's cluster dicts in caller order (for taint reasons)."""
+    """One batch's device answers, fetched on first use and looked up per (binding
+    slot, cluster). The filter reasons and the scores are separate device passes
+    (kp_filter_reasons, kp_score_batch), each run only when a Filter or Score asks:
+    a view that only answers the estimator (kp_max_available_replicas runs its own
+    pass over the one binding) never runs them. `clusters` are the snapshot's
+    cluster dicts in caller order (for taint reasons)."""
 
     def __init__(self, snap: Snapshot, batch: Batch, clusters: Optional[Sequence[dict]] = None):
         self.snap, self.batch, self.clusters = snap, batch, clusters
-        eng = snap.engine
         self.C = len(snap.names)
         self.index = {n: i for i, n in enumerate(snap.names)}
-        nb = batch.n
-        self.reasons = (C.c_uint32 * max(1, nb * self.C))()
-        eng._check(eng.L.kp_filter_reasons(eng.h, batch.h, self.reasons), "kp_filter_reasons")
-        self.scores = (C.c_int64 * max(1, nb * self.C))()
-        eng._check(eng.L.kp_score_batch(eng.h, batch.h, self.scores), "kp_score_batch")
+        self._reasons = self._scores = None
+        self.passes = []  # device passes run on this view, in order (for the tests)
+
+    @property
+    def reasons(self):
+        if self._reasons is None:
+            eng = self.snap.engine
+            r = (C.c_uint32 * max(1, self.batch.n * self.C))()
+            eng._check(eng.L.kp_filter_reasons(eng.h, self.batch.h, r), "kp_filter_reasons")
+            self._reasons = r
+            self.passes.append("kp_filter_reasons")
+        return self._reasons
+
+    @property
+    def scores(self):
+        if self._scores is None:
+            eng = self.snap.engine
+            r = (C.c_int64 * max(1, self.batch.n * self.C))()
+            eng._check(eng.L.kp_score_batch(eng.h, self.batch.h, r), "kp_score_batch")
+            self._scores = r
+            self.passes.append("kp_score_batch")
+        return self._scores
+
+    def cluster_index(self, cluster: str) -> int:
+        i = self.index.get(cluster)
+        if i is None:
+            raise UnknownCluster(f"cluster {cluster!r} is not in the engine's snapshot")
+        return i
 
     def reason(self, slot: int, cluster: str) -> int:
-        return int(self.reasons[slot * self.C + self.index[cluster]])
+        return int(self.reasons[slot * self.C + self.cluster_index(cluster)])
 
     def score(self, slot: int, cluster: str) -> int:
-        return int(self.scores[slot * self.C + self.index[cluster]])
+        return int(self.scores[slot * self.C + self.cluster_index(cluster)])
 
 
 class KpFilter:
@@ -185,7 +216,10 @@ class KpFilter:
 
     def filter(self, ctx) -> Optional[Result]:
         slot, cluster = ctx
-        w = self.view.reason(slot, cluster)
+        try:
+            w = self.view.reason(slot, cluster)
+        except UnknownCluster as err:  # framework.AsResult(err): an Error Result
+            return Result(ERROR, str(err.args[0]))
         code = w & 0xFF
         if code in (api.REASON_FIT, api.REASON_DELETING):
             return None
@@ -203,7 +237,10 @@ class KpScore:
         return "KpScore"
 
     def score(self, spec, cluster) -> Tuple[int, Optional[Result]]:
-        return self.view.score(spec, cluster), None
+        try:
+            return self.view.score(spec, cluster), None
+        except UnknownCluster as err:
+            return 0, Result(ERROR, str(err.args[0]))
 
     def score_extensions(self):
         return None
@@ -212,14 +249,22 @@ class KpScore:
 class KpEstimator:
     """ReplicaEstimator for the GeneralEstimator's place in GetReplicaEstimators()."""
 
-    def __init__(self, snap: Snapshot, batch: Batch):
+    def __init__(self, snap: Snapshot, batch: Optional[Batch]):
         self.snap, self.batch = snap, batch
+
+    def _indices(self, clusters: Sequence[str]) -> List[int]:
+        idx = {n: i for i, n in enumerate(self.snap.names)}
+        bad = [n for n in clusters if n not in idx]
+        if bad:
+            raise UnknownCluster(f"cluster {bad[0]!r} is not in the engine's snapshot")
+        return [idx[n] for n in clusters]
 
     def max_available_replicas(self, slot: int, clusters: Sequence[str]) -> List[Tuple[str, int]]:
         """[]TargetCluster in the request's cluster order (general.go:57-64)."""
         eng = self.snap.engine
-        idx = {n: i for i, n in enumerate(self.snap.names)}
-        ci = (C.c_uint32 * max(1, len(clusters)))(*[idx[n] for n in clusters])
+        ci = (C.c_uint32 * max(1, len(clusters)))(*self._indices(clusters))
+        if not clusters:
+            return []
         out = (C.c_int32 * max(1, len(clusters)))()
         eng._check(eng.L.kp_max_available_replicas(eng.h, self.batch.h, slot, ci, len(clusters), out),
                    "kp_max_available_replicas")
@@ -229,9 +274,10 @@ class KpEstimator:
         """[]ComponentSetEstimationResponse in request order (general.go:154-162)."""
         eng = self.snap.engine
         w = api.World()
+        ci = (C.c_uint32 * max(1, len(clusters)))(*self._indices(clusters))
+        if not clusters:  # (the Go shim's guard before &idx[0])
+            return []
         ca, nc = w.components(components)
-        idx = {n: i for i, n in enumerate(self.snap.names)}
-        ci = (C.c_uint32 * max(1, len(clusters)))(*[idx[n] for n in clusters])
         out = (C.c_int32 * max(1, len(clusters)))()
         eng._check(eng.L.kp_max_available_component_sets(eng.h, self.snap.h, ca, nc, ci, len(clusters), out),
                    "kp_max_available_component_sets")
@@ -271,7 +317,9 @@ class Shim:
 
     def __init__(self, engine, clusters: Sequence[dict], opts: Optional[api.kp_options] = None,
                  registry_names: Sequence[str] = ()):
-        opts = opts or api.options()
+        # a copy: the caller's kp_options stays as it was (reusing it for another
+        # snapshot must not carry this shim's out-of-tree count)
+        opts = api.kp_options.from_buffer_copy(opts) if opts is not None else api.options()
         opts.n_out_of_tree_plugins = out_of_tree_plugins(registry_names)
         self.clusters = list(clusters)
         self.snap = Snapshot(engine, self.clusters, opts)
@@ -311,7 +359,7 @@ class Shim:
 
     def score(self, spec: dict, cluster: str) -> Tuple[int, Optional[Result]]:
         view, slot = self.slot_of(spec)
-        return view.score(slot, cluster), None
+        return KpScore(view).score(slot, cluster)
 
     def max_available_replicas(self, requirements: Optional[dict], clusters: Sequence[str]) -> List[Tuple[str, int]]:
         key = requirements_key(requirements)

@@ -128,6 +128,37 @@ def test_replicate_cpusim():
     e0.close()
 
 
+def test_multi_failed_update_invalidates():
+    """A kp_multi_snapshot_update that fails on any device leaves the replicas possibly
+    different: the multi snapshot refuses batches and schedules (KP_ESTATE)
+    until it is rebuilt; a batch created before the failure is refused too."""
+    from karmada_amd.engine import EngineError
+    u = synth.Universe(6, 6, 60, 0, 50)
+    opts = api.options()
+    m = MultiEngine([0, 1], lib_path=CPUSIM)
+    s = m.snapshot(u.clusters, u.n_clusters, opts)
+    b = MultiBatch(s, u.binding_slice(0, u.n_bindings))
+    assert len(b.schedule()) == 50
+    w = api.World()
+    ca, n = w.clusters([{"name": "no-such-cluster"}])
+    with pytest.raises(EngineError, match="rc=-1"):
+        s.update_structs(ca, n)
+    with pytest.raises(EngineError, match="rc=-5"):
+        b.schedule()
+    with pytest.raises(EngineError, match="rc=-5"):
+        MultiBatch(s, u.binding_slice(0, u.n_bindings))
+    with pytest.raises(EngineError, match="rc=-5"):
+        s.update_structs(u.clusters, u.n_clusters)
+    b.close()
+    s.close()
+    s = m.snapshot(u.clusters, u.n_clusters, opts)  # rebuilt: usable again
+    b = MultiBatch(s, u.binding_slice(0, u.n_bindings))
+    compare(b.schedule(), oracle(u, opts), "multi after rebuild")
+    b.close()
+    s.close()
+    m.close()
+
+
 def test_multi_rejects_duplicate_devices():
     L = load_library(CPUSIM)
     devs = (C.c_int * 2)(0, 0)

@@ -306,3 +306,66 @@ def test_shim_refuses_out_of_tree_plugins(cpusim_engine):
     sh = plugins.Shim(cpusim_engine, shim_clusters(), registry_names=list(plugins.IN_TREE) + ["KpPlacement"])
     assert len(sh.schedule_batch([shim_spec()])) == 1
     sh.close()
+
+
+def test_shim_estimator_view_skips_filter_and_score(cpusim_engine):
+    """An estimator-only view (one binding per ReplicaRequirements content) answers
+    MaxAvailableReplicas through kp_max_available_replicas alone: the per-pair
+    filter-reason and score passes never run for it (every distinct
+    request used to pay kp_filter_reasons + kp_score_batch over the whole snapshot)."""
+    sh = plugins.Shim(cpusim_engine, shim_clusters())
+    assert sh.max_available_replicas({"resourceRequest": {"cpu": "1"}}, ["m0", "m1"]) == [("m0", 4), ("m1", 8)]
+    (view, _), = sh.est.values()
+    assert view.passes == []
+    # a Filter / Score view runs each pass once, on first use
+    a = shim_spec(env="prod")
+    sh.schedule_batch([a])
+    va = sh.by[id(a)][0]
+    assert va.passes == []
+    sh.filter(a, "m0"), sh.filter(a, "m1")
+    assert va.passes == ["kp_filter_reasons"]
+    sh.score(a, "m0"), sh.score(a, "m2")
+    assert va.passes == ["kp_filter_reasons", "kp_score_batch"]
+    sh.close()
+
+
+def test_shim_unknown_cluster_is_an_error(cpusim_engine):
+    """A cluster name the snapshot does not hold (added since the last update) is an
+    Error Result / exception, never the answer of cluster index 0 (a Go map's zero
+    value)."""
+    sh = plugins.Shim(cpusim_engine, shim_clusters())
+    a = shim_spec(env="prod")
+    sh.schedule_batch([a])
+    r = sh.filter(a, "m9")
+    assert r is not None and r.code == plugins.ERROR and "m9" in r.reasons[0]
+    s, r = sh.score(a, "m9")
+    assert s == 0 and r is not None and r.code == plugins.ERROR
+    with pytest.raises(plugins.UnknownCluster):
+        sh.max_available_replicas({"resourceRequest": {"cpu": "1"}}, ["m0", "m9"])
+    est = plugins.KpEstimator(sh.snap, None)
+    with pytest.raises(plugins.UnknownCluster):
+        est.max_available_component_sets([{"name": "a", "replicas": 1}], ["nope"])
+    sh.close()
+
+
+def test_shim_empty_cluster_lists(cpusim_engine):
+    """Empty request cluster lists answer an empty list (the Go shim's length guard
+    before &idx[0])."""
+    sh = plugins.Shim(cpusim_engine, shim_clusters(), opts=api.options(multi_templates=True))
+    assert sh.max_available_replicas({"resourceRequest": {"cpu": "1"}}, []) == []
+    est = plugins.KpEstimator(sh.snap, None)
+    assert est.max_available_component_sets([{"name": "a", "replicas": 1}], []) == []
+    sh.close()
+
+
+def test_shim_keeps_callers_options(cpusim_engine):
+    """The shim sets n_out_of_tree_plugins on a copy: the caller's kp_options object is
+    unchanged and can build another snapshot without this shim's count."""
+    opts = api.options()
+    names = list(plugins.IN_TREE) + ["KpPlacement", "MyScore"]
+    sh = plugins.Shim(cpusim_engine, shim_clusters(), opts=opts, registry_names=names)
+    assert opts.n_out_of_tree_plugins == 0
+    sh.close()
+    sh = plugins.Shim(cpusim_engine, shim_clusters(), opts=opts)
+    assert len(sh.schedule_batch([shim_spec()])) == 1
+    sh.close()
