@@ -35,6 +35,23 @@ def kernel_stack_flags(blob):
     return out
 
 
+def gpu_libraries():
+    """Every gfx950 library in the package: libkp.so, the test-only device self-tests
+    and any diagnostic variant (libkp_<name>.so; the round-4 illegal access in
+    gpurun_out/d8m.log came from such a variant, built before the fix)."""
+    import glob
+    return sorted(p for p in glob.glob(os.path.join(PKG, "libkp*.so"))
+                  if os.path.basename(p) not in ("libkp_cpusim.so", "libkpsynth.so"))
+
+
+@pytest.mark.parametrize("lib", gpu_libraries(), ids=os.path.basename)
+def test_no_dynamic_stack_in_any_gpu_library(lib):
+    flags = kernel_stack_flags(open(lib, "rb").read())
+    assert flags, f"{lib}: no kernel metadata found"
+    bad = sorted(n for n, dyn in flags if dyn)
+    assert not bad, f"{os.path.basename(lib)}: kernels with a dynamic (unsized) call stack: {bad}"
+
+
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libkp.so not built")
 def test_no_kernel_uses_a_dynamic_stack():
     blob = open(LIB, "rb").read()
