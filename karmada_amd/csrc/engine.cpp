@@ -1449,6 +1449,8 @@ struct Packer {
       else h.ovf_mode = OVF_PROGS;
       h.ovf_off = list(ovf);
       h.ovf_cnt = (int32_t)ovf.size();
+      // engine limit: the sortClusters key orders kMaxOvfTerms overflow orders (kp_algo.h)
+      if (h.ovf_mode == OVF_PROGS && h.ovf_cnt > kMaxOvfTerms) f |= BF_BAD;
       // enableOverflow (common.go:156-170)
       if (!b.has_cluster_affinity && b.n_cluster_affinities > 0 && b.observed_affinity_name.len > 0 && term &&
           term->n_overflow > 0)

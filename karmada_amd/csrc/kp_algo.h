@@ -86,27 +86,35 @@ KP_HD inline double kp_ceil(double x) {
 // ============================================================================
 // Sort key of sortClusters (spreadconstraint/util.go:43-61): ascending u64 order ==
 // (OverflowOrder asc, Score desc, AvailableReplicas desc, Name asc).
-// [63:54] overflow (10b) | [53] score==0 | [52:18] ~(avail + 2^33) (35b) | [17:0] rank
-// Scores are the in-tree plugin sums {0, 100}.
+// [63:58] overflow (6b, 63 = 1000 / beyond) | [57:51] 127 - score (7b) |
+// [50:18] ~(avail + 2^32) (33b) | [17:0] rank
+// Scores are framework scores in [0, 100] (MaxClusterScore, framework/interface.go:
+// 39-42); the in-tree sum is {0, 100}. AvailableReplicas = estimate + assigned, two
+// int32s, so it lies in [-2^32, 2^32). OverflowOrder is a term index below
+// kMaxOvfTerms or 1000 (getClusterOverflowOrder); the packer limits the terms.
 // ============================================================================
+constexpr int kMaxOvfTerms = 63;  // affinity term + overflow terms a key orders
 KP_HD inline uint64_t sort_key(int32_t ovf, int64_t score, int64_t avail, uint32_t rank) {
-  uint64_t o = (uint64_t)(ovf > 1023 ? 1023 : ovf) << 54;
-  uint64_t sc = (score > 0 ? 0ull : 1ull) << 53;
-  uint64_t a = ((1ull << 35) - 1) - (uint64_t)(avail + (1ll << 33));
-  return o | sc | ((a & ((1ull << 35) - 1)) << 18) | (uint64_t)(rank & 0x3ffff);
+  const uint64_t o = (uint64_t)(ovf >= kMaxOvfTerms ? kMaxOvfTerms : (ovf < 0 ? 0 : ovf)) << 58;
+  const uint64_t sc = (uint64_t)(127 - (score > 127 ? 127 : (score < 0 ? 0 : score))) << 51;
+  const uint64_t a = ((1ull << 33) - 1) - (uint64_t)(avail + (1ll << 32));
+  return o | sc | ((a & ((1ull << 33) - 1)) << 18) | (uint64_t)(rank & 0x3ffff);
 }
 KP_HD inline uint32_t key_rank(uint64_t k) { return (uint32_t)(k & 0x3ffff); }
 KP_HD inline int64_t key_avail(uint64_t k) {
-  uint64_t a = (k >> 18) & ((1ull << 35) - 1);
-  return (int64_t)(((1ull << 35) - 1) - a) - (1ll << 33);
+  const uint64_t a = (k >> 18) & ((1ull << 33) - 1);
+  return (int64_t)(((1ull << 33) - 1) - a) - (1ll << 32);
 }
-KP_HD inline int64_t key_score(uint64_t k) { return ((k >> 53) & 1) ? 0 : 100; }
-KP_HD inline int32_t key_ovf(uint64_t k) { return (int32_t)(k >> 54); }
+KP_HD inline int64_t key_score(uint64_t k) { return 127 - (int64_t)((k >> 51) & 127); }
+KP_HD inline int32_t key_ovf(uint64_t k) {
+  const int32_t o = (int32_t)(k >> 58);
+  return o == kMaxOvfTerms ? 1000 : o;
+}
 // (AvailableReplicas desc, then sortClusters position) for the swap step of
 // selectClustersByAvailableResource (select_clusters_by_cluster.go:55-78).
 KP_HD inline uint64_t avail_key(uint64_t k) {
-  uint64_t a = (k >> 18) & ((1ull << 35) - 1);
-  return (a << 29) | ((uint64_t)(k >> 54) << 19) | (((k >> 53) & 1) << 18) | (k & 0x3ffff);
+  const uint64_t a = (k >> 18) & ((1ull << 33) - 1);
+  return (a << 31) | ((k >> 58) << 25) | (((k >> 51) & 127) << 18) | (k & 0x3ffff);
 }
 
 // ============================================================================

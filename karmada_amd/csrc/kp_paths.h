@@ -721,12 +721,16 @@ serial:
 // ----------------------------------------------------------------------------
 // SEL_CLUSTER: selectBestClustersByCluster (select_clusters_by_cluster.go:25-102)
 // items: LDS buffer of kSmallMax*2 Items. Returns false -> slow path.
+// kKeyed: the candidates already hold their sortClusters keys in place (put_ckey).
+// n_sel: when set, the selection only: *n_sel = the selected count (items[0, n)),
+// -1 when a status was written; no assignment (the spread self-test, kp_spread_test).
 // ----------------------------------------------------------------------------
-template <class BLK>
+template <class BLK, bool kKeyed = false>
 KP_FI bool sel_cluster_fast(const BLK& B, const SelCtx& x, const Cands& cd, uint32_t* hist, Item* items,
-                            uint64_t* keys, void* scratch, int cap, size_t area_bytes) {
+                            uint64_t* keys, void* scratch, int cap, size_t area_bytes, int* n_sel = nullptr) {
   const BindHdr& h = *x.h;
   const int F = cd.F;
+  if (n_sel) *n_sel = -1;
   if ((int64_t)F < h.cluster_min) {
     if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_CLUSTER_MIN_GROUPS, 0);
     return true;
@@ -744,8 +748,10 @@ KP_FI bool sel_cluster_fast(const BLK& B, const SelCtx& x, const Cands& cd, uint
   }
   KP_STAMP_INIT
   // every candidate's sortClusters key once, in place of its (rank, estimate) pair
-  for (int i = B.tid(); i < F; i += B.nth()) put_ckey(cd, i, cand_key(x, cd, i, cd.v[i]));
-  B.sync();
+  if (!kKeyed) {
+    for (int i = B.tid(); i < F; i += B.nth()) put_ckey(cd, i, cand_key(x, cd, i, cd.v[i]));
+    B.sync();
+  }
   auto key = [&](int i) { return ckey(cd, i); };
   auto all = [&](int) { return true; };
   uint64_t kth = radix_select(B, hist, F, all, key, needCnt);
@@ -851,6 +857,10 @@ KP_FI bool sel_cluster_fast(const BLK& B, const SelCtx& x, const Cands& cd, uint
     }
   }
   KP_STAMP(x, 29);
+  if (n_sel) {
+    *n_sel = n;
+    return true;
+  }
   assign_small(B, x, items, n, scratch, cap, area_bytes);
   KP_STAMP(x, 30);
   return true;
@@ -1066,7 +1076,9 @@ KP_HD inline int64_t region_score_totals(int64_t cnt, int64_t sum_avail, int64_t
   return add64(mul64(target, 1000), sum_score / cnt);
 }
 
-template <class BLK>
+// kKeyed (here and in region_a, region_b): the candidates already hold their
+// sortClusters keys in place (put_ckey), e.g. with scores other than the in-tree ones.
+template <class BLK, bool kKeyed = false>
 KP_FI bool region_a_fast(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L, RegionOut* out) {
   const int F = cd.F;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1088,8 +1100,8 @@ KP_FI bool region_a_fast(const BLK& B, const SelCtx& x, const Cands& cd, RegionL
   B.sync();
   const bool dup = (h.flags & BF_GROUP_DUP) != 0;
   for (int i = B.tid(); i < F; i += B.nth()) {
-    const uint64_t k = cand_key(x, cd, i, cd.v[i]);
-    put_ckey(cd, i, k);
+    const uint64_t k = kKeyed ? ckey(cd, i) : cand_key(x, cd, i, cd.v[i]);
+    if (!kKeyed) put_ckey(cd, i, k);
     const int r = cd.g[i];
     if (r < 0) continue;
     const int64_t av = key_avail(k), sc = key_score(k);
@@ -1202,7 +1214,7 @@ KP_FI bool region_a_fast(const BLK& B, const SelCtx& x, const Cands& cd, RegionL
   return true;
 }
 
-template <class BLK>
+template <class BLK, bool kKeyed = false>
 KP_FI void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L, RegionOut* out) {
   const BindHdr& h = *x.h;
   const int R = x.s->n_regions;
@@ -1224,7 +1236,7 @@ KP_FI void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L,
   for (int i = B.tid(); i < cd.F; i += B.nth()) {
     int r = cd.g[i];
     if (r < 0) continue;
-    uint64_t k = cand_key(x, cd, i, cd.v[i]);
+    uint64_t k = kKeyed ? ckey(cd, i) : cand_key(x, cd, i, cd.v[i]);
     int64_t av = key_avail(k), sc = key_score(k);
     kp_atomic_add(&L.cnt[r], 1);
     kp_atomic_add((unsigned long long*)&L.sumAvail[r], (unsigned long long)av);
@@ -1264,7 +1276,7 @@ KP_FI void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L,
     for (int i = B.tid(); i < cd.F; i += B.nth()) {
       int r = cd.g[i];
       if (r < 0 || L.done[r]) continue;
-      uint64_t k = cand_key(x, cd, i, cd.v[i]);
+      uint64_t k = kKeyed ? ckey(cd, i) : cand_key(x, cd, i, cd.v[i]);
       if (L.wcnt[r] > 0 && k <= L.last[r]) continue;
       kp_atomic_min_u64(&L.minkey[r], k);
     }
@@ -1310,10 +1322,12 @@ KP_FI void region_a(const BLK& B, const SelCtx& x, const Cands& cd, RegionLds L,
 // Region stage B: selectBestClustersByRegion after the host group selection
 // (select_clusters_by_region.go:41-63). sel: selected region ids in path order.
 // ----------------------------------------------------------------------------
-template <class BLK>
+// n_sel: as sel_cluster_fast's (the selection only, no assignment).
+template <class BLK, bool kKeyed = false>
 KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_t* sel, int nsel, uint32_t* hist,
                     unsigned long long* heads, int32_t* rsel, Item* items, uint64_t* keys, void* scratch, int cap,
-                    size_t area_bytes) {
+                    size_t area_bytes, int* n_sel = nullptr) {
+  if (n_sel) *n_sel = -1;
   KP_STAMP_INIT
   const BindHdr& h = *x.h;
   const int R = x.s->n_regions;
@@ -1349,7 +1363,7 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
         kk[j] = 0;
         gg[j] = -1;
         if (i < cd.F && keep_of(i)) {
-          kk[j] = cand_key(x, cd, i, cd.v[i]);
+          kk[j] = kKeyed ? ckey(cd, i) : cand_key(x, cd, i, cd.v[i]);
           gg[j] = cd.g[i];
           keep |= 1u << j;
           mine++;
@@ -1365,14 +1379,14 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
           pos++;
         }
       cd2.F = tot;
-    } else {
+    } else if (!kKeyed) {
       for (int i = B.tid(); i < cd.F; i += B.nth()) put_ckey(cd, i, cand_key(x, cd, i, cd.v[i]));
     }
 #else
     int pos = 0;
     for (int i = 0; i < cd.F; i++)
       if (keep_of(i)) {  // pos <= i: slot pos was read before
-        const uint64_t k = cand_key(x, cd, i, cd.v[i]);
+        const uint64_t k = kKeyed ? ckey(cd, i) : cand_key(x, cd, i, cd.v[i]);
         const int16_t g = cd.g[i];
         put_ckey(cd, pos, k);
         cd.g[pos] = g;
@@ -1454,6 +1468,10 @@ KP_FI void region_b(const BLK& B, const SelCtx& x, const Cands& cd, const int32_
     n = nsel + m;
   }
   KP_STAMP(x, 19);
+  if (n_sel) {
+    *n_sel = n;
+    return;
+  }
   assign_small(B, x, items, n, scratch, cap, area_bytes);
   KP_STAMP(x, 20);
 }

@@ -24,6 +24,10 @@
 //  10  "distinct": config 3 with every binding's requests drawn independently (cpu
 //      milli uniform over [100, 4000], memory MiB over [128, 16384]), so nearly every
 //      binding is its own estimator class; performance only.
+//  11  "min0": config-4 clusters and spread constraints whose MinGroups are 0 (region
+//      and cluster), so calcGroupScore divides Replicas by 0 (+Inf, or NaN at
+//      Replicas 0, both MinInt64 on amd64: SURVEY hazard H4, group_clusters.go:
+//      248-249) on Divided bindings; parity only.
 //   9  "templates": multi-template workloads (spec.Components) for the
 //      MultiplePodTemplatesScheduling gate: most carry a cluster spread constraint
 //      with MinGroups = MaxGroups = 1 (isMultiTemplateSchedulingApplicable), over
@@ -147,7 +151,7 @@ void gvk(int g, std::string* gv, std::string* kind) {
 
 void gen_cluster(kps_world& w, uint32_t i, kp_cluster& c) {
   Rng r(key(w.seed, 1, i));
-  const int cfg = w.config == 10 ? 3 : w.config;  // config 10: config-3 clusters
+  const int cfg = w.config == 10 ? 3 : (w.config == 11 ? 4 : w.config);  // configs 10 / 11: config-3 / 4 clusters
   c.name = w.s(w.cname(i));
   // labels: 8 distinct keys of 16
   c.labels = w.a.alloc<kp_label>(8);
@@ -400,6 +404,39 @@ void gen_binding(kps_world& w, uint64_t i, kp_binding& b) {
       b.n_spread_constraints = 1;
     }
     b.spread_constraints = sc;
+  } else if (cfg == 11) {
+    const double x = r.unit();
+    kp_spread_constraint* sc = w.a.alloc<kp_spread_constraint>(2);
+    if (x < 0.45) {
+      sc[0] = {w.s("region"), {}, 2 + (int64_t)r.below(2), 0};
+      sc[1] = {w.s("cluster"), {}, 8, r.p(0.5) ? 0 : 4};
+      b.n_spread_constraints = 2;
+    } else if (x < 0.65) {
+      sc[0] = {w.s("cluster"), {}, 6, 2};  // (cluster first: the map keeps the last per field)
+      sc[1] = {w.s("region"), {}, 2, 0};
+      b.n_spread_constraints = 2;
+    } else if (x < 0.75) {
+      sc[0] = {w.s("region"), {}, 3, 0};  // region only: no cluster MaxGroups
+      b.n_spread_constraints = 1;
+    } else if (x < 0.9) {
+      sc[0] = {w.s("cluster"), {}, 8, 0};
+      b.n_spread_constraints = 1;
+    } else {
+      sc[0] = {w.s("region"), {}, 3, 1};
+      sc[1] = {w.s("cluster"), {}, 8, 3};
+      b.n_spread_constraints = 2;
+    }
+    b.spread_constraints = sc;
+    const double y = r.unit();
+    if (y < 0.4) {
+      b.replica_division_preference = w.s("Aggregated");
+      b.has_weight_preference = 0;
+      b.dynamic_weight = kp_str{nullptr, 0};
+    } else if (y < 0.55) {
+      b.replica_scheduling_type = w.s("Duplicated");
+    } else if (y < 0.6) {
+      b.replicas = 0;  // Replicas / MinGroups = 0 / 0: NaN
+    }
   }
   // previous placement (20%) and eviction (5%)
   if (r.p(0.2) && C > 0) {

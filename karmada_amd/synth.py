@@ -22,6 +22,7 @@ CONFIGS = {
     8: (64, 2_000),     # int32 wrap of replica sums, weights >= 2^31, parity only
     9: (2_000, 5_000),  # multi-template workloads (MultiplePodTemplatesScheduling), parity only
     10: (5_000, 100_000),  # config 3 with per-binding-distinct requests (estimator classes ~ bindings)
+    11: (5_000, 5_000),  # spread constraints with MinGroups 0, parity only
 }
 
 

@@ -1850,9 +1850,13 @@ i64 calcGroupScoreForDuplicate(const vector<DetailInfo>& clusters, const Binding
   return mul64(valid, kWeightUnit) + sumValid / valid;
 }
 // int64(math.Ceil(float64/float64)) with amd64 conversion of NaN/Inf/out-of-range (hazard H4)
+std::atomic<uint64_t> g_h4_hits{0};  // conversions that took the NaN/Inf branch (tests count them)
 i64 goCeilDivToInt64(i32 a, i64 b) {
   double q = std::ceil((double)a / (double)b);
-  if (std::isnan(q) || q >= 9223372036854775808.0 || q < -9223372036854775808.0) return INT64_MIN;
+  if (std::isnan(q) || q >= 9223372036854775808.0 || q < -9223372036854775808.0) {
+    g_h4_hits.fetch_add(1, std::memory_order_relaxed);
+    return INT64_MIN;
+  }
   return (i64)q;
 }
 // calcGroupScore (group_clusters.go:238-351)
@@ -2748,6 +2752,12 @@ int kpo_select_groups(const kp_str* names, const int64_t* values, const int64_t*
   auto sel = selectGroups(g, min_c, max_c, target);
   for (size_t i = 0; i < sel.size(); i++) out[i] = (uint32_t)(sel[i] - &g[0]);
   return (int)sel.size();
+}
+
+// calcGroupScore's conversions that took hazard H4's NaN/Inf branch since the last reset
+// (the parity tests check that a workload exercised it).
+uint64_t kpo_h4_hits(int reset) {
+  return reset ? g_h4_hits.exchange(0) : g_h4_hits.load();
 }
 
 int64_t kpo_calc_group_score(const kpo_candidate* cands, uint32_t n, const kp_binding* b, int64_t min_groups) {

@@ -131,6 +131,7 @@ int kpo_assign_replicas(const kpo_candidate* cands, uint32_t n, const kp_cluster
 int kpo_select_groups(const kp_str* names, const int64_t* values, const int64_t* weights,
                       uint32_t n, int64_t min_c, int64_t max_c, int64_t target, uint32_t* out);
 /* spreadconstraint.(GroupClustersInfo).calcGroupScore. */
+uint64_t kpo_h4_hits(int reset);
 int64_t kpo_calc_group_score(const kpo_candidate* cands, uint32_t n, const kp_binding* b,
                              int64_t min_groups);
 /* GroupClustersWithScore + SelectBestClusters from a scored cluster list with

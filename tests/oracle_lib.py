@@ -61,6 +61,8 @@ def lib():
     L.kpo_select_groups.argtypes = [C.POINTER(api.kp_str), C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.c_uint32,
                                     C.c_int64, C.c_int64, C.c_int64, C.POINTER(C.c_uint32)]
     L.kpo_calc_group_score.restype = C.c_int64
+    L.kpo_h4_hits.restype = C.c_uint64
+    L.kpo_h4_hits.argtypes = [C.c_int]
     L.kpo_calc_group_score.argtypes = [C.POINTER(kpo_candidate), C.c_uint32, C.POINTER(api.kp_binding), C.c_int64]
     L.kpo_select_clusters.argtypes = [C.POINTER(api.kp_cluster), C.POINTER(C.c_int64), C.POINTER(C.c_int32),
                                       C.c_uint32, C.POINTER(api.kp_binding), C.c_int32, C.POINTER(C.c_uint32),
