@@ -3128,7 +3128,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
                              (!bt->l_cluster.empty() || !bt->l_region.empty()) &&
                              kOrderWaves * ((order_lds_bytes(s->view.W, s->view.n_regions) + 15) & ~(size_t)15) <=
                                  e->max_lds &&
-                             kOrderWaves * ((region_a_order_lds_bytes(s->view.n_regions) + 15) & ~(size_t)15) <=
+                             kOrderWaves * ((region_a_order_lds_bytes(s->view.n_regions, s->view.W) + 15) & ~(size_t)15) <=
                                  e->max_lds;
   const bool orders = top || spread_orders;
   if (orders)
@@ -3254,7 +3254,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       KArgs ko = k;
       ko.n_order = nullptr;
       KPROF(st, "k_region_a_order", ko.n, -1, dev::region_a_order(st, ko, bt->rout, bt->rstat, bt->d_fba, bt->stats + 14,
-                                 (region_a_order_lds_bytes(R) + 15) & ~(size_t)15));
+                                 (region_a_order_lds_bytes(R, s->view.W) + 15) & ~(size_t)15));
       KArgs kf = k;
       kf.sub = bt->d_fba;
       kf.n_dev = bt->stats + 14;

@@ -728,17 +728,58 @@ KP_FI void body_select_all_stream(const BLK& B, int blk, unsigned char* smem, co
 // Outcome of a class-order selection (cluster_order_select, region_order_select).
 enum : int { ORD_NA = 0, ORD_DONE = 1, ORD_ITEMS = 2 };
 
-// The class-order selections apply to a binding without spec.Clusters (locality
-// score 0, assigned replicas 0) and without overflow tiers (order 0) whose class
-// row can be walked (k_class_order's ok: no MaxInt32, no negative estimate): its
-// sortClusters key is then (estimate desc, name asc), i.e. the class order filtered
-// by its feasibility row. Returns the class, or -1.
-KP_HD inline int32_t order_class(const KArgs& a, const SelCtx& x) {
+// The class-order selections apply to a binding without overflow tiers (order 0)
+// whose class row can be walked (k_class_order's ok: no MaxInt32, no negative
+// estimate): a candidate outside spec.Clusters then has the sortClusters key
+// (score 0, estimate desc, name asc), so those candidates are the class order
+// filtered by the feasibility row. spec.Clusters (at most kOrdTargets distinct
+// names, ClusterLocality on: `targets`) score 100, so the feasible ones sort ahead
+// of all the others, among themselves by their keys (ord_targets). Returns the
+// class, or -1.
+constexpr int kOrdTargets = 16;
+KP_HD inline bool ord_targets_ok(const BindHdr& h) {
+  return h.tgt_cnt <= kOrdTargets && (h.flags & BF_SCORE_LOCALITY) && !(h.flags & BF_DUP_TARGETS);
+}
+KP_HD inline int32_t order_class(const KArgs& a, const SelCtx& x, bool targets = false) {
   const BindHdr& h = *x.h;
   if (!a.ord || !a.cok || !a.bcls) return -1;
   const int32_t cls = a.bcls[x.b];
-  if (cls <= 0 || !a.cok[cls] || h.tgt_cnt != 0 || h.ovf_mode != OVF_ZERO || (h.flags & BF_BAD)) return -1;
+  if (cls <= 0 || !a.cok[cls] || h.ovf_mode != OVF_ZERO || (h.flags & BF_BAD)) return -1;
+  if (h.tgt_cnt != 0 && !(targets && ord_targets_ok(h))) return -1;
   return cls;
+}
+// The binding's feasible spec.Clusters entries as sortClusters keys (locality 100,
+// AvailableReplicas = estimate + assigned), ascending, in tk[0, n); tmp: kOrdTargets
+// entries of scratch. Returns n, or -1 when one has a negative AvailableReplicas (the
+// callers' prefix arguments need every AvailableReplicas >= 0). Needs x.tgt_bits.
+template <class BLK>
+KP_FI int ord_targets(const BLK& B, const SelCtx& x, uint64_t* tk, uint64_t* tmp) {
+  const BindHdr& h = *x.h;
+  const int T = h.tgt_cnt;
+  if (T == 0) return 0;  // block-uniform
+  int64_t bad = 0;
+  for (int j = B.tid(); j < T; j += B.nth()) {
+    const uint32_t r = (uint32_t)x.bv->ipool[h.tgt_off + 2 * j];
+    uint64_t k = ~0ull;
+    if (mask_test(x.frow, (int)r)) {
+      const int64_t av = (int64_t)est_at(x, (int)r) + (int64_t)x.bv->ipool[h.tgt_off + 2 * j + 1];
+      if (av < 0) bad = 1;
+      k = sort_key(0, 100, av, r);
+    }
+    tmp[j] = k;
+  }
+  if (B.sum64(bad) != 0) return -1;  // (its barrier also publishes tmp)
+  int n = 0;
+  for (int j = 0; j < T; j++) n += tmp[j] != ~0ull ? 1 : 0;
+  for (int j = B.tid(); j < T; j += B.nth()) {
+    const uint64_t k = tmp[j];
+    if (k == ~0ull) continue;
+    int p = 0;
+    for (int q = 0; q < T; q++) p += tmp[q] < k ? 1 : 0;  // (distinct names: distinct keys)
+    tk[p] = k;
+  }
+  B.sync();
+  return n;
 }
 KP_HD inline Item order_item(uint64_t e) {
   Item it;
@@ -757,10 +798,13 @@ KP_HD inline Item order_item(uint64_t e) {
 // one's, and a swap needs a strictly larger one), so only the resource check
 // remains. ORD_ITEMS: items[0, *n) in sortClusters order (at most max_items);
 // ORD_DONE: the status is written; ORD_NA: nothing written.
+// tk, tmp: kOrdTargets entries each (nullptr: bindings with spec.Clusters go ORD_NA);
+// the feasible targets come first (ord_targets), then the filtered class order.
 template <class BLK>
-KP_FI int cluster_order_select(const BLK& B, const KArgs& a, const SelCtx& x, Item* items, int max_items, int* n_out) {
+KP_FI int cluster_order_select(const BLK& B, const KArgs& a, const SelCtx& x, Item* items, int max_items, int* n_out,
+                               uint64_t* tk = nullptr, uint64_t* tmp = nullptr) {
   const BindHdr& h = *x.h;
-  const int32_t cls = order_class(a, x);
+  const int32_t cls = order_class(a, x, tk != nullptr);
   if (cls < 0) return ORD_NA;
   KP_STAMP_INIT
   const SnapView& s = *x.s;
@@ -787,17 +831,25 @@ KP_FI int cluster_order_select(const BLK& B, const KArgs& a, const SelCtx& x, It
     return ORD_DONE;
   }
   if (needCnt > max_items) return ORD_NA;
-  // walk the class order, nth entries per step, keeping the feasible ones in order
+  const int nt = h.tgt_cnt > 0 ? ord_targets(B, x, tk, tmp) : 0;
+  if (nt < 0) return ORD_NA;
+  const uint32_t* tb = h.tgt_cnt > 0 ? x.tgt_bits : nullptr;
+  // the feasible targets first, then the class order (nth entries per step), keeping
+  // the feasible non-targets in order
   const uint64_t* ord = a.ord + (size_t)cls * s.Cp;
-  int n = 0;
+  int n = nt < needCnt ? nt : (int)needCnt;
   int64_t tot = 0;
+  for (int j = B.tid(); j < n; j += B.nth()) {
+    items[j] = item_from_key(x, tk[j]);
+    tot += key_avail(tk[j]);
+  }
   for (int i0 = 0; i0 < s.C && n < needCnt; i0 += B.nth()) {
     const int i = i0 + B.tid();
     uint64_t e = 0;
     bool in = false;
     if (i < s.C) {
       e = ord[i];
-      in = mask_test(x.frow, (int)(uint32_t)e);
+      in = mask_test(x.frow, (int)(uint32_t)e) && !(tb && bit_test(tb, (int)(uint32_t)e));
     }
     int32_t cnt;
     const int32_t pos = n + B.excl_scan(in ? 1 : 0, &cnt);
@@ -811,7 +863,10 @@ KP_FI int cluster_order_select(const BLK& B, const KArgs& a, const SelCtx& x, It
   if (n > needCnt) n = (int)needCnt;
   tot = B.sum64(tot);
   KP_STAMP(x, 38);
-  if (need != -1 && tot < (int64_t)need) {  // selectClustersByAvailableResource: no swap can help
+  if (need != -1 && tot < (int64_t)need) {  // selectClustersByAvailableResource
+    // a target in the list: a rest cluster may hold more than a selected target, so
+    // the swap step may fire (the full kernel runs it); otherwise no swap can help
+    if (nt > 0) return ORD_NA;
     if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_CLUSTER_RESOURCE, needCnt);
     return ORD_DONE;
   }
@@ -841,7 +896,7 @@ KP_FI void body_select_cluster(const BLK& B, int blk, unsigned char* smem, const
                                                                                     : serial_scratch_bytes(scratch_cap);
   {
     int n = 0;
-    const int o = cluster_order_select(B, a, x, items, kSmallMax, &n);
+    const int o = cluster_order_select(B, a, x, items, kSmallMax, &n, keys, keys + kOrdTargets);
     if (o == ORD_DONE) return;
     if (o == ORD_ITEMS) {
       if (B.tid() == 0 && a.n_order) kp_atomic_add(a.n_order, 1u);
@@ -876,9 +931,11 @@ struct OrderArgs {
 };
 constexpr int kOrderItems = 64;  // selected-list capacity
 constexpr int kOrderEcap = 128;  // sel_all_fast's party list (>= 64 + kOrderItems)
+// slice: [red 64 | hpos 8R | rsel 4R | target heads 4R | items | target keys 16 B x
+// kOrdTargets | spec.Clusters bits | selected bits 8W | whist 2 KB | hist 1 KB | buf]
 KP_HD inline size_t order_lds_bytes(int W, int R) {
-  return 64 + 8 * (size_t)R + 4 * (size_t)((R + 3) & ~3) + sizeof(Item) * kOrderItems + 8 * (size_t)W + 2048 +
-         1024 + 8 * (size_t)kOrderEcap;
+  return 64 + 8 * (size_t)R + 2 * 4 * (size_t)((R + 3) & ~3) + sizeof(Item) * kOrderItems + 16 * kOrdTargets +
+         8 * (size_t)W + 8 * (size_t)W + 2048 + 1024 + 8 * (size_t)kOrderEcap;
 }
 template <class BLK>
 KP_FI void body_spread_order(const BLK& B, int blk, unsigned char* smem, const KArgs& a, const OrderArgs& o) {
@@ -890,19 +947,27 @@ KP_FI void body_spread_order(const BLK& B, int blk, unsigned char* smem, const K
   p += 8 * (size_t)R;
   int32_t* rs = (int32_t*)p;
   p += 4 * (size_t)((R + 3) & ~3);
+  int32_t* th = (int32_t*)p;
+  p += 4 * (size_t)((R + 3) & ~3);
   Item* items = (Item*)p;
   p += sizeof(Item) * kOrderItems;
+  uint64_t* tk = (uint64_t*)p;
+  p += 16 * kOrdTargets;
+  uint32_t* tgt = (uint32_t*)p;  // spec.Clusters bits (8W bytes: W u64 words)
+  p += 8 * (size_t)W;
   uint64_t* selb = (uint64_t*)p;
-  SelCtx x = make_ctx(a, b, nullptr);  // no spec.Clusters on this path: the target bitset is never read
+  const BindHdr& h0 = a.bv.hdr[b];
+  if (h0.tgt_cnt > 0 && ord_targets_ok(h0)) build_bits(B, tgt, 2 * W, a.bv.ipool, h0.tgt_off, h0.tgt_cnt, 2);
+  SelCtx x = make_ctx(a, b, tgt);
   int n = 0, st = ORD_NA;
   if (o.region) {
     const int nsel = o.rnsel[blk];
     if (nsel == -1000) return;  // stage A wrote the status
     if (nsel >= 0)
       st = region_order_select(B, a, x, o.rout + (size_t)blk * R, o.rsel + (size_t)blk * R, nsel, hpos, rs, items,
-                               kOrderItems, &n);
+                               kOrderItems, &n, tk, tk + kOrdTargets, th);
   } else {
-    st = cluster_order_select(B, a, x, items, kOrderItems, &n);
+    st = cluster_order_select(B, a, x, items, kOrderItems, &n, tk, tk + kOrdTargets);
   }
   if (st == ORD_DONE) return;
   int why = SLOW_NONE + 1;
@@ -935,38 +1000,123 @@ KP_FI void body_spread_order(const BLK& B, int blk, unsigned char* smem, const K
 // (region_walk_free) and calcGroupScoreForDuplicate counts only the valid
 // clusters; both need per-region sums over the feasible clusters, taken here
 // straight from the feasibility row and the class row (no candidate arrays).
-// LDS slice: [red 64 B | cnt R | dvalid R | sum 8R]. The others go to fb.
-KP_HD inline size_t region_a_order_lds_bytes(int R) { return 64 + 8 * (size_t)((R + 1) & ~1) + 8 * (size_t)R; }
+// spec.Clusters (ord_targets_ok): the feasible targets score 100 and lead their
+// region's sortClusters order, so a region holding one is walked exactly
+// (region_target_score) over its targets, then its class order.
+// LDS slice: [red 64 B | cnt R | dvalid R | tcnt R | tdv R | sum 8R | tsum 8R |
+// target keys 16 x kOrdTargets | spec.Clusters bits 8W]. The others go to fb.
+KP_HD inline size_t region_a_order_lds_bytes(int R, int W) {
+  return 64 + 4 * 4 * (size_t)((R + 3) & ~3) + 2 * 8 * (size_t)R + 16 * kOrdTargets + 8 * (size_t)W;
+}
+// calcGroupScore (group_clusters.go:238-351, divided) of a region with Tr >= 1
+// feasible targets (keys tk[0, nt), ascending; their AvailableReplicas sum St) and
+// cnt candidates summing sum: the walk breaks at the first n >= m with P(n) >=
+// target, P the prefix over the region's sortClusters order (targets, then its
+// class order: every AvailableReplicas >= 0, so P only grows and the break is at
+// max(m, n_sum), n_sum the first n with P(n) >= target). Every lane returns it.
+template <class BLK>
+KP_FI int64_t region_target_score(const BLK& B, const KArgs& a, const SelCtx& x, int32_t cls, const uint64_t* tk,
+                                  int nt, int r, int64_t Tr, int64_t St, int64_t cnt, int64_t sum, int64_t target,
+                                  int64_t m) {
+  const SnapView& s = a.s;
+  int64_t n_sum = -1;
+  {
+    int64_t k = 0, p = 0;
+    for (int j = 0; j < nt && n_sum < 0; j++) {
+      if (s.region_idx[key_rank(tk[j])] != r) continue;
+      k++;
+      p += key_avail(tk[j]);
+      if (p >= target) n_sum = k;
+    }
+  }
+  if (n_sum < 0 && (m <= cnt)) {
+    // the region's class-order entries (feasible, not targets) until Q(j) >= target - St
+    const int64_t need = target - St;
+    const uint64_t* ord = a.ord + (size_t)cls * s.Cp;
+    int64_t run = 0, cj = 0;
+    for (int i0 = 0; i0 < s.C && n_sum < 0; i0 += B.nth()) {
+      const int i = i0 + B.tid();
+      int64_t v = 0;
+      bool in = false;
+      if (i < s.C) {
+        const uint64_t e = ord[i];
+        const int c = (int)(uint32_t)e;
+        if (mask_test(x.frow, c) && !bit_test(x.tgt_bits, c) && s.region_idx[c] == r) {
+          in = true;
+          v = (int64_t)(int32_t)(e >> 32);
+        }
+      }
+      const int64_t tot = B.sum64(v);
+      uint64_t mm = B.wballot(in);
+      if (run + tot < need) {
+        run += tot;
+        cj += popc64(mm);
+        continue;
+      }
+      while (mm) {  // the break is in this chunk: its members in order (uniform)
+        const int l = (int)__builtin_ctzll(mm);
+        mm &= mm - 1;
+        cj++;
+        run += B.wread(v, l);
+        if (run >= need) {
+          n_sum = Tr + cj;
+          break;
+        }
+      }
+    }
+  }
+  const int64_t valid = n_sum < 0 ? -1 : (m > n_sum ? m : n_sum);
+  if (valid >= 1 && valid <= cnt)
+    return add64(mul64(target, 1000), (100 * (valid < Tr ? valid : Tr)) / valid);
+  if (sum < target) return add64(mul64(sum, 1000), (100 * Tr) / cnt);  // no break: the totals
+  return add64(mul64(target, 1000), (100 * Tr) / cnt);
+}
 template <class BLK>
 KP_FI void body_region_a_order(const BLK& B, int blk, unsigned char* smem, const KArgs& a, RegionOut* rout,
                                int32_t* rstat, int32_t* fb, uint32_t* fb_n) {
   if (blk >= a.n) return;
   const int b = a.list[blk];
-  SelCtx x = make_ctx(a, b, nullptr);  // no spec.Clusters on this path
-  const int32_t cls = order_class(a, x);
+  const SnapView& s = a.s;
+  const int R = s.n_regions, R4 = (R + 3) & ~3;
+  int32_t* cnt = (int32_t*)(smem + 64);
+  int32_t* dvalid = cnt + R4;
+  int32_t* tcnt = dvalid + R4;
+  int32_t* tdv = tcnt + R4;
+  unsigned long long* sum = (unsigned long long*)(tdv + R4);
+  int64_t* tsum = (int64_t*)(sum + R);
+  uint64_t* tk = (uint64_t*)(tsum + R);
+  uint32_t* tgt = (uint32_t*)(tk + 2 * kOrdTargets);
+  const BindHdr& h0 = a.bv.hdr[b];
+  if (h0.tgt_cnt > 0 && ord_targets_ok(h0)) build_bits(B, tgt, 2 * s.W, a.bv.ipool, h0.tgt_off, h0.tgt_cnt, 2);
+  SelCtx x = make_ctx(a, b, tgt);
+  const int32_t cls = order_class(a, x, true);
   if (cls < 0) {
     if (B.tid() == 0) fb[kp_atomic_add(fb_n, 1u)] = blk;
 #ifdef KP_STAMPS
     if (B.tid() == 0) {  // why: 55 no orders, 56 class 0, 57 row not walkable, 58 spec.Clusters, 59 other
-      const BindHdr& h0 = *x.h;
+      const BindHdr& h1 = *x.h;
       const int32_t c0 = a.bcls && a.ord ? a.bcls[b] : -1;
-      KP_COUNT(x, !a.ord || !a.bcls ? 55 : c0 <= 0 ? 56 : !a.cok[c0] ? 57 : h0.tgt_cnt != 0 ? 58 : 59, 1);
+      KP_COUNT(x, !a.ord || !a.bcls ? 55 : c0 <= 0 ? 56 : !a.cok[c0] ? 57 : h1.tgt_cnt != 0 ? 58 : 59, 1);
     }
 #endif
     return;
   }
-  const SnapView& s = a.s;
   const BindHdr& h = *x.h;
-  const int R = s.n_regions;
-  int32_t* cnt = (int32_t*)(smem + 64);
-  int32_t* dvalid = cnt + R;
-  unsigned long long* sum = (unsigned long long*)(smem + 64 + 8 * (size_t)((R + 1) & ~1));
   for (int r = B.tid(); r < R; r += B.nth()) {
     cnt[r] = 0;
     dvalid[r] = 0;
+    tcnt[r] = 0;
+    tdv[r] = 0;
     sum[r] = 0;
+    tsum[r] = 0;
   }
   B.sync();
+  const int nt = h.tgt_cnt > 0 ? ord_targets(B, x, tk, tk + kOrdTargets) : 0;
+  if (nt < 0) {
+    if (B.tid() == 0) fb[kp_atomic_add(fb_n, 1u)] = blk;
+    return;
+  }
+  const uint32_t* tb = h.tgt_cnt > 0 ? tgt : nullptr;
   const bool dup = (h.flags & BF_GROUP_DUP) != 0;
   const int32_t* row = x.erow;
   int64_t F = 0;
@@ -977,6 +1127,7 @@ KP_FI void body_region_a_order(const BLK& B, int blk, unsigned char* smem, const
       if (!((m >> l) & 1ull)) continue;
       const int c = w * 64 + l;
       F++;
+      if (tb && bit_test(tb, c)) continue;  // (a target: below)
       const int r = s.region_idx[c];
       if (r >= 0) {
         const int32_t e = row[c];
@@ -984,6 +1135,19 @@ KP_FI void body_region_a_order(const BLK& B, int blk, unsigned char* smem, const
         kp_atomic_add(&sum[r], (unsigned long long)e);
         if (dup && e >= h.replicas) kp_atomic_add(&dvalid[r], 1);
       }
+    }
+  }
+  for (int j = B.tid(); j < nt; j += B.nth()) {
+    const int r = s.region_idx[key_rank(tk[j])];
+    if (r < 0) continue;
+    const int64_t av = key_avail(tk[j]);
+    kp_atomic_add(&cnt[r], 1);
+    kp_atomic_add(&sum[r], (unsigned long long)av);
+    kp_atomic_add(&tcnt[r], 1);
+    kp_atomic_add((unsigned long long*)&tsum[r], (unsigned long long)av);
+    if (dup && av >= (int64_t)h.replicas) {
+      kp_atomic_add(&dvalid[r], 1);
+      kp_atomic_add(&tdv[r], 1);
     }
   }
   F = B.sum64(F);  // (its reduction also orders the LDS sums before the reads below)
@@ -996,10 +1160,20 @@ KP_FI void body_region_a_order(const BLK& B, int blk, unsigned char* smem, const
   }
   RegionOut* out = rout + (size_t)blk * R;
   const int64_t target = go_ceil_div_i64(h.replicas, h.region_min);
+  int64_t mg = h.cluster_min;  // clusterMinGroups, at least the group's minGroups
+  if (mg < h.region_min) mg = h.region_min;
   for (int r = B.tid(); r < R; r += B.nth()) {
     out[r].count = cnt[r];
-    if (dup) out[r].score = dvalid[r] == 0 ? 0 : mul64((int64_t)dvalid[r], 1000);
-    else out[r].score = region_score_totals(cnt[r], (int64_t)sum[r], 0, target);
+    if (dup) out[r].score = dvalid[r] == 0 ? 0 : add64(mul64((int64_t)dvalid[r], 1000), (100 * (int64_t)tdv[r]) / dvalid[r]);
+    else if (tcnt[r] == 0) out[r].score = region_score_totals(cnt[r], (int64_t)sum[r], 0, target);
+  }
+  if (!dup && nt > 0) {
+    for (int r = 0; r < R; r++) {  // the regions holding a target: walked (wave-uniform loop)
+      if (tcnt[r] == 0) continue;
+      const int64_t sc = region_target_score(B, a, x, cls, tk, nt, r, tcnt[r], tsum[r], cnt[r], (int64_t)sum[r],
+                                             target, mg);
+      if (B.tid() == 0) out[r].score = sc;
+    }
   }
   if (a.n_order && B.tid() == 0) kp_atomic_add(a.n_order, 1u);
   if (B.tid() == 0) rstat[blk] = 0;
@@ -1066,17 +1240,20 @@ KP_FI void body_region_a(const BLK& B, int blk, unsigned char* smem, const KArgs
 
 // selectBestClustersByRegion (select_clusters_by_region.go:41-63) over the
 // binding's estimator-class order (order_class): each selected region's head is
-// its first entry in that order, the rest are the next restCnt entries of the
-// selected regions that are not heads, and the candidate count comes from stage
+// its first entry in sortClusters order, the rest are the next restCnt entries of
+// the selected regions that are not heads, and the candidate count comes from stage
 // A's per-region counts, so the walk stops once the heads and the rest are found
-// instead of gathering every candidate. hpos, rsel: [R] LDS. ORD_ITEMS: items[0, *n)
+// instead of gathering every candidate. With spec.Clusters (tk != nullptr; tk, tmp:
+// kOrdTargets entries, th: [R]) the feasible targets precede every other candidate:
+// a selected region holding one has its first target as head, and the other targets
+// of the selected regions lead the rest. hpos, rsel: [R] LDS. ORD_ITEMS: items[0, *n)
 // = the heads in path order, then the rest in sortClusters order.
 template <class BLK>
 KP_FI int region_order_select(const BLK& B, const KArgs& a, const SelCtx& x, const RegionOut* ro, const int32_t* sel,
                               int nsel, unsigned long long* hpos, int32_t* rsel, Item* items, int max_items,
-                              int* n_out) {
+                              int* n_out, uint64_t* tk = nullptr, uint64_t* tmp = nullptr, int32_t* th = nullptr) {
   const BindHdr& h = *x.h;
-  const int32_t cls = order_class(a, x);
+  const int32_t cls = order_class(a, x, tk != nullptr);
   if (cls < 0 || !ro) return ORD_NA;
   KP_STAMP_INIT
   const SnapView& s = *x.s;
@@ -1090,42 +1267,74 @@ KP_FI int region_order_select(const BLK& B, const KArgs& a, const SelCtx& x, con
   for (int r = B.tid(); r < R; r += B.nth()) {
     hpos[r] = ~0ull;
     rsel[r] = -1;
+    if (th) th[r] = -1;
   }
   B.sync();
   for (int j = B.tid(); j < nsel; j += B.nth()) rsel[sel[j]] = j;
   B.sync();
+  const int nt = h.tgt_cnt > 0 ? ord_targets(B, x, tk, tmp) : 0;
+  if (nt < 0) return ORD_NA;
+  const uint32_t* tb = h.tgt_cnt > 0 ? x.tgt_bits : nullptr;
+  // target heads (a selected region's first target), then the other targets of the
+  // selected regions, in key order, lead the rest (every thread walks the <= 16)
+  int nth_ = 0, ntr = 0;
+  if (nt > 0) {
+    if (B.tid() == 0)
+      for (int j = 0; j < nt; j++) {
+        const int r = s.region_idx[key_rank(tk[j])];
+        if (r >= 0 && rsel[r] >= 0 && th[r] < 0) th[r] = j;
+      }
+    B.sync();
+    for (int j = 0; j < nt; j++) {
+      const int r = s.region_idx[key_rank(tk[j])];
+      if (r < 0 || rsel[r] < 0) continue;
+      if (th[r] == j) {
+        nth_++;
+      } else {
+        if (ntr < want && B.tid() == 0) items[nsel + ntr] = item_from_key(x, tk[j]);
+        ntr++;
+      }
+    }
+  }
+  const int64_t tw = ntr < want ? ntr : want;  // rest entries the targets fill
+  const int64_t want2 = want - tw;             // ... and the class order
+  const int nh_need = nsel - nth_;
   const uint64_t* ord = a.ord + (size_t)cls * s.Cp;
   KP_STAMP(x, 32);
   int nh = 0, nr = 0;
-  for (int i0 = 0; i0 < s.C && (nh < nsel || nr < want); i0 += B.nth()) {
+  for (int i0 = 0; i0 < s.C && (nh < nh_need || nr < want2); i0 += B.nth()) {
     const int i = i0 + B.tid();
     uint64_t e = 0;
     int r = -1;
     if (i < s.C) {
       e = ord[i];
       const int c = (int)(uint32_t)e;
-      if (mask_test(x.frow, c)) {
+      if (mask_test(x.frow, c) && !(tb && bit_test(tb, c))) {
         r = s.region_idx[c];
         if (r >= 0 && rsel[r] < 0) r = -1;
       }
     }
+    const bool thead = r >= 0 && th && th[r] >= 0;  // the region's head is a target
     // (a stale read is only larger: the minimum only falls)
-    if (r >= 0 && hpos[r] > (unsigned long long)i) kp_atomic_min_u64(&hpos[r], (unsigned long long)i);
+    if (r >= 0 && !thead && hpos[r] > (unsigned long long)i) kp_atomic_min_u64(&hpos[r], (unsigned long long)i);
     B.sync();
-    const bool head = r >= 0 && hpos[r] == (unsigned long long)i;
+    const bool head = r >= 0 && !thead && hpos[r] == (unsigned long long)i;
     const bool rest = r >= 0 && !head;
     int32_t cnt;
     const int32_t pk = B.excl_scan((rest ? 1 : 0) | (head ? 1 << 16 : 0), &cnt);
     const int32_t pos = nr + (pk & 0xffff);
-    if (rest && pos < want) items[nsel + pos] = order_item(e);
+    if (rest && pos < want2) items[nsel + tw + pos] = order_item(e);
     nr += cnt & 0xffff;
     nh += cnt >> 16;
     KP_COUNT(x, 36, 1);
   }
   B.sync();
   KP_STAMP(x, 33);
-  if (nh < nsel || nr < want) return ORD_NA;  // a selected region without a feasible cluster
-  for (int j = B.tid(); j < nsel; j += B.nth()) items[j] = order_item(ord[hpos[sel[j]]]);
+  if (nh < nh_need || nr < want2) return ORD_NA;  // a selected region without a feasible cluster
+  for (int j = B.tid(); j < nsel; j += B.nth()) {
+    const int r = sel[j];
+    items[j] = th && th[r] >= 0 ? item_from_key(x, tk[th[r]]) : order_item(ord[hpos[r]]);
+  }
   B.sync();
   KP_STAMP(x, 34);
   *n_out = nsel + (int)want;
@@ -1178,7 +1387,8 @@ KP_FI void body_region_b(const BLK& B, int blk, unsigned char* smem, const KArgs
   {
     int n = 0;
     if (region_order_select(B, a, x, rout ? rout + (size_t)blk * R : nullptr, rsel + (size_t)blk * R, nsel, heads, rs,
-                            items, kSmallMax, &n) == ORD_ITEMS) {
+                            items, kSmallMax, &n, keys, keys + kOrdTargets,
+                            (int32_t*)(keys + 2 * kOrdTargets)) == ORD_ITEMS) {
       if (B.tid() == 0 && a.n_order) kp_atomic_add(a.n_order, 1u);
       assign_small(B, x, items, n, p, scratch_cap, area_bytes);
       KP_STAMP(x, 35);
