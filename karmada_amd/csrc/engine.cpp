@@ -2621,12 +2621,9 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
 }
 
 // Bindings per estimator class below which a batch skips the class orders.
-static int64_t order_amort() {
-  static const int64_t v = [] {
-    const char* e = getenv("KP_ORDER_AMORT");
-    return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)4;
-  }();
-  return v;
+static int64_t order_amort() {  // (read per batch: tests switch it)
+  const char* e = getenv("KP_ORDER_AMORT");
+  return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)4;
 }
 
 int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindings, uint64_t n, kp_batch** out) {
@@ -2827,11 +2824,13 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   // one class per binding (per-binding requests) sorts a Cp row per binding instead,
   // so it keeps the full-candidate kernels (KP_ORDER_AMORT: bindings per class needed)
   const bool orders_pay = (int64_t)bt->crep.size() * order_amort() <= (int64_t)B;
+  // Without them k_select_top thresholds each binding's votes by a histogram instead of
+  // walking an order (kp_top.h), so its fallback list exists either way.
+  if (!bt->crep.empty()) a.add(&bt->d_fb, std::max(1, bt->n_all_dyn));
   if (s->C <= 16384 && !bt->crep.empty() && orders_pay && kRedBytes + 8 * (size_t)P <= e->max_lds) {
     a.add(&bt->d_ord, bt->crep.size() * (size_t)s->Cp);
     a.add(&bt->d_ctot, bt->crep.size());
     a.add(&bt->d_cok, bt->crep.size());
-    a.add(&bt->d_fb, std::max(1, bt->n_all_dyn));
     a.add(&bt->d_fbc, std::max<size_t>(1, bt->l_cluster.size()));
     a.add(&bt->d_fbr, std::max(1, nr));
     a.add(&bt->d_fba, std::max(1, nr));
@@ -3120,8 +3119,14 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   int top_cap = e->top_cap;
   while (top_cap > 64 && kTopWaves * ((top_lds_bytes(s->Cp, top_cap) + 15) & ~(size_t)15) > e->max_lds) top_cap /= 2;
   const int top_cap_small = std::min(e->top_cap_small, top_cap);
-  const bool top = bits && e->top_on && bt->d_ord != nullptr && bt->n_all_dyn > 0 &&
-                   kTopWaves * ((top_lds_bytes(s->Cp, top_cap) + 15) & ~(size_t)15) <= e->max_lds;
+  // (without class orders, k_select_top thresholds the votes by a histogram: KP_TOPK=0 keeps
+  // the full-candidate kernel there instead)
+  static const bool topk_on = [] {
+    const char* v = getenv("KP_TOPK");
+    return !v || atoi(v) != 0;
+  }();
+  const bool top = bits && e->top_on && (bt->d_ord != nullptr || (topk_on && bt->d_fb != nullptr)) &&
+                   bt->n_all_dyn > 0 && kTopWaves * ((top_lds_bytes(s->Cp, top_cap) + 15) & ~(size_t)15) <= e->max_lds;
   // class orders: k_select_top's walk, and the spread selections over them
   // (k_spread_order, k_region_a_order), each where its LDS slices fit the device
   const bool spread_orders = bits && e->top_on && bt->d_ord != nullptr &&
@@ -3130,7 +3135,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
                                  e->max_lds &&
                              kOrderWaves * ((region_a_order_lds_bytes(s->view.n_regions, s->view.W) + 15) & ~(size_t)15) <=
                                  e->max_lds;
-  const bool orders = top || spread_orders;
+  const bool orders = (top && bt->d_ord != nullptr) || spread_orders;
   if (orders)
     KPROF(sp, "k_class_order", bt->crep.size(), -1,
           dev::class_order(sp, s->view, bt->cls_rows, (int)bt->crep.size(), bt->d_ord, bt->d_ctot, bt->d_cok));

@@ -1564,11 +1564,12 @@ KP_HD void body_slow(const BLK& B, int blk, int grid, unsigned char* smem, const
   Item* items = (Item*)((uint64_t*)(cd.v + a.s.Cp) + P);
   int32_t* pos = (int32_t*)(items + a.s.Cp);
   unsigned char* ser = (unsigned char*)(pos + a.s.Cp);
+  // the select kernels appended the flagged bindings to slow_ids (same stream: complete)
+  const int nslow = (int)*(volatile uint32_t*)&a.stats[0];
+  if (blk >= nslow || blk >= a.n) return;  // (block-uniform) a slot without a binding is never touched
   for (int i = B.tid(); i < a.s.Cp; i += B.nth()) pos[i] = -1;
   B.sync();
   const bool tie_lds = (size_t)lds_sort >= 3072 + 8 * (size_t)sel_all_ecap(a.s.Cp) + 64;
-  // the select kernels appended the flagged bindings to slow_ids (same stream: complete)
-  const int nslow = (int)*(volatile uint32_t*)&a.stats[0];
   for (int idx = blk; idx < nslow && idx < a.n; idx += grid) {
     const int b = a.list[idx];
     const int why = a.slow[b];

@@ -97,6 +97,15 @@ KP_HD inline size_t top_lds_bytes(int Cp, int cap) {
          64;
 }
 
+// Octave bucket of a vote (8 buckets per power of two), monotone in the vote: the
+// histogram the no-class-order path (TopArgs::ord == nullptr) thresholds the votes by.
+KP_HD inline int vote_octave(int32_t v) {
+  if (v <= 0) return 0;
+  const int e = 31 - __builtin_clz((uint32_t)v);
+  const int m = e >= 3 ? (v >> (e - 3)) & 7 : (v << (3 - e)) & 7;
+  return 1 + 8 * e + m;  // 1..248
+}
+
 template <class BLK>
 KP_FI void top_fallback(const BLK& B, const KArgs& a, const TopArgs& t, int b) {
   if (B.tid() == 0) t.fb[kp_atomic_add(t.fb_n, 1u)] = b;
@@ -109,6 +118,7 @@ KP_FI void top_fallback(const BLK& B, const KArgs& a, const TopArgs& t, int b) {
 #define KP_TOP_GROUP 4
 #endif
 constexpr int kTopAhead = KP_TOP_AHEAD, kTopGroup = KP_TOP_GROUP;
+constexpr int kTopStream = 8;  // row chunks per step of the no-class-order passes
 static_assert(kTopAhead % kTopGroup == 0, "the ring holds whole groups");
 
 // Hand-off of a binding from wave 0's walk to its workgroup's selection (k_select_top_wg).
@@ -158,24 +168,25 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   const int32_t cls = a.bcls ? a.bcls[b] : 0;
   // the first chunks of the class order, loaded with the binding's header and row (the
   // walk is the first to read them; a binding that does not walk wastes a few L2 hits)
-  const uint64_t* ord = t.ord + (size_t)cls * s.Cp;
+  // (no class orders: the votes are thresholded by a histogram instead of a walk)
+  const uint64_t* ord = t.ord ? t.ord + (size_t)cls * s.Cp : nullptr;
   const int lane = B.tid() % B.wwidth();
   const int ww = B.wwidth();
   uint64_t ring[kTopAhead];
 #if defined(__clang__)
 #pragma unroll
 #endif
-  for (int q = 0; q < kTopAhead; q++) ring[q] = lane + q * ww < s.C ? ord[lane + q * ww] : 0;
+  for (int q = 0; q < kTopAhead; q++) ring[q] = ord && lane + q * ww < s.C ? ord[lane + q * ww] : 0;
   bool elig = a.bcls != nullptr && h->sel == SEL_ALL && (st == ST_DYNAMIC || st == ST_AGGREGATED) &&
               (fl & BF_WORKLOAD_ASSIGN) && !(fl & (BF_EMPTY_PROP | BF_BAD | BF_DUP_TARGETS | BF_OVERFLOW)) &&
-              h->ovf_mode == OVF_ZERO && h->replicas > 0 && t.ok[cls] != 0;
+              h->ovf_mode == OVF_ZERO && h->replicas > 0 && (!ord || t.ok[cls] != 0);
+  int64_t sch = 0;  // |scheduled replicas|
   if (elig) {  // no int32 wrap anywhere: every vote sum stays below the class total + |scheduled replicas|
-    int64_t sch = 0;
     for (int j = 0; j < h->tgt_cnt; j++) {
       const int32_t r = kp_ldu(a.bv.ipool + h->tgt_off + 2 * j + 1);
       sch += r < 0 ? -(int64_t)r : (int64_t)r;
     }
-    elig = t.tot[cls] + sch < (int64_t)kInt32Max / 2;
+    if (ord) elig = t.tot[cls] + sch < (int64_t)kInt32Max / 2;  // (else checked over the feasible votes below)
   }
   if (!elig) {
     top_fallback(B, a, t, b);
@@ -243,6 +254,171 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   const int32_t assigned = wrap32(asum);
   bool complete = false;
   KP_STAMP(x, 10);
+  // No class order (about one binding per estimator class, so sorting a row per
+  // binding costs more than walking it): one pass over the feasible row takes the
+  // votes of the non-scheduled candidates into an octave histogram (count and sum per
+  // bucket, in the slice's SelScratch, free until sel_all_fast), their total (the int32
+  // wrap check the class total makes otherwise) and, for a fresh / scale-up division,
+  // the subset: the deciding bucket is the highest one whose cumulative count and sum
+  // cover the walk's condition, and every candidate in or above it joins the subset —
+  // the walk's argument with vmin = that bucket's lower edge (a coarser vmin only adds
+  // candidates with votes >= it, ties included). The bucket is tracked as the pass goes
+  // (it only rises), so a candidate below it is never appended and the list is
+  // compacted to it when full. Bucket sums are u32: they only wrap when the total does,
+  // and the binding falls back then.
+  uint32_t* hc = ss.hist;
+  uint32_t* hs = (uint32_t*)ss.whist;
+  int64_t rsum = 0, rcnt = 0;
+  if (!ord) {
+    const bool walk = fresh || assigned < h->replicas;
+    const int32_t target = fresh ? h->replicas : sub32(h->replicas, assigned);
+    int64_t psum = 0;  // Aggregated scale up: the prior clusters lead the order
+    if (walk && agg && !fresh && apos != 0) {
+      for (int i = B.tid(); i < n; i += B.nth())
+        if (h->tgt_cnt > 0 && sched_rep_of(x, cd.r[i]) > 0) psum += cd.v[i];
+      psum = B.sum64(psum);
+    }
+    const bool collect = walk && !(agg && tsum >= (int64_t)target && psum >= (int64_t)target);
+    for (int i = B.tid(); i < 256; i += B.nth()) {
+      hc[i] = 0;
+      hs[i] = 0;
+    }
+    B.sync();
+    auto cov_at = [&](int64_t c, int64_t v) {
+      return tsum + v >= (int64_t)target && (agg ? psum + v >= (int64_t)target : c >= (int64_t)target);
+    };
+    // the deciding bucket of the histogram so far (-1: none covers yet); every thread
+    auto find_thr = [&]() -> int64_t {
+      B.sync();  // (the histogram updates before the reads)
+      int64_t thr = -1, run_c = 0, run_s = 0;
+      for (int j0 = 0; j0 < 256 && thr < 0; j0 += 4 * B.nth()) {
+        const int j = j0 + 4 * B.tid();  // this thread's 4 buckets, descending: 255 - j - q
+        int32_t c4 = 0, s4 = 0;
+        for (int q = 0; q < 4 && j + q < 256; q++) {
+          c4 += (int32_t)hc[255 - (j + q)];
+          s4 += (int32_t)hs[255 - (j + q)];
+        }
+        int32_t tc, ts;
+        const int32_t ec = B.excl_scan(c4, &tc);
+        const int32_t es = B.excl_scan(s4, &ts);
+        int64_t pc = run_c + ec, ps = run_s + es, mine = -1;
+        for (int q = 0; q < 4 && j + q < 256 && mine < 0; q++) {
+          pc += hc[255 - (j + q)];
+          ps += (int64_t)(int32_t)hs[255 - (j + q)];
+          if (cov_at(pc, ps)) mine = 255 - (j + q);
+        }
+        thr = B.max64(mine);  // the first (highest) bucket that covers
+        run_c += tc;
+        run_s += ts;
+      }
+      return thr;
+    };
+    // the list [n0, n) keeps the appended candidates whose bucket is >= lo
+    const int32_t n0 = n;
+    auto compact = [&](int64_t lo) {
+      int m = n0;
+      for (int i0 = n0; i0 < n; i0 += B.nth()) {
+        const int i = i0 + B.tid();
+        uint32_t r = 0;
+        int32_t v = 0;
+        bool keep = false;
+        if (i < n) {
+          r = cd.r[i];
+          v = cd.v[i];
+          keep = vote_octave(v) >= lo;
+        }
+        int32_t tot;
+        const int32_t pos = m + B.excl_scan(keep ? 1 : 0, &tot);  // (its barrier: reads before writes)
+        if (keep) {
+          cd.r[pos] = r;
+          cd.v[pos] = v;
+        }
+        m += tot;
+      }
+      B.sync();
+      n = m;
+    };
+    int64_t neg = 0, thr = -1;
+    bool over = false;
+    // kTopStream chunks per step: their row loads are issued together
+    for (int c0 = 0; c0 < s.C; c0 += kTopStream * B.nth()) {
+      int32_t vv[kTopStream];
+      bool ff[kTopStream];
+#if defined(__clang__)
+#pragma unroll
+#endif
+      for (int u = 0; u < kTopStream; u++) {
+        const int c = c0 + u * B.nth() + B.tid();
+        ff[u] = c < s.C && ((frow[c >> 6] >> (c & 63)) & 1ull) && !(h->tgt_cnt > 0 && bit_test(tgt, c));
+        vv[u] = ff[u] ? x.erow[c] : 0;
+      }
+#if defined(__clang__)
+#pragma unroll
+#endif
+      for (int u = 0; u < kTopStream; u++) {
+        vv[u] = est_merge(x, vv[u]);
+        if (!ff[u]) continue;
+        if (vv[u] < 0) {
+          neg = 1;
+          ff[u] = false;
+          continue;
+        }
+        const int bk = vote_octave(vv[u]);
+        kp_atomic_add(&hc[bk], 1u);
+        kp_atomic_add(&hs[bk], (uint32_t)vv[u]);
+        rsum += vv[u];
+        rcnt++;
+      }
+      if (!collect || over) continue;
+#if defined(__clang__)
+#pragma unroll
+#endif
+      for (int u = 0; u < kTopStream; u++) {
+        bool in = ff[u] && vote_octave(vv[u]) >= thr;
+        int32_t tot;
+        int32_t pos = B.excl_scan(in ? 1 : 0, &tot);
+        if (n + tot > t.cap && !over) {  // full: compact to the bucket as it stands now
+          thr = find_thr();
+          compact(thr);
+          in = in && vote_octave(vv[u]) >= thr;
+          pos = B.excl_scan(in ? 1 : 0, &tot);
+          if (n + tot > t.cap) over = true;
+        }
+        if (over) break;
+        if (in) {
+          cd.r[n + pos] = (uint32_t)(c0 + u * B.nth() + B.tid());
+          cd.v[n + pos] = vv[u];
+        }
+        n += tot;
+      }
+      if (!over) thr = find_thr();  // (its scans order this step's histogram updates)
+    }
+    B.sum2(rsum, neg);
+    rcnt = B.sum64(rcnt);  // (the reductions also order the histogram before the reads)
+    // negative votes / wrap risk (every vote sum the division takes is below this bound):
+    // every candidate
+    if (neg || rsum + (tsum < 0 ? -tsum : tsum) + sch >= (int64_t)kInt32Max / 2) {
+      top_fallback(B, a, t, b);
+      return;
+    }
+    if (collect) {
+      if (over) {
+        // past the capacity: the availability error needs only the votes' sum (below
+        // 2^30); otherwise every candidate (the full-candidate kernel)
+        if ((int64_t)(int32_t)(tsum + rsum) < (int64_t)target) {
+          if (B.tid() == 0)
+            sink_error(x, KP_STATUS_UNSCHEDULABLE, fresh ? KP_ERR_FRESH_NOT_ENOUGH : KP_ERR_SCALE_UP_NOT_ENOUGH,
+                       (int32_t)(tsum + rsum));
+          return;
+        }
+        top_fallback(B, a, t, b);
+        return;
+      }
+      thr = find_thr();
+      compact(thr);  // exactly the candidates in or above the deciding bucket
+      complete = (int64_t)(n - n0) == rcnt;
+    }
+  }
   if (fresh || assigned < h->replicas) {
     // fresh / scale up: walk the class order for the non-scheduled candidates
     const int32_t target = fresh ? h->replicas : sub32(h->replicas, assigned);
@@ -278,7 +454,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     // rest of the order. F - n0: the feasible candidates that are not scheduled.
     const int64_t unsched = F - (int64_t)n0;
     bool hopeless = false;
-    for (int g0 = 0; !cov0; g0 += kTopGroup * ww) {
+    for (int g0 = 0; ord && !cov0; g0 += kTopGroup * ww) {
       i0_last = g0 + (kTopGroup - 1) * ww;
       if (g0 >= s.C) {
         complete = true;

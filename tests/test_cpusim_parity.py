@@ -255,3 +255,30 @@ def test_cpusim_kernel_times():
         assert e.kernel_times() == {}
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("cap", [None, "64"], ids=["cap", "cap64"])
+@pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
+    (3, 3, 1000, 2000), (7, 17, 300, 1500), (6, 9, 700, 2000), (8, 4, 64, 1000), (8, 5, 16, 600), (10, 10, 2000, 1500),
+])
+def test_cpusim_top_histogram(config, seed, n_clusters, n_bindings, cap):
+    """k_select_top without class orders (KP_ORDER_AMORT forces it; config 10 takes it by
+    itself: about one estimator class per binding): each binding's feasible votes are
+    thresholded by an octave histogram instead of walking an order (kp_top.h), including
+    the wrap and negative-vote fallbacks of config 8."""
+    u = synth.Universe(config, seed, n_clusters, 0, n_bindings)
+    opts = api.options()
+    os.environ["KP_ORDER_AMORT"] = "1000000"
+    if cap:  # (read at engine creation) a small subset capacity: the list compactions and overflow
+        os.environ["KP_TOP_CAP"] = cap
+    times = []
+    try:
+        e = Engine(0, lib_path=CPUSIM)
+        got = run(e, u, opts, times=times)
+        e.close()
+    finally:
+        os.environ.pop("KP_ORDER_AMORT", None)
+        os.environ.pop("KP_TOP_CAP", None)
+    assert times[0]["n_top"] > 0
+    want = O.schedule_c(u.clusters, u.n_clusters, u.bindings, u.n_bindings, opts, O.FAST, 8)
+    compare(got, want, f"histogram config {config}")

@@ -104,6 +104,27 @@ def test_schedule_parity(engine, config, seed, n_clusters, n_bindings):
 
 
 @pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
+    (10, 10, 5000, 2000), (3, 3, 5000, 2000), (7, 17, 2000, 3000), (7, 18, 13, 2000), (6, 9, 700, 2000),
+    (8, 4, 64, 2000), (8, 6, 300, 1500),
+])
+def test_schedule_parity_top_histogram(engine, config, seed, n_clusters, n_bindings):
+    """k_select_top without class orders (config 10: about one estimator class per
+    binding; the others forced with KP_ORDER_AMORT): the votes thresholded by an octave
+    histogram instead of a walk of the class order (kp_top.h)."""
+    import os
+    u = synth.Universe(config, seed, n_clusters, 0, n_bindings)
+    opts = api.options()
+    os.environ["KP_ORDER_AMORT"] = "1000000"
+    try:
+        got = gpu_schedule(engine, u, opts)
+        t = engine.stage_times()
+    finally:
+        os.environ.pop("KP_ORDER_AMORT", None)
+    compare(got, oracle_schedule(u, opts), f"histogram config {config} seed {seed}")
+    assert t["n_top"] > 0
+
+
+@pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
     (3, 3, 500, 1000), (2, 2, 1000, 1000), (5, 5, 3000, 1200), (7, 17, 2000, 1000), (3, 3, 5000, 1000),
     # C >= 9000: the gathered SEL_ALL kernel needs more than 80 KB of LDS -> k_select_all_wide
     (6, 21, 9000, 600), (7, 22, 9000, 400), (3, 23, 10000, 300),

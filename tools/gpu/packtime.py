@@ -10,7 +10,7 @@ os.environ.setdefault("KP_PACK_TIMING", "1")
 from karmada_amd import api, synth  # noqa: E402
 from karmada_amd.engine import Batch, Engine, Snapshot  # noqa: E402
 
-eng = Engine(0)
+eng = Engine(0, lib_path=os.environ["KP_LIB"]) if os.environ.get("KP_LIB") else Engine(0)
 u = synth.Universe(3, 3, 5000, 0, 100000)
 snap = Snapshot.from_structs(eng, u.clusters, u.n_clusters, u.names, api.options())
 structs = u.binding_slice(0, u.n_bindings)
