@@ -256,18 +256,19 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   KP_STAMP(x, 10);
   // No class order (about one binding per estimator class, so sorting a row per
   // binding costs more than walking it): one pass over the feasible row takes the
-  // votes of the non-scheduled candidates into an octave histogram (count and sum per
-  // bucket, in the slice's SelScratch, free until sel_all_fast), their total (the int32
-  // wrap check the class total makes otherwise) and, for a fresh / scale-up division,
-  // the subset: the deciding bucket is the highest one whose cumulative count and sum
-  // cover the walk's condition, and every candidate in or above it joins the subset —
-  // the walk's argument with vmin = that bucket's lower edge (a coarser vmin only adds
-  // candidates with votes >= it, ties included). The bucket is tracked as the pass goes
-  // (it only rises), so a candidate below it is never appended and the list is
-  // compacted to it when full. Bucket sums are u32: they only wrap when the total does,
-  // and the binding falls back then.
-  uint32_t* hc = ss.hist;
-  uint32_t* hs = (uint32_t*)ss.whist;
+  // votes of the non-scheduled candidates, their total (the int32 wrap check the class
+  // total makes otherwise) and, for a fresh / scale-up division, the subset: an octave
+  // histogram of the votes (in the slice's SelScratch, free until sel_all_fast) finds
+  // the deciding bucket, the highest one whose cumulative votes cover the walk's
+  // condition, and every candidate in or above it joins the subset — the walk's
+  // argument with vmin = that bucket's lower edge (a coarser vmin only adds candidates
+  // with votes >= it, ties included). One quantity per bucket suffices: DynamicWeight
+  // covers once the count reaches the seats (in buckets >= 1 every vote is >= 1, so the
+  // sum then reaches them too, the scheduled votes being >= 0), Aggregated once
+  // min(tsum, psum) plus the sum reaches the target. The bucket only rises as the pass
+  // goes, so the list is compacted to it when it fills. The u32 sums only wrap when the
+  // total does, and the binding falls back then.
+  uint32_t* hq = ss.hist;
   int64_t rsum = 0, rcnt = 0;
   if (!ord) {
     const bool walk = fresh || assigned < h->replicas;
@@ -278,43 +279,42 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
         if (h->tgt_cnt > 0 && sched_rep_of(x, cd.r[i]) > 0) psum += cd.v[i];
       psum = B.sum64(psum);
     }
-    const bool collect = walk && !(agg && tsum >= (int64_t)target && psum >= (int64_t)target);
-    for (int i = B.tid(); i < 256; i += B.nth()) {
-      hc[i] = 0;
-      hs[i] = 0;
+    if (walk && tsum < 0) {  // (negative scheduled votes: the one-quantity argument needs >= 0)
+      top_fallback(B, a, t, b);
+      return;
     }
-    B.sync();
-    auto cov_at = [&](int64_t c, int64_t v) {
-      return tsum + v >= (int64_t)target && (agg ? psum + v >= (int64_t)target : c >= (int64_t)target);
-    };
-    // the deciding bucket of the histogram so far (-1: none covers yet); every thread
+    const bool collect = walk && !(agg && tsum >= (int64_t)target && psum >= (int64_t)target);
+    const int64_t base = agg ? (tsum < psum ? tsum : psum) : 0;
+    // the list [n0, n) keeps the appended candidates whose bucket is >= lo
+    const int32_t n0 = n;
+    // The deciding bucket from the list: it holds every candidate seen so far whose
+    // bucket is at or above the current one (and everything while none covers yet), so
+    // its histogram answers exactly for those buckets; -1: none covers (every candidate).
     auto find_thr = [&]() -> int64_t {
+      for (int i = B.tid(); i < 256; i += B.nth()) hq[i] = 0;
+      B.sync();
+      for (int i = n0 + B.tid(); i < n; i += B.nth()) {
+        const int32_t v = cd.v[i];
+        kp_atomic_add(&hq[vote_octave(v)], agg ? (uint32_t)v : 1u);
+      }
       B.sync();  // (the histogram updates before the reads)
-      int64_t thr = -1, run_c = 0, run_s = 0;
+      int64_t thr = -1, run = 0;
       for (int j0 = 0; j0 < 256 && thr < 0; j0 += 4 * B.nth()) {
         const int j = j0 + 4 * B.tid();  // this thread's 4 buckets, descending: 255 - j - q
-        int32_t c4 = 0, s4 = 0;
-        for (int q = 0; q < 4 && j + q < 256; q++) {
-          c4 += (int32_t)hc[255 - (j + q)];
-          s4 += (int32_t)hs[255 - (j + q)];
-        }
-        int32_t tc, ts;
-        const int32_t ec = B.excl_scan(c4, &tc);
-        const int32_t es = B.excl_scan(s4, &ts);
-        int64_t pc = run_c + ec, ps = run_s + es, mine = -1;
+        int32_t q4 = 0;
+        for (int q = 0; q < 4 && j + q < 256; q++) q4 += (int32_t)hq[255 - (j + q)];
+        int32_t tq;
+        int64_t pq = run + B.excl_scan(q4, &tq), mine = -1;
         for (int q = 0; q < 4 && j + q < 256 && mine < 0; q++) {
-          pc += hc[255 - (j + q)];
-          ps += (int64_t)(int32_t)hs[255 - (j + q)];
-          if (cov_at(pc, ps)) mine = 255 - (j + q);
+          const int bk = 255 - (j + q);
+          pq += hq[bk];
+          if (agg ? base + pq >= (int64_t)target : (bk >= 1 && pq >= (int64_t)target)) mine = bk;
         }
         thr = B.max64(mine);  // the first (highest) bucket that covers
-        run_c += tc;
-        run_s += ts;
+        run += tq;
       }
       return thr;
     };
-    // the list [n0, n) keeps the appended candidates whose bucket is >= lo
-    const int32_t n0 = n;
     auto compact = [&](int64_t lo) {
       int m = n0;
       for (int i0 = n0; i0 < n; i0 += B.nth()) {
@@ -340,6 +340,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     };
     int64_t neg = 0, thr = -1;
     bool over = false;
+    KP_STAMP(x, 70);
     // kTopStream chunks per step: their row loads are issued together
     for (int c0 = 0; c0 < s.C; c0 += kTopStream * B.nth()) {
       int32_t vv[kTopStream];
@@ -363,9 +364,6 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
           ff[u] = false;
           continue;
         }
-        const int bk = vote_octave(vv[u]);
-        kp_atomic_add(&hc[bk], 1u);
-        kp_atomic_add(&hs[bk], (uint32_t)vv[u]);
         rsum += vv[u];
         rcnt++;
       }
@@ -375,26 +373,31 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
 #endif
       for (int u = 0; u < kTopStream; u++) {
         bool in = ff[u] && vote_octave(vv[u]) >= thr;
-        int32_t tot;
-        int32_t pos = B.excl_scan(in ? 1 : 0, &tot);
-        if (n + tot > t.cap && !over) {  // full: compact to the bucket as it stands now
-          thr = find_thr();
+        uint64_t m = B.wballot(in);
+        if (n + popc64(m) > t.cap) {  // full: compact to the bucket as it stands now (it only rises)
+          const int64_t th2 = find_thr();
+          if (th2 > thr) thr = th2;
           compact(thr);
+          KP_COUNT(x, 72, 1);
           in = in && vote_octave(vv[u]) >= thr;
-          pos = B.excl_scan(in ? 1 : 0, &tot);
-          if (n + tot > t.cap) over = true;
+          m = B.wballot(in);
+          if (n + popc64(m) > t.cap) {
+            over = true;
+            break;
+          }
         }
-        if (over) break;
         if (in) {
-          cd.r[n + pos] = (uint32_t)(c0 + u * B.nth() + B.tid());
-          cd.v[n + pos] = vv[u];
+          const int pos = n + popc64(m & B.wlt());
+          cd.r[pos] = (uint32_t)(c0 + u * B.nth() + B.tid());
+          cd.v[pos] = vv[u];
         }
-        n += tot;
+        n += popc64(m);
       }
-      if (!over) thr = find_thr();  // (its scans order this step's histogram updates)
     }
     B.sum2(rsum, neg);
-    rcnt = B.sum64(rcnt);  // (the reductions also order the histogram before the reads)
+    rcnt = B.sum64(rcnt);  // (the reductions also order the histogram and the list before the reads)
+    KP_STAMP(x, 71);
+    KP_COUNT(x, 73, over ? 1 : 0);
     // negative votes / wrap risk (every vote sum the division takes is below this bound):
     // every candidate
     if (neg || rsum + (tsum < 0 ? -tsum : tsum) + sch >= (int64_t)kInt32Max / 2) {
@@ -414,9 +417,12 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
         top_fallback(B, a, t, b);
         return;
       }
-      thr = find_thr();
+      const int64_t th2 = find_thr();
+      if (th2 > thr) thr = th2;
       compact(thr);  // exactly the candidates in or above the deciding bucket
       complete = (int64_t)(n - n0) == rcnt;
+      KP_STAMP(x, 74);
+      KP_COUNT(x, 75, n);
     }
   }
   if (fresh || assigned < h->replicas) {
