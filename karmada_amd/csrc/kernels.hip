@@ -132,8 +132,13 @@ extern "C" __global__ void __launch_bounds__(64 * kFilterWaves) k_filter(SnapVie
 #endif
 // A launch over a device-appended list (a.n_dev) runs a grid-stride loop; otherwise
 // one workgroup per list entry (one iteration).
+// A workgroup without an entry returns before anything else: otherwise the body's
+// loop-invariant values, hoisted above the loop and spilled (the spread kernels spill),
+// are written to scratch by every lane of an idle grid (r05_pmc_config4: 138 MB per
+// launch of k_region_b with an empty fallback list).
 #define KP_LIST_LOOP(BODY)                                                       \
   const int n_ = a.n_dev ? (int)*a.n_dev : a.n;                                  \
+  if ((int)blockIdx.x >= n_) return;                                             \
   for (int blk = (int)blockIdx.x; blk < n_; blk += (int)gridDim.x) {             \
     BODY;                                                                        \
     __syncthreads();                                                             \

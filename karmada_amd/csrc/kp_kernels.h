@@ -341,8 +341,10 @@ KP_FI void body_select_all(const BLK& B, int blk, unsigned char* smem, const KAr
   cd.v = (int32_t*)(cd.r + a.s.Cp);
   SelScratch ss = carve_sel_scratch((unsigned char*)(cd.v + a.s.Cp), a.s.Cp);
   ss.dbg = a.dbg;
-  const BindHdr* h = &a.bv.hdr[b];
+  const BindHdr hloc = a.bv.hdr[b];  // registers: no reload after LDS stores
+  const BindHdr* h = &hloc;
   SelCtx x = make_ctx(a, b, tgt);
+  x.h = h;
   KP_STAMP(x, 0);
   const bool weights = h->strategy == ST_STATIC && h->sel == SEL_ALL;
   if (h->sel == SEL_ERR_UNSUPPORTED || (h->flags & BF_BAD)) {  // errors: only F (FitError first) is needed
@@ -443,8 +445,10 @@ KP_FI void body_select_static(const BLK& B, int blk, unsigned char* smem, const 
   uint64_t* cms = em + W;
   uint32_t* spo = (uint32_t*)(cms + W);
   uint32_t* eo = spo + W;
-  const BindHdr& h = a.bv.hdr[b];
+  const BindHdr hloc = a.bv.hdr[b];  // registers: no reload after LDS stores
+  const BindHdr& h = hloc;
   SelCtx x = make_ctx(a, b, nullptr);
+  x.h = &hloc;
   const bool wp = (h.flags & BF_HAS_WP) != 0;
   const int nr = wp ? h.sw_cnt : 0;
   // per-thread contiguous word runs (word order = rank order = name order)
@@ -956,9 +960,11 @@ KP_FI void body_spread_order(const BLK& B, int blk, unsigned char* smem, const K
   uint32_t* tgt = (uint32_t*)p;  // spec.Clusters bits (8W bytes: W u64 words)
   p += 8 * (size_t)W;
   uint64_t* selb = (uint64_t*)p;
-  const BindHdr& h0 = a.bv.hdr[b];
+  const BindHdr hloc = a.bv.hdr[b];  // registers: no reload after LDS stores
+  const BindHdr& h0 = hloc;
   if (h0.tgt_cnt > 0 && ord_targets_ok(h0)) build_bits(B, tgt, 2 * W, a.bv.ipool, h0.tgt_off, h0.tgt_cnt, 2);
   SelCtx x = make_ctx(a, b, tgt);
+  x.h = &hloc;
   int n = 0, st = ORD_NA;
   if (o.region) {
     const int nsel = o.rnsel[blk];
@@ -1086,9 +1092,11 @@ KP_FI void body_region_a_order(const BLK& B, int blk, unsigned char* smem, const
   int64_t* tsum = (int64_t*)(sum + R);
   uint64_t* tk = (uint64_t*)(tsum + R);
   uint32_t* tgt = (uint32_t*)(tk + 2 * kOrdTargets);
-  const BindHdr& h0 = a.bv.hdr[b];
+  const BindHdr hloc = a.bv.hdr[b];  // registers: no reload after LDS stores
+  const BindHdr& h0 = hloc;
   if (h0.tgt_cnt > 0 && ord_targets_ok(h0)) build_bits(B, tgt, 2 * s.W, a.bv.ipool, h0.tgt_off, h0.tgt_cnt, 2);
   SelCtx x = make_ctx(a, b, tgt);
+  x.h = &hloc;
   const int32_t cls = order_class(a, x, true);
   if (cls < 0) {
     if (B.tid() == 0) fb[kp_atomic_add(fb_n, 1u)] = blk;
@@ -1222,9 +1230,11 @@ KP_FI void body_region_a(const BLK& B, int blk, unsigned char* smem, const KArgs
   cd.r = (uint32_t*)p;
   cd.v = (int32_t*)(cd.r + a.s.Cp);
   cd.g = (int16_t*)(cd.v + a.s.Cp);
-  const BindHdr* h = &a.bv.hdr[b];
+  const BindHdr hloc = a.bv.hdr[b];  // registers: no reload after LDS stores
+  const BindHdr* h = &hloc;
   build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
   SelCtx x = make_ctx(a, b, tgt);
+  x.h = h;
   KP_STAMP(x, 22);
   cd.F = gather(B, x, cd, false);
   region_of_cands(B, a.s, cd);

@@ -160,11 +160,18 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   KP_STAMP_INIT
   const int b = a.list[blk];
   const SnapView& s = a.s;
-  const BindHdr* h = &a.bv.hdr[b];
+  // the header as a register copy: read through a.bv.hdr, its fields would be reloaded
+  // (each reload waiting on every load in flight) after every store or wave barrier
+  const BindHdr hloc = a.bv.hdr[b];
+  const BindHdr* h = &hloc;
   const int words = (s.Cp + 31) >> 5;
   // eligibility: SEL_ALL Dynamic/Aggregated workloads the subset argument covers
   const uint32_t fl = h->flags;
   const int st = h->strategy;
+  // (header fields the loops test, held in registers: read through h, the compiler reloads
+  // them after every LDS store it cannot tell from global memory, and each reload waits
+  // for every load in flight, the walk's prefetch ring included)
+  const bool has_tgt = kp_uniform(h->tgt_cnt) > 0;
   const int32_t cls = a.bcls ? a.bcls[b] : 0;
   // the first chunks of the class order, loaded with the binding's header and row (the
   // walk is the first to read them; a binding that does not walk wastes a few L2 hits)
@@ -198,6 +205,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   Cands cd = tc.cd;
   SelScratch ss = tc.ss;
   SelCtx x = make_ctx(a, b, tgt);
+  x.h = h;
   // (every read of the target bitset is behind tgt_cnt > 0)
   if (h->tgt_cnt > 0) build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
   int64_t F = 0;
@@ -276,7 +284,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     int64_t psum = 0;  // Aggregated scale up: the prior clusters lead the order
     if (walk && agg && !fresh && apos != 0) {
       for (int i = B.tid(); i < n; i += B.nth())
-        if (h->tgt_cnt > 0 && sched_rep_of(x, cd.r[i]) > 0) psum += cd.v[i];
+        if (has_tgt && sched_rep_of(x, cd.r[i]) > 0) psum += cd.v[i];
       psum = B.sum64(psum);
     }
     if (walk && tsum < 0) {  // (negative scheduled votes: the one-quantity argument needs >= 0)
@@ -350,7 +358,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
 #endif
       for (int u = 0; u < kTopStream; u++) {
         const int c = c0 + u * B.nth() + B.tid();
-        ff[u] = c < s.C && ((frow[c >> 6] >> (c & 63)) & 1ull) && !(h->tgt_cnt > 0 && bit_test(tgt, c));
+        ff[u] = c < s.C && ((frow[c >> 6] >> (c & 63)) & 1ull) && !(has_tgt && bit_test(tgt, c));
         vv[u] = ff[u] ? x.erow[c] : 0;
       }
 #if defined(__clang__)
@@ -433,7 +441,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     int64_t psum = 0;
     if (agg && !fresh && apos != 0) {
       for (int i = B.tid(); i < n; i += B.nth())
-        if (h->tgt_cnt > 0 && sched_rep_of(x, cd.r[i]) > 0) psum += cd.v[i];
+        if (has_tgt && sched_rep_of(x, cd.r[i]) > 0) psum += cd.v[i];
       psum = B.sum64(psum);
     }
     // The walk takes kTopGroup chunks of the class order per step: their feasibility
@@ -479,7 +487,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
         rg[q] = (uint32_t)e;
         vg[q] = (int32_t)(e >> 32);
         const bool valid = g0 + q * ww + lane < s.C;
-        fg[q] = valid && ((frow[rg[q] >> 6] >> (rg[q] & 63)) & 1ull) && !(h->tgt_cnt > 0 && bit_test(tgt, (int)rg[q]));
+        fg[q] = valid && ((frow[rg[q] >> 6] >> (rg[q] & 63)) & 1ull) && !(has_tgt && bit_test(tgt, (int)rg[q]));
         if (tie && valid) {
           past = past || vg[q] < tie_v;
           fg[q] = fg[q] && vg[q] == tie_v;
@@ -588,7 +596,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
       // 2^30), which needs only that sum; otherwise the full-candidate kernel decides.
       int64_t rest = 0;  // the votes of the feasible non-scheduled candidates
       for (int c = B.tid(); c < s.C; c += B.nth())
-        if (((frow[c >> 6] >> (c & 63)) & 1ull) && !(h->tgt_cnt > 0 && bit_test(tgt, c))) rest += est_at(x, c);
+        if (((frow[c >> 6] >> (c & 63)) & 1ull) && !(has_tgt && bit_test(tgt, c))) rest += est_at(x, c);
       rest = B.sum64(rest);
       if ((int64_t)(int32_t)(tsum + rest) < (int64_t)target) {
         if (B.tid() == 0)
@@ -648,7 +656,9 @@ KP_FI void body_select_top_wg(const GBLK& G, const WBLK& W, int blk, unsigned ch
   if (!hh.go) return;  // wave 0 wrote the result or handed the binding on
   const int b = a.list[blk];
   TopCarve tc = top_carve(slice, a.s, t.cap, a.dbg);
+  const BindHdr hloc = a.bv.hdr[b];  // registers: no reload after LDS stores
   SelCtx x = make_ctx(a, b, tc.tgt);
+  x.h = &hloc;
   x.frow = tc.frow;
   tc.cd.F = hh.n;
   const TopInfo ti{hh.F, hh.complete != 0};
