@@ -107,7 +107,7 @@ def kernel_bytes(name, units, Cp, n_classes, n_bind, n_targets, snap_bytes, R):
 def load_pmc(config, kernel):
     """Per-launch PMC figures of `kernel` from the committed summary (same bench
     command, default sizes): {hbm_bytes (FETCH_SIZE*2 + WRITE_SIZE), valu_insts, ...}."""
-    for rnd in ("r04", "r03", "r02"):  # the newest summary that holds the kernel
+    for rnd in ("r05", "r04", "r03", "r02"):  # the newest summary that holds the kernel
         try:
             with open(os.path.join(ROOT, "profiles", f"{rnd}_pmc_config{config}.json")) as f:
                 k = json.load(f).get("kernels", {}).get(kernel)

@@ -220,8 +220,8 @@ int class_order(stream_t, const SnapView& s, const int32_t* rows, int n_rows, ui
   return 0;
 }
 
-int select_top(stream_t, const KArgs& a, const TopArgs& t, size_t slice) {
-  grid(a.n, slice, [&](int blk, unsigned char* sm) { body_select_top(CpuBlk{(int64_t*)sm}, blk, sm, a, t); });
+int select_top(stream_t, const KArgs& a, const TopArgs& t, size_t slice, int) {
+  grid(a.n_dev ? (int)*a.n_dev : a.n, slice, [&](int blk, unsigned char* sm) { body_select_top(CpuBlk{(int64_t*)sm}, blk, sm, a, t); });
   return 0;
 }
 int select_top_wg(stream_t, const KArgs& a, const TopArgs& t, size_t smem) {
@@ -318,9 +318,10 @@ int offsets(stream_t, const int32_t* status, const uint32_t* count, int n, uint6
 }
 
 int compact(stream_t, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
-            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n) {
+            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n, const uint32_t* perm) {
   int64_t red[8];
-  for (int b = 0; b < n; b++) body_compact(CpuBlk{red}, b, start, count, offsets, in_idx, in_rep, out_idx, out_rep, n);
+  for (int b = 0; b < n; b++)
+    body_compact(CpuBlk{red}, b, start, count, offsets, in_idx, in_rep, out_idx, out_rep, n, perm);
   return 0;
 }
 

@@ -302,6 +302,9 @@ struct kp_engine {
   bool top_on = true;
   int top_cap = 1024;      // subset capacity of the large slice
   int top_cap_small = 256;  // ... and of the small one (bindings needing <= kTopSmallNeed)
+  // the large-slice bindings run at this capacity first (more waves per CU); those whose
+  // subset outgrows it run again at top_cap (0 / >= top_cap: one launch at top_cap)
+  int top_cap_mid = 0;
   bool top_split = true;    // the two slices' launches on two streams (KP_TOP_SPLIT=0: one)
   bool slow_order = true;   // k_slow orders candidates from the class orders (KP_SLOW_ORDER=0: sorts)
   bool top_wg = false;      // large-subset bindings on k_select_top_wg (KP_TOP_WG=1; measured slower)
@@ -374,7 +377,7 @@ struct kp_batch {
   // k_select_top: per-class candidate orders, row sums and walkability; its fallback list
   uint64_t* d_ord = nullptr;
   int64_t* d_ctot = nullptr;
-  int32_t *d_cok = nullptr, *d_fb = nullptr;
+  int32_t *d_cok = nullptr, *d_fb = nullptr, *d_ofb = nullptr;
   int32_t *d_fbc = nullptr, *d_fbr = nullptr;  // k_spread_order's fallback lists (cluster / region positions)
   int32_t* d_fba = nullptr;                     // k_region_a_order's fallback list
   std::vector<int32_t> sets_cls, l_sets;
@@ -392,9 +395,10 @@ struct kp_batch {
   unsigned long long* counter = nullptr;
   uint32_t* stats = nullptr;
   unsigned long long* dbg = nullptr;
-  uint32_t h_stats[16] = {};  // [0..7] slow-path counts, [8] component-set simulation overflow, [9] k_select_top
+  uint32_t h_stats[20] = {};  // [0..7] slow-path counts, [8] component-set simulation overflow, [9] k_select_top
                               // fallbacks, [10] / [11] cluster- / region-spread bindings selected over the class order,
                               // [12] / [13] k_spread_order's fallback list lengths, [14] k_region_a_order's
+                              // [16] k_select_top's capacity overflows (the top_cap_mid launch)
   uint32_t* out_idx = nullptr;
   int32_t* out_rep = nullptr;
   uint64_t* offsets_d = nullptr;
@@ -1970,6 +1974,7 @@ int kp_engine_create(int device, kp_engine** out) {
     e->top_cap = std::max(64, std::min(1024, atoi(v) & ~63));
     e->top_cap_small = std::min(e->top_cap_small, e->top_cap);
   }
+  if (const char* v = getenv("KP_TOP_CAP_MID")) e->top_cap_mid = std::max(0, std::min(1024, atoi(v) & ~63));
   unsigned hc = std::thread::hardware_concurrency();
   e->n_threads = (int)std::max(1u, std::min(16u, hc));
   *out = e;
@@ -2800,7 +2805,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->start, B);
   a.add(&bt->count, B);
   a.add(&bt->counter, 1);
-  a.add(&bt->stats, 16);
+  a.add(&bt->stats, 20);
 #if defined(KP_STAMPS) || defined(KP_SLOW_CHECK)
   a.add(&bt->dbg, kDbgSlots);
 #endif
@@ -2826,7 +2831,10 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   const bool orders_pay = (int64_t)bt->crep.size() * order_amort() <= (int64_t)B;
   // Without them k_select_top thresholds each binding's votes by a histogram instead of
   // walking an order (kp_top.h), so its fallback list exists either way.
-  if (!bt->crep.empty()) a.add(&bt->d_fb, std::max(1, bt->n_all_dyn));
+  if (!bt->crep.empty()) {
+    a.add(&bt->d_fb, std::max(1, bt->n_all_dyn));
+    a.add(&bt->d_ofb, std::max(1, bt->n_all_dyn));
+  }
   if (s->C <= 16384 && !bt->crep.empty() && orders_pay && kRedBytes + 8 * (size_t)P <= e->max_lds) {
     a.add(&bt->d_ord, bt->crep.size() * (size_t)s->Cp);
     a.add(&bt->d_ctot, bt->crep.size());
@@ -3125,7 +3133,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     const char* v = getenv("KP_TOPK");
     return !v || atoi(v) != 0;
   }();
-  const bool top = bits && e->top_on && (bt->d_ord != nullptr || (topk_on && bt->d_fb != nullptr)) &&
+  const bool top = bits && e->top_on && s->Cp <= kTopMaxCp && (bt->d_ord != nullptr || (topk_on && bt->d_fb != nullptr)) &&
                    bt->n_all_dyn > 0 && kTopWaves * ((top_lds_bytes(s->Cp, top_cap) + 15) & ~(size_t)15) <= e->max_lds;
   // class orders: k_select_top's walk, and the spread selections over them
   // (k_spread_order, k_region_a_order), each where its LDS slices fit the device
@@ -3166,13 +3174,22 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       // cluster-spread kernels use after it), so neither drains the CUs alone
       // (profiled steps keep both on one stream: each launch's HIP-event time is then its own)
       const bool split = e->top_split && !e->prof && bt->n_top_small > 0 && bt->n_all_dyn > bt->n_top_small;
+      // the large slice in two capacities: top_cap_mid first (its smaller LDS slices
+      // keep more waves per CU), then top_cap over the bindings whose subset outgrew it
+      // (a device-appended list, grid-stride waves; the capacity only bounds the subset,
+      // so both runs give the same answer)
+      const bool mid = e->top_cap_mid >= 64 && e->top_cap_mid < top_cap && !e->top_wg;
       for (int part = 0; part < 2; part++) {
         KArgs g = k;
-        const int cap_p = part == 0 ? top_cap_small : top_cap;
+        const int cap_p = part == 0 ? top_cap_small : (mid ? e->top_cap_mid : top_cap);
         g.list = bt->d_all + (part == 0 ? 0 : bt->n_top_small);
         g.n = part == 0 ? bt->n_top_small : bt->n_all_dyn - bt->n_top_small;
         if (g.n <= 0) continue;
         TopArgs ta{bt->d_ord, bt->d_ctot, bt->d_cok, bt->d_fb, bt->stats + 9, cap_p};
+        if (part == 1 && mid) {
+          ta.ofb = bt->d_ofb;
+          ta.ofb_n = bt->stats + 16;
+        }
         const size_t slice = (top_lds_bytes(s->Cp, cap_p) + 15) & ~(size_t)15;
         dev::stream_t sx_ = split && part == 1 ? e->stream3 : sp;
         if (split && part == 1) HIPCHK(dev::stream_wait(sx_, e->ev[4]));
@@ -3182,6 +3199,16 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
           KPROF(sx_, "k_select_top_wg", g.n, -1, dev::select_top_wg(sx_, g, ta, wg_lds));
         else
           KPROF(sx_, "k_select_top", g.n, -1, dev::select_top(sx_, g, ta, slice));
+        if (part == 1 && mid) {
+          KArgs o = k;
+          o.list = bt->d_ofb;
+          o.n = g.n;  // (the list's capacity; its length is stats[16])
+          o.n_dev = bt->stats + 16;
+          TopArgs tb{bt->d_ord, bt->d_ctot, bt->d_cok, bt->d_fb, bt->stats + 9, top_cap};
+          const size_t slice_l = (top_lds_bytes(s->Cp, top_cap) + 15) & ~(size_t)15;
+          // (units 0: the launch re-runs bindings the kernel's units already count)
+          KPROF(sx_, "k_select_top", 0, -1, dev::select_top(sx_, o, tb, slice_l, kTopOverGrid));
+        }
         if (split && part == 1) {
           HIPCHK(dev::event_record(e->ev[10], sx_));
           HIPCHK(dev::stream_wait(sp, e->ev[10]));  // both slices' fallbacks precede k_select_all
@@ -3370,7 +3397,8 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   // the device, then the per-binding arrays and the CSR copied back
   KPROF(st, "k_offsets", B, -1, dev::offsets(st, bt->status, bt->count, B, bt->offsets_d, bt->off_part));
   KPROF(st, "k_compact", B, -1,
-        dev::compact(st, bt->start, bt->count, bt->offsets_d, bt->out_idx, bt->out_rep, bt->cidx_d, bt->crep_d, B));
+        dev::compact(st, bt->start, bt->count, bt->offsets_d, bt->out_idx, bt->out_rep, bt->cidx_d, bt->crep_d, B,
+                     s->view.perm));
   bt->h_status.resize(B);
   bt->h_err.resize(B);
   bt->h_arg.resize(B);

@@ -170,6 +170,26 @@ extern "C" __global__ void __launch_bounds__(64 * kTopWaves, KP_TOP_MIN_WAVES) k
 #else
 ;
 #endif
+// k_select_top over a device-appended list (the capacity-overflow list: n_dev holds its
+// length, a.n its capacity): a bounded grid whose waves stride over the list
+extern "C" __global__ void __launch_bounds__(64 * kTopWaves) k_select_top_list(KArgs a, TopArgs t, int slice)
+#if KP_K(4)
+{
+  KP_SMEM;
+  const int w = (int)(threadIdx.x >> 6);
+  unsigned char* mine = smem + (size_t)w * (size_t)slice;
+  const int n_ = (int)*a.n_dev;
+  int blk = (int)blockIdx.x * kTopWaves + w;
+  if (blk >= n_) return;  // wave-uniform
+  const int step = (int)gridDim.x * kTopWaves;
+  for (; blk < n_; blk += step) {
+    body_select_top(WaveBlk{(int64_t*)mine}, blk, mine, a, t);
+    __builtin_amdgcn_wave_barrier();  // (the next binding re-carves the slice)
+  }
+}
+#else
+;
+#endif
 // The large-subset bindings: one workgroup each, wave 0 walks, the workgroup divides.
 extern "C" __global__ void __launch_bounds__(64 * kTopWgWaves) k_select_top_wg(KArgs a, TopArgs t)
 #if KP_K(4)
@@ -413,11 +433,11 @@ extern "C" __global__ void __launch_bounds__(kOffThreads) k_offsets_b(int n, uin
 extern "C" __global__ void __launch_bounds__(64) k_compact(const uint64_t* start, const uint32_t* count,
                                                            const uint64_t* offsets, const uint32_t* in_idx,
                                                            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep,
-                                                           int n)
+                                                           int n, const uint32_t* perm)
 #if KP_K(8)
 {
   __shared__ int64_t red[8];
-  body_compact(GpuBlk{red}, (int)blockIdx.x, start, count, offsets, in_idx, in_rep, out_idx, out_rep, n);
+  body_compact(GpuBlk{red}, (int)blockIdx.x, start, count, offsets, in_idx, in_rep, out_idx, out_rep, n, perm);
 }
 #else
 ;
@@ -609,13 +629,22 @@ int class_order(stream_t st, const SnapView& s, const int32_t* rows, int n_rows,
   return chk(hipGetLastError());
 }
 
-int select_top(stream_t st, const KArgs& a, const TopArgs& t, size_t slice) {
+int select_top(stream_t st, const KArgs& a, const TopArgs& t, size_t slice, int max_grid) {
   if (a.n <= 0) return 0;
   const size_t smem = slice * kTopWaves;
   if (smem > 65536 &&
       chk(hipFuncSetAttribute((const void*)k_select_top, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)))
     return -1;
-  hipLaunchKernelGGL(k_select_top, dim3((a.n + kTopWaves - 1) / kTopWaves), dim3(64 * kTopWaves), smem,
+  int grid = (a.n + kTopWaves - 1) / kTopWaves;
+  if (a.n_dev) {  // the list launch
+    if (max_grid > 0 && grid > max_grid) grid = max_grid;
+    if (smem > 65536 &&
+        chk(hipFuncSetAttribute((const void*)k_select_top_list, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)))
+      return -1;
+    hipLaunchKernelGGL(k_select_top_list, dim3(grid), dim3(64 * kTopWaves), smem, (hipStream_t)st, a, t, (int)slice);
+    return chk(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_select_top, dim3(grid), dim3(64 * kTopWaves), smem,
                      (hipStream_t)st, a, t, (int)slice);
   return chk(hipGetLastError());
 }
@@ -732,10 +761,10 @@ int offsets(stream_t st, const int32_t* status, const uint32_t* count, int n, ui
 }
 
 int compact(stream_t st, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
-            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n) {
+            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n, const uint32_t* perm) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_compact, dim3(n), dim3(64), 0, (hipStream_t)st, start, count, offsets, in_idx, in_rep, out_idx,
-                     out_rep, n);
+                     out_rep, n, perm);
   return chk(hipGetLastError());
 }
 

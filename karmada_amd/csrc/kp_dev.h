@@ -73,7 +73,9 @@ int class_order(stream_t st, const SnapView& s, const int32_t* rows, int n_rows,
 // SEL_ALL DynamicWeight / Aggregated bindings a.list[0, a.n) over their deciding
 // candidates (body_select_top), `slice` bytes of LDS per binding; the others are
 // appended to t.fb.
-int select_top(stream_t st, const KArgs& a, const TopArgs& t, size_t slice);
+// (a.n_dev set: the list's length is on the device, a.n its capacity; max_grid > 0
+// bounds the grid, whose waves then stride over the list)
+int select_top(stream_t st, const KArgs& a, const TopArgs& t, size_t slice, int max_grid = 0);
 // k_select_top_wg: one workgroup per binding (the large-subset bindings), smem = top_wg_lds_bytes
 int select_top_wg(stream_t st, const KArgs& a, const TopArgs& t, size_t smem);
 // selectGroups for n region bindings (one thread each): rsel/rnsel as the host
@@ -115,8 +117,9 @@ int reasons(stream_t st, const SnapView& s, const BatchView& bv, int b0, int nb,
 // CSR offsets[n + 1] of the per-binding results (counts of OK bindings), on the device;
 // part: ceil(n / kOffChunk) u64 of scratch.
 int offsets(stream_t st, const int32_t* status, const uint32_t* count, int n, uint64_t* off, uint64_t* part);
+// (in_idx holds snapshot ranks; out_idx gets perm[rank], the caller's cluster index)
 int compact(stream_t st, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
-            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n);
+            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n, const uint32_t* perm);
 
 }  // namespace dev
 }  // namespace kp

@@ -692,7 +692,7 @@ KP_FI void body_select_static(const BLK& B, int blk, unsigned char* smem, const 
       if (idx >= lo_i && idx < hi_i) r++;
     }
     const uint64_t o = base + eo[w] + (uint64_t)popc64(em[w] & below);
-    x.sink.out_idx[o] = s.perm[c];
+    x.sink.out_idx[o] = (uint32_t)c;  // (rank: k_compact maps it)
     x.sink.out_rep[o] = r;
   }
   KP_STAMP(x, 4);
@@ -1788,15 +1788,18 @@ KP_FI void body_offsets_b(const BLK& B, int blk, int nblk, int n, uint64_t* offs
   if (blk == nblk - 1 && B.tid() == 0) offsets[n] = (uint64_t)base + part[blk];
 }
 
-// Gathers per-binding results into CSR order (offsets from body_offsets).
+// Gathers per-binding results into CSR order (offsets from body_offsets). The select
+// kernels write snapshot ranks; the caller's cluster index is perm[rank], looked up
+// here (a streaming pass) rather than at the end of each binding's dependency chain.
 template <class BLK>
 KP_FI void body_compact(const BLK& B, int blk, const uint64_t* start, const uint32_t* count, const uint64_t* offsets,
-                        const uint32_t* in_idx, const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n) {
+                        const uint32_t* in_idx, const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n,
+                        const uint32_t* perm) {
   if (blk >= n) return;
   uint64_t s = start[blk], o = offsets[blk];
   uint32_t c = (uint32_t)(offsets[blk + 1] - o);  // 0 unless the status is OK (body_offsets)
   for (uint32_t i = B.tid(); i < c; i += B.nth()) {
-    out_idx[o + i] = in_idx[s + i];
+    out_idx[o + i] = perm[in_idx[s + i]];
     out_rep[o + i] = in_rep[s + i];
   }
 }

@@ -203,7 +203,7 @@ KP_FI void emit_each(const BLK& B, const SelCtx& x, const CS& cs, RepFn rep, boo
   cs.each([&](uint32_t rk, int32_t v) {
     const int32_t r = CS::kSettable ? v : rep(rk, v);
     if (keep_all || r > 0) {
-      x.sink.out_idx[o] = x.s->perm[rk];
+      x.sink.out_idx[o] = rk;  // (snapshot rank: k_compact maps it through perm)
       x.sink.out_rep[o] = r < 0 ? 0 : r;
       o++;
     }
@@ -243,7 +243,7 @@ KP_FI void emit_lists(const BLK& B, const SelCtx& x, uint64_t* pl, int np, RepFn
     const uint32_t rk = (uint32_t)(pl[i] >> 32);
     const int32_t r = (int32_t)(uint32_t)pl[i];
     if (r > 0) {
-      x.sink.out_idx[o] = x.s->perm[rk];
+      x.sink.out_idx[o] = rk;  // (snapshot rank: k_compact maps it through perm)
       x.sink.out_rep[o] = r;
       o++;
     }
@@ -253,7 +253,7 @@ KP_FI void emit_lists(const BLK& B, const SelCtx& x, uint64_t* pl, int np, RepFn
     if (!mask_test(x.frow, (int)rk)) continue;
     const int32_t r = trep(rk);
     if (r > 0) {
-      x.sink.out_idx[o] = x.s->perm[rk];
+      x.sink.out_idx[o] = rk;  // (snapshot rank: k_compact maps it through perm)
       x.sink.out_rep[o] = r;
       o++;
     }

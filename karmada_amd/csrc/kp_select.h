@@ -544,7 +544,7 @@ KP_HD inline void sink_serial(const SelCtx& x, const SerialScratch& sc, const Se
   k.start[b] = base;
   k.count[b] = (uint32_t)o.n;
   for (int i = 0; i < o.n; i++) {
-    k.out_idx[base + i] = x.s->perm[sc.rn[i]];
+    k.out_idx[base + i] = sc.rn[i];  // (rank: k_compact maps it)
     k.out_rep[base + i] = sc.rr[i];
   }
 }

@@ -82,6 +82,10 @@ struct TopArgs {
   int32_t* fb;          // fallback list (bindings for the full-candidate kernel)
   uint32_t* fb_n;       // its length
   int cap;              // subset capacity (LDS entries per wave)
+  // set: bindings whose subset outgrows cap go here instead (a larger-capacity launch
+  // takes them; its own overflow goes to fb)
+  int32_t* ofb = nullptr;
+  uint32_t* ofb_n = nullptr;
 };
 
 // Webster's party list / enumeration buffer of the subset path (u64 entries): larger
@@ -89,13 +93,43 @@ struct TopArgs {
 constexpr int kTopEcap = 256;
 // bindings whose Replicas + len(spec.Clusters) is at most this take the small slice
 constexpr int64_t kTopSmallNeed = 160;
+// workgroups of the launch over the capacity-overflow list (its length is on the device;
+// the waves stride over it): 256 CUs x 4 resident workgroups of the large slice
+constexpr int kTopOverGrid = 1024;
 KP_HD inline int top_ecap(int cap) { return cap < kTopEcap ? cap : kTopEcap; }
-// LDS slice of one binding: [red 64 B | frow W u64 | tgt bits | S ranks cap | S votes cap | SelScratch]
+// LDS slice of one binding: [red 64 B | frow W u64 | tgt bits | S votes cap | S ranks cap (u16) | SelScratch]
+// (the LDS a wave holds bounds the waves per CU, and this kernel runs as fast as it
+// keeps waves in flight: 16-bit ranks, so k_select_top needs Cp <= kTopMaxCp)
 KP_HD inline size_t top_lds_bytes(int Cp, int cap) {
   const int words = (Cp + 31) >> 5, W = Cp / 64;
-  return 64 + 8 * (size_t)W + 4 * (size_t)((words + 3) & ~3) + 8 * (size_t)cap + 3072 + 8 * (size_t)top_ecap(cap) +
+  return 64 + 8 * (size_t)W + 4 * (size_t)((words + 3) & ~3) + 6 * (size_t)cap + 3072 + 8 * (size_t)top_ecap(cap) +
          64;
 }
+constexpr int kTopMaxCp = 1 << 16;
+
+// The subset in LDS: votes and 16-bit ranks (k_select_top's bindings have no overflow
+// tiers, so no tier bits ride on the rank).
+struct TopSub {
+  uint16_t* r;
+  int32_t* v;
+  int32_t F;
+};
+// sel_all_fast's candidate set over a TopSub (as LdsCands over Cands)
+struct TopCands {
+  const TopSub* cd;
+  int tid, nth;
+  template <class Fn>
+  KP_FI void each(Fn fn) const {
+    for (int i = tid; i < cd->F; i += nth) fn((uint32_t)cd->r[i], cd->v[i]);
+  }
+  template <class Fn>
+  KP_FI void each_set(Fn fn) const {
+    for (int i = tid; i < cd->F; i += nth) cd->v[i] = fn((uint32_t)cd->r[i], cd->v[i]);
+  }
+  static constexpr bool kSettable = true;
+  KP_FI uint64_t okey(const SelCtx& x, uint32_t rk, int32_t v0) const { return cand_order_key(x, rk, v0); }
+  static constexpr bool kExact = false;
+};
 
 // Octave bucket of a vote (8 buckets per power of two), monotone in the vote: the
 // histogram the no-class-order path (TopArgs::ord == nullptr) thresholds the votes by.
@@ -107,8 +141,10 @@ KP_HD inline int vote_octave(int32_t v) {
 }
 
 template <class BLK>
-KP_FI void top_fallback(const BLK& B, const KArgs& a, const TopArgs& t, int b) {
-  if (B.tid() == 0) t.fb[kp_atomic_add(t.fb_n, 1u)] = b;
+KP_FI void top_fallback(const BLK& B, const KArgs& a, const TopArgs& t, int b, bool over_cap = false) {
+  if (B.tid() != 0) return;
+  if (over_cap && t.ofb) t.ofb[kp_atomic_add(t.ofb_n, 1u)] = b;
+  else t.fb[kp_atomic_add(t.fb_n, 1u)] = b;
 }
 
 #ifndef KP_TOP_AHEAD
@@ -132,7 +168,7 @@ struct TopHand {
 struct TopCarve {
   uint64_t* frow;
   uint32_t* tgt;
-  Cands cd;
+  TopSub cd;
   SelScratch ss;
 };
 KP_HD inline TopCarve top_carve(unsigned char* smem, const SnapView& s, int cap, unsigned long long* dbg) {
@@ -143,9 +179,10 @@ KP_HD inline TopCarve top_carve(unsigned char* smem, const SnapView& s, int cap,
   p += 8 * (size_t)s.W;
   c.tgt = (uint32_t*)p;
   p += 4 * (size_t)((words + 3) & ~3);
-  c.cd.r = (uint32_t*)p;
-  c.cd.v = (int32_t*)(c.cd.r + cap);
-  c.ss = carve_sel_scratch((unsigned char*)(c.cd.v + cap), 2 * cap);
+  c.cd.v = (int32_t*)p;
+  c.cd.r = (uint16_t*)(c.cd.v + cap);
+  c.cd.F = 0;
+  c.ss = carve_sel_scratch((unsigned char*)(c.cd.r + cap), 2 * cap);  // (cap % 64 == 0: 8-B aligned)
   c.ss.cap = top_ecap(cap);
   c.ss.dbg = dbg;
   return c;
@@ -202,7 +239,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   TopCarve tc = top_carve(smem, s, t.cap, a.dbg);
   uint64_t* frow = tc.frow;
   uint32_t* tgt = tc.tgt;
-  Cands cd = tc.cd;
+  TopSub cd = tc.cd;
   SelScratch ss = tc.ss;
   SelCtx x = make_ctx(a, b, tgt);
   x.h = h;
@@ -243,7 +280,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
       const int32_t sr = kp_ldu(a.bv.ipool + h->tgt_off + 2 * j + 1);
       const int32_t e = est_at(x, (int)r);  // the subset holds AllocatableReplicas (sel_all_fast adds
       if (pos < t.cap) {                     // the scheduled replicas to a fresh vote itself)
-        cd.r[pos] = r;
+        cd.r[pos] = (uint16_t)r;
         cd.v[pos] = e;
       }
       pos++;
@@ -256,7 +293,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     n = (int32_t)*ctr;  // (the reductions ordered the reservation)
   }
   if (n > t.cap) {
-    top_fallback(B, a, t, b);
+    top_fallback(B, a, t, b, true);
     return;
   }
   const int32_t assigned = wrap32(asum);
@@ -338,7 +375,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
         int32_t tot;
         const int32_t pos = m + B.excl_scan(keep ? 1 : 0, &tot);  // (its barrier: reads before writes)
         if (keep) {
-          cd.r[pos] = r;
+          cd.r[pos] = (uint16_t)r;
           cd.v[pos] = v;
         }
         m += tot;
@@ -396,7 +433,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
         }
         if (in) {
           const int pos = n + popc64(m & B.wlt());
-          cd.r[pos] = (uint32_t)(c0 + u * B.nth() + B.tid());
+          cd.r[pos] = (uint16_t)(c0 + u * B.nth() + B.tid());
           cd.v[pos] = vv[u];
         }
         n += popc64(m);
@@ -422,7 +459,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
                        (int32_t)(tsum + rsum));
           return;
         }
-        top_fallback(B, a, t, b);
+        top_fallback(B, a, t, b, true);
         return;
       }
       const int64_t th2 = find_thr();
@@ -525,7 +562,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
       for (int q = 0; q < kTopGroup; q++) {
         if (fg[q]) {
           const int pos = base + popc64(mg[q] & B.wlt());
-          cd.r[pos] = rg[q];
+          cd.r[pos] = (uint16_t)rg[q];
           cd.v[pos] = vg[q];
         }
         base += popc64(mg[q]);
@@ -604,7 +641,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
                      (int32_t)(tsum + rest));
         return;
       }
-      top_fallback(B, a, t, b);
+      top_fallback(B, a, t, b, !hopeless);
       return;
     }
   }
@@ -626,9 +663,9 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   int why;
   if (n <= B.nth()) {  // (wave-uniform) at most one candidate per lane, in registers
     const bool has = B.tid() < n;
-    why = sel_all_fast<true>(B, x, RegCands{has, has ? cd.r[B.tid()] : 0u, has ? cd.v[B.tid()] : 0}, ss, &ti);
+    why = sel_all_fast<true>(B, x, RegCands{has, has ? (uint32_t)cd.r[B.tid()] : 0u, has ? cd.v[B.tid()] : 0}, ss, &ti);
   } else {
-    why = sel_all_fast<true>(B, x, LdsCands{&cd, B.tid(), B.nth()}, ss, &ti);
+    why = sel_all_fast<true>(B, x, TopCands{&cd, B.tid(), B.nth()}, ss, &ti);
   }
   KP_STAMP(x, 12);
   if (why == SLOW_TOP_FULL) top_fallback(B, a, t, b);
@@ -662,7 +699,7 @@ KP_FI void body_select_top_wg(const GBLK& G, const WBLK& W, int blk, unsigned ch
   x.frow = tc.frow;
   tc.cd.F = hh.n;
   const TopInfo ti{hh.F, hh.complete != 0};
-  const int why = sel_all_fast<true>(G, x, LdsCands{&tc.cd, G.tid(), G.nth()}, tc.ss, &ti);
+  const int why = sel_all_fast<true>(G, x, TopCands{&tc.cd, G.tid(), G.nth()}, tc.ss, &ti);
   if (why == SLOW_TOP_FULL) top_fallback(G, a, t, b);
   else if (why != SLOW_NONE && G.tid() == 0) flag_slow(a, b, why);
 }

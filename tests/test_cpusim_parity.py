@@ -147,11 +147,15 @@ def test_cpusim_region_host_dfs(engine):
     compare(got, want, "region host DFS")
 
 
-@pytest.mark.parametrize("top_env", [{"KP_TOP_CAP": "64"}, {"KP_TOP": "0"}], ids=["cap64", "off"])
+@pytest.mark.parametrize("top_env", [{"KP_TOP_CAP": "64"}, {"KP_TOP": "0"}, {"KP_TOP_CAP_MID": "64"},
+                                     {"KP_TOP_CAP_MID": "64", "KP_TOP_CAP": "128"}],
+                         ids=["cap64", "off", "mid64", "mid64-cap128"])
 def test_cpusim_top_subsets(top_env):
     """k_select_top (kp_top.h) at its smallest subset capacity (most bindings hand back
-    to the full-candidate kernel through the device fallback list) and switched off:
-    the same placements as the oracle either way."""
+    to the full-candidate kernel through the device fallback list), switched off, and
+    with the large slice run first at a small capacity (KP_TOP_CAP_MID: the overflow list
+    run again at the full capacity, its own overflow to the full-candidate kernel): the
+    same placements as the oracle every way."""
     old = {k: os.environ.get(k) for k in top_env}
     os.environ.update(top_env)
     try:
@@ -171,8 +175,10 @@ def test_cpusim_top_subsets(top_env):
             compare(run(e, u, opts, times=times), want, f"{top_env} config {config}")
             if top_env.get("KP_TOP") == "0":
                 assert times[0]["n_top"] == 0
-            else:
+            elif top_env.get("KP_TOP_CAP") == "64":
                 assert times[0]["n_top_fallback"] > 0
+            else:
+                assert times[0]["n_top"] > 0
     finally:
         e.close()
 
@@ -257,7 +263,7 @@ def test_cpusim_kernel_times():
         e.close()
 
 
-@pytest.mark.parametrize("cap", [None, "64"], ids=["cap", "cap64"])
+@pytest.mark.parametrize("cap", [None, "64", "mid64"], ids=["cap", "cap64", "mid64"])
 @pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
     (3, 3, 1000, 2000), (7, 17, 300, 1500), (6, 9, 700, 2000), (8, 4, 64, 1000), (8, 5, 16, 600), (10, 10, 2000, 1500),
 ])
@@ -269,7 +275,9 @@ def test_cpusim_top_histogram(config, seed, n_clusters, n_bindings, cap):
     u = synth.Universe(config, seed, n_clusters, 0, n_bindings)
     opts = api.options()
     os.environ["KP_ORDER_AMORT"] = "1000000"
-    if cap:  # (read at engine creation) a small subset capacity: the list compactions and overflow
+    if cap == "mid64":  # (read at engine creation) the large slice first at 64, then at full capacity
+        os.environ["KP_TOP_CAP_MID"] = "64"
+    elif cap:  # a small subset capacity: the list compactions and overflow
         os.environ["KP_TOP_CAP"] = cap
     times = []
     try:
@@ -279,6 +287,7 @@ def test_cpusim_top_histogram(config, seed, n_clusters, n_bindings, cap):
     finally:
         os.environ.pop("KP_ORDER_AMORT", None)
         os.environ.pop("KP_TOP_CAP", None)
+        os.environ.pop("KP_TOP_CAP_MID", None)
     assert times[0]["n_top"] > 0
     want = O.schedule_c(u.clusters, u.n_clusters, u.bindings, u.n_bindings, opts, O.FAST, 8)
     compare(got, want, f"histogram config {config}")

@@ -124,6 +124,33 @@ def test_schedule_parity_top_histogram(engine, config, seed, n_clusters, n_bindi
     assert t["n_top"] > 0
 
 
+@pytest.mark.parametrize("mid", ["64", "128"])
+@pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
+    (3, 3, 5000, 3000), (7, 17, 2000, 3000), (6, 9, 700, 2000), (10, 10, 5000, 2000),
+])
+def test_schedule_parity_top_mid_capacity(config, seed, n_clusters, n_bindings, mid):
+    """k_select_top's large slice at a small first capacity (KP_TOP_CAP_MID): the bindings
+    whose subset outgrows it are appended to the overflow list and run again at the full
+    capacity by the grid-stride launch over that device list (engine.cpp), whose own
+    overflow goes to the full-candidate kernel: the oracle's placements."""
+    import os
+    from karmada_amd.engine import Engine
+    u = synth.Universe(config, seed, n_clusters, 0, n_bindings)
+    opts = api.options()
+    os.environ["KP_TOP_CAP_MID"] = mid  # (read at engine creation)
+    try:
+        e = Engine(0)
+    finally:
+        os.environ.pop("KP_TOP_CAP_MID", None)
+    try:
+        got = gpu_schedule(e, u, opts)
+        t = e.stage_times()
+    finally:
+        e.close()
+    compare(got, oracle_schedule(u, opts), f"mid capacity {mid} config {config} seed {seed}")
+    assert t["n_top"] > 0
+
+
 @pytest.mark.parametrize("config,seed,n_clusters,n_bindings", [
     (3, 3, 500, 1000), (2, 2, 1000, 1000), (5, 5, 3000, 1200), (7, 17, 2000, 1000), (3, 3, 5000, 1000),
     # C >= 9000: the gathered SEL_ALL kernel needs more than 80 KB of LDS -> k_select_all_wide
