@@ -90,7 +90,10 @@ struct TopArgs {
 
 // Webster's party list / enumeration buffer of the subset path (u64 entries): larger
 // party sets take its uncompacted passes over the subset (exact, kp_select.h).
-constexpr int kTopEcap = 256;
+#ifndef KP_TOP_ECAP
+#define KP_TOP_ECAP 192
+#endif
+constexpr int kTopEcap = KP_TOP_ECAP;
 // bindings whose Replicas + len(spec.Clusters) is at most this take the small slice
 constexpr int64_t kTopSmallNeed = 160;
 // workgroups of the launch over the capacity-overflow list (its length is on the device;
