@@ -68,11 +68,13 @@ def compulsory_bytes(n_bind, n_all, n_clusters, n_targets, snap_bytes, n_classes
     return pair, sel
 
 
-def kernel_bytes(name, units, Cp, n_classes, n_bind, n_targets, snap_bytes, R):
+def kernel_bytes(name, units, Cp, n_classes, n_bind, n_targets, snap_bytes, R, orders=True):
     """Compulsory HBM bytes of one kernel over the units (bindings or class rows) its
     launches covered: the records and feasibility rows it must read
     (256 + Cp/8 B per binding), the class rows (4 B/cluster) and orders (8 B/cluster)
-    it reads once, the results it writes (8 B per target, 28 B per binding)."""
+    it reads once, the results it writes (8 B per target, 28 B per binding).
+    orders=False: the batch built no class orders (k_select_top thresholds each
+    binding's votes by a histogram instead, kp_top.h), so only the class rows count."""
     if units == 0 and name not in ("k_offsets", "k_compact"):
         return 0.0  # (an empty fallback list: the launch found nothing to do)
     rec = B_BIND + Cp / 8.0
@@ -86,7 +88,7 @@ def kernel_bytes(name, units, Cp, n_classes, n_bind, n_targets, snap_bytes, R):
     if name == "k_class_order":
         return 12.0 * Cp * units
     if name in ("k_select_top", "k_select_top_wg"):
-        return units * (rec + 28) + 12.0 * Cp * n_classes + 8.0 * share
+        return units * (rec + 28) + (12.0 if orders else 4.0) * Cp * n_classes + 8.0 * share
     if name == "k_select_static":
         return units * (rec + 28) + 8.0 * share
     if name in ("k_spread_order", "k_region_a_order"):
@@ -509,7 +511,8 @@ def main():
             k["units"] = v["units"]
     kernels = []
     for name, v in kern.items():
-        by = kernel_bytes(name, v["units"], Cp, n_cls, B_rank, n_targets_rank, snap_bytes, 0)
+        by = kernel_bytes(name, v["units"], Cp, n_cls, B_rank, n_targets_rank, snap_bytes, 0,
+                          orders="k_class_order" in kern)
         kernels.append({"kernel": name, "ms": round(v["ms"], 4), "launches": v["launches"], "units": v["units"],
                         "bytes": round(by), "gbs": round(by / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None})
     kernels.sort(key=lambda x: -x["ms"])
