@@ -395,6 +395,11 @@ struct kp_batch {
   unsigned long long* counter = nullptr;
   uint32_t* stats = nullptr;
   unsigned long long* dbg = nullptr;
+  // launch arguments of the kernels that read them through a pointer (kp_launch.h
+  // SelectExtra::dargs): kArgSlots device slots and their page-locked host staging
+  KArgs* d_kargs = nullptr;
+  KArgs* h_kargs = nullptr;
+  size_t h_kargs_bytes = 0;
   uint32_t h_stats[20] = {};  // [0..7] slow-path counts, [8] component-set simulation overflow, [9] k_select_top
                               // fallbacks, [10] / [11] cluster- / region-spread bindings selected over the class order,
                               // [12] / [13] k_spread_order's fallback list lengths, [14] k_region_a_order's
@@ -447,6 +452,7 @@ struct kp_batch {
     quiesce();
     buf_pool().put(-1, h_cidx, h_cidx_bytes);
     buf_pool().put(-1, h_crep, h_crep_bytes);
+    buf_pool().put(-1, h_kargs, h_kargs_bytes);
     if (est) dev::release(est);
   }
   std::vector<RegionOut> h_rout;
@@ -2806,6 +2812,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->count, B);
   a.add(&bt->counter, 1);
   a.add(&bt->stats, 20);
+  a.add(&bt->d_kargs, kArgSlots);
 #if defined(KP_STAMPS) || defined(KP_SLOW_CHECK)
   a.add(&bt->dbg, kDbgSlots);
 #endif
@@ -2865,6 +2872,11 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   }
   const auto tp1 = std::chrono::steady_clock::now();
   HIPCHK(a.alloc());
+  bt->h_kargs = (KArgs*)pinned_get(sizeof(KArgs) * kArgSlots, &bt->h_kargs_bytes);
+  if (!bt->h_kargs) {
+    e->err = "kp_batch_create: page-locked launch-argument slots";
+    return KP_EDEVICE;
+  }
   bt->create_stream = e->stream;  // (an early return below waits for the uploads queued so far)
   const auto tp2 = std::chrono::steady_clock::now();
   auto up = [&](void* d, const void* h, size_t bytes) {
@@ -3100,6 +3112,18 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   sx.lds_area = bt->slow_lds;
   sx.lds_sort = bt->slow_sort;
   const int cap = kSmallMax + kTgtSmallMax + 16;
+  // A launch's KArgs copied to its own device slot (ordered before the launch on its
+  // stream): the select kernels that keep pointers into their arguments read them there
+  // (kp_launch.h SelectExtra::dargs). One slot per launch within this call.
+  int kslot = 0;
+  auto with_args = [&](const KArgs& k, dev::stream_t sq) -> SelectExtra {
+    SelectExtra r = sx;
+    if (kslot >= kArgSlots) return r;  // (dargs stays null: the launch reports EINVAL)
+    bt->h_kargs[kslot] = k;
+    if (dev::h2d(bt->d_kargs + kslot, bt->h_kargs + kslot, sizeof(KArgs), sq) == 0) r.dargs = bt->d_kargs + kslot;
+    kslot++;
+    return r;
+  };
   HIPCHK(dev::event_record(e->ev[3], sp));
   if (bits) {
     KPROF(sp, est_class_name(fast), bt->crep.size(), -1,
@@ -3220,7 +3244,11 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       f.n = bt->n_all_dyn;
       f.n_dev = bt->stats + 9;
       if (stream_all)
-        KPROF(sp, "k_select_all_stream", 0, 9, dev::select(sp, SEL_LAUNCH_ALL_STREAM, f, sel_stream_lds_bytes(s->Cp), cap, sx));
+        {  // (argument slot copied before the launch is timed)
+          const SelectExtra sxa1 = with_args(f, sp);
+          KPROF(sp, "k_select_all_stream", 0, 9,
+                dev::select(sp, SEL_LAUNCH_ALL_STREAM, f, sel_stream_lds_bytes(s->Cp), cap, sxa1));
+        }
       else
         KPROF(sp, sel_name(SEL_LAUNCH_ALL, smem_all(s)), 0, 9, dev::select(sp, SEL_LAUNCH_ALL, f, smem_all(s), cap, sx));
     } else if (na > 0) {
@@ -3243,7 +3271,11 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       KArgs g = k;
       g.list = bt->d_all + rest0;
       g.n = k.n - rest0;
-      KPROF(sp, "k_select_all_stream", g.n, -1, dev::select(sp, SEL_LAUNCH_ALL_STREAM, g, sel_stream_lds_bytes(s->Cp), cap, sx));
+      {  // (argument slot copied before the launch is timed)
+        const SelectExtra sxa2 = with_args(g, sp);
+        KPROF(sp, "k_select_all_stream", g.n, -1,
+              dev::select(sp, SEL_LAUNCH_ALL_STREAM, g, sel_stream_lds_bytes(s->Cp), cap, sxa2));
+      }
     }
   }
   HIPCHK(dev::event_record(e->ev[8], sp));  // k_select_all alone: ev[7] -> ev[8]
@@ -3265,8 +3297,11 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       k.sub = bt->d_fbc;
       k.n_dev = bt->stats + 12;
     }
-    KPROF(s3, sel_name(SEL_LAUNCH_CLUSTER, smem_cluster(s, cap)), k.n_dev ? 0 : k.n, k.n_dev ? 12 : -1,
-          dev::select(s3, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sx));
+    {  // (argument slot copied before the launch is timed)
+      const SelectExtra sxa3 = with_args(k, s3);
+      KPROF(s3, sel_name(SEL_LAUNCH_CLUSTER, smem_cluster(s, cap)), k.n_dev ? 0 : k.n, k.n_dev ? 12 : -1,
+            dev::select(s3, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sxa3));
+    }
     HIPCHK(dev::event_record(e->ev[15], s3));
   }
   // k_slow after every kernel that flags bindings (SEL_ALL on stream2, cluster spread
@@ -3290,11 +3325,17 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       KArgs kf = k;
       kf.sub = bt->d_fba;
       kf.n_dev = bt->stats + 14;
-      KPROF(st, sel_name(SEL_LAUNCH_REGION_A, smem_region_a(s)), 0, 14,
-            dev::select(st, SEL_LAUNCH_REGION_A, kf, smem_region_a(s), cap, sx));
+      {  // (argument slot copied before the launch is timed)
+        const SelectExtra sxa4 = with_args(kf, st);
+        KPROF(st, sel_name(SEL_LAUNCH_REGION_A, smem_region_a(s)), 0, 14,
+              dev::select(st, SEL_LAUNCH_REGION_A, kf, smem_region_a(s), cap, sxa4));
+      }
     } else {
-      KPROF(st, sel_name(SEL_LAUNCH_REGION_A, smem_region_a(s)), k.n, -1,
-            dev::select(st, SEL_LAUNCH_REGION_A, k, smem_region_a(s), cap, sx));
+      {  // (argument slot copied before the launch is timed)
+        const SelectExtra sxa5 = with_args(k, st);
+        KPROF(st, sel_name(SEL_LAUNCH_REGION_A, smem_region_a(s)), k.n, -1,
+              dev::select(st, SEL_LAUNCH_REGION_A, k, smem_region_a(s), cap, sxa5));
+      }
     }
     // selectGroups: on the device (one thread per binding) unless the snapshot
     // has more regions than its arrays hold; bindings whose DFS exceeds the node
@@ -3357,8 +3398,11 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       k.sub = bt->d_fbr;
       k.n_dev = bt->stats + 13;
     }
-    KPROF(st, sel_name(SEL_LAUNCH_REGION_B, smem_region_b(s, cap)), k.n_dev ? 0 : k.n, k.n_dev ? 13 : -1,
-          dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sx));
+    {  // (argument slot copied before the launch is timed)
+      const SelectExtra sxa6 = with_args(k, st);
+      KPROF(st, sel_name(SEL_LAUNCH_REGION_B, smem_region_b(s, cap)), k.n_dev ? 0 : k.n, k.n_dev ? 13 : -1,
+            dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sxa6));
+    }
   }
   // k_slow after every kernel that flags bindings (SEL_ALL on stream2, cluster spread on
   // stream3; the region chain, queued above, flags none), beside the region chain. With a
@@ -3381,7 +3425,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       k.ord = orders ? bt->d_ord : nullptr;  // sortClusters order from the class orders (kp_kernels.h)
       k.cok = orders ? bt->d_cok : nullptr;
       if (!e->slow_order) k.ord = nullptr;
-      SelectExtra sxs = sx;
+      SelectExtra sxs = with_args(k, s3);
       sxs.grid = (int)std::min<uint32_t>((uint32_t)bt->slow_grid, nslow);
       KPROF(s3, "k_slow", 0, 0,
             dev::select(s3, SEL_LAUNCH_SLOW, k,

@@ -264,9 +264,11 @@ extern "C" __global__ void __launch_bounds__(1024) k_class_order(SnapView s, con
 #ifndef KP_STREAM_MIN_WAVES
 #define KP_STREAM_MIN_WAVES 6
 #endif
-extern "C" __global__ void __launch_bounds__(KP_STREAM_THREADS, KP_STREAM_MIN_WAVES) k_select_all_stream(KArgs a)
+extern "C" __global__ void __launch_bounds__(KP_STREAM_THREADS, KP_STREAM_MIN_WAVES)
+    k_select_all_stream(const KArgs* __restrict__ pa)
 #if KP_K(3)
 {
+  const KArgs& a = *pa;
   KP_SMEM;
   KP_LIST_LOOP(body_select_all_stream(GpuBlk{(int64_t*)smem}, blk, smem, a))
 }
@@ -290,19 +292,25 @@ extern "C" __global__ void __launch_bounds__(1024) k_select_all_wide(KArgs a)
 // (C up to ~8.6k; fewer waves per barrier), 512 when it leaves one (wider hides
 // latency). 4 / 3 waves per SIMD bound the VGPRs at 128 / 168.
 #define KP_SPREAD_KERNELS(SUF, T, MINW, IC, IA, IB)                                                                  \
-  extern "C" __global__ void __launch_bounds__(T, MINW) k_select_cluster##SUF(KArgs a, int cap) IC({            \
+  extern "C" __global__ void __launch_bounds__(T, MINW) k_select_cluster##SUF(const KArgs* __restrict__ pa, int cap) \
+      IC({                                                                                                     \
+    const KArgs& a = *pa;                                                                                      \
     KP_SMEM;                                                                                                   \
     KP_LIST_LOOP(body_select_cluster(GpuBlk{(int64_t*)smem}, a.sub ? a.sub[blk] : blk, smem, a, cap))         \
   })                                                                                                           \
-  extern "C" __global__ void __launch_bounds__(T, MINW) k_region_a##SUF(KArgs a, RegionOut* rout, int32_t* rstat) \
+  extern "C" __global__ void __launch_bounds__(T, MINW) k_region_a##SUF(const KArgs* __restrict__ pa, RegionOut* rout, \
+                                                                      int32_t* rstat)                          \
       IA({                                                                                                     \
+        const KArgs& a = *pa;                                                                                  \
         KP_SMEM;                                                                                               \
         KP_LIST_LOOP(body_region_a(GpuBlk{(int64_t*)smem}, a.sub ? a.sub[blk] : blk, smem, a, rout, rstat))   \
       })                                                                                                       \
-  extern "C" __global__ void __launch_bounds__(T, MINW) k_region_b##SUF(KArgs a, const int32_t* rsel,           \
+  extern "C" __global__ void __launch_bounds__(T, MINW) k_region_b##SUF(const KArgs* __restrict__ pa,           \
+                                                                      const int32_t* rsel,                     \
                                                                       const int32_t* rnsel,                    \
                                                                       const RegionOut* rout, int cap)          \
       IB({                                                                                                     \
+        const KArgs& a = *pa;                                                                                  \
         KP_SMEM;                                                                                               \
         KP_LIST_LOOP(body_region_b(GpuBlk{(int64_t*)smem}, a.sub ? a.sub[blk] : blk, smem, a, rsel, rnsel, rout, cap)) \
       })
@@ -322,10 +330,11 @@ extern "C" __global__ void __launch_bounds__(256) k_region_groups(const RegionOu
 #else
 ;
 #endif
-extern "C" __global__ void __launch_bounds__(kSlowBlock) k_slow(KArgs a, unsigned char* scratch, size_t slot_bytes,
-                                                                int cap, int lds_area, int lds_sort)
+extern "C" __global__ void __launch_bounds__(kSlowBlock) k_slow(const KArgs* __restrict__ pa, unsigned char* scratch,
+                                                                size_t slot_bytes, int cap, int lds_area, int lds_sort)
 #if KP_K(7)
 {
+  const KArgs& a = *pa;
   KP_SMEM;
   body_slow(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, (int)gridDim.x, smem, a, scratch, slot_bytes, cap, lds_area, lds_sort);
 }
@@ -571,6 +580,8 @@ static int spread_grid(const KArgs& a) { return a.n_dev ? std::min(a.n, 256 * 4)
 int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x) {
   if (a.n <= 0) return 0;
   hipStream_t h = (hipStream_t)st;
+  const KArgs* pa = x.dargs;  // (the kernels other than k_select_all read their KArgs from it)
+  if (!pa && which != SEL_LAUNCH_ALL) return chk(hipErrorInvalidValue);
   switch (which) {
     case SEL_LAUNCH_ALL: {
       // a device-appended list: a persistent grid of a few workgroups per CU
@@ -583,31 +594,31 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
     }
     case SEL_LAUNCH_ALL_STREAM:
       hipLaunchKernelGGL(k_select_all_stream, dim3(a.n_dev ? std::min(a.n, 256 * 8) : a.n), dim3(KP_STREAM_THREADS),
-                         smem, h, a);
+                         smem, h, pa);
       break;
     case SEL_LAUNCH_CLUSTER:
       if (smem > kLdsPerCu / 2)
-        hipLaunchKernelGGL(k_select_cluster_wide, dim3(spread_grid(a)), dim3(512), smem, h, a, cap);
+        hipLaunchKernelGGL(k_select_cluster_wide, dim3(spread_grid(a)), dim3(512), smem, h, pa, cap);
       else
-        hipLaunchKernelGGL(k_select_cluster, dim3(spread_grid(a)), dim3(256), smem, h, a, cap);
+        hipLaunchKernelGGL(k_select_cluster, dim3(spread_grid(a)), dim3(256), smem, h, pa, cap);
       break;
     case SEL_LAUNCH_REGION_A:
       if (smem > kLdsPerCu / 2)
-        hipLaunchKernelGGL(k_region_a_wide, dim3(spread_grid(a)), dim3(512), smem, h, a, x.rout, x.rstat);
+        hipLaunchKernelGGL(k_region_a_wide, dim3(spread_grid(a)), dim3(512), smem, h, pa, x.rout, x.rstat);
       else
-        hipLaunchKernelGGL(k_region_a, dim3(spread_grid(a)), dim3(256), smem, h, a, x.rout, x.rstat);
+        hipLaunchKernelGGL(k_region_a, dim3(spread_grid(a)), dim3(256), smem, h, pa, x.rout, x.rstat);
       break;
     case SEL_LAUNCH_REGION_B:
       if (smem > kLdsPerCu / 2)
-        hipLaunchKernelGGL(k_region_b_wide, dim3(spread_grid(a)), dim3(512), smem, h, a, x.rsel, x.rnsel, x.rout, cap);
+        hipLaunchKernelGGL(k_region_b_wide, dim3(spread_grid(a)), dim3(512), smem, h, pa, x.rsel, x.rnsel, x.rout, cap);
       else
-        hipLaunchKernelGGL(k_region_b, dim3(spread_grid(a)), dim3(256), smem, h, a, x.rsel, x.rnsel, x.rout, cap);
+        hipLaunchKernelGGL(k_region_b, dim3(spread_grid(a)), dim3(256), smem, h, pa, x.rsel, x.rnsel, x.rout, cap);
       break;
     case SEL_LAUNCH_SLOW:
       if (smem > 65536 &&
           chk(hipFuncSetAttribute((const void*)k_slow, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)))
         return -1;
-      hipLaunchKernelGGL(k_slow, dim3(x.grid), dim3(kSlowBlock), smem, h, a, x.scratch, x.slot_bytes, cap, x.lds_area,
+      hipLaunchKernelGGL(k_slow, dim3(x.grid), dim3(kSlowBlock), smem, h, pa, x.scratch, x.slot_bytes, cap, x.lds_area,
                          x.lds_sort);
       break;
     default:

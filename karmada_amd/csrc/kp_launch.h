@@ -56,7 +56,13 @@ struct SelectExtra {
   int grid = 0;                      // slow path persistent grid
   int lds_area = 0;                  // slow path: LDS bytes for the small serial problems
   int lds_sort = 0;                  // slow path: LDS bytes for the candidate sorts (0: global slot)
+  // the launch's KArgs in device memory: the kernels whose bodies keep pointers into
+  // their arguments (SelCtx: &a.s, &a.bv) across calls take them by pointer, since a
+  // by-value kernel argument would be copied to scratch by every wave (~34 KB per wave)
+  const KArgs* dargs = nullptr;
 };
+// device KArgs slots per batch (one per such launch in a schedule call)
+constexpr int kArgSlots = 16;
 
 constexpr int kBlock = 256;
 constexpr int kSlowBlock = 512;  // k_slow: wider for the LDS bitonic sort

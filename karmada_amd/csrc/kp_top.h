@@ -236,6 +236,19 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     if (ord) elig = t.tot[cls] + sch < (int64_t)kInt32Max / 2;  // (else checked over the feasible votes below)
   }
   if (!elig) {
+    if (a.bcls != nullptr && (h->sel == SEL_ERR_UNSUPPORTED || (fl & BF_BAD))) {
+      // an error result needs only F (select_all_common's order: the bad request, the
+      // FitError, then the unsupported spread constraint, select_clusters.go:54), so
+      // it is written here instead of gathering every candidate in k_select_all
+      SelCtx x = make_ctx(a, b, nullptr);
+      x.h = h;
+      int64_t F = 0;
+      for (int w = B.tid(); w < s.W; w += B.nth()) F += popc64(x.frow[w]);
+      F = B.sum64(F);
+      if (pre_checks(B, x, (int)F)) return;
+      if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_SPREAD_UNSUPPORTED, 0);
+      return;
+    }
     top_fallback(B, a, t, b);
     return;
   }
