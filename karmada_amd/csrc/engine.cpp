@@ -300,7 +300,7 @@ struct kp_engine {
   // k_select_top (kp_top.h): on, and its subset capacity per binding (LDS entries);
   // KP_TOP=0 / KP_TOP_CAP=<n> at engine creation (tests, tuning)
   bool top_on = true;
-  int top_cap = 896;       // subset capacity of the large slice (LDS: 7 workgroups of two waves per CU)
+  int top_cap = 832;       // subset capacity of the large slice (LDS: 8 workgroups of two waves per CU)
   int top_cap_small = 256;  // ... and of the small one (bindings needing <= kTopSmallNeed)
   // the large-slice bindings run at this capacity first (more waves per CU); those whose
   // subset outgrows it run again at top_cap (0 / >= top_cap: one launch at top_cap)

@@ -541,6 +541,13 @@ KP_HD inline T kp_atomic_add(T* p, T v) {
   return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
 #endif
 }
+KP_HD inline uint32_t kp_atomic_and(uint32_t* p, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return atomicAnd(p, v);
+#else
+  return __atomic_fetch_and(p, v, __ATOMIC_RELAXED);
+#endif
+}
 KP_HD inline uint32_t kp_atomic_or(uint32_t* p, uint32_t v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return atomicOr(p, v);

@@ -91,7 +91,7 @@ struct TopArgs {
 // Webster's party list / enumeration buffer of the subset path (u64 entries): larger
 // party sets take its uncompacted passes over the subset (exact, kp_select.h).
 #ifndef KP_TOP_ECAP
-#define KP_TOP_ECAP 192
+#define KP_TOP_ECAP 160
 #endif
 constexpr int kTopEcap = KP_TOP_ECAP;
 // bindings whose Replicas + len(spec.Clusters) is at most this take the small slice
@@ -100,13 +100,13 @@ constexpr int64_t kTopSmallNeed = 160;
 // the waves stride over it): 256 CUs x 4 resident workgroups of the large slice
 constexpr int kTopOverGrid = 1024;
 KP_HD inline int top_ecap(int cap) { return cap < kTopEcap ? cap : kTopEcap; }
-// LDS slice of one binding: [red 64 B | frow W u64 | tgt bits | S votes cap | S ranks cap (u16) | SelScratch]
+// LDS slice of one binding: [red 64 B | mask W u64 | S votes cap | S ranks cap (u16) | SelScratch]
 // (the LDS a wave holds bounds the waves per CU, and this kernel runs as fast as it
-// keeps waves in flight: 16-bit ranks, so k_select_top needs Cp <= kTopMaxCp)
+// keeps waves in flight: 16-bit ranks, so k_select_top needs Cp <= kTopMaxCp; one
+// Cp-bit mask serves as the walk's candidate set and then as the target bits)
 KP_HD inline size_t top_lds_bytes(int Cp, int cap) {
-  const int words = (Cp + 31) >> 5, W = Cp / 64;
-  return 64 + 8 * (size_t)W + 4 * (size_t)((words + 3) & ~3) + 6 * (size_t)cap + 3072 + 8 * (size_t)top_ecap(cap) +
-         64;
+  const int W = Cp / 64;
+  return 64 + 8 * (size_t)W + 6 * (size_t)cap + 3072 + 8 * (size_t)top_ecap(cap) + 64;
 }
 constexpr int kTopMaxCp = 1 << 16;
 
@@ -166,22 +166,21 @@ struct TopHand {
   int64_t F;
 };
 
-// The LDS slice of one binding: [red 64 B | frow W u64 | tgt bits | S ranks cap | S votes cap |
-// SelScratch], carved the same way by every wave that reads it.
+// The LDS slice of one binding: [red 64 B | mask W u64 | S votes cap | S ranks cap |
+// SelScratch], carved the same way by every wave that reads it. The mask holds the
+// feasibility row, then (after the scheduled clusters are taken) the feasible clusters
+// that are not scheduled (the walk's candidates), then the feasible scheduled clusters
+// (the division's target bits: it reads feasibility only for targets).
 struct TopCarve {
   uint64_t* frow;
-  uint32_t* tgt;
   TopSub cd;
   SelScratch ss;
 };
 KP_HD inline TopCarve top_carve(unsigned char* smem, const SnapView& s, int cap, unsigned long long* dbg) {
-  const int words = (s.Cp + 31) >> 5;
   TopCarve c;
   unsigned char* p = smem + 64;
   c.frow = (uint64_t*)p;
   p += 8 * (size_t)s.W;
-  c.tgt = (uint32_t*)p;
-  p += 4 * (size_t)((words + 3) & ~3);
   c.cd.v = (int32_t*)p;
   c.cd.r = (uint16_t*)(c.cd.v + cap);
   c.cd.F = 0;
@@ -189,6 +188,15 @@ KP_HD inline TopCarve top_carve(unsigned char* smem, const SnapView& s, int cap,
   c.ss.cap = top_ecap(cap);
   c.ss.dbg = dbg;
   return c;
+}
+
+// The scheduled replicas of a spec.Clusters entry by its rank (the target list, scanned:
+// k_select_top keeps no target bits until its division)
+KP_HD inline int32_t target_rep(const SelCtx& x, uint32_t rank) {
+  const BindHdr& h = *x.h;
+  for (int j = 0; j < h.tgt_cnt; j++)
+    if ((uint32_t)x.bv->ipool[h.tgt_off + 2 * j] == rank) return x.bv->ipool[h.tgt_off + 2 * j + 1];
+  return 0;
 }
 
 // hand: wave 0 of a k_select_top_wg workgroup stops after the walk and leaves the
@@ -204,7 +212,6 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   // (each reload waiting on every load in flight) after every store or wave barrier
   const BindHdr hloc = a.bv.hdr[b];
   const BindHdr* h = &hloc;
-  const int words = (s.Cp + 31) >> 5;
   // eligibility: SEL_ALL Dynamic/Aggregated workloads the subset argument covers
   const uint32_t fl = h->flags;
   const int st = h->strategy;
@@ -254,13 +261,11 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   }
   TopCarve tc = top_carve(smem, s, t.cap, a.dbg);
   uint64_t* frow = tc.frow;
-  uint32_t* tgt = tc.tgt;
   TopSub cd = tc.cd;
   SelScratch ss = tc.ss;
-  SelCtx x = make_ctx(a, b, tgt);
+  // (no target bits until the division: the walk's mask excludes the targets itself)
+  SelCtx x = make_ctx(a, b, nullptr);
   x.h = h;
-  // (every read of the target bitset is behind tgt_cnt > 0)
-  if (h->tgt_cnt > 0) build_bits(B, tgt, words, a.bv.ipool, h->tgt_off, h->tgt_cnt, 2);
   int64_t F = 0;
   for (int w = B.tid(); w < s.W; w += B.nth()) {
     const uint64_t m = x.frow[w];
@@ -282,6 +287,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   const bool agg = st == ST_AGGREGATED;
   uint32_t* ctr = (uint32_t*)smem;  // subset length
   int64_t asum = 0, apos = 0, tsum = 0;
+  int64_t psum_t = 0;  // the votes of the scheduled clusters with replicas > 0 (the prior clusters)
   int32_t n = 0;
   if (h->tgt_cnt > 0) {  // (none: an empty subset and zero sums, no reductions)
     if (B.tid() == 0) *ctr = 0;
@@ -303,11 +309,19 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
       asum += sr;
       apos += sr > 0 ? 1 : 0;
       tsum += fresh ? add32(e, sr) : e;
+      psum_t += sr > 0 ? e : 0;
     }
     B.sum2(asum, apos);
-    tsum = B.sum64(tsum);
+    B.sum2(tsum, psum_t);
     n = (int32_t)*ctr;  // (the reductions ordered the reservation)
+    // the mask drops the scheduled clusters: it is the walk's candidate set from here
+    for (int j = B.tid(); j < h->tgt_cnt; j += B.nth()) {
+      const uint32_t r = (uint32_t)kp_ldu(a.bv.ipool + h->tgt_off + 2 * j);
+      kp_atomic_and((uint32_t*)frow + (r >> 5), ~(1u << (r & 31)));
+    }
+    B.sync();
   }
+  const int32_t nsched = n;  // the subset's first nsched entries: the feasible scheduled clusters
   if (n > t.cap) {
     top_fallback(B, a, t, b, true);
     return;
@@ -334,12 +348,8 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   if (!ord) {
     const bool walk = fresh || assigned < h->replicas;
     const int32_t target = fresh ? h->replicas : sub32(h->replicas, assigned);
-    int64_t psum = 0;  // Aggregated scale up: the prior clusters lead the order
-    if (walk && agg && !fresh && apos != 0) {
-      for (int i = B.tid(); i < n; i += B.nth())
-        if (has_tgt && sched_rep_of(x, cd.r[i]) > 0) psum += cd.v[i];
-      psum = B.sum64(psum);
-    }
+    // Aggregated scale up: the prior clusters lead the order
+    const int64_t psum = walk && agg && !fresh && apos != 0 ? psum_t : 0;
     if (walk && tsum < 0) {  // (negative scheduled votes: the one-quantity argument needs >= 0)
       top_fallback(B, a, t, b);
       return;
@@ -411,7 +421,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
 #endif
       for (int u = 0; u < kTopStream; u++) {
         const int c = c0 + u * B.nth() + B.tid();
-        ff[u] = c < s.C && ((frow[c >> 6] >> (c & 63)) & 1ull) && !(has_tgt && bit_test(tgt, c));
+        ff[u] = c < s.C && ((frow[c >> 6] >> (c & 63)) & 1ull);  // (the mask: feasible, not scheduled)
         vv[u] = ff[u] ? x.erow[c] : 0;
       }
 #if defined(__clang__)
@@ -491,12 +501,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     const int32_t target = fresh ? h->replicas : sub32(h->replicas, assigned);
     // Aggregated scale up with prior clusters: they lead the order (resortAvailableClusters,
     // assignment.go:151-178); their votes count toward the cut before any walked one
-    int64_t psum = 0;
-    if (agg && !fresh && apos != 0) {
-      for (int i = B.tid(); i < n; i += B.nth())
-        if (has_tgt && sched_rep_of(x, cd.r[i]) > 0) psum += cd.v[i];
-      psum = B.sum64(psum);
-    }
+    const int64_t psum = agg && !fresh && apos != 0 ? psum_t : 0;
     // The walk takes kTopGroup chunks of the class order per step: their feasibility
     // tests (LDS lookups of the binding's row) are issued together, their entries are
     // appended in order, and coverage is decided once per step over the group, with its
@@ -540,7 +545,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
         rg[q] = (uint32_t)e;
         vg[q] = (int32_t)(e >> 32);
         const bool valid = g0 + q * ww + lane < s.C;
-        fg[q] = valid && ((frow[rg[q] >> 6] >> (rg[q] & 63)) & 1ull) && !(has_tgt && bit_test(tgt, (int)rg[q]));
+        fg[q] = valid && ((frow[rg[q] >> 6] >> (rg[q] & 63)) & 1ull);  // (feasible, not scheduled)
         if (tie && valid) {
           past = past || vg[q] < tie_v;
           fg[q] = fg[q] && vg[q] == tie_v;
@@ -623,7 +628,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
         int64_t above = 0;
         for (int j = lane; j < n; j += ww) {
           uint32_t vq = (uint32_t)cd.v[j];
-          if (j < n0 && fresh) vq += (uint32_t)sched_rep_of(x, cd.r[j]);
+          if (j < n0 && fresh) vq += (uint32_t)target_rep(x, cd.r[j]);
           above += vq > vm ? ((vq - 1) / vm + 1) / 2 : 0;
         }
         if (B.sum64(above) >= (int64_t)target) break;  // (wave-uniform)
@@ -649,7 +654,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
       // 2^30), which needs only that sum; otherwise the full-candidate kernel decides.
       int64_t rest = 0;  // the votes of the feasible non-scheduled candidates
       for (int c = B.tid(); c < s.C; c += B.nth())
-        if (((frow[c >> 6] >> (c & 63)) & 1ull) && !(has_tgt && bit_test(tgt, c))) rest += est_at(x, c);
+        if ((frow[c >> 6] >> (c & 63)) & 1ull) rest += est_at(x, c);
       rest = B.sum64(rest);
       if ((int64_t)(int32_t)(tsum + rest) < (int64_t)target) {
         if (B.tid() == 0)
@@ -661,6 +666,16 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
       return;
     }
   }
+  if (has_tgt) {
+    // the mask becomes the feasible scheduled clusters (the subset's first nsched
+    // entries): the division's target bits, and the only feasibility it reads
+    for (int w = B.tid(); w < s.W; w += B.nth()) frow[w] = 0;
+    B.sync();
+    for (int i = B.tid(); i < nsched; i += B.nth())
+      kp_atomic_or((uint32_t*)frow + (cd.r[i] >> 5), 1u << (cd.r[i] & 31));
+    B.sync();
+  }
+  x.tgt_bits = (const uint32_t*)frow;
   KP_STAMP(x, 11);
 #if defined(KP_TOP_EXIT) && KP_TOP_EXIT == 2
   if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, n);
@@ -710,7 +725,7 @@ KP_FI void body_select_top_wg(const GBLK& G, const WBLK& W, int blk, unsigned ch
   const int b = a.list[blk];
   TopCarve tc = top_carve(slice, a.s, t.cap, a.dbg);
   const BindHdr hloc = a.bv.hdr[b];  // registers: no reload after LDS stores
-  SelCtx x = make_ctx(a, b, tc.tgt);
+  SelCtx x = make_ctx(a, b, (const uint32_t*)tc.frow);  // (wave 0 left the target bits there)
   x.h = &hloc;
   x.frow = tc.frow;
   tc.cd.F = hh.n;
