@@ -46,7 +46,12 @@ KP_FI void body_class_order(const BLK& B, int k, uint64_t* keys, int P, const Sn
     keys[i] = key;
   }
   B.sync();
-  for (int len = 2; len <= P; len <<= 1)  // bitonic sort, ascending
+  // Bitonic sort, ascending. Thread t owns i = t + nth*q, so a stage whose partner
+  // distance j is below the wave width pairs lanes of one wave: its writes need only
+  // the wave's own ordering before the next such stage; a workgroup barrier follows the
+  // stages with j >= 64 and the last stage of each len >= 64 (the next len starts with
+  // j = len). 91 barriers -> 28 at P = 8 192.
+  for (int len = 2; len <= P; len <<= 1)
     for (int j = len >> 1; j > 0; j >>= 1) {
       for (int i = B.tid(); i < P; i += B.nth()) {
         const int l = i ^ j;
@@ -59,7 +64,8 @@ KP_FI void body_class_order(const BLK& B, int k, uint64_t* keys, int P, const Sn
           }
         }
       }
-      B.sync();
+      if (j >= 64 || (j == 1 && len >= 64)) B.sync();
+      else B.wsync();
     }
   for (int i = B.tid(); i < s.C; i += B.nth()) {
     const uint64_t key = keys[i];
