@@ -3125,22 +3125,28 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     return r;
   };
   HIPCHK(dev::event_record(e->ev[3], sp));
+  // component-set classes (BF_SETS bindings): their class rows (after the estimator
+  // classes' rows, before k_class_order reads them all), and in the pair-row mode those
+  // bindings' own rows rebuilt from them (feasible clusters only)
+  auto sets_rows = [&]() -> int {
+    for (size_t j = 0; j < bt->sets_cls.size(); j++)
+      KPROF(sp, "k_sets_rows", 1, -1,
+            dev::sets_rows(sp, s->view, bt->d_sets_args + j, bt->d_sets_off, bt->d_sets_scratch,
+                           bt->cls_rows + (size_t)bt->sets_cls[j] * s->Cp, bt->d_sets_ovf + j));
+    return KP_OK;
+  };
   if (bits) {
     KPROF(sp, est_class_name(fast), bt->crep.size(), -1,
           dev::est_class(sp, s->view, bt->view, bt->d_crep, (int)bt->crep.size(), bt->cls_rows, fast));
-    HIPCHK(dev::event_record(e->ev[5], sp));
+    if (int rc = sets_rows()) return rc;
+    HIPCHK(dev::event_record(e->ev[5], sp));  // every class row is written (k_class_order's input)
     KPROF(sp, "k_filter", B, -1, dev::filter(sp, s->view, bt->view, bt->fmask));
   } else {
     KPROF(sp, pair_name(fast), B, -1,
           dev::pair(sp, s->view, bt->view, nullptr, 0, B, bt->fmask, bt->est, nullptr, 0, md_cap, smem_pair(s, md_cap),
                     fast));
+    if (int rc = sets_rows()) return rc;
   }
-  // component-set classes (BF_SETS bindings): their class rows, and in the pair-row
-  // mode those bindings' own rows rebuilt from them (feasible clusters only)
-  for (size_t j = 0; j < bt->sets_cls.size(); j++)
-    KPROF(sp, "k_sets_rows", 1, -1,
-          dev::sets_rows(sp, s->view, bt->d_sets_args + j, bt->d_sets_off, bt->d_sets_scratch,
-                         bt->cls_rows + (size_t)bt->sets_cls[j] * s->Cp, bt->d_sets_ovf + j));
   if (!bits && !bt->l_sets.empty())
     KPROF(sp, "k_rows_from_class", bt->l_sets.size(), -1,
           dev::rows_from_class(sp, s->view, bt->view, bt->d_sets_list, (int)bt->l_sets.size(), bt->d_bcls,
@@ -3168,9 +3174,19 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
                              kOrderWaves * ((region_a_order_lds_bytes(s->view.n_regions, s->view.W) + 15) & ~(size_t)15) <=
                                  e->max_lds;
   const bool orders = (top && bt->d_ord != nullptr) || spread_orders;
-  if (orders)
-    KPROF(sp, "k_class_order", bt->crep.size(), -1,
-          dev::class_order(sp, s->view, bt->cls_rows, (int)bt->crep.size(), bt->d_ord, bt->d_ctot, bt->d_cok));
+  if (orders) {
+    // k_class_order reads only the class rows (k_est_class), so it runs on stream3 beside
+    // k_filter and stream2 waits for it (profiled runs keep it on stream2: each kernel's
+    // event time is then its own)
+    dev::stream_t so = e->prof ? sp : e->stream3;
+    if (so != sp) HIPCHK(dev::stream_wait(so, e->ev[5]));
+    KPROF(so, "k_class_order", bt->crep.size(), -1,
+          dev::class_order(so, s->view, bt->cls_rows, (int)bt->crep.size(), bt->d_ord, bt->d_ctot, bt->d_cok));
+    if (so != sp) {
+      HIPCHK(dev::event_record(e->ev[6], so));
+      HIPCHK(dev::stream_wait(sp, e->ev[6]));
+    }
+  }
   HIPCHK(dev::event_record(e->ev[4], sp));
   HIPCHK(dev::stream_wait(st, e->ev[4]));  // every pair row precedes the rest
   HIPCHK(dev::event_record(e->ev[1], st));
