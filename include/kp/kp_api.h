@@ -636,7 +636,9 @@ int kp_snapshot_replicate(kp_engine* e, const kp_snapshot* src, kp_snapshot** ou
  * concurrently (one host thread per device, no cross-device traffic) and returns one
  * CSR in binding order, identical to kp_schedule_batch over the whole batch on one
  * device. Result buffers belong to the batch and stay valid until its next
- * kp_multi_schedule or destruction. */
+ * kp_multi_schedule or destruction. Verified on the host build (several simulated
+ * devices, tests/test_multi.py) and on one physical GPU only: the cross-device
+ * replication (hipMemcpyPeerAsync) has not run on two or more GPUs yet. */
 typedef struct kp_multi kp_multi;
 typedef struct kp_multi_snapshot kp_multi_snapshot;
 typedef struct kp_multi_batch kp_multi_batch;
