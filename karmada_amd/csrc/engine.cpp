@@ -3259,14 +3259,13 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       f.list = bt->d_fb;
       f.n = bt->n_all_dyn;
       f.n_dev = bt->stats + 9;
-      if (stream_all)
-        {  // (argument slot copied before the launch is timed)
-          const SelectExtra sxa1 = with_args(f, sp);
-          KPROF(sp, "k_select_all_stream", 0, 9,
-                dev::select(sp, SEL_LAUNCH_ALL_STREAM, f, sel_stream_lds_bytes(s->Cp), cap, sxa1));
-        }
-      else
+      if (stream_all) {
+        const SelectExtra sxa1 = with_args(f, sp);  // (the slot is copied before the launch is timed)
+        KPROF(sp, "k_select_all_stream", 0, 9,
+              dev::select(sp, SEL_LAUNCH_ALL_STREAM, f, sel_stream_lds_bytes(s->Cp), cap, sxa1));
+      } else {
         KPROF(sp, sel_name(SEL_LAUNCH_ALL, smem_all(s)), 0, 9, dev::select(sp, SEL_LAUNCH_ALL, f, smem_all(s), cap, sx));
+      }
     } else if (na > 0) {
       KArgs g = k;
       g.n = na;
@@ -3287,7 +3286,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       KArgs g = k;
       g.list = bt->d_all + rest0;
       g.n = k.n - rest0;
-      {  // (argument slot copied before the launch is timed)
+      {  // (the argument slot is copied before the launch is timed)
         const SelectExtra sxa2 = with_args(g, sp);
         KPROF(sp, "k_select_all_stream", g.n, -1,
               dev::select(sp, SEL_LAUNCH_ALL_STREAM, g, sel_stream_lds_bytes(s->Cp), cap, sxa2));
@@ -3313,7 +3312,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       k.sub = bt->d_fbc;
       k.n_dev = bt->stats + 12;
     }
-    {  // (argument slot copied before the launch is timed)
+    {  // (the argument slot is copied before the launch is timed)
       const SelectExtra sxa3 = with_args(k, s3);
       KPROF(s3, sel_name(SEL_LAUNCH_CLUSTER, smem_cluster(s, cap)), k.n_dev ? 0 : k.n, k.n_dev ? 12 : -1,
             dev::select(s3, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sxa3));
@@ -3341,13 +3340,13 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       KArgs kf = k;
       kf.sub = bt->d_fba;
       kf.n_dev = bt->stats + 14;
-      {  // (argument slot copied before the launch is timed)
+      {  // (the argument slot is copied before the launch is timed)
         const SelectExtra sxa4 = with_args(kf, st);
         KPROF(st, sel_name(SEL_LAUNCH_REGION_A, smem_region_a(s)), 0, 14,
               dev::select(st, SEL_LAUNCH_REGION_A, kf, smem_region_a(s), cap, sxa4));
       }
     } else {
-      {  // (argument slot copied before the launch is timed)
+      {  // (the argument slot is copied before the launch is timed)
         const SelectExtra sxa5 = with_args(k, st);
         KPROF(st, sel_name(SEL_LAUNCH_REGION_A, smem_region_a(s)), k.n, -1,
               dev::select(st, SEL_LAUNCH_REGION_A, k, smem_region_a(s), cap, sxa5));
@@ -3414,7 +3413,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       k.sub = bt->d_fbr;
       k.n_dev = bt->stats + 13;
     }
-    {  // (argument slot copied before the launch is timed)
+    {  // (the argument slot is copied before the launch is timed)
       const SelectExtra sxa6 = with_args(k, st);
       KPROF(st, sel_name(SEL_LAUNCH_REGION_B, smem_region_b(s, cap)), k.n_dev ? 0 : k.n, k.n_dev ? 13 : -1,
             dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sxa6));
