@@ -32,6 +32,13 @@ import os
 import sys
 import time
 
+# Hardware queues per process (read once, when the HIP runtime starts; nothing here has
+# touched the GPU yet). Each engine drives three HIP streams (SEL_ALL, cluster spread, the
+# region chain) and the bench keeps four engines in flight; with HIP's default of 4
+# queues those 12 streams share 4 in-order queues and the lanes' kernels serialize
+# (DESIGN.md §5 "Round 5"). 16 gives every stream its own queue.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -545,6 +552,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "inflight": len(lanes),
+        "hip_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
         # the timed window: from the (warmup x inflight)-th completed step to the K-th
         # completion after it, every lane mid-stream (module docstring)
         "timed_window": {"warmup_completions": n_warm, "timed_completions": args.steps,
