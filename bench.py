@@ -36,8 +36,10 @@ import time
 # touched the GPU yet). Each engine drives three HIP streams (SEL_ALL, cluster spread, the
 # region chain) and the bench keeps four engines in flight; with HIP's default of 4
 # queues those 12 streams share 4 in-order queues and the lanes' kernels serialize
-# (DESIGN.md §5 "Round 5"). 16 gives every stream its own queue.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# (DESIGN.md §5 "Round 5"). 16 gives every stream its own queue. The GPU boxes export
+# GPU_MAX_HW_QUEUES=4 (HIP's default), so the bench sets it outright; KP_HW_QUEUES
+# chooses another count (at most 32).
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(32, int(os.environ.get("KP_HW_QUEUES", "16")))))
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
