@@ -33,13 +33,12 @@ import sys
 import time
 
 # Hardware queues per process (read once, when the HIP runtime starts; nothing here has
-# touched the GPU yet). Each engine drives three HIP streams (SEL_ALL, cluster spread, the
-# region chain) and the bench keeps four engines in flight; with HIP's default of 4
-# queues those 12 streams share 4 in-order queues and the lanes' kernels serialize
-# (DESIGN.md §5 "Round 5"). 16 gives every stream its own queue. The GPU boxes export
-# GPU_MAX_HW_QUEUES=4 (HIP's default), so the bench sets it outright; KP_HW_QUEUES
-# chooses another count (at most 32).
-os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(32, int(os.environ.get("KP_HW_QUEUES", "16")))))
+# touched the GPU yet). HIP maps a process's streams onto GPU_MAX_HW_QUEUES in-order
+# hardware queues (4 by default, what the GPU boxes export); streams that share a queue
+# run in order. The bench keeps the environment's setting (KP_HW_QUEUES overrides it)
+# and sizes the engines' streams to it (KP_STREAMS, main(); DESIGN.md §5 "Round 6").
+if os.environ.get("KP_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(32, int(os.environ["KP_HW_QUEUES"]))))
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -250,7 +249,15 @@ def main():
                     help="batches in flight per GPU: engines (own HIP streams) driven by as many host threads, "
                          "so one batch's result copy-back and host steps overlap another's kernels")
     args = ap.parse_args()
+    if args.steps < 1:
+        sys.exit("bench.py: --steps must be >= 1 (the timed window ends at the K-th completion)")
 
+    # One HIP stream per engine when several batches are in flight: the lanes' streams then
+    # fit HIP's default 4 hardware queues instead of sharing them in order (same-box A/B at 4
+    # queues, profiles/r06_streams_ab.jsonl: 3 streams x 4 lanes 64.4-66.5 M/s, 1 x 4
+    # 72.3-80.0 M/s; DESIGN.md §5 "Round 6"). KP_STREAMS set in the environment wins.
+    if args.inflight > 1:
+        os.environ.setdefault("KP_STREAMS", "1")
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -352,8 +359,8 @@ def main():
                 if clock["done"] >= n_warm + args.steps:
                     break
             r = b_k.schedule_raw()
-            now = time.perf_counter()
             with lock:
+                now = time.perf_counter()  # (stamped in completion order, under the lock)
                 clock["done"] += 1
                 d = clock["done"]
                 if d == n_warm:
@@ -554,7 +561,10 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "inflight": len(lanes),
-        "hip_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+        # the hardware-queue count requested of the HIP runtime (GPU_MAX_HW_QUEUES; unset:
+        # HIP's default 4) and the streams each engine drives
+        "hip_hw_queues_requested": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+        "streams_per_engine": int(os.environ.get("KP_STREAMS", "3")),
         # the timed window: from the (warmup x inflight)-th completed step to the K-th
         # completion after it, every lane mid-stream (module docstring)
         "timed_window": {"warmup_completions": n_warm, "timed_completions": args.steps,

@@ -318,10 +318,15 @@ enum {
   KP_ERR_RESULT_CAPACITY = 14,       /* engine limit, no reference site: a serial result list
                                         outgrew the batch's result pool (arg = its length);
                                         never expected, reported instead of written */
-  KP_ERR_SETS_CAPACITY = 15          /* engine limit, no reference site: the binding's
+  KP_ERR_SETS_CAPACITY = 15,         /* engine limit, no reference site: the binding's
                                         MaxAvailableComponentSets simulation needed more than
                                         the device's node runs in one cluster (arg = the
                                         cluster's caller index); only that binding fails */
+  KP_ERR_OVERFLOW_TERMS = 16         /* engine limit, no reference site: the observed
+                                        ClusterAffinities term plus its overflow affinities
+                                        number more than 63, the orders the sortClusters key
+                                        holds (getClusterOverflowOrder, common.go:156-170,
+                                        takes any number); arg = that count */
 };
 
 /* Per-batch results, engine-owned, valid until the next call on the engine.

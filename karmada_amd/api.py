@@ -251,6 +251,7 @@ ERR_NAMES = {
     5: "cluster_resource", 6: "spread_unsupported", 7: "no_clusters", 8: "unsupported_strategy",
     9: "overflow_not_enough", 10: "fresh_not_enough", 11: "scale_down_not_enough",
     12: "scale_up_not_enough", 13: "undefined_strategy", 14: "result_capacity", 15: "sets_capacity",
+    16: "overflow_terms",
 }
 
 

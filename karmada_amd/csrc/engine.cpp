@@ -1460,7 +1460,8 @@ struct Packer {
       h.ovf_off = list(ovf);
       h.ovf_cnt = (int32_t)ovf.size();
       // engine limit: the sortClusters key orders kMaxOvfTerms overflow orders (kp_algo.h)
-      if (h.ovf_mode == OVF_PROGS && h.ovf_cnt > kMaxOvfTerms) f |= BF_BAD;
+      // (reported as KP_ERR_OVERFLOW_TERMS, not as a malformed request)
+      if (h.ovf_mode == OVF_PROGS && h.ovf_cnt > kMaxOvfTerms) f |= BF_BAD | BF_LIMIT_OVF;
       // enableOverflow (common.go:156-170)
       if (!b.has_cluster_affinity && b.n_cluster_affinities > 0 && b.observed_affinity_name.len > 0 && term &&
           term->n_overflow > 0)
@@ -1965,8 +1966,23 @@ int kp_engine_create(int device, kp_engine** out) {
   if (device < 0 || dev::device_count() <= device) return KP_EDEVICE;
   auto* e = new kp_engine();
   e->device = device;
-  if (dev::set_device(device) || dev::stream_create(&e->stream) || dev::stream_create(&e->stream2) ||
-      dev::stream_create(&e->stream3)) {
+  // KP_STREAMS: distinct HIP streams per engine (default 3). HIP maps a process's streams
+  // onto GPU_MAX_HW_QUEUES hardware queues (4 by default) round-robin, and streams that
+  // share a queue run in order: several engines in one process (batches in flight) then
+  // fit the default queues with fewer streams each. 2: the result/region stream and the
+  // SEL_ALL stream are one (the class orders and the large select_top slice keep their
+  // own); 1: every launch of the call in one stream.
+  int n_streams = 3;
+  if (const char* v = getenv("KP_STREAMS")) n_streams = std::max(1, std::min(3, atoi(v)));
+  bool fail = dev::set_device(device) || dev::stream_create(&e->stream);
+  if (!fail && n_streams >= 3) fail = dev::stream_create(&e->stream2) != 0;
+  else e->stream2 = e->stream;
+  if (!fail && n_streams >= 2) fail = dev::stream_create(&e->stream3) != 0;
+  else e->stream3 = e->stream2;
+  if (fail) {
+    if (e->stream3 && e->stream3 != e->stream2 && e->stream3 != e->stream) dev::stream_destroy(e->stream3);
+    if (e->stream2 && e->stream2 != e->stream) dev::stream_destroy(e->stream2);
+    if (e->stream) dev::stream_destroy(e->stream);
     delete e;
     return KP_EDEVICE;
   }
@@ -1993,9 +2009,10 @@ void kp_engine_destroy(kp_engine* e) {
   for (auto& ev : e->ev)
     if (ev) dev::event_destroy(ev);
   for (auto& ev : e->pev) dev::event_destroy(ev);
+  // (aliases: KP_STREAMS < 3)
+  if (e->stream3 && e->stream3 != e->stream2 && e->stream3 != e->stream) dev::stream_destroy(e->stream3);
+  if (e->stream2 && e->stream2 != e->stream) dev::stream_destroy(e->stream2);
   if (e->stream) dev::stream_destroy(e->stream);
-  if (e->stream2) dev::stream_destroy(e->stream2);
-  if (e->stream3) dev::stream_destroy(e->stream3);
   delete e;
 }
 

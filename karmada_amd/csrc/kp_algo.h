@@ -829,7 +829,7 @@ KP_HD inline int64_t locality_score(const BindHdr& h, const uint32_t* tgt_bits, 
 // Result sink
 // ============================================================================
 struct Sink {
-  uint32_t* out_idx;   // caller cluster index
+  uint32_t* out_idx;   // snapshot rank (k_compact maps it through perm to the caller's index)
   int32_t* out_rep;
   unsigned long long* counter;
   int32_t* status;

@@ -81,7 +81,8 @@ KP_FI void region_of_cands(const BLK& B, const SnapView& s, const Cands& cd) {
 template <class BLK>
 KP_FI bool pre_checks(const BLK& B, const SelCtx& x, int F) {
   if (x.h->flags & BF_BAD) {
-    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, 0);
+    const bool lim = (x.h->flags & BF_LIMIT_OVF) != 0;  // the engine's overflow-term limit
+    if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, lim ? KP_ERR_OVERFLOW_TERMS : KP_ERR_NONE, lim ? x.h->ovf_cnt : 0);
     return true;
   }
   if (F == 0) {  // FitError (generic_scheduler.go:84-89)

@@ -97,6 +97,8 @@ enum : uint32_t {
   BF_BAD = 1u << 15,            // packing error (unparsable quantity): status ERROR
   BF_DUP_TARGETS = 1u << 16,    // spec.Clusters names repeat: serial exact path
   BF_NEED_AVAIL = 1u << 17,     // selection reads AvailableReplicas
+  BF_LIMIT_OVF = 1u << 18,      // with BF_BAD: an engine limit (more overflow terms than the
+                                // sortClusters key orders), not a malformed request
 };
 enum : int32_t { ST_NONE = 0, ST_DUPLICATED, ST_AGGREGATED, ST_STATIC, ST_DYNAMIC };
 enum : int32_t { SEL_ALL = 0, SEL_CLUSTER, SEL_REGION, SEL_ERR_UNSUPPORTED };

@@ -208,3 +208,55 @@ def test_single_binding_overflow_tiers_result_pool(cpusim_engine):
         assert got[0]["err"] != 14, got  # KP_ERR_RESULT_CAPACITY
         assert got == want, (d["replicas"], got, want)
     snap.close()
+
+
+# ---- the overflow-term limit: 63 orders in the sortClusters key ------------------------
+def overflow_terms_case(engine, n_terms):
+    """One binding whose observed ClusterAffinities term carries n_terms - 1 overflow
+    affinities (getClusterOverflowOrder, common.go:156-170, takes any number): up to 63
+    the engine schedules it as the oracle does; past that it reports the engine limit
+    KP_ERR_OVERFLOW_TERMS (16) with the term count, not a malformed request."""
+    w = api.World()
+    cl = [{"name": f"m{i}", "labels": {"tier": str(i % 4)}, "apiEnablements": APPS,
+           "resourceSummary": {"allocatable": {"cpu": str(4 + i), "pods": "110"}}} for i in range(12)]
+    ca, nc = w.clusters(cl)
+
+    def aff(v):
+        return {"labelSelector": {"matchLabels": {"tier": v}}}
+    ovf = [aff(str(1 + k % 3)) for k in range(n_terms - 1)]
+    d = {"uid": "ovf-%d" % n_terms, "replicas": 9, "replicaRequirements": {"resourceRequest": {"cpu": "1"}},
+         "schedulerObservedAffinityName": "t",
+         "placement": {"clusterAffinities": [dict(aff("0"), affinityName="t", overflowAffinities=ovf)],
+                       "replicaScheduling": {"replicaSchedulingType": "Divided",
+                                             "replicaDivisionPreference": "Weighted",
+                                             "weightPreference": {"dynamicWeight": "AvailableReplicas"}}}}
+    opts = api.options()
+    snap = Snapshot.from_structs(engine, ca, nc, [c["name"] for c in cl], opts)
+    bs, n = w.bindings([d])
+    b = Batch(snap, structs=(bs, n))
+    got = b.schedule()
+    b.close()
+    snap.close()
+    want = O.schedule_c(ca, nc, bs, n, opts, O.FAST, 1)
+    return got[0], want[0]
+
+
+@pytest.mark.parametrize("n_terms", [63, 64])
+def test_overflow_terms_limit(cpusim_engine, n_terms):
+    got, want = overflow_terms_case(cpusim_engine, n_terms)
+    if n_terms <= 63:
+        assert got == want
+        assert got["status"] == 0, got
+    else:
+        assert got["status"] == 3 and got["err"] == 16 and got["arg"] == n_terms, got
+        assert want["status"] == 0  # (the reference schedules it)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_terms", [63, 64])
+def test_overflow_terms_limit_gpu(gpu_engine, n_terms):
+    got, want = overflow_terms_case(gpu_engine, n_terms)
+    if n_terms <= 63:
+        assert got == want
+    else:
+        assert got["status"] == 3 and got["err"] == 16 and got["arg"] == n_terms, got
