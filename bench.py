@@ -27,6 +27,7 @@ peak with compulsory bytes, plus the counter-derived DRAM bytes
 kernel from the committed PMC summary (profiles/r03_pmc_config<N>.json, else r02).
 """
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -244,6 +245,8 @@ def main():
     ap.add_argument("--check", type=int, default=1000,
                     help="bindings of the timed batch re-checked against the oracle after timing (0: off)")
     ap.add_argument("--e2e-reps", type=int, default=5, help="timed pack+upload+schedule repetitions (0: off)")
+    ap.add_argument("--e2e-churn", type=float, default=0.1,
+                    help="share of bindings at a new generation per end-to-end cycle (the rest reuse their records)")
     ap.add_argument("--lib", default=None, help="engine library (default karmada_amd/libkp.so)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="batches in flight per GPU: engines (own HIP streams) driven by as many host threads, "
@@ -469,7 +472,8 @@ def main():
         s_k.close()
         e_k.close()
     batch.close()
-    e2e = e2e_pipe = None
+    e2e = e2e_pipe = e2e_reuse = None
+    reuse_hits = 0.0
     if args.e2e_reps > 0:
         structs = u.binding_slice(0, u.n_bindings)
         ts = []
@@ -496,12 +500,50 @@ def main():
         for x in th:
             x.join()
         e2e_pipe = (time.perf_counter() - t1) / (2 * args.e2e_reps)
+        # the same pipeline with packed records reused across cycles (kp_pack_cache, keyed by
+        # (uid, metadata.generation)): each cycle re-schedules the batch with a different
+        # `churn` share of its bindings at a new generation (re-packed), the rest unchanged
+        # (their records copied); every lane's cache is warmed by one cycle first
+        import numpy as np
+        from karmada_amd.engine import PackCache
+        n_b = u.n_bindings
+        base_keys = api.binding_keys(structs[0], n_b, [1] * n_b)
+        kdt = np.dtype({"names": ["ptr", "len", "gen"], "formats": ["<u8", "<u4", "<i8"], "offsets": [0, 8, 16],
+                        "itemsize": C.sizeof(api.kp_binding_key)})
+
+        def cycle_keys(c):  # generation 1 + (cycles in which the binding changed so far)
+            ks = (api.kp_binding_key * n_b).from_buffer_copy(base_keys)
+            g = np.frombuffer(ks, dtype=kdt)["gen"]
+            idx = np.arange(n_b)
+            for q in range(1, c + 1):
+                g[(idx * 2654435761 + q * 40503) % 1000 < int(1000 * args.e2e_churn)] += 1
+            return ks
+        lanes_keys = [[cycle_keys(c) for c in range(args.e2e_reps + 1)] for _ in range(2)]
+        caches = [PackCache(eng), PackCache(eng2)]
+        for j, sn in enumerate((snap, snap2)):
+            Batch(sn, structs=structs, cache=caches[j], keys=lanes_keys[j][0]).close()  # (warm)
+
+        def drain_keyed(j, sn):
+            for c in range(1, args.e2e_reps + 1):
+                b3 = Batch(sn, structs=structs, cache=caches[j], keys=lanes_keys[j][c])
+                b3.schedule_raw()
+                b3.close()
+        t1 = time.perf_counter()
+        th = [threading.Thread(target=drain_keyed, args=(j, sn)) for j, sn in enumerate((snap, snap2))]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        e2e_reuse = (time.perf_counter() - t1) / (2 * args.e2e_reps)
+        reuse_hits = caches[0].stats()["last_hits"] / max(1, n_b)
+        for c_ in caches:
+            c_.close()
         snap2.close()
         eng2.close()
         if dist is not None:
-            t = torch.tensor([e2e, e2e_pipe], dtype=torch.float64, device=tdev)
+            t = torch.tensor([e2e, e2e_pipe, e2e_reuse], dtype=torch.float64, device=tdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            e2e, e2e_pipe = float(t[0].item()), float(t[1].item())
+            e2e, e2e_pipe, e2e_reuse = float(t[0].item()), float(t[1].item()), float(t[2].item())
 
     def avg(k):
         return sum(x[k] for x in st_all) / len(st_all)
@@ -599,10 +641,15 @@ def main():
                       "call_total": round(avg("total_ms"), 3)},
         "filter_mode": "bitset filter + estimator classes" if bits else "per-binding pair rows",
         "estimator_classes": int(last["n_classes"]) if bits else None,
-        # bindings/s including host packing + upload: pipelined over two engines (the
-        # value), and one batch at a time (end_to_end_serial_ms per batch)
-        "end_to_end_value": round(total / e2e_pipe, 1) if e2e_pipe else None,
-        "end_to_end_ms": round(1e3 * e2e_pipe, 2) if e2e_pipe else None,
+        # bindings/s including host packing + upload, pipelined over two engines: the
+        # value re-schedules each batch with `churn` of its bindings at a new generation and
+        # the rest's packed records reused (kp_batch_create_keyed); fresh: every binding
+        # packed anew; end_to_end_serial_ms: one fresh batch at a time
+        "end_to_end_value": round(total / e2e_reuse, 1) if e2e_reuse else None,
+        "end_to_end_ms": round(1e3 * e2e_reuse, 2) if e2e_reuse else None,
+        "end_to_end_reuse": {"churn": args.e2e_churn, "records_reused": round(reuse_hits, 4)},
+        "end_to_end_fresh_value": round(total / e2e_pipe, 1) if e2e_pipe else None,
+        "end_to_end_fresh_ms": round(1e3 * e2e_pipe, 2) if e2e_pipe else None,
         "end_to_end_serial_ms": round(1e3 * e2e, 2) if e2e else None,
         "setup_s": {"generate": round(gen_s, 2), "snapshot_pack_upload": round(snap_s, 3),
                     "binding_pack_upload": round(pack_s, 3)},

@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define KP_ABI_VERSION 13
+#define KP_ABI_VERSION 14
 
 /* ------------------------------------------------------------------------- */
 /* Object model                                                              */
@@ -438,6 +438,42 @@ int kp_snapshot_import(kp_engine* e, const void* bytes, uint64_t n_bytes, kp_sna
 int kp_batch_create(kp_engine* e, const kp_snapshot* s, const kp_binding* bindings,
                     uint64_t n_bindings, kp_batch** out);
 void kp_batch_destroy(kp_batch* b);
+
+/* ---- packed-record reuse across scheduling cycles --------------------------------
+ * The scheduler re-runs Schedule for bindings whose spec did not change: Duplicated and
+ * non-workload bindings on every reconcile, bindings with terminating target clusters,
+ * requeued failures (pkg/scheduler/scheduler.go:437-468); a changed spec moves
+ * metadata.generation. A kp_pack_cache keeps each binding's packed record (its binding
+ * header and pool slices, snapshot ids resolved) keyed by (metadata.uid,
+ * metadata.generation), and kp_batch_create_keyed copies a record instead of re-packing
+ * the binding when the key matches and so do the status fields the record depends on
+ * (status.schedulerObservedAffinityName, spec.rescheduleTriggeredAt,
+ * status.lastScheduledTime, compared field by field). Records are tied to the snapshot's
+ * dictionaries: a different snapshot, or a kp_snapshot_update that grew them
+ * (dict_grew = 1), empties the cache. The batch is byte-for-byte the one
+ * kp_batch_create packs from the same bindings. A cache is used by one call at a time. */
+typedef struct kp_pack_cache kp_pack_cache;
+typedef struct kp_binding_key {
+  kp_str uid;         /* metadata.uid */
+  int64_t generation; /* metadata.generation */
+} kp_binding_key;
+typedef struct kp_pack_cache_stats {
+  uint64_t hits, misses; /* over the cache's lifetime */
+  uint64_t entries;      /* records held */
+  uint64_t last_hits;    /* of the last kp_batch_create_keyed */
+} kp_pack_cache_stats;
+/* max_entries: records kept (0: 4M); past it the cache is emptied before the next batch. */
+int kp_pack_cache_create(uint64_t max_entries, kp_pack_cache** out);
+void kp_pack_cache_destroy(kp_pack_cache* c);
+int kp_pack_cache_get_stats(const kp_pack_cache* c, kp_pack_cache_stats* out);
+/* Diagnostic: a 64-bit digest of a batch's packed host image (binding headers, pools,
+ * routes, and each binding's estimator class as its first binding), equal for two
+ * batches exactly when they pack the same records (the tests compare keyed and fresh). */
+int kp_batch_digest(const kp_batch* b, uint64_t* out);
+/* kp_batch_create with keys[i] for bindings[i] (keys[i].uid empty: never cached). */
+int kp_batch_create_keyed(kp_engine* e, const kp_snapshot* s, const kp_binding* bindings,
+                          const kp_binding_key* keys, uint64_t n_bindings, kp_pack_cache* cache,
+                          kp_batch** out);
 
 /* genericScheduler.Schedule for every binding of the batch. */
 int kp_schedule_batch(kp_engine* e, kp_batch* b, kp_results* out);

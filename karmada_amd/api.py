@@ -173,6 +173,24 @@ class kp_results(C.Structure):
                 ("cluster_idx", C.POINTER(u32)), ("replicas", C.POINTER(i32)), ("n_targets", u64)]
 
 
+class kp_binding_key(C.Structure):
+    _fields_ = [("uid", kp_str), ("generation", i64)]
+
+
+class kp_pack_cache_stats(C.Structure):
+    _fields_ = [("hits", u64), ("misses", u64), ("entries", u64), ("last_hits", u64)]
+
+
+def binding_keys(bindings, n, generations):
+    """kp_binding_key per binding: its uid (kp_binding.uid, shared, not copied) and the
+    given metadata.generation."""
+    ks = (kp_binding_key * max(1, n))()
+    for i in range(n):
+        ks[i].uid = bindings[i].uid
+        ks[i].generation = int(generations[i])
+    return ks
+
+
 class kp_affinity_results(C.Structure):
     _fields_ = [("results", kp_results), ("affinity_index", C.POINTER(i32)), ("attempts", C.POINTER(i32)),
                 ("rounds", C.c_uint32)]

@@ -15,6 +15,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <tuple>
 #include <string>
 #include <string_view>
@@ -321,8 +322,15 @@ struct kp_engine {
   std::vector<kp_kernel_time> ktimes;
 };
 
+// Snapshot epochs: unique per snapshot object and renewed when kp_snapshot_update grows
+// its dictionaries, so packed records (kp_pack_cache) know which ids they resolved against.
+static uint64_t next_snap_epoch() {
+  static std::atomic<uint64_t> n{0};
+  return ++n;
+}
 struct kp_snapshot {
   kp_engine* e = nullptr;
+  uint64_t epoch = next_snap_epoch();
   kp_options opts{};
   int C = 0, Cp = 0, W = 0;
   Dict str, keys, gvk, res, regions;
@@ -345,7 +353,7 @@ struct kp_snapshot {
   SnapView view{};
 };
 
-constexpr int kDbgSlots = 96;  // diagnostic builds: phase stamps and counters (kp_select.h)
+// diagnostic builds: phase stamps and counters, kDbgSlots x kDbgSpread (kp_select.h)
 struct kp_batch {
   kp_snapshot* snap = nullptr;
   int B = 0;
@@ -2150,9 +2158,11 @@ int kp_snapshot_update(kp_engine* e, kp_snapshot* s, const kp_cluster* clusters,
     }
   apply_rows(s, rows, used);
   s->blob.clear();
-  if (dict_grew)  // region ids index the batches' region buffers: a changed region set counts too
-    *dict_grew = s->str.names.size() != n_str || s->keys.names.size() != n_keys || s->gvk.names.size() != n_gvk ||
-                 s->res.names.size() != n_res || s->regions.names != regions0;
+  // region ids index the batches' region buffers: a changed region set counts too
+  const bool grew = s->str.names.size() != n_str || s->keys.names.size() != n_keys || s->gvk.names.size() != n_gvk ||
+                    s->res.names.size() != n_res || s->regions.names != regions0;
+  if (dict_grew) *dict_grew = grew ? 1 : 0;
+  if (grew) s->epoch = next_snap_epoch();  // (packed records resolved against the old dictionaries)
   s->dev.reset();
   return upload_snapshot(e, s);
 }
@@ -2429,7 +2439,146 @@ inline void pf_strings(const kp_binding& b) {
     }
 }
 
-bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* bt) {
+// Shifts a packed binding's pool references by (di, dl, dt, dp, dn) (ipool, lpool, tols,
+// progs, instrs): its header, the program ids in its ipool lists, its programs'
+// instruction offsets and its instructions' list offsets. ip: the binding's ipool slice
+// (index = header offset - h.ip_beg, taken before the shift); pr / in: its program and
+// instruction slices. pack_parallel's chunk merge applies the same shifts.
+static void shift_binding(BindHdr& h, int32_t* ip, Prog* pr, int n_pr, Instr* in, int n_in, int32_t di, int32_t dl,
+                          int32_t dt, int32_t dp, int32_t dn) {
+  for (int j = 0; j < h.filt_cnt; j++) ip[h.filt_off - h.ip_beg + j] += dp;
+  for (int j = 0; j < h.ovf_cnt; j++) ip[h.ovf_off - h.ip_beg + j] += dp;
+  for (int j = 0; j < h.sw_cnt; j++) ip[h.sw_off - h.ip_beg + j] += dp;
+  h.tgt_off += di, h.evict_off += di, h.filt_off += di, h.ovf_off += di, h.sw_off += di;
+  h.sreq_off += di, h.mreq_off += di, h.ip_beg += di, h.ip_end += di;
+  h.sw_w_off += dl, h.sreq_q_off += dl, h.mreq_q_off += dl;
+  h.tol_off += dt;
+  h.pr_beg += dp, h.pr_end += dp;
+  h.in_beg += dn, h.in_end += dn;
+  for (int j = 0; j < n_pr; j++) pr[j].ins_off += dn;
+  for (int j = 0; j < n_in; j++) {
+    Instr& x = in[j];
+    if (x.op == OP_EXCLUDE || x.op == OP_NAMES) x.a += di;
+    else if (x.op == OP_LBL_IN || x.op == OP_LBL_NOTIN || x.op == OP_FLD_IN || x.op == OP_FLD_NOTIN ||
+             x.op == OP_ZONE_IN || x.op == OP_ZONE_NOTIN)
+      x.b += di;
+  }
+}
+
+// One binding's packed record (kp_pack_cache), one allocation: this struct (the header
+// with every pool reference relative to the record's own slices, the key and the status
+// fields it was packed with), then its slices (lpool, instrs, tols, progs, ipool) and the
+// uid, observed-affinity-name and estimator-class-key bytes.
+struct PackRec {
+  uint64_t key;
+  int64_t gen, rt_ns, lst_ns;
+  uint8_t has_rt, has_lst, nonworkload;  // nonworkload: bcls -1 (the estimator skipped)
+  int32_t n_ip, n_lp, n_tol, n_pr, n_in;
+  uint32_t uid_len, aff_len, cls_len;
+  BindHdr h;
+  unsigned char* tail() const { return (unsigned char*)(this + 1); }
+  int64_t* lp() const { return (int64_t*)tail(); }
+  Instr* in() const { return (Instr*)(lp() + n_lp); }
+  Tol* tol() const { return (Tol*)(in() + n_in); }
+  Prog* pr() const { return (Prog*)(tol() + n_tol); }
+  int32_t* ip() const { return (int32_t*)(pr() + n_pr); }
+  const char* uid() const { return (const char*)(ip() + n_ip); }
+  const char* aff() const { return uid() + uid_len; }
+  const char* cls() const { return aff() + aff_len; }
+  static PackRec* make(int n_ip, int n_lp, int n_tol, int n_pr, int n_in, size_t n_str) {
+    const size_t bytes = sizeof(PackRec) + 8 * (size_t)n_lp + sizeof(Instr) * (size_t)n_in +
+                         sizeof(Tol) * (size_t)n_tol + sizeof(Prog) * (size_t)n_pr + 4 * (size_t)n_ip + n_str;
+    auto* r = (PackRec*)::operator new(bytes, std::align_val_t(alignof(PackRec)));
+    r->n_ip = n_ip, r->n_lp = n_lp, r->n_tol = n_tol, r->n_pr = n_pr, r->n_in = n_in;
+    return r;
+  }
+  static void free(PackRec* r) { ::operator delete((void*)r, std::align_val_t(alignof(PackRec))); }
+  bool same(const kp_binding_key& k, const kp_binding& b) const {
+    return gen == k.generation && uid_len == k.uid.len && memcmp(uid(), k.uid.ptr, uid_len) == 0 &&
+           has_rt == b.has_reschedule_triggered_at && has_lst == b.has_last_scheduled_time &&
+           (!has_rt || rt_ns == b.reschedule_triggered_at_ns) && (!has_lst || lst_ns == b.last_scheduled_time_ns) &&
+           std::string_view(aff(), aff_len) == SV(b.observed_affinity_name);
+  }
+};
+
+// The records by key hash: kCacheShards open-addressed tables (linear probing, load <= 1/2;
+// each slot holds the key beside the pointer, so a probe touches the table only), read-only
+// while the packing threads look records up, filled shard by shard after.
+constexpr int kCacheShards = 64;
+struct PackTable {
+  struct Slot {
+    uint64_t key;  // 0: empty
+    PackRec* r;
+  };
+  std::vector<Slot> slot;
+  uint64_t n = 0;
+  static size_t home(uint64_t key, size_t cap) { return (size_t)((key >> 6) * 0x9e3779b97f4a7c15ull >> 20) & (cap - 1); }
+  const Slot* home_slot(uint64_t key) const { return slot.empty() ? nullptr : &slot[home(key, slot.size())]; }
+  const PackRec* find(uint64_t key) const {
+    if (slot.empty()) return nullptr;
+    const size_t cap = slot.size();
+    for (size_t i = home(key, cap);; i = (i + 1) & (cap - 1)) {
+      if (slot[i].key == key) return slot[i].r;
+      if (!slot[i].key) return nullptr;
+    }
+  }
+  void put(PackRec* r) {  // (replaces a record of the same key)
+    if (2 * (n + 1) > slot.size()) {
+      std::vector<Slot> old(std::max<size_t>(64, 2 * slot.size()), Slot{0, nullptr});
+      old.swap(slot);
+      n = 0;
+      for (const Slot& x : old)
+        if (x.key) put(x.r);
+    }
+    const size_t cap = slot.size();
+    for (size_t i = home(r->key, cap);; i = (i + 1) & (cap - 1)) {
+      if (!slot[i].key) {
+        slot[i] = Slot{r->key, r};
+        n++;
+        return;
+      }
+      if (slot[i].key == r->key) {
+        PackRec::free(slot[i].r);
+        slot[i].r = r;
+        return;
+      }
+    }
+  }
+  void clear() {
+    for (Slot& x : slot)
+      if (x.key) PackRec::free(x.r), x = Slot{0, nullptr};
+    n = 0;
+  }
+  ~PackTable() { clear(); }
+};
+}  // extern "C"
+
+struct kp_pack_cache {
+  uint64_t epoch = 0;  // the snapshot epoch the records resolved against (0: none yet)
+  uint64_t max_entries = (uint64_t)4 << 20;
+  uint64_t hits = 0, misses = 0, last_hits = 0;
+  PackTable shard[kCacheShards];
+  uint64_t entries() const {
+    uint64_t e = 0;
+    for (const auto& t : shard) e += t.n;
+    return e;
+  }
+  void clear() {
+    for (auto& t : shard) t.clear();
+  }
+};
+
+extern "C" {
+static inline uint64_t cache_key(const kp_binding_key& k) {
+  uint64_t h = 1469598103934665603ull;  // FNV-1a over the uid bytes, then the generation
+  for (uint32_t i = 0; i < k.uid.len; i++) h = (h ^ (uint8_t)k.uid.ptr[i]) * 1099511628211ull;
+  h ^= (uint64_t)k.generation * 0x9e3779b97f4a7c15ull;
+  h ^= h >> 29;
+  return h ? h : 1;
+}
+
+bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* bt, const kp_binding_key* keys = nullptr,
+                   kp_pack_cache* cache = nullptr) {
   int T = host_cpus();
   if (const char* v = getenv("KP_PACK_THREADS")) T = atoi(v);
   T = std::max(1, std::min(T, n / 4096));
@@ -2445,11 +2594,28 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
   bt->bcls.resize(n);
   std::vector<std::vector<std::string>> tkeys(T);
   std::vector<std::string> terr(T);
-  std::vector<double> tms(T, 0.0);
+  std::vector<double> tms(T, 0.0), tstart(T, 0.0);
+  const auto tpack0 = std::chrono::steady_clock::now();
   std::atomic<int> next_chunk(0);
   bt->route.resize(n);
   std::vector<uint64_t> chunk_cap(K + 1, 0);  // result slots per chunk (out_off prefix sums)
   std::vector<int> tmax_tgt(T, 0), tmax_tiers(T, 1);
+  // kp_pack_cache: records of another snapshot epoch, or past the size cap, are dropped
+  // first; new records collect per (chunk, shard) and go into the shards after the pack
+  if (cache && (cache->epoch != s->epoch || cache->entries() > cache->max_entries)) {
+    cache->clear();
+    cache->epoch = s->epoch;
+  }
+  std::vector<std::vector<PackRec*>> newrecs(cache ? (size_t)K * kCacheShards : 0);
+  struct RecGuard {  // records not handed to the cache (a failed batch) are freed
+    std::vector<std::vector<PackRec*>>* v;
+    ~RecGuard() {
+      for (auto& x : *v)
+        for (PackRec* r : x)
+          if (r) PackRec::free(r);
+    }
+  } rec_guard{&newrecs};
+  std::vector<uint64_t> thits(T, 0);
   auto run = [&](int t) {
     const auto tt0 = std::chrono::steady_clock::now();
     struct Stamp {
@@ -2457,6 +2623,7 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       double* out;
       ~Stamp() { *out = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
     } stamp{tt0, &tms[t]};
+    tstart[t] = std::chrono::duration<double, std::milli>(tt0 - tpack0).count();
     Packer pk{s, nullptr};
     SvMap<int32_t> ids;
     std::string key;
@@ -2469,13 +2636,72 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       uint64_t cap = 0;  // (chunk and thread totals kept in registers: the shared arrays are
       int max_tgt = 0, max_tiers = 1;  // written once per chunk, not once per binding)
       const int hi = lo[k + 1];
+      // kp_pack_cache lookups run ahead of the packing in stages, each prefetching what the
+      // next one reads: the uid bytes (8 ahead), the key hash and its table slot (4 ahead), the
+      // record (2 ahead); bindings without a record get the packer's own prefetches instead
+      constexpr int kRing = 16;
+      uint64_t ck_ring[kRing];
+      const PackRec* rec_ring[kRing];
+      auto keyed_at = [&](int j) { return cache && j < hi && keys[j].uid.len > 0; };
+      auto stage_hash = [&](int j) {
+        if (!keyed_at(j)) return;
+        const uint64_t c = cache_key(keys[j]);
+        ck_ring[j % kRing] = c;
+        pf(cache->shard[c % kCacheShards].home_slot(c));
+      };
+      auto stage_rec = [&](int j) {
+        const PackRec* r = nullptr;
+        if (keyed_at(j)) {
+          const uint64_t c = ck_ring[j % kRing];
+          r = cache->shard[c % kCacheShards].find(c);
+          if (r)
+            for (int o = 0; o < 8; o++) pf((const char*)r + 64 * o);
+        }
+        rec_ring[j % kRing] = r;
+        if (!r && j < hi) pf_arrays(bindings[j]);
+      };
       for (int q = lo[k]; q < std::min(hi, lo[k] + 3); q++) pf_struct(&bindings[q]);
-      if (lo[k] + 1 < hi) pf_arrays(bindings[lo[k] + 1]);
+      if (cache) {
+        for (int q = lo[k]; q < std::min(hi, lo[k] + 8); q++)
+          if (keyed_at(q)) pf(keys[q].uid.ptr);
+        for (int q = lo[k]; q < lo[k] + 4; q++) stage_hash(q);
+        for (int q = lo[k]; q < lo[k] + 2; q++) stage_rec(q);
+      } else if (lo[k] + 1 < hi) {
+        pf_arrays(bindings[lo[k] + 1]);
+      }
       for (int i = lo[k]; i < hi; i++) {
         if (i + 3 < hi) pf_struct(&bindings[i + 3]);
-        if (i + 2 < hi) pf_arrays(bindings[i + 2]);
-        if (i + 1 < hi) pf_strings(bindings[i + 1]);
-        pk.pack(bindings[i], bt->hdr[i]);
+        if (cache) {
+          if (keyed_at(i + 8)) pf(keys[i + 8].uid.ptr);
+          stage_hash(i + 4);
+          stage_rec(i + 2);
+          if (i + 1 < hi && !rec_ring[(i + 1) % kRing]) pf_strings(bindings[i + 1]);
+        } else {
+          if (i + 2 < hi) pf_arrays(bindings[i + 2]);
+          if (i + 1 < hi) pf_strings(bindings[i + 1]);
+        }
+        // a cached record (kp_pack_cache): the same key, generation and status fields
+        const bool keyed = keyed_at(i);
+        const uint64_t ck = keyed ? ck_ring[i % kRing] : 0;
+        const PackRec* hit = keyed ? rec_ring[i % kRing] : nullptr;
+        if (hit && !hit->same(keys[i], bindings[i])) hit = nullptr;
+        Pools& P = pl[k];
+        const size_t ip0 = P.ipool.size(), lp0 = P.lpool.size(), to0 = P.tols.size(), pr0 = P.progs.size(),
+                     in0 = P.instrs.size();
+        if (hit) {  // the record's slices appended, its references shifted onto them
+          BindHdr& h = bt->hdr[i];
+          h = hit->h;
+          P.ipool.insert(P.ipool.end(), hit->ip(), hit->ip() + hit->n_ip);
+          P.lpool.insert(P.lpool.end(), hit->lp(), hit->lp() + hit->n_lp);
+          P.tols.insert(P.tols.end(), hit->tol(), hit->tol() + hit->n_tol);
+          P.progs.insert(P.progs.end(), hit->pr(), hit->pr() + hit->n_pr);
+          P.instrs.insert(P.instrs.end(), hit->in(), hit->in() + hit->n_in);
+          shift_binding(h, P.ipool.data() + ip0, P.progs.data() + pr0, hit->n_pr, P.instrs.data() + in0, hit->n_in,
+                        (int32_t)ip0, (int32_t)lp0, (int32_t)to0, (int32_t)pr0, (int32_t)in0);
+          thits[t]++;
+        } else {
+          pk.pack(bindings[i], bt->hdr[i]);
+        }
         {
           const BindHdr& h = bt->hdr[i];
           cap += h.out_cap;
@@ -2483,28 +2709,64 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
           max_tgt = std::max(max_tgt, (int)h.tgt_cnt);
           max_tiers = std::max(max_tiers, (int)h.ovf_cnt + 2);  // primary, each overflow term, unmatched
         }
-        if (bt->hdr[i].flags & BF_NONWORKLOAD_EST) {
+        bool nonworkload = false;
+        if (hit) {
+          nonworkload = hit->nonworkload;
+          if (!nonworkload) key.assign(hit->cls(), hit->cls_len);
+        } else if (bt->hdr[i].flags & BF_NONWORKLOAD_EST) {
+          nonworkload = true;
+        } else {
+          if (bt->hdr[i].flags & BF_SETS) {
+            // a component-set class: key 'S' + the resolved SetsArgs (est_key's keys
+            // start with the 0/1 ReplicaRequirements word, never 'S')
+            std::string err;
+            const int rc = build_sets_args(s, bindings[i].components, bindings[i].n_components, &A, &err);
+            if (rc == KP_EINVAL) {
+              bt->hdr[i].flags = (bt->hdr[i].flags & ~(uint32_t)BF_SETS) | BF_BAD;  // status ERROR, as a bad request
+            } else if (rc != KP_OK) {
+              if (terr[t].empty()) terr[t] = err;
+              bt->hdr[i].flags &= ~(uint32_t)BF_SETS;
+            }
+            bt->route[i] = route_of(s->view, bt->hdr[i], pl[k].lpool.data());  // (flags changed)
+          }
+          if (bt->hdr[i].flags & BF_SETS) {
+            key.assign(1, 'S');
+            key.append((const char*)&A, sizeof(A));
+          } else {
+            est_key(bt->hdr[i], pl[k], &key);
+          }
+        }
+        if (keyed && !hit) {  // a new record: the binding's slices, references relative to them
+          const kp_binding& bb = bindings[i];
+          const uint32_t ul = keys[i].uid.len, al = bb.observed_affinity_name.len,
+                         cl = nonworkload ? 0u : (uint32_t)key.size();
+          PackRec* r = PackRec::make((int)(P.ipool.size() - ip0), (int)(P.lpool.size() - lp0),
+                                     (int)(P.tols.size() - to0), (int)(P.progs.size() - pr0),
+                                     (int)(P.instrs.size() - in0), (size_t)ul + al + cl);
+          r->key = ck;
+          r->gen = keys[i].generation;
+          r->has_rt = bb.has_reschedule_triggered_at;
+          r->has_lst = bb.has_last_scheduled_time;
+          r->rt_ns = r->has_rt ? bb.reschedule_triggered_at_ns : 0;
+          r->lst_ns = r->has_lst ? bb.last_scheduled_time_ns : 0;
+          r->nonworkload = nonworkload ? 1 : 0;
+          r->uid_len = ul, r->aff_len = al, r->cls_len = cl;
+          r->h = bt->hdr[i];
+          std::copy(P.ipool.begin() + (long)ip0, P.ipool.end(), r->ip());
+          std::copy(P.lpool.begin() + (long)lp0, P.lpool.end(), r->lp());
+          std::copy(P.tols.begin() + (long)to0, P.tols.end(), r->tol());
+          std::copy(P.progs.begin() + (long)pr0, P.progs.end(), r->pr());
+          std::copy(P.instrs.begin() + (long)in0, P.instrs.end(), r->in());
+          if (ul) memcpy((char*)r->uid(), keys[i].uid.ptr, ul);
+          if (al) memcpy((char*)r->aff(), bb.observed_affinity_name.ptr, al);
+          if (cl) memcpy((char*)r->cls(), key.data(), cl);
+          shift_binding(r->h, r->ip(), r->pr(), r->n_pr, r->in(), r->n_in, -(int32_t)ip0, -(int32_t)lp0,
+                        -(int32_t)to0, -(int32_t)pr0, -(int32_t)in0);
+          newrecs[(size_t)k * kCacheShards + ck % kCacheShards].push_back(r);
+        }
+        if (nonworkload) {
           bt->bcls[i] = -1;
           continue;
-        }
-        if (bt->hdr[i].flags & BF_SETS) {
-          // a component-set class: key 'S' + the resolved SetsArgs (est_key's keys
-          // start with the 0/1 ReplicaRequirements word, never 'S')
-          std::string err;
-          const int rc = build_sets_args(s, bindings[i].components, bindings[i].n_components, &A, &err);
-          if (rc == KP_EINVAL) {
-            bt->hdr[i].flags = (bt->hdr[i].flags & ~(uint32_t)BF_SETS) | BF_BAD;  // status ERROR, as a bad request
-          } else if (rc != KP_OK) {
-            if (terr[t].empty()) terr[t] = err;
-            bt->hdr[i].flags &= ~(uint32_t)BF_SETS;
-          }
-          bt->route[i] = route_of(s->view, bt->hdr[i], pl[k].lpool.data());  // (flags changed)
-        }
-        if (bt->hdr[i].flags & BF_SETS) {
-          key.assign(1, 'S');
-          key.append((const char*)&A, sizeof(A));
-        } else {
-          est_key(bt->hdr[i], pl[k], &key);
         }
         auto it = ids.find(key);
         if (it == ids.end()) {
@@ -2624,6 +2886,23 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
     }
   };
   on_threads(merge);
+  if (cache) {  // the new records into the shards (thread t fills shards t, t + T, ...)
+    on_threads([&](int t) {
+      for (int sh = t; sh < kCacheShards; sh += T) {
+        PackTable& tab = cache->shard[sh];
+        for (int k = 0; k < K; k++)
+          for (PackRec*& r : newrecs[(size_t)k * kCacheShards + sh]) {
+            tab.put(r);
+            r = nullptr;
+          }
+      }
+    });
+    uint64_t h = 0;
+    for (uint64_t x : thits) h += x;
+    cache->hits += h;
+    cache->misses += (uint64_t)n - h;
+    cache->last_hits = h;
+  }
   // a class's representative: its first binding
   size_t left = bt->crep.size() - 1;
   for (int i = 0; i < n && left; i++) {
@@ -2638,6 +2917,8 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
     fprintf(stderr, "pack_parallel: %d threads, %d chunks, pack %.1f ms, merge+classes %.1f ms; per thread", T, K,
             ms(tq0, tq1), ms(tq1, std::chrono::steady_clock::now()));
     for (double x : tms) fprintf(stderr, " %.1f", x);
+    fprintf(stderr, "; started at");
+    for (double x : tstart) fprintf(stderr, " %.1f", x);
     fprintf(stderr, "\n");
 #ifdef KP_PACK_PROF
     fprintf(stderr, "pack sections (Mcycles, cumulative): gvk %.1f targets %.1f tolerations %.1f affinity %.1f "
@@ -2654,7 +2935,56 @@ static int64_t order_amort() {  // (read per batch: tests switch it)
   return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)4;
 }
 
+static int batch_create_impl(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindings, uint64_t n,
+                             const kp_binding_key* keys, kp_pack_cache* cache, kp_batch** out);
 int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindings, uint64_t n, kp_batch** out) {
+  return batch_create_impl(e, sc, bindings, n, nullptr, nullptr, out);
+}
+int kp_batch_create_keyed(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindings, const kp_binding_key* keys,
+                          uint64_t n, kp_pack_cache* cache, kp_batch** out) {
+  if (!cache || (n && !keys)) return KP_EINVAL;
+  return batch_create_impl(e, sc, bindings, n, keys, cache, out);
+}
+int kp_batch_digest(const kp_batch* b, uint64_t* out) {
+  if (!b || !out) return KP_EINVAL;
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](const void* p, size_t n) {
+    const unsigned char* c = (const unsigned char*)p;
+    for (size_t i = 0; i < n; i++) h = (h ^ c[i]) * 1099511628211ull;
+  };
+  mix(b->hdr.data(), sizeof(BindHdr) * b->hdr.size());
+  mix(b->ipool.data(), 4 * b->ipool.size());
+  mix(b->lpool.data(), 8 * b->lpool.size());
+  mix(b->tols.data(), sizeof(Tol) * b->tols.size());
+  mix(b->progs.data(), sizeof(Prog) * b->progs.size());
+  mix(b->instrs.data(), sizeof(Instr) * b->instrs.size());
+  mix(b->route.data(), b->route.size());
+  for (size_t i = 0; i < b->bcls.size(); i++) {  // the class by its first binding (ids follow thread order)
+    const int32_t g = b->bcls[i];
+    const int32_t rep = g > 0 && (size_t)g < b->crep.size() ? b->crep[g] : -1;
+    mix(&rep, 4);
+  }
+  *out = h;
+  return KP_OK;
+}
+int kp_pack_cache_create(uint64_t max_entries, kp_pack_cache** out) {
+  if (!out) return KP_EINVAL;
+  auto* c = new kp_pack_cache();
+  if (max_entries) c->max_entries = max_entries;
+  *out = c;
+  return KP_OK;
+}
+void kp_pack_cache_destroy(kp_pack_cache* c) { delete c; }
+int kp_pack_cache_get_stats(const kp_pack_cache* c, kp_pack_cache_stats* out) {
+  if (!c || !out) return KP_EINVAL;
+  out->hits = c->hits;
+  out->misses = c->misses;
+  out->entries = c->entries();
+  out->last_hits = c->last_hits;
+  return KP_OK;
+}
+static int batch_create_impl(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindings, uint64_t n,
+                             const kp_binding_key* keys, kp_pack_cache* cache, kp_batch** out) {
   if (!e || !sc || !out || (n && !bindings)) return KP_EINVAL;
   if (n > (uint64_t)INT32_MAX) return KP_ENOTSUP;
   (void)dev::set_device(e->device);
@@ -2672,7 +3002,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
                  " has n_components > 0 but no components (the MultiplePodTemplatesScheduling gate reads them)";
         return KP_EINVAL;
       }
-  if (!pack_parallel(s, bindings, (int)n, bt)) {
+  if (!pack_parallel(s, bindings, (int)n, bt, keys, cache)) {
     e->err = bt->err.empty() ? "batch pools exceed 2^31 entries" : bt->err;
     return KP_ENOTSUP;
   }
@@ -2831,7 +3161,7 @@ int kp_batch_create(kp_engine* e, const kp_snapshot* sc, const kp_binding* bindi
   a.add(&bt->stats, 20);
   a.add(&bt->d_kargs, kArgSlots);
 #if defined(KP_STAMPS) || defined(KP_SLOW_CHECK)
-  a.add(&bt->dbg, kDbgSlots);
+  a.add(&bt->dbg, kDbgSlots * kDbgSpread);
 #endif
   // [0, out_cap): per-binding slots; [out_cap, 2 out_cap): serial results past their slot
   a.add(&bt->out_idx, std::max<uint64_t>(1, 2 * bt->out_cap));
@@ -3103,7 +3433,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   ka.slow_ids = bt->d_slowlist;
   ka.dbg = bt->dbg;
 #if defined(KP_STAMPS) || defined(KP_SLOW_CHECK)
-  HIPCHK(dev::fill(bt->dbg, 0, kDbgSlots * 8, st));
+  HIPCHK(dev::fill(bt->dbg, 0, kDbgSlots * kDbgSpread * 8, st));
 #endif
   dev::stream_t sp = e->stream2;
   HIPCHK(dev::event_record(e->ev[0], st));
@@ -3567,9 +3897,11 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   tm.n_region_order = spread_orders ? bt->h_stats[11] : 0u;
 #if defined(KP_STAMPS) || defined(KP_SLOW_CHECK)
   {
-    unsigned long long h[kDbgSlots];
-    HIPCHK(dev::d2h(h, bt->dbg, sizeof(h), st));
+    std::vector<unsigned long long> hv((size_t)kDbgSlots * kDbgSpread);
+    HIPCHK(dev::d2h(hv.data(), bt->dbg, 8 * hv.size(), st));
     HIPCHK(dev::sync(st));
+    unsigned long long h[kDbgSlots] = {};
+    for (size_t q = 0; q < hv.size(); q++) h[q % kDbgSlots] += hv[q];
     fprintf(stderr, "kp stamps (s_memtime ticks, summed over workgroups):");
     for (int i = 0; i < kDbgSlots; i++)
       if (h[i]) fprintf(stderr, " [%d]=%llu", i, h[i]);

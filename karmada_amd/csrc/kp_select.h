@@ -90,26 +90,37 @@ struct SelCtx {
 KP_HD inline int32_t est_merge(const SelCtx& x, int32_t r) { return x.merge ? cal_merge_bf(x.mrep, r) : r; }
 KP_HD inline int32_t est_at(const SelCtx& x, int c) { return est_merge(x, x.erow[c]); }
 
-// Diagnostic phase stamps (a separate -DKP_STAMPS build; never in libkp.so).
+// Diagnostic phase stamps (a separate -DKP_STAMPS build; never in libkp.so). Each
+// workgroup adds into one of kDbgSpread copies of the kDbgSlots counters (by its index),
+// so the atomics of concurrent waves do not contend for one address (a contended atomic
+// holds back every later load of its wave, which the stamps would then count); the host
+// sums the copies.
+constexpr int kDbgSlots = 96;
+#if defined(KP_STAMPS)
+constexpr int kDbgSpread = 256;
+#else
+constexpr int kDbgSpread = 1;
+#endif
+#define KP_DBG_AT(i) ((i) + kDbgSlots * (int)(blockIdx.x & (kDbgSpread - 1)))
 #if defined(KP_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
 #define KP_STAMP_INIT unsigned long long kp_t0 = __builtin_amdgcn_s_memtime();
 #define KP_STAMP(ctx_, i)                                                \
   do {                                                                   \
     if (threadIdx.x == 0 && (ctx_).dbg) {                                \
       unsigned long long t = __builtin_amdgcn_s_memtime();               \
-      atomicAdd(&(ctx_).dbg[i], t - kp_t0);                              \
+      atomicAdd(&(ctx_).dbg[KP_DBG_AT(i)], t - kp_t0);                   \
       kp_t0 = t;                                                         \
     }                                                                    \
   } while (0)
 #define KP_COUNT(ctx_, i, v)                                             \
   do {                                                                   \
-    if (threadIdx.x == 0 && (ctx_).dbg) atomicAdd(&(ctx_).dbg[i], (unsigned long long)(v)); \
+    if (threadIdx.x == 0 && (ctx_).dbg) atomicAdd(&(ctx_).dbg[KP_DBG_AT(i)], (unsigned long long)(v)); \
   } while (0)
 #define KP_STAMPD(dbg, i)                                                \
   do {                                                                   \
     if (threadIdx.x == 0 && (dbg)) {                                     \
       unsigned long long t = __builtin_amdgcn_s_memtime();               \
-      atomicAdd(&(dbg)[i], t - kp_t0);                                   \
+      atomicAdd(&(dbg)[KP_DBG_AT(i)], t - kp_t0);                        \
       kp_t0 = t;                                                         \
     }                                                                    \
   } while (0)

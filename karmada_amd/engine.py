@@ -25,7 +25,7 @@ from karmada_amd import api
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libkp.so")
-KP_ABI_VERSION = 13
+KP_ABI_VERSION = 14
 
 _LIBS = {}
 
@@ -33,7 +33,8 @@ _LIBS = {}
 EXPORTS = (
     "kp_abi_version", "kp_engine_create", "kp_engine_destroy", "kp_last_error", "kp_snapshot_create",
     "kp_snapshot_destroy", "kp_snapshot_export", "kp_snapshot_import", "kp_snapshot_update", "kp_batch_create",
-    "kp_batch_destroy",
+    "kp_batch_destroy", "kp_batch_create_keyed", "kp_batch_digest", "kp_pack_cache_create", "kp_pack_cache_destroy",
+    "kp_pack_cache_get_stats",
     "kp_schedule_batch", "kp_schedule_affinities", "kp_filter_batch", "kp_filter_reasons", "kp_score_batch", "kp_max_available_replicas", "kp_max_available_component_sets",
     "kp_model_grades", "kp_node_max_replicas", "kp_node_max_component_sets", "kp_last_stage_times",
     "kp_engine_set_threads", "kp_snapshot_replicate", "kp_engine_set_profile", "kp_last_kernel_times",
@@ -69,6 +70,12 @@ def load_library(path: str = LIB_PATH):
     L.kp_snapshot_destroy.argtypes = [vp]
     L.kp_batch_create.argtypes = [vp, vp, C.POINTER(api.kp_binding), C.c_uint64, C.POINTER(vp)]
     L.kp_batch_destroy.argtypes = [vp]
+    L.kp_batch_digest.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.kp_pack_cache_create.argtypes = [C.c_uint64, C.POINTER(vp)]
+    L.kp_pack_cache_destroy.argtypes = [vp]
+    L.kp_pack_cache_get_stats.argtypes = [vp, C.POINTER(api.kp_pack_cache_stats)]
+    L.kp_batch_create_keyed.argtypes = [vp, vp, C.POINTER(api.kp_binding), C.POINTER(api.kp_binding_key), C.c_uint64,
+                                        vp, C.POINTER(vp)]
     L.kp_schedule_batch.argtypes = [vp, vp, C.POINTER(api.kp_results)]
     L.kp_schedule_affinities.argtypes = [vp, vp, C.POINTER(api.kp_binding), C.c_uint64,
                                          C.POINTER(api.kp_affinity_results)]
@@ -292,10 +299,43 @@ class Snapshot:
             pass
 
 
-class Batch:
-    """A batch of ResourceBindings packed against one snapshot (kp_batch)."""
+class PackCache:
+    """Packed binding records kept across scheduling cycles (kp_pack_cache): a binding
+    whose (metadata.uid, metadata.generation) and scheduler status fields match a record
+    is copied instead of re-packed (pkg/scheduler/scheduler.go:437-468 re-runs Schedule
+    for bindings whose spec did not change)."""
 
-    def __init__(self, snap: Snapshot, bindings: Sequence[dict] = (), structs=None):
+    def __init__(self, engine: "Engine", max_entries: int = 0):
+        self.L = engine.L
+        h = C.c_void_p()
+        if self.L.kp_pack_cache_create(max_entries, C.byref(h)) != KP_OK:
+            raise EngineError("kp_pack_cache_create failed")
+        self.h = h
+
+    def stats(self) -> dict:
+        st = api.kp_pack_cache_stats()
+        self.L.kp_pack_cache_get_stats(self.h, C.byref(st))
+        return {"hits": st.hits, "misses": st.misses, "entries": st.entries, "last_hits": st.last_hits}
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.kp_pack_cache_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Batch:
+    """A batch of ResourceBindings packed against one snapshot (kp_batch). With `cache`
+    and `keys` ((uid, generation) per binding, api.binding_keys) it is created through
+    kp_batch_create_keyed: bindings whose record the cache holds skip packing."""
+
+    def __init__(self, snap: Snapshot, bindings: Sequence[dict] = (), structs=None, cache: "PackCache" = None,
+                 keys=None, generations: Sequence[int] = None):
         self.snap = snap
         eng = snap.engine
         if structs is None:
@@ -306,7 +346,14 @@ class Batch:
             ba, n = structs
         self.n = n
         h = C.c_void_p()
-        eng._check(eng.L.kp_batch_create(eng.h, snap.h, ba, n, C.byref(h)), "kp_batch_create")
+        if cache is not None:
+            if keys is None:  # (uid from each binding, metadata.generation given)
+                keys = api.binding_keys(ba, n, generations if generations is not None else [0] * n)
+            self._keys = keys
+            eng._check(eng.L.kp_batch_create_keyed(eng.h, snap.h, ba, keys, n, cache.h, C.byref(h)),
+                       "kp_batch_create_keyed")
+        else:
+            eng._check(eng.L.kp_batch_create(eng.h, snap.h, ba, n, C.byref(h)), "kp_batch_create")
         self.h = h
 
     def close(self):
@@ -319,6 +366,12 @@ class Batch:
             self.close()
         except Exception:
             pass
+
+    def digest(self) -> int:
+        """kp_batch_digest: the packed image's digest (equal for equal packs)."""
+        d = C.c_uint64()
+        self.snap.engine._check(self.snap.engine.L.kp_batch_digest(self.h, C.byref(d)), "kp_batch_digest")
+        return d.value
 
     def schedule_raw(self) -> api.kp_results:
         r = api.kp_results()

@@ -31,7 +31,7 @@ import json
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 from karmada_amd import api
-from karmada_amd.engine import Batch, Snapshot
+from karmada_amd.engine import Batch, PackCache, Snapshot
 
 SUCCESS, UNSCHEDULABLE, ERROR = 0, 1, 2  # framework.Code (interface.go:124-133)
 
@@ -328,9 +328,15 @@ class Shim:
         self.est: Dict[str, Tuple[BatchView, int]] = {}  # requirements content -> (view, slot)
         self.live: Dict[int, int] = {}                   # id(view) -> specs still registered
         self.batches_created = 0
+        # packed records kept across cycles, keyed by (uid, metadata.generation): the Go
+        # shim's kp_pack_cache (INTEGRATION.md ScheduleBatchKeyed)
+        self.pack_cache = PackCache(engine)
 
-    def _view(self, specs: Sequence[dict]) -> BatchView:
-        b = Batch(self.snap, list(specs))
+    def _view(self, specs: Sequence[dict], generations: Optional[Sequence[int]] = None) -> BatchView:
+        if generations is None:
+            b = Batch(self.snap, list(specs))
+        else:
+            b = Batch(self.snap, list(specs), cache=self.pack_cache, generations=generations)
         self.batches_created += 1
         return BatchView(self.snap, b, self.clusters)
 
@@ -340,8 +346,11 @@ class Shim:
             self.keep[id(sp)] = sp
         self.live[id(view)] = self.live.get(id(view), 0) + len(specs)
 
-    def schedule_batch(self, specs: Sequence[dict]) -> List[dict]:
-        view = self._view(specs)
+    def schedule_batch(self, specs: Sequence[dict], generations: Optional[Sequence[int]] = None) -> List[dict]:
+        """ScheduleBatch; with `generations` (metadata.generation per spec, the spec's "uid"
+        as the other half of the key) ScheduleBatchKeyed: records of unchanged bindings
+        are reused from earlier cycles instead of re-packed (kp_batch_create_keyed)."""
+        view = self._view(specs, generations)
         self._register(view, specs)
         return view.batch.schedule()
 
@@ -402,4 +411,5 @@ class Shim:
             view.batch.close()
         self.by.clear()
         self.est.clear()
+        self.pack_cache.close()
         self.snap.close()

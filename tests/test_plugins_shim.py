@@ -369,3 +369,19 @@ def test_shim_keeps_callers_options(cpusim_engine):
     sh = plugins.Shim(cpusim_engine, shim_clusters(), opts=opts)
     assert len(sh.schedule_batch([shim_spec()])) == 1
     sh.close()
+
+
+def test_shim_keyed_batches_reuse_records(cpusim_engine):
+    """ScheduleBatchKeyed: a second cycle over the same (uid, generation) reuses every
+    packed record and schedules as a fresh pack; a bumped generation re-packs that one."""
+    sh = plugins.Shim(cpusim_engine, shim_clusters())
+    specs = [dict(shim_spec(env=e, replicas=r), uid="uid-%d" % i)
+             for i, (e, r) in enumerate([("prod", 2), ("dev", 3), (None, 5), ("prod", 1)])]
+    first = sh.schedule_batch(specs, generations=[1, 1, 1, 1])
+    assert sh.pack_cache.stats()["last_hits"] == 0
+    again = sh.schedule_batch(specs, generations=[1, 1, 1, 1])
+    assert sh.pack_cache.stats()["last_hits"] == 4
+    assert again == first == sh.schedule_batch(specs)
+    sh.schedule_batch(specs, generations=[1, 2, 1, 1])
+    assert sh.pack_cache.stats()["last_hits"] == 3
+    sh.close()
