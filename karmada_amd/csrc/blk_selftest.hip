@@ -9,6 +9,7 @@
 
 #include "kp_blk.h"
 #include "kp_pdq.h"
+#include "kp_select.h"
 
 using namespace kp;
 
@@ -240,6 +241,64 @@ extern "C" int kp_pdq_selftest(const int32_t* reps, const int32_t* offs, int nl,
   (void)hipFree(dr);
   (void)hipFree(doffs);
   (void)hipFree(dn);
+  (void)hipFree(dok);
+  int declined = 0;
+  for (int j = 0; j < nl; j++) declined += ok[j] ? 0 : 1;
+  return declined;
+}
+
+// ---------------------------------------------------------------------------
+// webster_reg (kp_select.h): Webster with one party per lane of one wave, in
+// registers (k_select_top's subsets of <= 64 candidates). List j (at most 64 votes,
+// party i = cluster rank i) with N[j] seats and the name order desc[j]; the host
+// compares the seats with the oracle's AllocateWebsterSeats.
+// ---------------------------------------------------------------------------
+extern "C" __global__ void __launch_bounds__(64) k_webster_reg_test(const int64_t* votes, const int32_t* offs,
+                                                                    const int32_t* Ns, const int32_t* descs,
+                                                                    int32_t* seats, int32_t* ok) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  WaveBlk B{(int64_t*)smem};
+  const int a = offs[blockIdx.x], n = offs[blockIdx.x + 1] - a;
+  const int l = B.lane();
+  const bool has = l < n;
+  const int64_t v = has ? votes[a + l] : 0;
+  const int64_t V = B.sum64(v);
+  bool okb = false;
+  const WebRes w = webster_reg(B, has, (uint32_t)l, v, Ns[blockIdx.x], descs[blockIdx.x] != 0, V, &okb);
+  if (has) seats[a + l] = web_seats(w, v, (uint32_t)l);
+  if (l == 0) ok[blockIdx.x] = okb ? 1 : 0;
+}
+
+// Runs nl lists; seats_out gets every party's seats. Returns the number of lists
+// webster_reg declined (its step bound), or -1 on a HIP error.
+extern "C" int kp_webster_reg_selftest(const int64_t* votes, const int32_t* offs, const int32_t* Ns,
+                                       const int32_t* descs, int nl, int32_t* seats_out, char* msg, int msg_len) {
+  const int total = offs[nl];
+  int64_t* dv;
+  int32_t *doffs, *dN, *dd, *ds, *dok;
+  if (hipMalloc(&dv, 8 * (size_t)(total + 1)) || hipMalloc(&doffs, 4 * (size_t)(nl + 1)) ||
+      hipMalloc(&dN, 4 * (size_t)nl) || hipMalloc(&dd, 4 * (size_t)nl) || hipMalloc(&ds, 4 * (size_t)(total + 1)) ||
+      hipMalloc(&dok, 4 * (size_t)nl)) {
+    snprintf(msg, msg_len, "hipMalloc failed");
+    return -1;
+  }
+  (void)hipMemcpy(dv, votes, 8 * (size_t)total, hipMemcpyHostToDevice);
+  (void)hipMemcpy(doffs, offs, 4 * (size_t)(nl + 1), hipMemcpyHostToDevice);
+  (void)hipMemcpy(dN, Ns, 4 * (size_t)nl, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dd, descs, 4 * (size_t)nl, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_webster_reg_test, dim3(nl), dim3(64), 64, 0, dv, doffs, dN, dd, ds, dok);
+  if (hipDeviceSynchronize() != hipSuccess) {
+    snprintf(msg, msg_len, "kernel failed: %s", hipGetErrorString(hipGetLastError()));
+    return -1;
+  }
+  std::vector<int32_t> ok(nl);
+  (void)hipMemcpy(seats_out, ds, 4 * (size_t)total, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(ok.data(), dok, 4 * (size_t)nl, hipMemcpyDeviceToHost);
+  (void)hipFree(dv);
+  (void)hipFree(doffs);
+  (void)hipFree(dN);
+  (void)hipFree(dd);
+  (void)hipFree(ds);
   (void)hipFree(dok);
   int declined = 0;
   for (int j = 0; j < nl; j++) declined += ok[j] ? 0 : 1;

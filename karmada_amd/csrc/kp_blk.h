@@ -270,6 +270,10 @@ struct GpuBlk {
   KP_INLINE int wwidth() const { return 64; }
   KP_INLINE uint64_t wballot(bool p) const { return __ballot(p); }
   KP_INLINE uint64_t wlt() const { return (1ull << lane()) - 1; }  // lanes below this one
+  template <class T>
+  KP_INLINE T wread(T v, int l) const {  // lane l's value (l wave-uniform)
+    return kp_readlane(v, l);
+  }
   KP_INLINE uint64_t wminu64(uint64_t v) const {  // the wave's minimum (no workgroup barrier)
     return wave_reduce(v, [](uint64_t a, uint64_t b) { return a < b ? a : b; }, (uint64_t)~0ull);
   }

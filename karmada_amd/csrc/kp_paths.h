@@ -381,9 +381,14 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
   // BF_FRESH; the prior-cluster sum is 0 unless some prior has replicas).
   const bool fresh = (h.flags & BF_FRESH) != 0;
   auto tgt = [&](uint32_t rk) { return h.tgt_cnt > 0 && bit_test(x.tgt_bits, (int)rk); };
-  // this pass also takes Webster's vote totals and octave histogram (WebPre)
-  for (int i = B.tid(); i < 256; i += B.nth()) ss.hist[i] = 0;
-  if (B.tid() == 0) *web_ctr(ss) = 0;
+  // this pass also takes Webster's vote totals and octave histogram (WebPre); one
+  // candidate per lane of one wave (RegCands) takes webster_reg instead, which needs no
+  // histogram
+  const bool reg = std::is_same<CS, RegCands>::value && B.nwaves() == 1;
+  if (!reg) {
+    for (int i = B.tid(); i < 256; i += B.nth()) ss.hist[i] = 0;
+    if (B.tid() == 0) *web_ctr(ss) = 0;
+  }
   int64_t asum = 0, apos = 0;
   TgtCands{&x, B.tid(), B.nth()}.each([&](uint32_t, int32_t v) {
     asum += v;
@@ -407,7 +412,7 @@ KP_FI int sel_all_fast(const BLK& B, const SelCtx& x, const CS& cs, const SelScr
     ds.nparty++;
     if (v > 0) {
       ds.P++;
-      kp_atomic_add(&ss.hist[vote_bin((uint32_t)v)], 1u);
+      if (!reg) kp_atomic_add(&ss.hist[vote_bin((uint32_t)v)], 1u);
     }
     if (pr) {
       ds.sp += v;
@@ -597,7 +602,25 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
   // DynamicWeight: the parties are every candidate with the votes sel_all_fast's pass
   // summed (vote32), so its totals and histogram stand in for Webster's first pass
   const WebPre wp{pre ? pre->vtot : 0, pre ? pre->vmax : 0, pre ? pre->P : 0};
-  WebRes w = webster_par(B, parties, target, desc, ss, pre && st != ST_AGGREGATED ? &wp : nullptr);
+  WebRes w;
+  bool reg_ok = false;
+  if constexpr (std::is_same<CS, RegCands>::value) {
+    if (B.nwaves() == 1) {  // one party per lane in registers (sel_all_fast skipped the histogram)
+      bool party = false;
+      uint32_t prk = 0;
+      int64_t pv = 0;
+      parties([&](uint32_t rk, int64_t v) {
+        party = true;
+        prk = rk;
+        pv = v;
+      });
+      const int64_t V = pre && st != ST_AGGREGATED ? pre->vtot : B.sum64(party ? pv : 0);
+      w = webster_reg(B, party, prk, pv, target, desc, V, &reg_ok);
+      if (!reg_ok) w = webster_par(B, parties, target, desc, ss, nullptr);
+    }
+  }
+  if constexpr (!std::is_same<CS, RegCands>::value) w = webster_par(B, parties, target, desc, ss, pre && st != ST_AGGREGATED ? &wp : nullptr);
+  else if (B.nwaves() != 1) w = webster_par(B, parties, target, desc, ss, pre && st != ST_AGGREGATED ? &wp : nullptr);
   KP_STAMP(x, 4);
 #if defined(KP_TOP_EXIT) && KP_TOP_EXIT == 4
   if (B.tid() == 0) sink_error(x, KP_STATUS_ERROR, KP_ERR_NONE, (int64_t)w.tie);

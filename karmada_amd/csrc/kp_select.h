@@ -1098,6 +1098,96 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   return webster_tail(B, r, parties, tstar, N, desc, sc, ecap, compact, np, Lb, pl);
 }
 
+// webster_par for a single-wave block holding at most one party per lane in registers
+// (k_select_top's subsets of <= 64 candidates, RegCands): the same t* and tie threshold,
+// with no LDS. At t0 = V/2N each party holds s = #{k : prio(v, k) >= t0} = round(Nv/V)
+// priorities, within one party per lane / 2 of N in total (so at most 32 steps); the
+// smallest held priority is dropped (or the largest next one added) one at a time by a
+// wave min / max, and only the lane that gave it recomputes its next one. The tie group
+// at t* is ordered by tie_key as webster_tail orders it: each tied lane counts the tied
+// keys below its own (the keys are distinct: one party per cluster rank). V: the parties'
+// vote total. `ok` is false (nothing decided) when the count is off by more than the
+// step bound, which the rounding argument excludes: the caller runs webster_par then.
+template <class BLK>
+KP_FI WebRes webster_reg(const BLK& B, bool party, uint32_t rk, int64_t v, int32_t N, bool desc, int64_t V,
+                         bool* ok) {
+  WebRes r;
+  r.N = N;
+  r.desc = desc;
+  r.t = 0;
+  r.tie = 0;
+  *ok = true;
+  if (V == 0) {
+    r.mode = 0;
+    return r;
+  }
+  if (N <= 0) {
+    r.mode = 1;
+    return r;
+  }
+  r.mode = 2;
+  const int64_t capN = (int64_t)N;
+  const double t0 = (double)V / (2.0 * (double)N);
+  int64_t s = party ? w_count(v, t0, capN + 1, true) : 0;
+  const int64_t C = B.sum64(s);
+  const int64_t steps = C >= capN ? C - capN : capN - C;
+  if (steps > 64) {
+    *ok = false;
+    return r;
+  }
+  const int lane = B.lane();
+  double tstar;
+  if (C >= capN) {  // drop the smallest held priorities: t* is the smallest one left
+    uint64_t cand = party && s > 0 ? kp_dbits(w_prio(v, s - 1)) : ~0ull;
+    for (int64_t left = steps;; left--) {
+      const uint64_t m = B.minu64(cand);
+      if (left == 0) {
+        tstar = kp_bitsd(m);
+        break;
+      }
+      const int win = __builtin_ctzll(B.wballot(cand == m));
+      if (lane == win) {
+        s--;
+        cand = s > 0 ? kp_dbits(w_prio(v, s - 1)) : ~0ull;
+      }
+    }
+  } else {  // add the largest next priorities: t* is the last one added
+    uint64_t cand = party ? kp_dbits(w_prio(v, s)) : 0ull;
+    for (int64_t left = steps;; left--) {
+      const uint64_t m = (uint64_t)B.max64((int64_t)cand);  // (positive doubles: below 2^63)
+      if (left == 1) {
+        tstar = kp_bitsd(m);
+        break;
+      }
+      const int win = __builtin_ctzll(B.wballot(cand == m));
+      if (lane == win) {
+        s++;
+        cand = kp_dbits(w_prio(v, s));
+      }
+    }
+  }
+  r.t = tstar;
+  r.rt = 1.0 / tstar;
+  // seats strictly above t*, then the tie group at t* (webster_tail)
+  const int64_t base = party ? w_count_r(v, tstar, r.rt, capN + 1, false) : 0;
+  const bool tie = party && w_prio(v, base) == tstar;
+  int64_t S = base, T = tie ? 1 : 0;
+  B.sum2(S, T);
+  const int64_t M = capN - S;
+  if (M >= T) {
+    r.tie = ~0ull;
+  } else {
+    // the M-th smallest tie key (1-based): the tied lane with M - 1 tied keys below its own
+    const uint64_t key = tie ? tie_key(base, rk, desc) : ~0ull;
+    const uint64_t tmask = B.wballot(tie);
+    int64_t below = 0;
+    for (uint64_t m = tmask; m; m &= m - 1) below += B.wread(key, __builtin_ctzll(m)) < key ? 1 : 0;
+    const uint64_t sel = B.wballot(tie && below == M - 1);
+    r.tie = B.wread(key, sel ? __builtin_ctzll(sel) : 0);
+  }
+  return r;
+}
+
 // Largest value v* over a value set (values in [0, 2^31)) such that the values
 // >= v* sum to at least `target` (>= 1; the caller guarantees the total reaches
 // it): an 8-bit radix descent with value-weighted bins. `vals(fn)` calls fn(v)
