@@ -38,6 +38,23 @@ def test_bench_two_ranks_gloo():
     assert two["scheduled_ok"] == one["scheduled_ok"]
 
 
+def test_bench_four_ranks_gloo_config5_whole_csr():
+    """Four rank processes over config 5's mix (SEL_ALL StaticWeight, Dynamic/Aggregated
+    and spread constraints, interleaved), cost-balanced shards (dist.shard_range_weighted):
+    every binding of the gathered CSR is re-checked against the oracle (--check covers each
+    rank's whole shard), and the totals equal one rank over the same universe."""
+    common = ["--config", "5", "--clusters", "300", "--check", "400", "--inflight", "1"]
+    four = line(run(common + ["--gpus", "4", "--bindings", "100"], {"KP_CPUSIM_THREADS": "1"}))
+    one = line(run(common + ["--gpus", "1", "--bindings", "400"]))
+    assert four["n_gpus"] == 4 and len(four["per_rank_ms"]) == 4
+    assert four["config"]["bindings_total"] == 400 == one["config"]["bindings_total"]
+    # the shards are cut by cost, not by count, yet cover the universe: every binding checked once
+    assert four["parity_checked"] == 400 and four["parity_bad"] == 0
+    assert one["parity_checked"] == 400 and one["parity_bad"] == 0
+    assert four["result_targets"] == one["result_targets"]
+    assert four["scheduled_ok"] == one["scheduled_ok"]
+
+
 def test_bench_gpus_must_match_world_size():
     p = run(["--gpus", "2", "--bindings", "50"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0 and "WORLD_SIZE" in (p.stderr + p.stdout)
