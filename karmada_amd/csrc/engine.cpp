@@ -1004,7 +1004,10 @@ int upload_snapshot(kp_engine* e, kp_snapshot* s) {
 // Binding packing
 // ============================================================================
 // Host-side pools of packed bindings (kp_batch's, or one packing thread's).
-struct Pools {
+// (aligned to two cache lines: the packing threads fill adjacent chunks' pools at once, and
+// every push_back writes its vector's end pointer; packed 120-B structs shared lines, and
+// 16 threads packed at about a third of the single-thread rate per binding)
+struct alignas(128) Pools {
   std::vector<int32_t> ipool;
   std::vector<int64_t> lpool;
   std::vector<Tol> tols;
@@ -2615,7 +2618,7 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
           if (r) PackRec::free(r);
     }
   } rec_guard{&newrecs};
-  std::vector<uint64_t> thits(T, 0);
+  std::vector<uint64_t> thits(T, 0);  // (added once per chunk: adjacent slots share a line)
   auto run = [&](int t) {
     const auto tt0 = std::chrono::steady_clock::now();
     struct Stamp {
@@ -2633,8 +2636,8 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       if (k >= K) break;
       owner[k] = t;
       pk.bt = &pl[k];
-      uint64_t cap = 0;  // (chunk and thread totals kept in registers: the shared arrays are
-      int max_tgt = 0, max_tiers = 1;  // written once per chunk, not once per binding)
+      uint64_t cap = 0, hits = 0;  // (chunk and thread totals kept in registers: the shared
+      int max_tgt = 0, max_tiers = 1;  // arrays are written once per chunk, not once per binding)
       const int hi = lo[k + 1];
       // kp_pack_cache lookups run ahead of the packing in stages, each prefetching what the
       // next one reads: the uid bytes (8 ahead), the key hash and its table slot (4 ahead), the
@@ -2698,7 +2701,7 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
           P.instrs.insert(P.instrs.end(), hit->in(), hit->in() + hit->n_in);
           shift_binding(h, P.ipool.data() + ip0, P.progs.data() + pr0, hit->n_pr, P.instrs.data() + in0, hit->n_in,
                         (int32_t)ip0, (int32_t)lp0, (int32_t)to0, (int32_t)pr0, (int32_t)in0);
-          thits[t]++;
+          hits++;
         } else {
           pk.pack(bindings[i], bt->hdr[i]);
         }
@@ -2776,6 +2779,7 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
         bt->bcls[i] = it->second;
       }
       chunk_cap[k + 1] = cap;
+      thits[t] += hits;
       tmax_tgt[t] = std::max(tmax_tgt[t], max_tgt);
       tmax_tiers[t] = std::max(tmax_tiers[t], max_tiers);
     }
