@@ -308,6 +308,10 @@ struct kp_engine {
   int top_cap_mid = 0;
   bool top_split = true;    // the two slices' launches on two streams (KP_TOP_SPLIT=0: one)
   bool slow_order = true;   // k_slow orders candidates from the class orders (KP_SLOW_ORDER=0: sorts)
+  // with a region chain (whose host steps synchronise anyway) the fallback kernels over
+  // device-appended lists are launched only after their counts are read back, so none runs
+  // with an empty list (KP_GATE_FB=0: always launched, each workgroup reading the count)
+  bool gate_fb = true;
   bool top_wg = false;      // large-subset bindings on k_select_top_wg (KP_TOP_WG=1; measured slower)
   // per-kernel timing of kp_schedule_batch (kp_engine_set_profile): an event pair
   // around every launch on its own stream, folded by kernel name after the batch
@@ -2002,6 +2006,7 @@ int kp_engine_create(int device, kp_engine** out) {
   if (const char* v = getenv("KP_TOP")) e->top_on = atoi(v) != 0;
   if (const char* v = getenv("KP_TOP_SPLIT")) e->top_split = atoi(v) != 0;
   if (const char* v = getenv("KP_SLOW_ORDER")) e->slow_order = atoi(v) != 0;
+  if (const char* v = getenv("KP_GATE_FB")) e->gate_fb = atoi(v) != 0;
   if (const char* v = getenv("KP_TOP_WG")) e->top_wg = atoi(v) != 0;
   if (const char* v = getenv("KP_TOP_CAP")) {  // (tests: one capacity for both slices)
     e->top_cap = std::max(64, std::min(1024, atoi(v) & ~63));
@@ -3545,6 +3550,13 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   // pair kernel there), cluster spread on stream3, the region chain on stream, so a
   // latency-bound kernel shares the CUs with the others instead of running alone.
   HIPCHK(dev::event_record(e->ev[7], sp));
+  // Fallback launches over device-appended lists, with a region chain (e->gate_fb): their
+  // counts are read back where the host synchronises anyway (the region chain, k_slow's
+  // count), so a list left empty launches nothing; the SEL_ALL and cluster-spread
+  // fallbacks move to stream3 after that read, before k_slow.
+  const bool gate = e->gate_fb && !bt->l_region.empty();
+  bool defer_all = false, defer_all_stream = false, defer_cl = false;
+  KArgs f_def{}, cl_def{};
   if (!bt->l_all.empty()) {
     KArgs k = ka;
     k.list = bt->d_all;
@@ -3610,7 +3622,11 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       f.list = bt->d_fb;
       f.n = bt->n_all_dyn;
       f.n_dev = bt->stats + 9;
-      if (stream_all) {
+      if (gate) {
+        f_def = f;
+        defer_all = true;
+        defer_all_stream = stream_all;
+      } else if (stream_all) {
         const SelectExtra sxa1 = with_args(f, sp);  // (the slot is copied before the launch is timed)
         KPROF(sp, "k_select_all_stream", 0, 9,
               dev::select(sp, SEL_LAUNCH_ALL_STREAM, f, sel_stream_lds_bytes(s->Cp), cap, sxa1));
@@ -3663,7 +3679,10 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       k.sub = bt->d_fbc;
       k.n_dev = bt->stats + 12;
     }
-    {  // (the argument slot is copied before the launch is timed)
+    if (gate && k.n_dev) {
+      cl_def = k;
+      defer_cl = true;
+    } else {  // (the argument slot is copied before the launch is timed)
       const SelectExtra sxa3 = with_args(k, s3);
       KPROF(s3, sel_name(SEL_LAUNCH_CLUSTER, smem_cluster(s, cap)), k.n_dev ? 0 : k.n, k.n_dev ? 12 : -1,
             dev::select(s3, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sxa3));
@@ -3691,8 +3710,14 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       KArgs kf = k;
       kf.sub = bt->d_fba;
       kf.n_dev = bt->stats + 14;
-      {  // (the argument slot is copied before the launch is timed)
-        const SelectExtra sxa4 = with_args(kf, st);
+      uint32_t nfa = 1;
+      if (gate) {  // (the grid is then sized by the count: spread_grid)
+        HIPCHK(dev::d2h(&nfa, bt->stats + 14, 4, st));
+        HIPCHK(dev::sync(st));
+      }
+      if (nfa > 0) {  // (the argument slot is copied before the launch is timed)
+        SelectExtra sxa4 = with_args(kf, st);
+        if (gate) sxa4.list_grid = (int)nfa;
         KPROF(st, sel_name(SEL_LAUNCH_REGION_A, smem_region_a(s)), 0, 14,
               dev::select(st, SEL_LAUNCH_REGION_A, kf, smem_region_a(s), cap, sxa4));
       }
@@ -3764,8 +3789,14 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       k.sub = bt->d_fbr;
       k.n_dev = bt->stats + 13;
     }
-    {  // (the argument slot is copied before the launch is timed)
-      const SelectExtra sxa6 = with_args(k, st);
+    uint32_t nfb = 1;
+    if (gate && k.n_dev) {
+      HIPCHK(dev::d2h(&nfb, bt->stats + 13, 4, st));
+      HIPCHK(dev::sync(st));
+    }
+    if (nfb > 0) {  // (the argument slot is copied before the launch is timed)
+      SelectExtra sxa6 = with_args(k, st);
+      if (gate && k.n_dev) sxa6.list_grid = (int)nfb;
       KPROF(st, sel_name(SEL_LAUNCH_REGION_B, smem_region_b(s, cap)), k.n_dev ? 0 : k.n, k.n_dev ? 13 : -1,
             dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sxa6));
     }
@@ -3778,26 +3809,51 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   // region kernels (config 4: 3.87 -> 3.74 ms). Without one the wait costs more than it
   // saves (config 3: 2.00 -> 2.20 ms with four batches in flight), so k_slow is queued.
   HIPCHK(dev::stream_wait(s3, e->ev[8]));
-  if (!bt->l_slow.empty()) {
-    uint32_t nslow = (uint32_t)bt->slow_grid;
-    if (!bt->l_region.empty()) {
-      HIPCHK(dev::d2h(&nslow, bt->stats, 4, s3));
-      HIPCHK(dev::sync(s3));
+  uint32_t nslow = (uint32_t)bt->slow_grid;
+  if (!bt->l_region.empty() && (gate || !bt->l_slow.empty())) {
+    uint32_t hs[16];  // (stats [0] flagged, [9] SEL_ALL fallbacks, [12] cluster-spread fallbacks)
+    HIPCHK(dev::d2h(hs, bt->stats, sizeof(hs), s3));
+    HIPCHK(dev::sync(s3));
+    nslow = hs[0];
+    bool more = false;  // a deferred fallback runs: it may flag bindings for k_slow
+    if (defer_all && hs[9] > 0) {
+      const KArgs& f = f_def;
+      if (defer_all_stream) {
+        SelectExtra sxa1 = with_args(f, s3);
+        sxa1.list_grid = (int)hs[9];
+        KPROF(s3, "k_select_all_stream", hs[9], -1,
+              dev::select(s3, SEL_LAUNCH_ALL_STREAM, f, sel_stream_lds_bytes(s->Cp), cap, sxa1));
+      } else {
+        SelectExtra sxg = sx;
+        sxg.list_grid = (int)hs[9];
+        KPROF(s3, sel_name(SEL_LAUNCH_ALL, smem_all(s)), hs[9], -1,
+              dev::select(s3, SEL_LAUNCH_ALL, f, smem_all(s), cap, sxg));
+      }
+      more = true;
     }
-    if (nslow > 0) {
-      KArgs k = ka;
-      k.list = bt->d_slowlist;
-      k.n = (int)bt->l_slow.size();
-      k.ord = orders ? bt->d_ord : nullptr;  // sortClusters order from the class orders (kp_kernels.h)
-      k.cok = orders ? bt->d_cok : nullptr;
-      if (!e->slow_order) k.ord = nullptr;
-      SelectExtra sxs = with_args(k, s3);
-      sxs.grid = (int)std::min<uint32_t>((uint32_t)bt->slow_grid, nslow);
-      KPROF(s3, "k_slow", 0, 0,
-            dev::select(s3, SEL_LAUNCH_SLOW, k,
-                        kRedBytes + 512 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area + sx.lds_sort,
-                        bt->slow_cap, sxs));
+    if (defer_cl && hs[12] > 0) {
+      const KArgs& k = cl_def;
+      SelectExtra sxa3 = with_args(k, s3);
+      sxa3.list_grid = (int)hs[12];
+      KPROF(s3, sel_name(SEL_LAUNCH_CLUSTER, smem_cluster(s, cap)), hs[12], -1,
+            dev::select(s3, SEL_LAUNCH_CLUSTER, k, smem_cluster(s, cap), cap, sxa3));
+      more = true;
     }
+    if (more) nslow = (uint32_t)bt->slow_grid;  // (the kernel reads the final count itself)
+  }
+  if (!bt->l_slow.empty() && nslow > 0) {
+    KArgs k = ka;
+    k.list = bt->d_slowlist;
+    k.n = (int)bt->l_slow.size();
+    k.ord = orders ? bt->d_ord : nullptr;  // sortClusters order from the class orders (kp_kernels.h)
+    k.cok = orders ? bt->d_cok : nullptr;
+    if (!e->slow_order) k.ord = nullptr;
+    SelectExtra sxs = with_args(k, s3);
+    sxs.grid = (int)std::min<uint32_t>((uint32_t)bt->slow_grid, nslow);
+    KPROF(s3, "k_slow", 0, 0,
+          dev::select(s3, SEL_LAUNCH_SLOW, k,
+                      kRedBytes + 512 + 4 * (size_t)(((s->Cp + 31) >> 5) + 4) + sx.lds_area + sx.lds_sort,
+                      bt->slow_cap, sxs));
   }
   HIPCHK(dev::event_record(e->ev[9], s3));
   HIPCHK(dev::stream_wait(st, e->ev[8]));

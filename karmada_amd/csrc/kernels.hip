@@ -575,7 +575,10 @@ int filter(stream_t st, const SnapView& s, const BatchView& bv, uint64_t* fmask)
 }
 
 // one workgroup per list entry, or over a device-appended list a persistent grid
-static int spread_grid(const KArgs& a) { return a.n_dev ? std::min(a.n, 256 * 4) : a.n; }
+static int spread_grid(const KArgs& a, const SelectExtra& x) {
+  const int g = a.n_dev ? std::min(a.n, 256 * 4) : a.n;
+  return a.n_dev && x.list_grid > 0 ? std::min(g, x.list_grid) : g;
+}
 
 int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const SelectExtra& x) {
   if (a.n <= 0) return 0;
@@ -585,7 +588,8 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
   switch (which) {
     case SEL_LAUNCH_ALL: {
       // a device-appended list: a persistent grid of a few workgroups per CU
-      const int g = a.n_dev ? std::min(a.n, 256 * 4) : a.n;
+      int g = a.n_dev ? std::min(a.n, 256 * 4) : a.n;
+      if (a.n_dev && x.list_grid > 0) g = std::min(g, x.list_grid);
       if (smem > kLdsPerCu / 2 && !getenv("KP_SEL_THREADS"))  // one workgroup per CU: go wide
         hipLaunchKernelGGL(k_select_all_wide, dim3(g), dim3(1024), smem, h, a);
       else
@@ -593,26 +597,28 @@ int select(stream_t st, int which, const KArgs& a, size_t smem, int cap, const S
       break;
     }
     case SEL_LAUNCH_ALL_STREAM:
-      hipLaunchKernelGGL(k_select_all_stream, dim3(a.n_dev ? std::min(a.n, 256 * 8) : a.n), dim3(KP_STREAM_THREADS),
+      hipLaunchKernelGGL(k_select_all_stream,
+                         dim3(a.n_dev ? std::min(std::min(a.n, 256 * 8), x.list_grid > 0 ? x.list_grid : a.n) : a.n),
+                         dim3(KP_STREAM_THREADS),
                          smem, h, pa);
       break;
     case SEL_LAUNCH_CLUSTER:
       if (smem > kLdsPerCu / 2)
-        hipLaunchKernelGGL(k_select_cluster_wide, dim3(spread_grid(a)), dim3(512), smem, h, pa, cap);
+        hipLaunchKernelGGL(k_select_cluster_wide, dim3(spread_grid(a, x)), dim3(512), smem, h, pa, cap);
       else
-        hipLaunchKernelGGL(k_select_cluster, dim3(spread_grid(a)), dim3(256), smem, h, pa, cap);
+        hipLaunchKernelGGL(k_select_cluster, dim3(spread_grid(a, x)), dim3(256), smem, h, pa, cap);
       break;
     case SEL_LAUNCH_REGION_A:
       if (smem > kLdsPerCu / 2)
-        hipLaunchKernelGGL(k_region_a_wide, dim3(spread_grid(a)), dim3(512), smem, h, pa, x.rout, x.rstat);
+        hipLaunchKernelGGL(k_region_a_wide, dim3(spread_grid(a, x)), dim3(512), smem, h, pa, x.rout, x.rstat);
       else
-        hipLaunchKernelGGL(k_region_a, dim3(spread_grid(a)), dim3(256), smem, h, pa, x.rout, x.rstat);
+        hipLaunchKernelGGL(k_region_a, dim3(spread_grid(a, x)), dim3(256), smem, h, pa, x.rout, x.rstat);
       break;
     case SEL_LAUNCH_REGION_B:
       if (smem > kLdsPerCu / 2)
-        hipLaunchKernelGGL(k_region_b_wide, dim3(spread_grid(a)), dim3(512), smem, h, pa, x.rsel, x.rnsel, x.rout, cap);
+        hipLaunchKernelGGL(k_region_b_wide, dim3(spread_grid(a, x)), dim3(512), smem, h, pa, x.rsel, x.rnsel, x.rout, cap);
       else
-        hipLaunchKernelGGL(k_region_b, dim3(spread_grid(a)), dim3(256), smem, h, pa, x.rsel, x.rnsel, x.rout, cap);
+        hipLaunchKernelGGL(k_region_b, dim3(spread_grid(a, x)), dim3(256), smem, h, pa, x.rsel, x.rnsel, x.rout, cap);
       break;
     case SEL_LAUNCH_SLOW:
       if (smem > 65536 &&

@@ -54,6 +54,8 @@ struct SelectExtra {
   unsigned char* scratch = nullptr;  // slow path global scratch
   size_t slot_bytes = 0;
   int grid = 0;                      // slow path persistent grid
+  int list_grid = 0;                 // > 0: caps the grid of a launch over a device-appended list
+                                     // (its count read back by the host: no idle workgroups)
   int lds_area = 0;                  // slow path: LDS bytes for the small serial problems
   int lds_sort = 0;                  // slow path: LDS bytes for the candidate sorts (0: global slot)
   // the launch's KArgs in device memory: the kernels whose bodies keep pointers into
