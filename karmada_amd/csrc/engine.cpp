@@ -310,8 +310,10 @@ struct kp_engine {
   bool slow_order = true;   // k_slow orders candidates from the class orders (KP_SLOW_ORDER=0: sorts)
   // with a region chain (whose host steps synchronise anyway) the fallback kernels over
   // device-appended lists are launched only after their counts are read back, so none runs
-  // with an empty list (KP_GATE_FB=0: always launched, each workgroup reading the count)
-  bool gate_fb = true;
+  // with an empty list (KP_GATE_FB=0: always launched, each workgroup reading the count;
+  // 2: only the SEL_ALL and cluster-spread fallbacks, at k_slow's existing count read,
+  // not the region fallbacks, whose reads add two host waits to the region chain)
+  int gate_fb = 1;
   bool top_wg = false;      // large-subset bindings on k_select_top_wg (KP_TOP_WG=1; measured slower)
   // per-kernel timing of kp_schedule_batch (kp_engine_set_profile): an event pair
   // around every launch on its own stream, folded by kernel name after the batch
@@ -2006,7 +2008,7 @@ int kp_engine_create(int device, kp_engine** out) {
   if (const char* v = getenv("KP_TOP")) e->top_on = atoi(v) != 0;
   if (const char* v = getenv("KP_TOP_SPLIT")) e->top_split = atoi(v) != 0;
   if (const char* v = getenv("KP_SLOW_ORDER")) e->slow_order = atoi(v) != 0;
-  if (const char* v = getenv("KP_GATE_FB")) e->gate_fb = atoi(v) != 0;
+  if (const char* v = getenv("KP_GATE_FB")) e->gate_fb = atoi(v);
   if (const char* v = getenv("KP_TOP_WG")) e->top_wg = atoi(v) != 0;
   if (const char* v = getenv("KP_TOP_CAP")) {  // (tests: one capacity for both slices)
     e->top_cap = std::max(64, std::min(1024, atoi(v) & ~63));
@@ -3554,7 +3556,8 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   // counts are read back where the host synchronises anyway (the region chain, k_slow's
   // count), so a list left empty launches nothing; the SEL_ALL and cluster-spread
   // fallbacks move to stream3 after that read, before k_slow.
-  const bool gate = e->gate_fb && !bt->l_region.empty();
+  const bool gate = e->gate_fb != 0 && !bt->l_region.empty();
+  const bool gate_region = gate && e->gate_fb == 1;
   bool defer_all = false, defer_all_stream = false, defer_cl = false;
   KArgs f_def{}, cl_def{};
   if (!bt->l_all.empty()) {
@@ -3711,13 +3714,13 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       kf.sub = bt->d_fba;
       kf.n_dev = bt->stats + 14;
       uint32_t nfa = 1;
-      if (gate) {  // (the grid is then sized by the count: spread_grid)
+      if (gate_region) {  // (the grid is then sized by the count: spread_grid)
         HIPCHK(dev::d2h(&nfa, bt->stats + 14, 4, st));
         HIPCHK(dev::sync(st));
       }
       if (nfa > 0) {  // (the argument slot is copied before the launch is timed)
         SelectExtra sxa4 = with_args(kf, st);
-        if (gate) sxa4.list_grid = (int)nfa;
+        if (gate_region) sxa4.list_grid = (int)nfa;
         KPROF(st, sel_name(SEL_LAUNCH_REGION_A, smem_region_a(s)), 0, 14,
               dev::select(st, SEL_LAUNCH_REGION_A, kf, smem_region_a(s), cap, sxa4));
       }
@@ -3790,13 +3793,13 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       k.n_dev = bt->stats + 13;
     }
     uint32_t nfb = 1;
-    if (gate && k.n_dev) {
+    if (gate_region && k.n_dev) {
       HIPCHK(dev::d2h(&nfb, bt->stats + 13, 4, st));
       HIPCHK(dev::sync(st));
     }
     if (nfb > 0) {  // (the argument slot is copied before the launch is timed)
       SelectExtra sxa6 = with_args(k, st);
-      if (gate && k.n_dev) sxa6.list_grid = (int)nfb;
+      if (gate_region && k.n_dev) sxa6.list_grid = (int)nfb;
       KPROF(st, sel_name(SEL_LAUNCH_REGION_B, smem_region_b(s, cap)), k.n_dev ? 0 : k.n, k.n_dev ? 13 : -1,
             dev::select(st, SEL_LAUNCH_REGION_B, k, smem_region_b(s, cap), cap, sxa6));
     }

@@ -316,6 +316,26 @@ extern "C" __global__ void __launch_bounds__(1024) k_select_all_wide(KArgs a)
       })
 KP_SPREAD_KERNELS(, 256, 3, KP_IMPL5, KP_IMPL10, KP_IMPL12)
 KP_SPREAD_KERNELS(_wide, 512, 4, KP_IMPL9, KP_IMPL11, KP_IMPL13)
+// The same with each thread's DFS arrays in LDS (GroupsLds, R planes), 64 threads per
+// workgroup: the private arrays (2.3 KB per thread) lived in scratch.
+constexpr int kGroupsLdsThreads = 64;
+extern "C" __global__ void __launch_bounds__(kGroupsLdsThreads) k_region_groups_lds(
+    const RegionOut* rout, const int32_t* rstat, const BindHdr* hdr, const int32_t* list, int n, int R, int32_t* rsel,
+    int32_t* rnsel, uint32_t* nhost)
+#if KP_K(6)
+{
+  KP_SMEM;
+  const int j = (int)(blockIdx.x * kGroupsLdsThreads + threadIdx.x);
+  if (j >= n) return;
+  GroupsLds m{(int32_t*)smem + threadIdx.x,
+              (int64_t*)(smem + (size_t)7 * R * kGroupsLdsThreads * 4) + threadIdx.x, R, kGroupsLdsThreads};
+  const int32_t k = region_groups_one_lds(m, rout + (size_t)j * R, rstat[j], hdr[list[j]], R, rsel + (size_t)j * R);
+  if (k == kGroupsHost) atomicAdd(nhost, 1u);
+  rnsel[j] = k;
+}
+#else
+;
+#endif
 extern "C" __global__ void __launch_bounds__(256) k_region_groups(const RegionOut* rout, const int32_t* rstat,
                                                                   const BindHdr* hdr, const int32_t* list, int n, int R,
                                                                   int32_t* rsel, int32_t* rnsel, uint32_t* nhost)
@@ -709,8 +729,13 @@ int select_static(stream_t st, const KArgs& a, size_t slice) {
 int region_groups(stream_t st, const RegionOut* rout, const int32_t* rstat, const BindHdr* hdr, const int32_t* list,
                   int n, int R, int32_t* rsel, int32_t* rnsel, uint32_t* nhost) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(k_region_groups, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)st, rout, rstat, hdr, list, n,
-                     R, rsel, rnsel, nhost);
+  const size_t lds = groups_lds_bytes(R, kGroupsLdsThreads);
+  if (R >= 1 && lds <= 65536 && !getenv("KP_GROUPS_PRIV"))
+    hipLaunchKernelGGL(k_region_groups_lds, dim3((n + kGroupsLdsThreads - 1) / kGroupsLdsThreads), dim3(kGroupsLdsThreads),
+                       lds, (hipStream_t)st, rout, rstat, hdr, list, n, R, rsel, rnsel, nhost);
+  else
+    hipLaunchKernelGGL(k_region_groups, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)st, rout, rstat, hdr, list, n,
+                       R, rsel, rnsel, nhost);
   return chk(hipGetLastError());
 }
 

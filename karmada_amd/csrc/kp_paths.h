@@ -936,28 +936,54 @@ struct RegionLds {
   unsigned long long* last;
 };
 
-KP_HD inline int32_t select_groups_dev(const RegionOut* ro, int R, int64_t minC, int64_t maxC, int64_t target,
-                                       int32_t* sel) {
-  int32_t sid[kGroupMax], sv[kGroupMax];
-  int64_t sw[kGroupMax];
+// The DFS's per-binding arrays: in private memory (GroupsPriv), or one thread's slice
+// of a workgroup's LDS (GroupsLds: k_region_groups, one thread per binding, whose
+// 2.3 KB of private arrays per thread went to scratch and moved 11x its compulsory
+// bytes at config 4). Both give the same answers (the same code over either).
+struct GroupsPriv {
+  int32_t a[7][kGroupMax];
+  int64_t b[kGroupMax];
+};
+// [7 int32 planes of G][G int64] per thread, strided by the workgroup width: entry i of
+// plane k of thread t at (k * G + i) * nth + t (consecutive threads, consecutive banks).
+struct GroupsLds {
+  int32_t* p32;  // (already offset by the thread)
+  int64_t* p64;
+  int G, nth;
+};
+KP_HD inline size_t groups_lds_bytes(int G, int nth) { return (size_t)nth * (size_t)G * (7 * 4 + 8); }
+KP_HD inline int32_t& garr(GroupsPriv& m, int k, int i) { return m.a[k][i]; }
+KP_HD inline int64_t& garr64(GroupsPriv& m, int i) { return m.b[i]; }
+KP_HD inline int32_t& garr(GroupsLds& m, int k, int i) { return m.p32[((size_t)k * m.G + i) * m.nth]; }
+KP_HD inline int64_t& garr64(GroupsLds& m, int i) { return m.p64[(size_t)i * m.nth]; }
+template <class M>
+KP_HD inline int32_t select_groups_in(M& m, const RegionOut* ro, int R, int64_t minC, int64_t maxC, int64_t target,
+                                      int32_t* sel) {
+#define sid(i) garr(m, 0, (i))
+#define sv(i) garr(m, 1, (i))
+#define st(i) garr(m, 2, (i))
+#define nx(i) garr(m, 3, (i))
+#define best(i) garr(m, 4, (i))
+#define w(i) garr(m, 5, (i))
+#define idx(i) garr(m, 6, (i))
+#define sw(i) garr64(m, (i))
   int n = 0;
   for (int r = 0; r < R; r++)
     if (ro[r].count > 0) {
       int j = n++;  // insertion by (value asc, weight desc, id asc) (select_groups.go:140-151)
-      while (j > 0 && (sv[j - 1] > ro[r].count || (sv[j - 1] == ro[r].count && sw[j - 1] < ro[r].score))) {
-        sid[j] = sid[j - 1];
-        sv[j] = sv[j - 1];
-        sw[j] = sw[j - 1];
+      while (j > 0 && (sv(j - 1) > ro[r].count || (sv(j - 1) == ro[r].count && sw(j - 1) < ro[r].score))) {
+        sid(j) = sid(j - 1);
+        sv(j) = sv(j - 1);
+        sw(j) = sw(j - 1);
         j--;
       }
-      sid[j] = r;
-      sv[j] = ro[r].count;
-      sw[j] = ro[r].score;
+      sid(j) = r;
+      sv(j) = ro[r].count;
+      sw(j) = ro[r].score;
     }
   if ((int64_t)n < minC) return -KP_ERR_REGION_MIN_GROUPS;  // select_clusters_by_region.go:30-32
   if (n == 0) return -KP_ERR_REGION_CLUSTER_MIN;
   // ---- pass 1: DFS (findFeasiblePaths), best path by (weight desc, value desc, id asc)
-  int32_t st[kGroupMax], nx[kGroupMax], best[kGroupMax];
   int depth = 0, bl = -1;
   int64_t sum = 0, wsum = 0, bw = 0, bv = 0, nodes = 0;
   const bool nobt = (int64_t)n == minC;  // select_groups.go:179-182: no backtracking
@@ -970,17 +996,17 @@ KP_HD inline int32_t select_groups_dev(const RegionOut* ro, int R, int64_t minC,
         bl = depth;
         bw = wsum;
         bv = sum;
-        for (int k = 0; k < depth; k++) best[k] = st[k];
+        for (int k = 0; k < depth; k++) best(k) = st(k);
       }
     } else if (depth < maxC) {
-      nx[depth] = depth == 0 ? 0 : st[depth - 1] + 1;
-      down = nx[depth] < n;
+      nx(depth) = depth == 0 ? 0 : st(depth - 1) + 1;
+      down = nx(depth) < n;
     }
     if (down) {
-      const int i = nx[depth];
-      st[depth] = i;
-      sum += sv[i];
-      wsum += sw[i];
+      const int i = nx(depth);
+      st(depth) = i;
+      sum += sv(i);
+      wsum += sw(i);
       depth++;
       continue;
     }
@@ -989,14 +1015,14 @@ KP_HD inline int32_t select_groups_dev(const RegionOut* ro, int R, int64_t minC,
     while (depth > 0) {
       depth--;
       if (nobt) break;
-      const int i = st[depth];
-      sum -= sv[i];
-      wsum -= sw[i];
-      nx[depth] = i + 1;
-      if (nx[depth] < n) {
-        st[depth] = nx[depth];
-        sum += sv[st[depth]];
-        wsum += sw[st[depth]];
+      const int i = st(depth);
+      sum -= sv(i);
+      wsum -= sw(i);
+      nx(depth) = i + 1;
+      if (nx(depth) < n) {
+        st(depth) = nx(depth);
+        sum += sv(st(depth));
+        wsum += sw(st(depth));
         depth++;
         more = true;
         break;
@@ -1006,15 +1032,14 @@ KP_HD inline int32_t select_groups_dev(const RegionOut* ro, int R, int64_t minC,
   }
   if (bl < 0) return -KP_ERR_REGION_CLUSTER_MIN;  // no feasible path (select_clusters_by_region.go:37-39)
   // ---- best path in weight order (sortGroups: weight desc, name asc; ids are name ranks)
-  int32_t w[kGroupMax];
   for (int k = 0; k < bl; k++) {
     int j = k;
-    const int32_t g = best[k];
-    while (j > 0 && (sw[w[j - 1]] < sw[g] || (sw[w[j - 1]] == sw[g] && sid[w[j - 1]] > sid[g]))) {
-      w[j] = w[j - 1];
+    const int32_t g = best(k);
+    while (j > 0 && (sw(w(j - 1)) < sw(g) || (sw(w(j - 1)) == sw(g) && sid(w(j - 1)) > sid(g)))) {
+      w(j) = w(j - 1);
       j--;
     }
-    w[j] = g;
+    w(j) = g;
   }
   // ---- prioritizePaths: walk to the first later subpath while one exists
   int fl = bl;
@@ -1024,26 +1049,25 @@ KP_HD inline int32_t select_groups_dev(const RegionOut* ro, int R, int64_t minC,
     int64_t pw = 0, pv = 0;
     int64_t qw = 0, qv = 0;
     for (int j = 1; j < fl; j++) {
-      qw += sw[w[j - 1]];
-      qv += sv[w[j - 1]];
+      qw += sw(w(j - 1));
+      qv += sv(w(j - 1));
       if (qw > fw || !(qv >= target && j >= minC && j <= maxC)) continue;
       // visited by the DFS: no proper prefix in index order is feasible (nor the
       // root); without backtracking only the chain 0,1,2,.. is visited
-      int32_t idx[kGroupMax];
       for (int k = 0; k < j; k++) {
-        int m = k;
-        while (m > 0 && idx[m - 1] > w[k]) {
-          idx[m] = idx[m - 1];
-          m--;
+        int q = k;
+        while (q > 0 && idx(q - 1) > w(k)) {
+          idx(q) = idx(q - 1);
+          q--;
         }
-        idx[m] = w[k];
+        idx(q) = w(k);
       }
       bool visited = !(0 >= target && 0 >= minC && 0 <= maxC);  // the root returns when feasible
       int64_t ps = 0;
       for (int k = 0; k < j && visited; k++) {
-        if (nobt && idx[k] != k) visited = false;
+        if (nobt && idx(k) != k) visited = false;
         if (k > 0 && ps >= target && k >= minC && k <= maxC) visited = false;
-        ps += sv[idx[k]];
+        ps += sv(idx(k));
       }
       if (!visited) continue;
       if (pick < 0 || qw > pw || (qw == pw && qv > pv)) {
@@ -1057,9 +1081,23 @@ KP_HD inline int32_t select_groups_dev(const RegionOut* ro, int R, int64_t minC,
     fw = pw;
   }
   if (fl == 0) return -KP_ERR_REGION_CLUSTER_MIN;  // the empty root path
-  for (int k = 0; k < fl; k++) sel[k] = sid[w[k]];
+  for (int k = 0; k < fl; k++) sel[k] = sid(w(k));
   return fl;
+#undef sid
+#undef sv
+#undef st
+#undef nx
+#undef best
+#undef w
+#undef idx
+#undef sw
 }
+KP_HD inline int32_t select_groups_dev(const RegionOut* ro, int R, int64_t minC, int64_t maxC, int64_t target,
+                                       int32_t* sel) {
+  GroupsPriv m;
+  return select_groups_in(m, ro, R, minC, maxC, target, sel);
+}
+
 
 // The group-combination step of one region binding (the host step it replaces:
 // engine.cpp kp_schedule_batch). rstat != 0: stage A already finalized it.
@@ -1067,6 +1105,13 @@ KP_HD inline int32_t region_groups_one(const RegionOut* ro, int32_t rstat, const
   if (rstat != 0) return -1000;
   for (int r = 0; r < R; r++) sel[r] = -1;
   return select_groups_dev(ro, R, h.region_min, h.region_max, h.cluster_min, sel);
+}
+// ... with the DFS arrays in the thread's LDS slice (k_region_groups_lds; G = R planes)
+KP_HD inline int32_t region_groups_one_lds(GroupsLds& m, const RegionOut* ro, int32_t rstat, const BindHdr& h, int R,
+                                           int32_t* sel) {
+  if (rstat != 0) return -1000;
+  for (int r = 0; r < R; r++) sel[r] = -1;
+  return select_groups_in(m, ro, R, h.region_min, h.region_max, h.cluster_min, sel);
 }
 KP_HD inline int64_t go_ceil_div_i64(int32_t a, int64_t b) {
   double q = kp_ceil((double)a / (double)b);

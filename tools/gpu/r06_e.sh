@@ -8,3 +8,4 @@ for G in 1 0; do
   KP_GATE_FB=$G $S 300 e_c4_g$G.json python -u bench.py --config 4 --steps 200 --no-cpu --check 300 --e2e-reps 0 || exit $?
   KP_GATE_FB=$G $S 400 e_c5_g$G.json python -u bench.py --config 5 --steps 10 --warmup 2 --no-cpu --check 300 --e2e-reps 0 || exit $?
 done
+bash tools/gpu/prof_pmc.sh r06c4 --config 4
