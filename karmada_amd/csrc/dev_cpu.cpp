@@ -136,14 +136,15 @@ int pair(stream_t, const SnapView& s, const BatchView& bv, const int32_t* list, 
 }
 
 int est_class(stream_t, const SnapView& s, const BatchView& bv, const int32_t* rep, int n_rows, int32_t* rows,
-              int fast) {
-  grid(n_rows, 4 * kTmplDense, [&](int k, unsigned char* sm) {
+              int fast, const int32_t* klist, const uint64_t* fmask) {
+  grid(n_rows, 4 * kTmplDense + (fmask ? 4 * (size_t)s.Cp : 0), [&](int i, unsigned char* sm) {
     const CpuBlk B{(int64_t*)sm};
+    const int k = klist ? klist[i] : i;
     switch (fast) {
-      case EST_MIXED: body_est_class<EST_MIXED>(B, k, sm, s, bv, rep, rows); break;
-      case EST_SUMMARY: body_est_class<EST_SUMMARY>(B, k, sm, s, bv, rep, rows); break;
-      case EST_MODEL8: body_est_class<EST_MODEL8>(B, k, sm, s, bv, rep, rows); break;
-      case EST_MODEL16: body_est_class<EST_MODEL16>(B, k, sm, s, bv, rep, rows); break;
+      case EST_MIXED: body_est_class<EST_MIXED>(B, k, sm, s, bv, rep, rows, fmask); break;
+      case EST_SUMMARY: body_est_class<EST_SUMMARY>(B, k, sm, s, bv, rep, rows, fmask); break;
+      case EST_MODEL8: body_est_class<EST_MODEL8>(B, k, sm, s, bv, rep, rows, fmask); break;
+      case EST_MODEL16: body_est_class<EST_MODEL16>(B, k, sm, s, bv, rep, rows, fmask); break;
       default: break;
     }
   });

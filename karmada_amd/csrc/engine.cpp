@@ -385,6 +385,12 @@ struct kp_batch {
   // a representative binding per class; their raw GeneralEstimator rows [n][Cp]
   std::vector<int32_t> bcls, crep;
   int32_t *d_bcls = nullptr, *d_crep = nullptr, *cls_rows = nullptr;
+  // Estimator classes serving one binding, in a batch without class orders (est_single):
+  // their rows hold only that binding's feasible clusters, written after k_filter
+  // (k_est_class over l_cls_single with the feasibility rows); l_cls_full: the others.
+  bool est_single = false;
+  std::vector<int32_t> l_cls_full, l_cls_single;
+  int32_t *d_cls_full = nullptr, *d_cls_single = nullptr;
   // component-set classes (BF_SETS): class id and resolved component list of each;
   // their rows are MaxAvailableComponentSets per cluster (k_sets_rows), and in the
   // pair-row mode the BF_SETS bindings' rows are rebuilt from them (k_rows_from_class)
@@ -3200,7 +3206,25 @@ static int batch_create_impl(kp_engine* e, const kp_snapshot* sc, const kp_bindi
     a.add(&bt->d_fb, std::max(1, bt->n_all_dyn));
     a.add(&bt->d_ofb, std::max(1, bt->n_all_dyn));
   }
-  if (s->C <= 16384 && !bt->crep.empty() && orders_pay && kRedBytes + 8 * (size_t)P <= e->max_lds) {
+  const bool with_orders = s->C <= 16384 && !bt->crep.empty() && orders_pay && kRedBytes + 8 * (size_t)P <= e->max_lds;
+  // singleton classes: feasible entries only, when every reader gathers feasible candidates
+  // (no class orders, which sort whole rows; no spread lists; no component-set classes)
+  static const bool est_single_on = [] {
+    const char* v = getenv("KP_EST_SINGLE");
+    return !v || atoi(v) != 0;
+  }();
+  if (est_single_on && !with_orders && bt->crep.size() > 1 && bt->l_cluster.empty() && bt->l_region.empty() &&
+      bt->sets_cls.empty()) {
+    std::vector<int32_t> cnt(bt->crep.size(), 0);
+    for (uint64_t i = 0; i < n; i++) cnt[(size_t)std::max(0, bt->bcls[i])]++;
+    for (size_t g = 0; g < bt->crep.size(); g++) (g > 0 && cnt[g] == 1 ? bt->l_cls_single : bt->l_cls_full).push_back((int32_t)g);
+    bt->est_single = !bt->l_cls_single.empty();
+    if (bt->est_single) {
+      a.add(&bt->d_cls_full, bt->l_cls_full.size());
+      a.add(&bt->d_cls_single, bt->l_cls_single.size());
+    }
+  }
+  if (with_orders) {
     a.add(&bt->d_ord, bt->crep.size() * (size_t)s->Cp);
     a.add(&bt->d_ctot, bt->crep.size());
     a.add(&bt->d_cok, bt->crep.size());
@@ -3256,6 +3280,10 @@ static int batch_create_impl(kp_engine* e, const kp_snapshot* sc, const kp_bindi
     HIPCHK(up(bt->d_sets_args, bt->sets_args.data(), sizeof(SetsArgs) * bt->sets_args.size()));
     HIPCHK(up(bt->d_sets_off, sets_off.data(), 8 * sets_off.size()));
     HIPCHK(up(bt->d_sets_list, bt->l_sets.data(), 4 * bt->l_sets.size()));
+  }
+  if (bt->est_single) {
+    HIPCHK(up(bt->d_cls_full, bt->l_cls_full.data(), 4 * bt->l_cls_full.size()));
+    HIPCHK(up(bt->d_cls_single, bt->l_cls_single.data(), 4 * bt->l_cls_single.size()));
   }
   HIPCHK(up(bt->d_all, bt->l_all.data(), 4 * bt->l_all.size()));
   HIPCHK(up(bt->d_cluster, bt->l_cluster.data(), 4 * bt->l_cluster.size()));
@@ -3383,6 +3411,15 @@ static const char* pair_name(int fast) {
   }
   return "k_pair";
 }
+static const char* est_class_feasible_name(int fast) {
+  switch (fast) {
+    case EST_SUMMARY: return "k_est_class_summary (feasible)";
+    case EST_MODEL8: return "k_est_class_m8 (feasible)";
+    case EST_MODEL16: return "k_est_class_m16 (feasible)";
+    default: break;
+  }
+  return "k_est_class (feasible)";
+}
 static const char* est_class_name(int fast) {
   switch (fast) {
     case EST_SUMMARY: return "k_est_class_summary";
@@ -3494,11 +3531,17 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     return KP_OK;
   };
   if (bits) {
-    KPROF(sp, est_class_name(fast), bt->crep.size(), -1,
-          dev::est_class(sp, s->view, bt->view, bt->d_crep, (int)bt->crep.size(), bt->cls_rows, fast));
+    const bool single = bt->est_single;
+    const int n_full = single ? (int)bt->l_cls_full.size() : (int)bt->crep.size();
+    KPROF(sp, est_class_name(fast), n_full, -1,
+          dev::est_class(sp, s->view, bt->view, bt->d_crep, n_full, bt->cls_rows, fast, single ? bt->d_cls_full : nullptr));
     if (int rc = sets_rows()) return rc;
     HIPCHK(dev::event_record(e->ev[5], sp));  // every class row is written (k_class_order's input)
     KPROF(sp, "k_filter", B, -1, dev::filter(sp, s->view, bt->view, bt->fmask));
+    if (single)  // the singleton classes' feasible entries, from the feasibility rows
+      KPROF(sp, est_class_feasible_name(fast), bt->l_cls_single.size(), -1,
+            dev::est_class(sp, s->view, bt->view, bt->d_crep, (int)bt->l_cls_single.size(), bt->cls_rows, fast,
+                           bt->d_cls_single, bt->fmask));
   } else {
     KPROF(sp, pair_name(fast), B, -1,
           dev::pair(sp, s->view, bt->view, nullptr, 0, B, bt->fmask, bt->est, nullptr, 0, md_cap, smem_pair(s, md_cap),

@@ -109,10 +109,12 @@ KP_PAIR_FAST(k_pair_fast_m16, EST_MODEL16)
 // Estimator-class rows (kp_filter.h), one instance per estimator kind.
 #define KP_EST_CLASS(NAME, KIND)                                                                              \
   extern "C" __global__ void __launch_bounds__(kBlock) NAME(SnapView s, BatchView bv, const int32_t* rep,      \
-                                                             int32_t* rows)                                   \
+                                                             int32_t* rows, const int32_t* klist,             \
+                                                             const uint64_t* fmask)                           \
       KP_IMPL1({                                                                                              \
         KP_SMEM;                                                                                              \
-        body_est_class<KIND>(GpuBlk{(int64_t*)smem}, (int)blockIdx.x, smem, s, bv, rep, rows);                \
+        const int k = klist ? klist[blockIdx.x] : (int)blockIdx.x;                                            \
+        body_est_class<KIND>(GpuBlk{(int64_t*)smem}, k, smem, s, bv, rep, rows, fmask);                       \
       })
 KP_EST_CLASS(k_est_class, EST_MIXED)
 KP_EST_CLASS(k_est_class_summary, EST_SUMMARY)
@@ -575,7 +577,7 @@ int pair(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* lis
 }
 
 int est_class(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* rep, int n_rows, int32_t* rows,
-              int fast) {
+              int fast, const int32_t* klist, const uint64_t* fmask) {
   if (n_rows <= 0) return 0;
   auto* k = fast == EST_MIXED     ? k_est_class
             : fast == EST_SUMMARY ? k_est_class_summary
@@ -583,7 +585,12 @@ int est_class(stream_t st, const SnapView& s, const BatchView& bv, const int32_t
             : fast == EST_MODEL16 ? k_est_class_m16
                                   : nullptr;
   if (!k) return chk(hipErrorInvalidValue);
-  hipLaunchKernelGGL(k, dim3(n_rows), dim3(kBlock), kRedBytes + 4 * kTmplDense, (hipStream_t)st, s, bv, rep, rows);
+  // (the feasible mode compacts the representative's feasible clusters into LDS)
+  const size_t smem = kRedBytes + 4 * kTmplDense + (fmask ? 4 * (size_t)s.Cp : 0);
+  if (smem > 65536 &&
+      chk(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)))
+    return -1;
+  hipLaunchKernelGGL(k, dim3(n_rows), dim3(kBlock), smem, (hipStream_t)st, s, bv, rep, rows, klist, fmask);
   return chk(hipGetLastError());
 }
 

@@ -57,10 +57,12 @@ int peer_copy(void* dst, int dst_dev, const void* src, int src_dev, size_t bytes
 // Pair rows of bindings list[b0 + i] (or b0 + i when list is null), i < nb.
 int pair(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* list, int b0, int nb, uint64_t* fmask,
          int32_t* est, int64_t* score, int est_mode, int md_cap, size_t smem, int fast = 0);
-// Estimator-class rows: rows[k][Cp] for k < n_rows (body_est_class; row 0 MaxInt32),
-// class k's representative binding rep[k]; fast = EST_* kind (not EST_GENERIC).
+// Estimator-class rows: rows[k][Cp] for k = klist[i] (k = i when klist is null), i < n_rows
+// (body_est_class; row 0 MaxInt32), class k's representative binding rep[k]; fast = EST_*
+// kind (not EST_GENERIC). fmask set: only the entries of the representative's feasible
+// clusters (the singleton classes of a batch without class orders, after k_filter).
 int est_class(stream_t st, const SnapView& s, const BatchView& bv, const int32_t* rep, int n_rows, int32_t* rows,
-              int fast);
+              int fast, const int32_t* klist = nullptr, const uint64_t* fmask = nullptr);
 // Feasibility rows fmask[b][W] of every binding by bitset algebra (body_filter;
 // requires s.n_bits > 0).
 int filter(stream_t st, const SnapView& s, const BatchView& bv, uint64_t* fmask);

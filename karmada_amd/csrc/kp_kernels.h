@@ -259,9 +259,12 @@ KP_FI void pair_one(const BLK& B, int b, unsigned char* smem, const SnapView& s,
 // (est_compute_bf, the pair kernel's arithmetic) for every cluster, from the
 // class's representative binding rep[k]; row 0 (non-workload bindings, whose
 // calAvailableReplicas is MaxInt32, core/util.go:69-73) is MaxInt32.
+// fmask set (a class serving one binding, in a batch without class orders): only the
+// entries of that binding's feasible clusters, the only ones any select kernel reads
+// (they gather feasible candidates; at config 10 the full rows were 2 GB of writes).
 template <int Fast, class BLK>
 KP_FI void body_est_class(const BLK& B, int k, unsigned char* smem, const SnapView& s, const BatchView& bv,
-                          const int32_t* rep, int32_t* rows) {
+                          const int32_t* rep, int32_t* rows, const uint64_t* fmask = nullptr) {
   int32_t* row = rows + (size_t)k * s.Cp;
   if (k == 0) {
     for (int c = B.tid(); c < s.Cp; c += B.nth()) row[c] = kInt32Max;
@@ -274,6 +277,28 @@ KP_FI void body_est_class(const BLK& B, int k, unsigned char* smem, const SnapVi
   for (int t = B.tid(); t < kTmplDense; t += B.nth()) md[t] = rr && t < s.n_tmpl ? template_md(s, bv, h, t) : 0;
   B.sync();
   const MdTab mdt = md_regs(md);
+  if (fmask) {
+    // the feasible clusters compacted into LDS first (one word per thread per pass, a
+    // scan of the popcounts), so the lanes compute dense instead of idling on the
+    // infeasible ~2/3 of a row
+    const uint64_t* fr = fmask + (size_t)rep[k] * s.W;
+    int32_t* list = md + kTmplDense;
+    int F = 0;
+    for (int w0 = 0; w0 < s.W; w0 += B.nth()) {
+      const int w = w0 + B.tid();
+      const uint64_t m = w < s.W ? fr[w] : 0ull;
+      int32_t tot;
+      int32_t pos = F + B.excl_scan(popc64(m), &tot);
+      for (uint64_t q = m; q; q &= q - 1) list[pos++] = 64 * w + __builtin_ctzll(q);
+      F += tot;
+    }
+    B.sync();
+    for (int i = B.tid(); i < F; i += B.nth()) {
+      const int c = list[i];
+      row[c] = est_compute_bf<Fast>(s, bv, h, c, mdt.v, est_load<Fast>(s, bv, h, c, ldcol(s.flags, c)));
+    }
+    return;
+  }
   for (int c = B.tid(); c < s.Cp; c += B.nth())
     row[c] = est_compute_bf<Fast>(s, bv, h, c, mdt.v, est_load<Fast>(s, bv, h, c, ldcol(s.flags, c)));
 }

@@ -615,7 +615,13 @@ KP_FI int divide_par(const BLK& B, const SelCtx& x, const CS& cs, int32_t target
         pv = v;
       });
       const int64_t V = pre && st != ST_AGGREGATED ? pre->vtot : B.sum64(party ? pv : 0);
-      w = webster_reg(B, party, prk, pv, target, desc, V, &reg_ok);
+      KP_STAMP(x, 56);  // (stamps build: [56] the party pass, [57] webster_reg, [4] webster_par after a refusal)
+      int nsteps = 0;
+      w = webster_reg(B, party, prk, pv, target, desc, V, &reg_ok, &nsteps);
+      KP_STAMP(x, 57);
+      KP_COUNT(x, 58, nsteps);
+      KP_COUNT(x, 59, 1);
+      KP_COUNT(x, 60, reg_ok ? 0 : 1);
       if (!reg_ok) w = webster_par(B, parties, target, desc, ss, nullptr);
     }
   }

@@ -854,6 +854,9 @@ KP_FI WebRes webster_tail(const BLK& B, WebRes r, Parties parties, double tstar,
 }
 
 KP_HD inline uint32_t* web_ctr(const SelScratch& sc) { return (uint32_t*)sc.whist + 511; }  // party list fill counter
+template <class BLK>
+KP_FI WebRes webster_reg(const BLK& B, bool party, uint32_t rk, int64_t v, int32_t N, bool desc, int64_t V, bool* ok,
+                         int* nsteps = nullptr);
 template <class BLK, class Parties>
 KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc, const SelScratch& sc,
                          const WebPre* pre = nullptr) {
@@ -954,7 +957,22 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   // largest next ones (prio(v, s)), one block-wide min or max per step. Parties
   // below Lb hold no priority >= t* (t* >= the N-th largest vote >= Lb, or Lb = 1),
   // so the list decides t*. The held counts live in buf[0, np) until webster_tail.
-  if (compact && np > 0 && np <= ecap) {
+  // One wave (k_select_top's subsets past 64 candidates): the list holds one party per lane,
+  // so webster_reg runs the same adjustment in registers (the winner alone recomputes its
+  // priority; no pass over the list per step) and the same tie selection.
+  if (B.nwaves() == 1 && compact && np > 0 && np <= ecap && np <= B.nth()) {
+    const bool party = B.tid() < np;
+    const uint64_t e = party ? pl[B.tid()] : 0ull;
+    bool ok = false;
+    WebRes w = webster_reg(B, party, (uint32_t)(e >> 32), (int64_t)(uint32_t)e, N, desc, V, &ok);
+    if (ok) {
+      w.compact = true;
+      w.np = np;
+      w.Lb = Lb;
+      w.pl = pl;
+      return w;
+    }
+  } else if (compact && np > 0 && np <= ecap) {
     constexpr int64_t kAdjMax = 64;
     const double t0 = (double)V / (2.0 * (double)N);
     int64_t C = 0;
@@ -1109,8 +1127,8 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
 // vote total. `ok` is false (nothing decided) when the count is off by more than the
 // step bound, which the rounding argument excludes: the caller runs webster_par then.
 template <class BLK>
-KP_FI WebRes webster_reg(const BLK& B, bool party, uint32_t rk, int64_t v, int32_t N, bool desc, int64_t V,
-                         bool* ok) {
+KP_FI WebRes webster_reg(const BLK& B, bool party, uint32_t rk, int64_t v, int32_t N, bool desc, int64_t V, bool* ok,
+                         int* nsteps) {
   WebRes r;
   r.N = N;
   r.desc = desc;
@@ -1131,6 +1149,7 @@ KP_FI WebRes webster_reg(const BLK& B, bool party, uint32_t rk, int64_t v, int32
   int64_t s = party ? w_count(v, t0, capN + 1, true) : 0;
   const int64_t C = B.sum64(s);
   const int64_t steps = C >= capN ? C - capN : capN - C;
+  if (nsteps) *nsteps = (int)steps;
   if (steps > 64) {
     *ok = false;
     return r;

@@ -265,6 +265,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
     top_fallback(B, a, t, b);
     return;
   }
+  KP_STAMPD(a.dbg, 62);  // (stamps build: [62] header and eligibility, [9] the row copy)
   TopCarve tc = top_carve(smem, s, t.cap, a.dbg);
   uint64_t* frow = tc.frow;
   TopSub cd = tc.cd;
@@ -672,6 +673,7 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
       return;
     }
   }
+  KP_STAMP(x, 61);  // ([61] the walk or histogram pass, [11] the target mask)
   if (has_tgt) {
     // the mask becomes the feasible scheduled clusters (the subset's first nsched
     // entries): the division's target bits, and the only feasibility it reads
