@@ -118,7 +118,7 @@ def kernel_bytes(name, units, Cp, n_classes, n_bind, n_targets, snap_bytes, R, o
 def load_pmc(config, kernel):
     """Per-launch PMC figures of `kernel` from the committed summary (same bench
     command, default sizes): {hbm_bytes (FETCH_SIZE*2 + WRITE_SIZE), valu_insts, ...}."""
-    for rnd in ("r05", "r04", "r03", "r02"):  # the newest summary that holds the kernel
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):  # the newest summary that holds the kernel
         try:
             with open(os.path.join(ROOT, "profiles", f"{rnd}_pmc_config{config}.json")) as f:
                 k = json.load(f).get("kernels", {}).get(kernel)
@@ -590,6 +590,11 @@ def main():
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": round(pmc["hbm_bytes"] * klaunch) if pmc and pmc.get("hbm_bytes") else None,
+            # the same with FETCH_SIZE as counted (the x2 gfx950 correction holds for wide
+            # coalesced reads only; this kernel's reads are mostly 8-64 B per lane)
+            "traffic_fetch_raw": (round((pmc["fetch_bytes_x2"] / 2 + pmc["write_bytes"]) * klaunch)
+                                  if pmc and pmc.get("fetch_bytes_x2") is not None and pmc.get("write_bytes") is not None
+                                  else None),
             "kernel": kname, "kernel_ms": round(kms, 4), "algorithmic_bytes": round(kbytes),
             "dram_frac": pmc_frac("hbm_bytes", HBM_PEAK_GBS), "valu_frac": pmc_frac("valu_insts", VALU_PEAK_GINST)}
     step_bytes = pair_b + sel_b

@@ -385,6 +385,8 @@ struct kp_batch {
   // a representative binding per class; their raw GeneralEstimator rows [n][Cp]
   std::vector<int32_t> bcls, crep;
   int32_t *d_bcls = nullptr, *d_crep = nullptr, *cls_rows = nullptr;
+  int32_t* d_all_cls = nullptr;  // the estimator class of each l_all entry (KArgs::lcls)
+  std::vector<int32_t> l_all_cls;
   // Estimator classes serving one binding, in a batch without class orders (est_single):
   // their rows hold only that binding's feasible clusters, written after k_filter
   // (k_est_class over l_cls_single with the feasibility rows); l_cls_full: the others.
@@ -3164,6 +3166,7 @@ static int batch_create_impl(kp_engine* e, const kp_snapshot* sc, const kp_bindi
   a.add(&bt->d_crep, bt->crep.size());
   a.add(&bt->cls_rows, bt->crep.size() * (size_t)s->Cp);
   a.add(&bt->d_all, std::max<size_t>(1, bt->l_all.size()));
+  a.add(&bt->d_all_cls, std::max<size_t>(1, bt->l_all.size()));
   a.add(&bt->d_cluster, std::max<size_t>(1, bt->l_cluster.size()));
   a.add(&bt->d_region, std::max<size_t>(1, bt->l_region.size()));
   a.add(&bt->d_slowlist, std::max<size_t>(1, bt->l_slow.size()));
@@ -3286,6 +3289,9 @@ static int batch_create_impl(kp_engine* e, const kp_snapshot* sc, const kp_bindi
     HIPCHK(up(bt->d_cls_single, bt->l_cls_single.data(), 4 * bt->l_cls_single.size()));
   }
   HIPCHK(up(bt->d_all, bt->l_all.data(), 4 * bt->l_all.size()));
+  bt->l_all_cls.resize(bt->l_all.size());
+  for (size_t i = 0; i < bt->l_all.size(); i++) bt->l_all_cls[i] = bt->bcls[bt->l_all[i]];
+  HIPCHK(up(bt->d_all_cls, bt->l_all_cls.data(), 4 * bt->l_all_cls.size()));
   HIPCHK(up(bt->d_cluster, bt->l_cluster.data(), 4 * bt->l_cluster.size()));
   HIPCHK(up(bt->d_region, bt->l_region.data(), 4 * bt->l_region.size()));
   HIPCHK(up(bt->d_cs, bt->l_cs.data(), 4 * bt->l_cs.size()));
@@ -3632,6 +3638,7 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
         KArgs g = k;
         const int cap_p = part == 0 ? top_cap_small : (mid ? e->top_cap_mid : top_cap);
         g.list = bt->d_all + (part == 0 ? 0 : bt->n_top_small);
+        g.lcls = bt->d_all_cls + (part == 0 ? 0 : bt->n_top_small);
         g.n = part == 0 ? bt->n_top_small : bt->n_all_dyn - bt->n_top_small;
         if (g.n <= 0) continue;
         TopArgs ta{bt->d_ord, bt->d_ctot, bt->d_cok, bt->d_fb, bt->stats + 9, cap_p};

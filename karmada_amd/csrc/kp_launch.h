@@ -35,6 +35,9 @@ struct KArgs {
   // set (with n_dev): loop index j stands for list position sub[j] (a device-appended
   // fallback list of positions, so per-position arrays such as rsel stay aligned)
   const int32_t* sub = nullptr;
+  // set: the estimator class of list[i] (k_select_top loads it with the list entry, so the
+  // class order and class flags load one dependent global load earlier)
+  const int32_t* lcls = nullptr;
 };
 
 enum : int {

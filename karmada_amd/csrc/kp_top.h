@@ -163,6 +163,7 @@ KP_FI void top_fallback(const BLK& B, const KArgs& a, const TopArgs& t, int b, b
 #define KP_TOP_GROUP 4
 #endif
 constexpr int kTopAhead = KP_TOP_AHEAD, kTopGroup = KP_TOP_GROUP;
+constexpr int kTopRowRegs = 2;  // feasibility-row words preloaded per lane (C <= 8192 in full)
 constexpr int kTopStream = 8;  // row chunks per step of the no-class-order passes
 static_assert(kTopAhead % kTopGroup == 0, "the ring holds whole groups");
 
@@ -213,7 +214,18 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   if (blk >= a.n) return;
   KP_STAMP_INIT
   const int b = a.list[blk];
+  const int32_t cls = a.lcls ? a.lcls[blk] : (a.bcls ? a.bcls[b] : 0);
   const SnapView& s = a.s;
+  // the feasibility row's first kTopRowRegs words per lane, loaded with the header (the
+  // row copy below is then not one more memory latency after the eligibility checks)
+  uint64_t fw[kTopRowRegs];
+#if defined(__clang__)
+#pragma unroll
+#endif
+  for (int q = 0; q < kTopRowRegs; q++) {
+    const int w = (int)(B.tid() % B.wwidth()) + q * B.wwidth();
+    fw[q] = w < s.W ? a.fmask[(size_t)b * s.W + w] : 0ull;
+  }
   // the header as a register copy: read through a.bv.hdr, its fields would be reloaded
   // (each reload waiting on every load in flight) after every store or wave barrier
   const BindHdr hloc = a.bv.hdr[b];
@@ -225,7 +237,6 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   // them after every LDS store it cannot tell from global memory, and each reload waits
   // for every load in flight, the walk's prefetch ring included)
   const bool has_tgt = kp_uniform(h->tgt_cnt) > 0;
-  const int32_t cls = a.bcls ? a.bcls[b] : 0;
   // the first chunks of the class order, loaded with the binding's header and row (the
   // walk is the first to read them; a binding that does not walk wastes a few L2 hits)
   // (no class orders: the votes are thresholded by a histogram instead of a walk)
@@ -273,11 +284,33 @@ KP_FI void body_select_top(const BLK& B, int blk, unsigned char* smem, const KAr
   // (no target bits until the division: the walk's mask excludes the targets itself)
   SelCtx x = make_ctx(a, b, nullptr);
   x.h = h;
+  if (a.bcls) {  // (the class from the list: make_ctx's reload of bcls[b] is dead)
+    x.erow = a.est + (size_t)cls * s.Cp;
+    x.mrep = cls ? h->replicas : kInt32Max;
+  }
   int64_t F = 0;
-  for (int w = B.tid(); w < s.W; w += B.nth()) {
-    const uint64_t m = x.frow[w];
-    frow[w] = m;
-    F += popc64(m);
+  if (B.nth() == B.wwidth()) {  // (one wave: the preloaded words, then any past them)
+#if defined(__clang__)
+#pragma unroll
+#endif
+    for (int q = 0; q < kTopRowRegs; q++) {
+      const int w = B.tid() + q * B.wwidth();
+      if (w < s.W) {
+        frow[w] = fw[q];
+        F += popc64(fw[q]);
+      }
+    }
+    for (int w = B.tid() + kTopRowRegs * B.wwidth(); w < s.W; w += B.nth()) {
+      const uint64_t m = x.frow[w];
+      frow[w] = m;
+      F += popc64(m);
+    }
+  } else {
+    for (int w = B.tid(); w < s.W; w += B.nth()) {
+      const uint64_t m = x.frow[w];
+      frow[w] = m;
+      F += popc64(m);
+    }
   }
   F = B.sum64(F);  // (also orders the frow copy before the walk)
   x.frow = frow;   // every later feasibility test reads the LDS copy
