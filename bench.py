@@ -182,6 +182,17 @@ def cpu_baseline(u, opts, budget_s):
     }
 
 
+def timed_gaps(clock, n_warm, steps, cap=64):
+    """Intervals between consecutive completions inside the timed window (ms), with the
+    lane that completed; at most `cap` of them."""
+    st = clock["stamps"]
+    lo = max(0, n_warm - 1)
+    out = []
+    for i in range(lo + 1, min(len(st), n_warm + steps)):
+        out.append([round(1e3 * (st[i][0] - st[i - 1][0]), 3), st[i][1]])
+    return out[:cap]
+
+
 def parity_check(u, results, opts, n_check, seed):
     """Oracle (FAST mode) on n_check bindings sampled from the timed batch, compared
     with each given result list (status, error, multiset of targets): the serial
@@ -350,7 +361,7 @@ def main():
     # once the K-th timed step has completed
     n_warm = args.warmup * len(lanes)
     lock = threading.Lock()
-    clock = {"done": 0, "t0": None, "t1": None}
+    clock = {"done": 0, "t0": None, "t1": None, "stamps": []}
     if n_warm == 0:
         clock["t0"] = "at start"
 
@@ -366,6 +377,7 @@ def main():
                 now = time.perf_counter()  # (stamped in completion order, under the lock)
                 clock["done"] += 1
                 d = clock["done"]
+                clock["stamps"].append((now, k))
                 if d == n_warm:
                     clock["t0"] = now
                 elif d == n_warm + args.steps:
@@ -377,6 +389,12 @@ def main():
         with lock:
             st_all.extend(st)
 
+    # The lanes' batches were just packed on every CPU the process may use: under a cgroup
+    # CPU quota (16 CPUs on the GPU boxes) that burst can exhaust the current quota period,
+    # and the lane threads would then be throttled inside the short timed window. Idle for a
+    # few periods first (setup, outside the timed region).
+    if len(lanes) > 1:
+        time.sleep(float(os.environ.get("KP_BENCH_SETTLE_S", "0.3")))
     barrier_sync()
     t_start = time.perf_counter()
     if clock["t0"] == "at start":
@@ -615,6 +633,9 @@ def main():
         # the timed window: from the (warmup x inflight)-th completed step to the K-th
         # completion after it, every lane mid-stream (module docstring)
         "timed_window": {"warmup_completions": n_warm, "timed_completions": args.steps,
+                         # gaps between consecutive completions in the window (ms, lane): a
+                         # stall shows as one long gap, a uniformly slow run as even ones
+                         "gaps_ms": timed_gaps(clock, n_warm, args.steps),
                          "total_completions": clock["done"],
                          "lanes_wall_s": round(lanes_wall, 3)},
         # one batch at a time on one engine (nothing overlapped): ms per batch and the rate

@@ -319,10 +319,15 @@ int offsets(stream_t, const int32_t* status, const uint32_t* count, int n, uint6
 }
 
 int compact(stream_t, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
-            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n, const uint32_t* perm) {
+            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n, const uint32_t* perm, uint32_t* h_idx,
+            int32_t* h_rep, uint64_t h_cap) {
   int64_t red[8];
   for (int b = 0; b < n; b++)
-    body_compact(CpuBlk{red}, b, start, count, offsets, in_idx, in_rep, out_idx, out_rep, n, perm);
+    body_compact(CpuBlk{red}, b, start, count, offsets, in_idx, in_rep, out_idx, out_rep, n, perm, h_idx, h_rep, h_cap);
+  return 0;
+}
+int host_device_ptr(void* host, void** dev) {
+  *dev = host;
   return 0;
 }
 

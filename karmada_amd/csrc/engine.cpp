@@ -314,6 +314,14 @@ struct kp_engine {
   // 2: only the SEL_ALL and cluster-spread fallbacks, at k_slow's existing count read,
   // not the region fallbacks, whose reads add two host waits to the region chain)
   int gate_fb = 1;
+  // KP_ZC=1: k_compact writes the result CSR into the page-locked buffers over the bus
+  // (no copy, no size read-back); measured slower with batches in flight (its workgroups
+  // hold CUs while their stores cross the bus: 51-53 vs 71-85 M/s), so off
+  bool zc = false;
+  // KP_SPEC_COPY=1: a batch scheduled again copies its previous CSR size ahead of the
+  // total's read-back (one host round trip per call); measured no better with batches in
+  // flight (59.7-81.5 vs 69.2-88.9 M/s, same box), so off
+  bool spec_copy = false;
   bool top_wg = false;      // large-subset bindings on k_select_top_wg (KP_TOP_WG=1; measured slower)
   // per-kernel timing of kp_schedule_batch (kp_engine_set_profile): an event pair
   // around every launch on its own stream, folded by kernel name after the batch
@@ -449,6 +457,7 @@ struct kp_batch {
   uint32_t* h_cidx = nullptr;
   int32_t* h_crep = nullptr;
   uint64_t h_res_cap = 0;
+  uint64_t last_tot = 0;  // the previous call's CSR size (the speculative copy)
   size_t h_cidx_bytes = 0, h_crep_bytes = 0;  // their pooled block sizes
   // The batch's device arena and page-locked buffers go back to the process-wide
   // pools on destruction, where another batch (of any engine) may take them at
@@ -2017,6 +2026,8 @@ int kp_engine_create(int device, kp_engine** out) {
   if (const char* v = getenv("KP_TOP_SPLIT")) e->top_split = atoi(v) != 0;
   if (const char* v = getenv("KP_SLOW_ORDER")) e->slow_order = atoi(v) != 0;
   if (const char* v = getenv("KP_GATE_FB")) e->gate_fb = atoi(v);
+  if (const char* v = getenv("KP_ZC")) e->zc = atoi(v) != 0;
+  if (const char* v = getenv("KP_SPEC_COPY")) e->spec_copy = atoi(v) != 0;
   if (const char* v = getenv("KP_TOP_WG")) e->top_wg = atoi(v) != 0;
   if (const char* v = getenv("KP_TOP_CAP")) {  // (tests: one capacity for both slices)
     e->top_cap = std::max(64, std::min(1024, atoi(v) & ~63));
@@ -3915,9 +3926,23 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   // results -> host, compacted to CSR: offsets scanned and results compacted on
   // the device, then the per-binding arrays and the CSR copied back
   KPROF(st, "k_offsets", B, -1, dev::offsets(st, bt->status, bt->count, B, bt->offsets_d, bt->off_part));
+  // With page-locked result buffers from an earlier call (their capacity known before the
+  // launch), k_compact also writes the CSR straight into them over the bus (e->zc): the
+  // call then needs no host round trip for the CSR's size and no copy after it, so an
+  // engine's stream stays queued to its end (several engines in flight no longer idle the
+  // GPU while each one reads its total back). A total past the capacity takes the copy.
+  uint32_t* zc_idx = nullptr;
+  int32_t* zc_rep = nullptr;
+  if (e->zc && bt->h_cidx && bt->h_crep && bt->h_res_cap > 0) {
+    void *di = nullptr, *dr = nullptr;
+    if (dev::host_device_ptr(bt->h_cidx, &di) == 0 && dev::host_device_ptr(bt->h_crep, &dr) == 0) {
+      zc_idx = (uint32_t*)di;
+      zc_rep = (int32_t*)dr;
+    }
+  }
   KPROF(st, "k_compact", B, -1,
         dev::compact(st, bt->start, bt->count, bt->offsets_d, bt->out_idx, bt->out_rep, bt->cidx_d, bt->crep_d, B,
-                     s->view.perm));
+                     s->view.perm, zc_idx, zc_rep, zc_idx ? bt->h_res_cap : 0));
   bt->h_status.resize(B);
   bt->h_err.resize(B);
   bt->h_arg.resize(B);
@@ -3927,6 +3952,17 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   HIPCHK(dev::d2h(bt->h_arg.data(), bt->arg, 8 * (size_t)B, st));
   HIPCHK(dev::d2h(bt->h_offsets.data(), bt->offsets_d, 8 * (size_t)(B + 1), st));
   HIPCHK(dev::d2h(bt->h_stats, bt->stats, sizeof(bt->h_stats), st));
+  // A batch scheduled again copies its previous call's CSR size ahead of the read-back of
+  // this call's total (the rest, if this total is larger, after it): one host round trip
+  // per call instead of two, so the stream has the copy queued behind the kernels.
+  uint64_t spec = 0;
+  if (!zc_idx && bt->h_cidx && bt->h_crep && e->spec_copy) {
+    spec = std::min<uint64_t>(bt->last_tot, bt->h_res_cap);
+    if (spec) {
+      HIPCHK(dev::d2h(bt->h_cidx, bt->cidx_d, 4 * spec, st));
+      HIPCHK(dev::d2h(bt->h_crep, bt->crep_d, 4 * spec, st));
+    }
+  }
   HIPCHK(dev::sync(st));
   std::vector<uint32_t> sets_ovf(bt->sets_cls.size(), 0);
   if (!sets_ovf.empty()) {
@@ -3935,7 +3971,12 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   }
   double tc0 = now_ms();
   const uint64_t tot = bt->h_offsets[B];
+  bool copy = zc_idx == nullptr;  // (written by k_compact unless the total outgrew the buffers)
+  uint64_t have = zc_idx ? tot : spec;  // entries already in the page-locked buffers
+  bt->last_tot = tot;
   if (tot > bt->h_res_cap || !bt->h_cidx) {
+    copy = true;
+    have = 0;
     buf_pool().put(-1, bt->h_cidx, bt->h_cidx_bytes);
     buf_pool().put(-1, bt->h_crep, bt->h_crep_bytes);
     bt->h_cidx = nullptr;
@@ -3950,11 +3991,11 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
     }
     bt->h_res_cap = std::min(bt->h_cidx_bytes, bt->h_crep_bytes) / 4;
   }
-  if (tot) {
-    HIPCHK(dev::d2h(bt->h_cidx, bt->cidx_d, 4 * tot, st));
-    HIPCHK(dev::d2h(bt->h_crep, bt->crep_d, 4 * tot, st));
+  if (copy && tot > have) {
+    HIPCHK(dev::d2h(bt->h_cidx + have, bt->cidx_d + have, 4 * (tot - have), st));
+    HIPCHK(dev::d2h(bt->h_crep + have, bt->crep_d + have, 4 * (tot - have), st));
+    HIPCHK(dev::sync(st));
   }
-  HIPCHK(dev::sync(st));
   // A component-set class whose simulation outgrew the device's node runs in some
   // cluster (kSetsRunsMax): its bindings report KP_ERR_SETS_CAPACITY, every other
   // binding keeps its result (the CSR is re-packed without their targets).

@@ -464,11 +464,13 @@ extern "C" __global__ void __launch_bounds__(kOffThreads) k_offsets_b(int n, uin
 extern "C" __global__ void __launch_bounds__(64) k_compact(const uint64_t* start, const uint32_t* count,
                                                            const uint64_t* offsets, const uint32_t* in_idx,
                                                            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep,
-                                                           int n, const uint32_t* perm)
+                                                           int n, const uint32_t* perm, uint32_t* h_idx,
+                                                           int32_t* h_rep, uint64_t h_cap)
 #if KP_K(8)
 {
   __shared__ int64_t red[8];
-  body_compact(GpuBlk{red}, (int)blockIdx.x, start, count, offsets, in_idx, in_rep, out_idx, out_rep, n, perm);
+  body_compact(GpuBlk{red}, (int)blockIdx.x, start, count, offsets, in_idx, in_rep, out_idx, out_rep, n, perm, h_idx,
+               h_rep, h_cap);
 }
 #else
 ;
@@ -540,7 +542,11 @@ float event_ms(event_t a, event_t b) {
 
 int alloc(void** p, size_t bytes) { return chk(hipMalloc(p, bytes)); }
 void release(void* p) { (void)hipFree(p); }
-int host_alloc(void** p, size_t bytes) { return chk(hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault)); }
+// (mapped and coherent: the result CSR is written into it by k_compact, uncached, and read
+// by the host after the stream's synchronisation)
+int host_alloc(void** p, size_t bytes) {
+  return chk(hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocMapped | hipHostMallocCoherent));
+}
 void host_release(void* p) {
   if (p) (void)hipHostFree(p);
 }
@@ -810,12 +816,14 @@ int offsets(stream_t st, const int32_t* status, const uint32_t* count, int n, ui
 }
 
 int compact(stream_t st, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
-            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n, const uint32_t* perm) {
+            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n, const uint32_t* perm, uint32_t* h_idx,
+            int32_t* h_rep, uint64_t h_cap) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(k_compact, dim3(n), dim3(64), 0, (hipStream_t)st, start, count, offsets, in_idx, in_rep, out_idx,
-                     out_rep, n, perm);
+                     out_rep, n, perm, h_idx, h_rep, h_cap);
   return chk(hipGetLastError());
 }
+int host_device_ptr(void* host, void** dev) { return chk(hipHostGetDevicePointer(dev, host, 0)); }
 
 }  // namespace dev
 }  // namespace kp

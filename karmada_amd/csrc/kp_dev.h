@@ -120,8 +120,13 @@ int reasons(stream_t st, const SnapView& s, const BatchView& bv, int b0, int nb,
 // part: ceil(n / kOffChunk) u64 of scratch.
 int offsets(stream_t st, const int32_t* status, const uint32_t* count, int n, uint64_t* off, uint64_t* part);
 // (in_idx holds snapshot ranks; out_idx gets perm[rank], the caller's cluster index)
+// h_idx / h_rep (device addresses of page-locked host buffers, h_cap entries each): the
+// CSR entries below h_cap are also written there, over the bus, by the kernel itself.
 int compact(stream_t st, const uint64_t* start, const uint32_t* count, const uint64_t* offsets, const uint32_t* in_idx,
-            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n, const uint32_t* perm);
+            const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n, const uint32_t* perm,
+            uint32_t* h_idx = nullptr, int32_t* h_rep = nullptr, uint64_t h_cap = 0);
+// The device address of page-locked host memory from host_alloc (the same on the host build).
+int host_device_ptr(void* host, void** dev);
 
 }  // namespace dev
 }  // namespace kp

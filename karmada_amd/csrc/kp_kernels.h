@@ -1820,13 +1820,20 @@ KP_FI void body_offsets_b(const BLK& B, int blk, int nblk, int n, uint64_t* offs
 template <class BLK>
 KP_FI void body_compact(const BLK& B, int blk, const uint64_t* start, const uint32_t* count, const uint64_t* offsets,
                         const uint32_t* in_idx, const int32_t* in_rep, uint32_t* out_idx, int32_t* out_rep, int n,
-                        const uint32_t* perm) {
+                        const uint32_t* perm, uint32_t* h_idx = nullptr, int32_t* h_rep = nullptr,
+                        uint64_t h_cap = 0) {
   if (blk >= n) return;
   uint64_t s = start[blk], o = offsets[blk];
   uint32_t c = (uint32_t)(offsets[blk + 1] - o);  // 0 unless the status is OK (body_offsets)
   for (uint32_t i = B.tid(); i < c; i += B.nth()) {
-    out_idx[o + i] = perm[in_idx[s + i]];
-    out_rep[o + i] = in_rep[s + i];
+    const uint32_t ci = perm[in_idx[s + i]];
+    const int32_t cr = in_rep[s + i];
+    out_idx[o + i] = ci;
+    out_rep[o + i] = cr;
+    if (o + i < h_cap) {  // the page-locked host copy (coalesced stores over the bus)
+      h_idx[o + i] = ci;
+      h_rep[o + i] = cr;
+    }
   }
 }
 
