@@ -259,6 +259,9 @@ def main():
     ap.add_argument("--e2e-churn", type=float, default=0.1,
                     help="share of bindings at a new generation per end-to-end cycle (the rest reuse their records)")
     ap.add_argument("--lib", default=None, help="engine library (default karmada_amd/libkp.so)")
+    ap.add_argument("--per-lane", type=int, default=None,
+                    help="batches per in-flight lane (2: the lane submits its next batch before collecting "
+                         "the last, kp_schedule_batch_submit/_collect; default 2 with several lanes)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="batches in flight per GPU: engines (own HIP streams) driven by as many host threads, "
                          "so one batch's result copy-back and host steps overlap another's kernels")
@@ -349,11 +352,17 @@ def main():
     # in-flight batches: engine k schedules the same packed bindings (its own snapshot
     # replica and batch); steps are split over them, each step = one whole batch
     import threading
-    lanes = [(eng, snap, batch)]
+    # per_lane 2: each lane alternates two batches of the same bindings, submitting the next
+    # before collecting the last (kp_schedule_batch_submit / _collect), so its engine's
+    # stream stays queued while the host reads a batch back
+    per_lane = args.per_lane if args.per_lane is not None else (2 if args.inflight > 1 else 1)
+    per_lane = max(1, min(2, per_lane))
+    lanes = [(eng, snap, batch, Batch(snap, structs=u.binding_slice(0, u.n_bindings)) if per_lane > 1 else None)]
     for _ in range(1, max(1, args.inflight)):
         e2 = Engine(local, lib_path=os.path.join(ROOT, args.lib)) if args.lib else Engine(local)
         s2 = Snapshot.from_bytes(e2, snap.to_bytes(), u.names)
-        lanes.append((e2, s2, Batch(s2, structs=u.binding_slice(0, u.n_bindings))))
+        lanes.append((e2, s2, Batch(s2, structs=u.binding_slice(0, u.n_bindings)),
+                      Batch(s2, structs=u.binding_slice(0, u.n_bindings)) if per_lane > 1 else None))
     st_all = []
     results = [None] * len(lanes)
     # completions counted over all lanes: the first n_warm are the warm-up (every lane
@@ -366,13 +375,22 @@ def main():
         clock["t0"] = "at start"
 
     def drive(k):
-        e_k, _, b_k = lanes[k]
+        e_k, _, b_k, b_k2 = lanes[k]
         st = []
+        pair = [b_k, b_k2] if b_k2 is not None else None
+        i = 0
+        if pair:
+            pair[0].submit()
         while True:
             with lock:
                 if clock["done"] >= n_warm + args.steps:
                     break
-            r = b_k.schedule_raw()
+            if pair:
+                pair[(i + 1) % 2].submit()  # the next batch queued behind this one
+                r = pair[i % 2].collect()
+                i += 1
+            else:
+                r = b_k.schedule_raw()
             with lock:
                 now = time.perf_counter()  # (stamped in completion order, under the lock)
                 clock["done"] += 1
@@ -386,6 +404,8 @@ def main():
             results[k] = r
             if timed:
                 st.append(e_k.stage_times())
+        if pair:  # the batch still in flight (after the window; its results stay unread)
+            pair[i % 2].collect()
         with lock:
             st_all.extend(st)
 
@@ -485,10 +505,14 @@ def main():
     # serial: one batch at a time; pipelined: two engines on this GPU, each packing
     # its next batch on the host while the other's batch runs on the device (a
     # scheduler draining its queue), timed over 2 x e2e_reps batches.
-    for e_k, s_k, b_k in lanes[1:]:
+    for e_k, s_k, b_k, b_k2 in lanes[1:]:
         b_k.close()
+        if b_k2 is not None:
+            b_k2.close()
         s_k.close()
         e_k.close()
+    if lanes[0][3] is not None:
+        lanes[0][3].close()
     batch.close()
     e2e = e2e_pipe = e2e_reuse = None
     reuse_hits = 0.0
@@ -626,6 +650,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "inflight": len(lanes),
+        "batches_per_lane": per_lane,
         # the hardware-queue count requested of the HIP runtime (GPU_MAX_HW_QUEUES; unset:
         # HIP's default 4) and the streams each engine drives
         "hip_hw_queues_requested": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),

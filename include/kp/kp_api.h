@@ -477,6 +477,16 @@ int kp_batch_create_keyed(kp_engine* e, const kp_snapshot* s, const kp_binding* 
 
 /* genericScheduler.Schedule for every binding of the batch. */
 int kp_schedule_batch(kp_engine* e, kp_batch* b, kp_results* out);
+/* kp_schedule_batch in two halves, for a caller that keeps batches in flight (a scheduler
+ * draining its queue): _submit queues the batch's kernels and per-binding read-backs on the
+ * engine's stream (it waits only where the region chain's host step does) and returns;
+ * _collect waits for them, copies the CSR back and fills *out exactly as kp_schedule_batch
+ * does. A batch holds one submitted call at a time (KP_ESTATE otherwise); an engine may hold
+ * several submitted batches, collected in any order. Submitting the next batch before
+ * collecting the last keeps the GPU queue fed while the host reads results back. Not with
+ * kp_engine_set_profile (KP_EINVAL). */
+int kp_schedule_batch_submit(kp_engine* e, kp_batch* b);
+int kp_schedule_batch_collect(kp_engine* e, kp_batch* b, kp_results* out);
 
 /* Scheduler.scheduleResourceBindingWithClusterAffinities (scheduler.go:618-684),
  * batched: bindings with n_cluster_affinities > 0 start at getAffinityIndex of their

@@ -331,6 +331,7 @@ struct kp_engine {
     int units_stat;  // >= 0: the count is device-side, h_stats[units_stat]
   };
   bool prof = false;
+  uint64_t submit_seq = 0;  // schedule calls submitted on this engine (stage timing validity)
   std::vector<dev::event_t> pev;
   std::vector<KProf> pk;
   std::vector<kp_kernel_time> ktimes;
@@ -368,6 +369,15 @@ struct kp_snapshot {
 };
 
 // diagnostic builds: phase stamps and counters, kDbgSlots x kDbgSpread (kp_select.h)
+// The state schedule_submit leaves for schedule_finish (one submitted call per batch).
+struct SchedPend {
+  bool live = false, empty = false, zc = false, bits = false, top = false, spread_orders = false;
+  int fast = 0;
+  double t0 = 0, th0 = 0, th1 = 0;
+  uint64_t spec = 0, seq = 0;
+  dev::event_t ev = nullptr;  // recorded after the call's last read-back (kept across calls)
+};
+
 struct kp_batch {
   kp_snapshot* snap = nullptr;
   int B = 0;
@@ -458,6 +468,7 @@ struct kp_batch {
   int32_t* h_crep = nullptr;
   uint64_t h_res_cap = 0;
   uint64_t last_tot = 0;  // the previous call's CSR size (the speculative copy)
+  SchedPend pend;         // a submitted call (schedule_submit) awaiting schedule_finish
   size_t h_cidx_bytes = 0, h_crep_bytes = 0;  // their pooled block sizes
   // The batch's device arena and page-locked buffers go back to the process-wide
   // pools on destruction, where another batch (of any engine) may take them at
@@ -478,6 +489,12 @@ struct kp_batch {
         ev = nullptr;
       }
     fenced = false;
+    if (pend.ev) {  // a submitted call never collected: its work uses the buffers
+      if (pend.live) (void)dev::event_sync(pend.ev);
+      dev::event_destroy(pend.ev);
+      pend.ev = nullptr;
+    }
+    pend.live = false;
   }
   ~kp_batch() {
     quiesce();
@@ -3455,8 +3472,13 @@ static int refuse_out_of_tree(kp_engine* e, const kp_snapshot* s) {
   return KP_ENOTSUP;
 }
 
-static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
-  if (!e || !bt || !out) return KP_EINVAL;
+// A schedule call in two halves: schedule_submit queues every launch and the per-binding
+// read-backs of a batch (the region chain's host steps included) and records bt->pend.ev;
+// schedule_finish waits for that event, copies the CSR back and fills the results.
+// kp_schedule_batch runs both; kp_schedule_batch_submit / _collect let a caller keep the
+// next batch's kernels queued on the engine's stream while it collects the previous one.
+static int schedule_submit(kp_engine* e, kp_batch* bt) {
+  if (!e || !bt) return KP_EINVAL;
   if (int rc = refuse_out_of_tree(e, bt->snap)) return rc;
   (void)dev::set_device(e->device);
   kp_snapshot* s = bt->snap;
@@ -3464,10 +3486,17 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   double t0 = now_ms();
   kp_stage_times tm{};
   dev::stream_t st = e->stream;
+  SchedPend& pd = bt->pend;
+  {
+    const dev::event_t ev = pd.ev;  // (the event is kept across calls)
+    pd = SchedPend{};
+    pd.ev = ev;
+  }
+  pd.t0 = t0;
+  pd.seq = ++e->submit_seq;
   if (B == 0) {
-    memset(out, 0, sizeof(*out));
-    bt->h_offsets.assign(1, 0);
-    out->offsets = bt->h_offsets.data();
+    pd.empty = true;
+    pd.live = true;
     return KP_OK;
   }
   if (!bt->l_region.empty() && s->view.n_regions != bt->n_regions) {
@@ -3952,6 +3981,13 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   HIPCHK(dev::d2h(bt->h_arg.data(), bt->arg, 8 * (size_t)B, st));
   HIPCHK(dev::d2h(bt->h_offsets.data(), bt->offsets_d, 8 * (size_t)(B + 1), st));
   HIPCHK(dev::d2h(bt->h_stats, bt->stats, sizeof(bt->h_stats), st));
+  pd.zc = zc_idx != nullptr;
+  pd.bits = bits;
+  pd.fast = fast;
+  pd.top = top;
+  pd.spread_orders = spread_orders;
+  pd.th0 = th0;
+  pd.th1 = th1;
   // A batch scheduled again copies its previous call's CSR size ahead of the read-back of
   // this call's total (the rest, if this total is larger, after it): one host round trip
   // per call instead of two, so the stream has the copy queued behind the kernels.
@@ -3963,7 +3999,42 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
       HIPCHK(dev::d2h(bt->h_crep, bt->crep_d, 4 * spec, st));
     }
   }
-  HIPCHK(dev::sync(st));
+  pd.spec = spec;
+  if (!pd.ev && dev::event_create(&pd.ev)) {
+    pd.ev = nullptr;
+    e->err = "kp_schedule_batch: event";
+    return KP_EDEVICE;
+  }
+  HIPCHK(dev::event_record(pd.ev, st));
+  pd.live = true;
+  return KP_OK;
+}
+
+static int schedule_finish(kp_engine* e, kp_batch* bt, kp_results* out) {
+  if (!e || !bt || !out) return KP_EINVAL;
+  SchedPend& pd = bt->pend;
+  if (!pd.live) {
+    e->err = "kp_schedule_batch_collect: the batch has no submitted call";
+    return KP_ESTATE;
+  }
+  pd.live = false;
+  (void)dev::set_device(e->device);
+  kp_snapshot* s = bt->snap;
+  const int B = bt->B;
+  if (pd.empty) {
+    memset(out, 0, sizeof(*out));
+    bt->h_offsets.assign(1, 0);
+    out->offsets = bt->h_offsets.data();
+    return KP_OK;
+  }
+  dev::stream_t st = e->stream;
+  const double t0 = pd.t0, th0 = pd.th0, th1 = pd.th1;
+  const bool bits = pd.bits, top = pd.top, spread_orders = pd.spread_orders;
+  const int fast = pd.fast;
+  const uint64_t spec = pd.spec;
+  const bool zc = pd.zc;
+  kp_stage_times tm{};
+  HIPCHK(dev::event_sync(pd.ev));
   std::vector<uint32_t> sets_ovf(bt->sets_cls.size(), 0);
   if (!sets_ovf.empty()) {
     HIPCHK(dev::d2h(sets_ovf.data(), bt->d_sets_ovf, 4 * sets_ovf.size(), st));
@@ -3971,8 +4042,8 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   }
   double tc0 = now_ms();
   const uint64_t tot = bt->h_offsets[B];
-  bool copy = zc_idx == nullptr;  // (written by k_compact unless the total outgrew the buffers)
-  uint64_t have = zc_idx ? tot : spec;  // entries already in the page-locked buffers
+  bool copy = !zc;  // (written by k_compact unless the total outgrew the buffers)
+  uint64_t have = zc ? tot : spec;  // entries already in the page-locked buffers
   bt->last_tot = tot;
   if (tot > bt->h_res_cap || !bt->h_cidx) {
     copy = true;
@@ -4028,25 +4099,28 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   // pair: the pair launch, or k_est_class + k_filter (stream2; filter: k_filter
   // alone); select: from the point where they are complete to the end of the last
   // select kernel.
-  const float ms_pair = dev::event_ms(e->ev[3], e->ev[4]);
-  const float ms_filter = bits ? dev::event_ms(e->ev[5], e->ev[4]) : 0.f;
-  const float ms_sel = dev::event_ms(e->ev[1], e->ev[2]);
+  // (the engine's events time this call unless a later submit has re-recorded them)
+  const bool timed = pd.seq == e->submit_seq;
+  auto ems = [&](int a, int b) { return timed ? dev::event_ms(e->ev[a], e->ev[b]) : 0.f; };
+  const float ms_pair = ems(3, 4);
+  const float ms_filter = bits ? ems(5, 4) : 0.f;
+  const float ms_sel = ems(1, 2);
   tm.pair_launches = bits ? 2 : 1;
   tm.pair_kind = (uint32_t)fast;
   tm.pair_kernel_ms = ms_pair;
   tm.select_kernel_ms = ms_sel;
   tm.filter_kernel_ms = ms_filter;
-  tm.sel_all_kernel_ms = dev::event_ms(e->ev[7], e->ev[8]);
+  tm.sel_all_kernel_ms = ems(7, 8);
   tm.n_sel_all = (uint32_t)bt->l_all.size();
   tm.bits = bits ? 1u : 0u;
   tm.n_classes = bits ? (uint32_t)bt->crep.size() : 0u;
   tm.n_slow = bt->h_stats[0];
   tm.n_top = top ? (uint32_t)bt->n_all_dyn : 0u;
   tm.n_top_fallback = top ? bt->h_stats[9] : 0u;
-  tm.top_kernel_ms = top ? dev::event_ms(e->ev[12], e->ev[13]) : 0.f;
+  tm.top_kernel_ms = top ? ems(12, 13) : 0.f;
   tm.n_cluster = (uint32_t)bt->l_cluster.size();
   tm.n_cluster_order = spread_orders ? bt->h_stats[10] : 0u;
-  tm.cluster_kernel_ms = bt->l_cluster.empty() ? 0.f : dev::event_ms(e->ev[14], e->ev[15]);
+  tm.cluster_kernel_ms = bt->l_cluster.empty() ? 0.f : ems(14, 15);
   tm.n_region = (uint32_t)bt->l_region.size();
   tm.n_region_order = spread_orders ? bt->h_stats[11] : 0u;
 #if defined(KP_STAMPS) || defined(KP_SLOW_CHECK)
@@ -4085,7 +4159,26 @@ static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
   out->n_targets = tot_out;
   return KP_OK;
 }
+static int schedule_batch_impl(kp_engine* e, kp_batch* bt, kp_results* out) {
+  if (!out) return KP_EINVAL;
+  if (int rc = schedule_submit(e, bt)) return rc;
+  return schedule_finish(e, bt, out);
+}
 int kp_schedule_batch(kp_engine* e, kp_batch* bt, kp_results* out) { return batch_fence(e, bt, schedule_batch_impl(e, bt, out)); }
+int kp_schedule_batch_submit(kp_engine* e, kp_batch* bt) {
+  if (e && e->prof) {
+    e->err = "kp_schedule_batch_submit: per-kernel profiling covers kp_schedule_batch only";
+    return KP_EINVAL;
+  }
+  if (bt && bt->pend.live) {
+    e->err = "kp_schedule_batch_submit: the batch's previous call is not collected";
+    return KP_ESTATE;
+  }
+  return batch_fence(e, bt, schedule_submit(e, bt));
+}
+int kp_schedule_batch_collect(kp_engine* e, kp_batch* bt, kp_results* out) {
+  return batch_fence(e, bt, schedule_finish(e, bt, out));
+}
 
 // Runs the pair kernel and returns the rank-ordered device row pointers.
 static int run_pair(kp_engine* e, kp_batch* bt, int64_t* score, int est_mode, int b0, int nb) {

@@ -35,7 +35,7 @@ EXPORTS = (
     "kp_snapshot_destroy", "kp_snapshot_export", "kp_snapshot_import", "kp_snapshot_update", "kp_batch_create",
     "kp_batch_destroy", "kp_batch_create_keyed", "kp_batch_digest", "kp_pack_cache_create", "kp_pack_cache_destroy",
     "kp_pack_cache_get_stats",
-    "kp_schedule_batch", "kp_schedule_affinities", "kp_filter_batch", "kp_filter_reasons", "kp_score_batch", "kp_max_available_replicas", "kp_max_available_component_sets",
+    "kp_schedule_batch", "kp_schedule_batch_submit", "kp_schedule_batch_collect", "kp_schedule_affinities", "kp_filter_batch", "kp_filter_reasons", "kp_score_batch", "kp_max_available_replicas", "kp_max_available_component_sets",
     "kp_model_grades", "kp_node_max_replicas", "kp_node_max_component_sets", "kp_last_stage_times",
     "kp_engine_set_threads", "kp_snapshot_replicate", "kp_engine_set_profile", "kp_last_kernel_times",
     "kp_multi_create", "kp_multi_destroy", "kp_multi_last_error", "kp_multi_devices", "kp_multi_engine",
@@ -77,6 +77,8 @@ def load_library(path: str = LIB_PATH):
     L.kp_batch_create_keyed.argtypes = [vp, vp, C.POINTER(api.kp_binding), C.POINTER(api.kp_binding_key), C.c_uint64,
                                         vp, C.POINTER(vp)]
     L.kp_schedule_batch.argtypes = [vp, vp, C.POINTER(api.kp_results)]
+    L.kp_schedule_batch_submit.argtypes = [vp, vp]
+    L.kp_schedule_batch_collect.argtypes = [vp, vp, C.POINTER(api.kp_results)]
     L.kp_schedule_affinities.argtypes = [vp, vp, C.POINTER(api.kp_binding), C.c_uint64,
                                          C.POINTER(api.kp_affinity_results)]
     L.kp_filter_batch.argtypes = [vp, vp, C.POINTER(C.c_uint64)]
@@ -377,6 +379,18 @@ class Batch:
         r = api.kp_results()
         eng = self.snap.engine
         eng._check(eng.L.kp_schedule_batch(eng.h, self.h, C.byref(r)), "kp_schedule_batch")
+        return r
+
+    def submit(self):
+        """kp_schedule_batch_submit: queue this batch's schedule call (collect() finishes it)."""
+        eng = self.snap.engine
+        eng._check(eng.L.kp_schedule_batch_submit(eng.h, self.h), "kp_schedule_batch_submit")
+
+    def collect(self) -> api.kp_results:
+        """kp_schedule_batch_collect: the results of the submitted call (as schedule_raw)."""
+        r = api.kp_results()
+        eng = self.snap.engine
+        eng._check(eng.L.kp_schedule_batch_collect(eng.h, self.h, C.byref(r)), "kp_schedule_batch_collect")
         return r
 
     def schedule(self) -> List[dict]:
