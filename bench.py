@@ -261,7 +261,7 @@ def main():
     ap.add_argument("--lib", default=None, help="engine library (default karmada_amd/libkp.so)")
     ap.add_argument("--per-lane", type=int, default=None,
                     help="batches per in-flight lane (2: the lane submits its next batch before collecting "
-                         "the last, kp_schedule_batch_submit/_collect; default 2 with several lanes)")
+                         "the last, kp_schedule_batch_submit/_collect; default 1)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="batches in flight per GPU: engines (own HIP streams) driven by as many host threads, "
                          "so one batch's result copy-back and host steps overlap another's kernels")
@@ -355,7 +355,9 @@ def main():
     # per_lane 2: each lane alternates two batches of the same bindings, submitting the next
     # before collecting the last (kp_schedule_batch_submit / _collect), so its engine's
     # stream stays queued while the host reads a batch back
-    per_lane = args.per_lane if args.per_lane is not None else (2 if args.inflight > 1 else 1)
+    # (default 1: two per lane measured slower, 58.3-69.8 vs 67.7-85.6 M/s on one box,
+    # profiles/r06_ab/perlane_*.json: more batches' kernels overlap on the GPU)
+    per_lane = args.per_lane if args.per_lane is not None else 1
     per_lane = max(1, min(2, per_lane))
     lanes = [(eng, snap, batch, Batch(snap, structs=u.binding_slice(0, u.n_bindings)) if per_lane > 1 else None)]
     for _ in range(1, max(1, args.inflight)):
