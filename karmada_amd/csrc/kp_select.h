@@ -966,6 +966,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     bool ok = false;
     WebRes w = webster_reg(B, party, (uint32_t)(e >> 32), (int64_t)(uint32_t)e, N, desc, V, &ok);
     if (ok) {
+      KP_COUNT(sc, 80, 1);
       w.compact = true;
       w.np = np;
       w.Lb = Lb;
@@ -1015,6 +1016,7 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
       return webster_tail(B, r, parties, tstar, N, desc, sc, ecap, compact, np, Lb, pl);
     }
   }
+  KP_STAMPD(sc.dbg, 76);  // (stamps build: [76] the quota adjustment, [77] the first-seat rank, [78] enumeration)
   // Every seat a first seat: with P >= N parties of positive votes and the largest
   // vote below 3 v_N (v_N = the N-th largest vote), every second priority vmax/3 is
   // below v_N (exactly: fl(vmax/3) < v_N by far more than its rounding), so the N
@@ -1036,7 +1038,11 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     B.sync();
     const int64_t vN = *slot;
     B.sync();
-    if (vmax < 3 * vN) return webster_tail(B, r, parties, (double)vN, N, desc, sc, ecap, compact, np, Lb, pl);
+    KP_STAMPD(sc.dbg, 77);
+    if (vmax < 3 * vN) {
+      KP_COUNT(sc, 79, 1);
+      return webster_tail(B, r, parties, (double)vN, N, desc, sc, ecap, compact, np, Lb, pl);
+    }
   }
   auto cnt2 = [&](double ta, double tb, int64_t* ca, int64_t* cb) {
     int64_t a = 0, b = 0;
@@ -1113,6 +1119,9 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
     B.sync();
     tstar = bitsd(rank_select(B, sc.buf, E, (int64_t)N - chi, true, (uint64_t*)sc.whist));
   }
+  KP_STAMPD(sc.dbg, 78);
+  KP_COUNT(sc, 81, 1);
+  KP_COUNT(sc, 82, np);
   return webster_tail(B, r, parties, tstar, N, desc, sc, ecap, compact, np, Lb, pl);
 }
 
