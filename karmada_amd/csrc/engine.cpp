@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <condition_variable>
 #include <functional>
 #include <map>
 #include <memory>
@@ -1776,6 +1777,76 @@ int host_cpus() {
   return n;
 }
 
+// Process-wide worker threads for the packer's per-thread phases (pack, merge, cache
+// inserts): each phase of each batch used to start and join its own threads (three rounds
+// of 16 per batch with kp_pack_cache), and two engines packing at once started 32 at a time.
+// run(T, fn) calls fn(t) once for every t in [0, T), the caller taking tasks too; jobs of
+// concurrent callers interleave task by task. Workers are started lazily, never joined.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* p = new HostPool();  // (never destroyed: workers may be blocked in wait)
+    return *p;
+  }
+  void run(int T, const std::function<void(int)>& fn) {
+    if (T <= 1) {
+      if (T == 1) fn(0);
+      return;
+    }
+    ensure(T - 1);
+    Job j;
+    j.fn = &fn;
+    j.T = T;
+    j.left = T;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.push_back(&j);
+    }
+    cv_.notify_all();
+    for (;;) {  // the caller takes tasks of its own job until none is left to start
+      int t;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (j.next >= j.T) break;
+        t = j.next++;
+        if (j.next >= j.T) q_.erase(std::find(q_.begin(), q_.end(), &j));
+      }
+      fn(t);
+      std::lock_guard<std::mutex> g(mu_);
+      j.left--;
+    }
+    std::unique_lock<std::mutex> g(mu_);
+    done_.wait(g, [&] { return j.left == 0; });
+  }
+
+ private:
+  struct Job {
+    const std::function<void(int)>* fn = nullptr;
+    int T = 0, next = 0, left = 0;
+  };
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  std::vector<Job*> q_;
+  int n_workers_ = 0;
+  void ensure(int n) {
+    std::lock_guard<std::mutex> g(mu_);
+    for (; n_workers_ < n; n_workers_++) std::thread([this] { loop(); }).detach();
+  }
+  void loop() {
+    std::unique_lock<std::mutex> g(mu_);
+    for (;;) {
+      cv_.wait(g, [&] { return !q_.empty(); });
+      Job* j = q_.front();
+      const int t = j->next++;
+      if (j->next >= j->T) q_.erase(q_.begin());
+      g.unlock();
+      (*j->fn)(t);
+      g.lock();
+      if (--j->left == 0) done_.notify_all();
+    }
+  }
+};
+
 template <class F>
 void parallel_for(int n, int threads, F fn) {
   if (n <= 0) return;
@@ -2827,15 +2898,7 @@ bool pack_parallel(kp_snapshot* s, const kp_binding* bindings, int n, kp_batch* 
       tmax_tiers[t] = std::max(tmax_tiers[t], max_tiers);
     }
   };
-  auto on_threads = [&](auto fn) {
-    if (T == 1) {
-      fn(0);
-      return;
-    }
-    std::vector<std::thread> th;
-    for (int t = 0; t < T; t++) th.emplace_back(fn, t);
-    for (auto& x : th) x.join();
-  };
+  auto on_threads = [&](auto fn) { HostPool::get().run(T, std::function<void(int)>(fn)); };
   const auto tq0 = std::chrono::steady_clock::now();
   on_threads(run);
   const auto tq1 = std::chrono::steady_clock::now();

@@ -1106,14 +1106,15 @@ KP_FI WebRes webster_par(const BLK& B, Parties all_parties, int32_t N, bool desc
   } else {
     // enumerate the <= 64 priorities in [lo, hi); t* is the (N - chi)-th largest
     const double tl = bitsd(lo), th = bitsd(hi);
+    const double rl = 1.0 / tl, rh = 1.0 / th;  // (w_count_r: the same counts, no division per party)
     int32_t mine = 0;
     parties([&](uint32_t, int64_t v) {
-      mine += (int32_t)(w_count(v, tl, capN, true) - w_count(v, th, capN, true));
+      mine += (int32_t)(w_count_r(v, tl, rl, capN, true) - w_count_r(v, th, rh, capN, true));
     });
     int32_t E;
     int32_t pos = B.excl_scan(mine, &E);
     parties([&](uint32_t, int64_t v) {
-      int64_t k0 = w_count(v, th, capN, true), k1 = w_count(v, tl, capN, true);
+      int64_t k0 = w_count_r(v, th, rh, capN, true), k1 = w_count_r(v, tl, rl, capN, true);
       for (int64_t k = k0; k < k1; k++) sc.buf[pos++] = dbits(w_prio(v, k));
     });
     B.sync();
