@@ -262,7 +262,9 @@ def main():
     ap.add_argument("--per-lane", type=int, default=None,
                     help="batches per in-flight lane (2: the lane submits its next batch before collecting "
                          "the last, kp_schedule_batch_submit/_collect; default 1)")
-    ap.add_argument("--inflight", type=int, default=4,
+    # (6: the driver's exact command on two boxes, 5 runs each, means 74.9 / 74.2 M/s at 4 lanes,
+    # 80.1 / 85.3 at 6, 86.0 at 8 with a wider spread; profiles/r06_ab/inflight_*.json)
+    ap.add_argument("--inflight", type=int, default=6,
                     help="batches in flight per GPU: engines (own HIP streams) driven by as many host threads, "
                          "so one batch's result copy-back and host steps overlap another's kernels")
     args = ap.parse_args()
