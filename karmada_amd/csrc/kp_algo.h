@@ -461,7 +461,10 @@ struct EstOps {
   int64_t av[kReqUnroll];                  // summary available of request j < kReqUnroll
 };
 template <int Fast = EST_GENERIC>
-KP_HD inline EstOps est_load(const SnapView& s, const BatchView& bv, const BindHdr& h, int c, uint32_t f) {
+// md (the binding's MaxDivided per template, uniform; estimator-class rows only): the
+// model-node counts of templates whose MaxDivided is 0 are not loaded (their product is 0)
+KP_HD inline EstOps est_load(const SnapView& s, const BatchView& bv, const BindHdr& h, int c, uint32_t f,
+                             const int32_t* md = nullptr) {
   EstOps o;
   o.f = f;
   o.allowed = ldcol(s.allowed, c);
@@ -472,7 +475,7 @@ KP_HD inline EstOps est_load(const SnapView& s, const BatchView& bv, const BindH
 KP_UNROLL
     for (int t = 0; t < kTmplDense; t++) {
       o.mt[t] = 0;
-      if (t < Fast && model) o.mt[t] = ldcol(s.mt_cnt + (size_t)t * s.Cp, c);
+      if (t < Fast && model && (!md || kp_uniform(md[t]) != 0)) o.mt[t] = ldcol(s.mt_cnt + (size_t)t * s.Cp, c);
     }
   } else if (Fast == EST_SUMMARY) {
   } else if (Fast == EST_MIXED) {

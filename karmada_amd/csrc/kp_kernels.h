@@ -295,12 +295,12 @@ KP_FI void body_est_class(const BLK& B, int k, unsigned char* smem, const SnapVi
     B.sync();
     for (int i = B.tid(); i < F; i += B.nth()) {
       const int c = list[i];
-      row[c] = est_compute_bf<Fast>(s, bv, h, c, mdt.v, est_load<Fast>(s, bv, h, c, ldcol(s.flags, c)));
+      row[c] = est_compute_bf<Fast>(s, bv, h, c, mdt.v, est_load<Fast>(s, bv, h, c, ldcol(s.flags, c), mdt.v));
     }
     return;
   }
   for (int c = B.tid(); c < s.Cp; c += B.nth())
-    row[c] = est_compute_bf<Fast>(s, bv, h, c, mdt.v, est_load<Fast>(s, bv, h, c, ldcol(s.flags, c)));
+    row[c] = est_compute_bf<Fast>(s, bv, h, c, mdt.v, est_load<Fast>(s, bv, h, c, ldcol(s.flags, c), mdt.v));
 }
 
 // Pair-row mode, BF_SETS binding list[blk]: its calAvailableReplicas row from its
