@@ -72,10 +72,23 @@ constexpr int kArgSlots = 16;
 constexpr int kBlock = 256;
 constexpr int kSlowBlock = 512;  // k_slow: wider for the LDS bitonic sort
 // waves per workgroup of the one-wave-per-binding kernels (each wave its own LDS slice)
-constexpr int kTopWaves = 2;     // k_select_top (small workgroups: LDS is granted per workgroup)
-constexpr int kTopWgWaves = 4;   // k_select_top_wg: one binding per workgroup of this many waves
-constexpr int kStaticWaves = 4;  // k_select_static
-constexpr int kOrderWaves = 4;   // k_spread_order, k_region_a_order
+// Waves per workgroup of the one-wave-per-binding kernels. LDS is granted per workgroup and
+// held until its last wave ends, so a finished binding's slice waits for its neighbours':
+// k_select_top at 1 / 2 / 4 waves per workgroup 0.751 / 0.819 / 0.935 ms (same box,
+// profiles/r06_ab/waves_*.json).
+#ifndef KP_TOP_WAVES
+#define KP_TOP_WAVES 1
+#endif
+#ifndef KP_STATIC_WAVES
+#define KP_STATIC_WAVES 4
+#endif
+#ifndef KP_ORDER_WAVES
+#define KP_ORDER_WAVES 4
+#endif
+constexpr int kTopWaves = KP_TOP_WAVES;        // k_select_top
+constexpr int kTopWgWaves = 4;                 // k_select_top_wg: one binding per workgroup of this many waves
+constexpr int kStaticWaves = KP_STATIC_WAVES;  // k_select_static
+constexpr int kOrderWaves = KP_ORDER_WAVES;    // k_spread_order, k_region_a_order
 constexpr int kPairStage = 4096;  // bytes of per-binding predicate data staged in LDS
 constexpr int kTsetMax = 4096;    // distinct taint lists answered once per binding (LDS bits)
 
