@@ -523,10 +523,25 @@ int stream_create(stream_t* s) {
   return 0;
 }
 void stream_destroy(stream_t s) { (void)hipStreamDestroy((hipStream_t)s); }
-int sync(stream_t s) { return chk(hipStreamSynchronize((hipStream_t)s)); }
+// KP_SYNC_BLOCK=1: host waits sleep in the driver (hipEventBlockingSync) instead of polling,
+// so lane threads waiting on their batches leave the process's CPU quota to the others
+static bool blocking_sync() {
+  static const bool on = [] {
+    const char* v = getenv("KP_SYNC_BLOCK");
+    return v && atoi(v) != 0;
+  }();
+  return on;
+}
+int sync(stream_t s) {
+  if (!blocking_sync()) return chk(hipStreamSynchronize((hipStream_t)s));
+  thread_local hipEvent_t ev = nullptr;  // (one per host thread, kept for the process)
+  if (!ev && chk(hipEventCreateWithFlags(&ev, hipEventBlockingSync | hipEventDisableTiming))) return -1;
+  if (chk(hipEventRecord(ev, (hipStream_t)s))) return -1;
+  return chk(hipEventSynchronize(ev));
+}
 int event_create(event_t* e) {
   hipEvent_t h;
-  if (chk(hipEventCreate(&h))) return -1;
+  if (chk(hipEventCreateWithFlags(&h, blocking_sync() ? hipEventBlockingSync : hipEventDefault))) return -1;
   *e = h;
   return 0;
 }
