@@ -277,6 +277,10 @@ def main():
     # 72.3-80.0 M/s; DESIGN.md §5 "Round 6"). KP_STREAMS set in the environment wins.
     if args.inflight > 1:
         os.environ.setdefault("KP_STREAMS", "1")
+        # The lanes' host waits sleep instead of polling (hipEventBlockingSync), leaving the
+        # box's CPU quota to the lanes with host work (same box, driver's command, four runs
+        # each: 93.0-98.8 vs 76.2-95.3 M/s, profiles/r06_ab/sync_*.json)
+        os.environ.setdefault("KP_SYNC_BLOCK", "1")
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -659,6 +663,7 @@ def main():
         # HIP's default 4) and the streams each engine drives
         "hip_hw_queues_requested": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
         "streams_per_engine": int(os.environ.get("KP_STREAMS", "3")),
+        "host_wait": "blocking" if os.environ.get("KP_SYNC_BLOCK", "0") not in ("", "0") else "polling",
         # the timed window: from the (warmup x inflight)-th completed step to the K-th
         # completion after it, every lane mid-stream (module docstring)
         "timed_window": {"warmup_completions": n_warm, "timed_completions": args.steps,
